@@ -1,0 +1,253 @@
+"""Mamba-TasNet hot path, CPU restatement — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Restates (citations relative to /root/reference/Mamba-TasNet):
+  selective_scan       modules/mamba/selective_scan_interface.py:91-157 (selective_scan_ref)
+  causal_conv1d        semantics of causal_conv1d_cuda.causal_conv1d_fwd as pinned by the
+                       in-tree fallback modules/mamba/bimamba.py:278-279 (act(conv1d(x)[..., :L]))
+  rms_norm             mamba-ssm 1.1.3.post1 ops/triton/layernorm.py RMSNorm (un-vendored;
+                       x * rsqrt(mean(x^2) + eps) * w) — parity unpinned, formula restated
+  mamba_inner          MambaInnerFnNoOutProj.forward selective_scan_interface.py:164-229
+  BiMambaV2            modules/mamba/bimamba.py:39-174 (params), :176-253 (v2 forward)
+  Block                modules/mamba/bimamba.py:409-462 (fused_add_norm=False path)
+  MambaBlocksSequential modules/mamba_blocks.py:87-212
+  ChannelwiseLayerNorm speechbrain 1.0.0 lobes/models/conv_tasnet.py (un-vendored; EPS 1e-8,
+                       biased var over channels) — parity unpinned
+  MaskNet              modules/mamba_masknet.py:13-139
+  Encoder / Decoder    speechbrain dual_path.Encoder/Decoder, in-tree copies
+                       baseline/avse2/model.py:14-37
+  compute_forward      train_wsj0mix.py:86-111
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+# ----------------------------------------------------------------------------- ops
+
+def selective_scan(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
+                   return_last_state=False, acc_dtype=torch.float32):
+    """Sequential recurrence h_t = exp(dt*A) h_{t-1} + dt*B_t*u_t; y_t = <C_t, h_t>.
+
+    u, delta, z: (b, d, l); A: (d, n); B, C: (b, n, l) or (b, g, n, l); D, delta_bias: (d,).
+    Follows selective_scan_ref (selective_scan_interface.py:91-157) for real A.
+    """
+    dtype_in = u.dtype
+    u = u.to(acc_dtype)
+    dt = delta.to(acc_dtype)
+    if delta_bias is not None:
+        dt = dt + delta_bias.to(acc_dtype)[:, None]
+    if delta_softplus:
+        dt = F.softplus(dt)
+    b, d, l = u.shape
+    n = A.shape[1]
+    A = A.to(acc_dtype)
+
+    def expand(M):
+        M = M.to(acc_dtype)
+        if M.dim() == 3:  # (b, n, l): shared across d
+            return M[:, None, :, :]
+        g = M.shape[1]    # (b, g, n, l): group g serves d/g channels
+        return M.repeat_interleave(d // g, dim=1)
+
+    Bx, Cx = expand(B), expand(C)                      # (b, d|1, n, l)
+    dA = torch.exp(dt[:, :, None, :] * A[None, :, :, None])     # (b, d, n, l)
+    dBu = (dt * u)[:, :, None, :] * Bx                            # (b, d, n, l)
+    h = torch.zeros(b, d, n, dtype=acc_dtype)
+    ys = []
+    for t in range(l):
+        h = dA[..., t] * h + dBu[..., t]
+        ys.append((h * Cx[..., t]).sum(-1))
+    y = torch.stack(ys, dim=-1) if l > 0 else torch.zeros(b, d, 0, dtype=acc_dtype)
+    out = y if D is None else y + u * D.to(acc_dtype)[:, None]
+    if z is not None:
+        out = out * F.silu(z.to(acc_dtype))
+    out = out.to(dtype_in)
+    return (out, h) if return_last_state else out
+
+
+def causal_conv1d(x, weight, bias=None, silu=False):
+    """Depthwise causal conv: x (b, d, l), weight (d, w), bias (d,) -> (b, d, l)."""
+    d, w = weight.shape
+    y = F.conv1d(x, weight[:, None, :], bias, padding=w - 1, groups=d)[..., : x.shape[-1]]
+    return F.silu(y) if silu else y
+
+
+def rms_norm(x, weight, eps=1e-5):
+    xf = x.float()
+    return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * weight.float()).to(x.dtype)
+
+
+def mamba_inner(xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias):
+    """MambaInnerFnNoOutProj forward (selective_scan_interface.py:164-229): returns out_z (b, d, l)."""
+    b, _, l = xz.shape
+    r = dt_proj_w.shape[1]
+    n = A.shape[1]
+    x, z = xz.chunk(2, dim=1)
+    xc = causal_conv1d(x, conv_w.reshape(conv_w.shape[0], -1), conv_b, silu=True)
+    x_dbl = xc.transpose(1, 2).reshape(b * l, -1) @ x_proj_w.t()           # (bl, r+2n)
+    delta = (dt_proj_w @ x_dbl[:, :r].t()).reshape(-1, b, l).transpose(0, 1)  # (b, d, l)
+    Bm = x_dbl[:, r:r + n].reshape(b, l, n).transpose(1, 2)[:, None]         # (b, 1, n, l)
+    Cm = x_dbl[:, r + n:].reshape(b, l, n).transpose(1, 2)[:, None]
+    return selective_scan(xc, delta, A, Bm, Cm, D, z, dt_bias, delta_softplus=True)
+
+
+# ----------------------------------------------------------------------------- modules
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim, eps=1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        return rms_norm(x, self.weight, self.eps)
+
+
+class BiMambaV2(nn.Module):
+    """Parameters / keys of bimamba.Mamba with bimamba_type='v2' (bimamba.py:39-174)."""
+
+    def __init__(self, d_model, d_state=16, d_conv=4, expand=2):
+        super().__init__()
+        self.d_model, self.d_state, self.d_conv = d_model, d_state, d_conv
+        self.d_inner = expand * d_model
+        self.dt_rank = math.ceil(d_model / 16)
+        di, r, n = self.d_inner, self.dt_rank, d_state
+        self.in_proj = nn.Linear(d_model, 2 * di, bias=False)
+        self.conv1d = nn.Conv1d(di, di, d_conv, groups=di, padding=d_conv - 1, bias=True)
+        self.x_proj = nn.Linear(di, r + 2 * n, bias=False)
+        self.dt_proj = nn.Linear(r, di, bias=True)
+        self.A_log = nn.Parameter(torch.zeros(di, n))
+        self.D = nn.Parameter(torch.ones(di))
+        self.A_b_log = nn.Parameter(torch.zeros(di, n))
+        self.conv1d_b = nn.Conv1d(di, di, d_conv, groups=di, padding=d_conv - 1, bias=True)
+        self.x_proj_b = nn.Linear(di, r + 2 * n, bias=False)
+        self.dt_proj_b = nn.Linear(r, di, bias=True)
+        self.D_b = nn.Parameter(torch.ones(di))
+        self.out_proj = nn.Linear(di, d_model, bias=False)
+
+    def forward(self, h):                       # (b, l, d_model), bimamba.py:176-253
+        xz = F.linear(h, self.in_proj.weight).transpose(1, 2)            # (b, 2di, l)
+        A = -torch.exp(self.A_log.float())
+        A_b = -torch.exp(self.A_b_log.float())
+        f = mamba_inner(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
+                        self.dt_proj.weight, A, self.D.float(), self.dt_proj.bias.float())
+        bk = mamba_inner(xz.flip(-1), self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
+                         self.dt_proj_b.weight, A_b, self.D_b.float(), self.dt_proj_b.bias.float())
+        y = 0.5 * f + 0.5 * bk.flip(-1)
+        return F.linear(y.transpose(1, 2), self.out_proj.weight)
+
+
+class Block(nn.Module):
+    def __init__(self, d_model, mixer, eps=1e-5):
+        super().__init__()
+        self.mixer = mixer
+        self.norm = RMSNorm(d_model, eps)
+
+    def forward(self, h, residual=None):
+        residual = h + residual if residual is not None else h
+        return self.mixer(self.norm(residual)), residual
+
+
+class MambaBlocksSequential(nn.Module):
+    def __init__(self, n_mamba, d_model, d_state=16, expand=2, d_conv=4, eps=1e-5):
+        super().__init__()
+        self.layers = nn.Sequential(*[Block(d_model, BiMambaV2(d_model, d_state, d_conv, expand), eps)
+                                      for _ in range(n_mamba)])
+        self.norm_f = RMSNorm(d_model, eps)
+
+    def forward(self, x):
+        h, res = x, None
+        for layer in self.layers:
+            h, res = layer(h, res)
+        res = h + res if res is not None else h
+        return self.norm_f(res)
+
+
+class ChannelwiseLayerNorm(nn.Module):
+    """speechbrain conv_tasnet.ChannelwiseLayerNorm: input (M, K, N), stats over N."""
+
+    def __init__(self, channels, eps=1e-8):
+        super().__init__()
+        self.eps = eps
+        self.gamma = nn.Parameter(torch.ones(1, 1, channels))
+        self.beta = nn.Parameter(torch.zeros(1, 1, channels))
+
+    def forward(self, y):
+        mean = y.mean(dim=2, keepdim=True)
+        var = ((y - mean) ** 2).mean(dim=2, keepdim=True)
+        return self.gamma * (y - mean) / torch.pow(var + self.eps, 0.5) + self.beta
+
+
+class ChannelsLastConv1x1(nn.Module):
+    """speechbrain nnet.CNN.Conv1d(kernel_size=1, bias=False): (B, L, Cin) -> (B, L, Cout); key conv.weight."""
+
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv = nn.Conv1d(cin, cout, 1, bias=False)
+
+    def forward(self, x):
+        return self.conv(x.transpose(1, 2)).transpose(1, 2)
+
+
+class MaskNet(nn.Module):
+    def __init__(self, enc_dim, bot_dim, n_spk=2, n_mamba=16, d_model=256, d_state=16, expand=2, d_conv=4):
+        super().__init__()
+        self.n_spk = n_spk
+        self.layer_norm = ChannelwiseLayerNorm(enc_dim)
+        self.bottleneck_conv1x1 = ChannelsLastConv1x1(enc_dim, bot_dim)
+        self.mamba_net = MambaBlocksSequential(n_mamba, d_model, d_state, expand, d_conv)
+        self.mask_conv1x1 = ChannelsLastConv1x1(bot_dim, n_spk * enc_dim)
+
+    def forward(self, mixture_w):               # (M, N, K) -> (n_spk, M, N, K); mamba_masknet.py:101-139
+        x = mixture_w.permute(0, 2, 1)
+        Bn, L, D = x.shape
+        y = self.mask_conv1x1(self.mamba_net(self.bottleneck_conv1x1(self.layer_norm(x))))
+        return F.relu(y.reshape(Bn, L, self.n_spk, D).permute(2, 0, 3, 1))
+
+
+class Encoder(nn.Module):
+    def __init__(self, kernel_size=16, out_channels=512):
+        super().__init__()
+        self.conv1d = nn.Conv1d(1, out_channels, kernel_size, stride=kernel_size // 2, bias=False)
+
+    def forward(self, x):                       # (B, T) -> (B, N, L)
+        return F.relu(self.conv1d(x[:, None, :]))
+
+
+class Decoder(nn.ConvTranspose1d):
+    def forward(self, x):                       # (B, N, L) -> (B, T')
+        y = super().forward(x)
+        return y.squeeze(1)
+
+
+class MambaTasNet(nn.Module):
+    """Encoder + MaskNet + Decoder with train_wsj0mix.py:86-111 compute_forward semantics."""
+
+    def __init__(self, N=512, kernel_size=16, n_mamba=32, n_spk=2, d_state=16, expand=2, d_conv=4):
+        super().__init__()
+        self.num_spks = n_spk
+        self.encoder = Encoder(kernel_size, N)
+        self.masknet = MaskNet(N, N, n_spk, n_mamba, N, d_state, expand, d_conv)
+        self.decoder = Decoder(N, 1, kernel_size, stride=kernel_size // 2, bias=False)
+
+    def forward(self, mix):                     # (B, T) -> (B, T, n_spk)
+        mix_w = self.encoder(mix)
+        est_mask = self.masknet(mix_w)
+        sep_h = torch.stack([mix_w] * self.num_spks) * est_mask
+        est = torch.stack([self.decoder(sep_h[i]) for i in range(self.num_spks)], dim=-1)
+        T = mix.shape[1]
+        if T > est.shape[1]:
+            est = F.pad(est, (0, 0, 0, T - est.shape[1]))
+        else:
+            est = est[:, :T, :]
+        return est
+
+
+MAMBA_TASNET_SIZES = {  # hparams/WSJ0Mix/mambatasnet_{XS,S,M,L}.yaml
+    "XS": dict(N=128, n_mamba=16),
+    "S": dict(N=256, n_mamba=16),
+    "M": dict(N=256, n_mamba=32),
+    "L": dict(N=512, n_mamba=32),
+}
