@@ -1,0 +1,222 @@
+"""avse1 AV speech-enhancement baseline on MI355X (drop-in for baseline/avse1/model.py:AVNet).
+
+Module tree and state_dict keys are identical to the reference (Lightning checkpoints load with
+``load_lightning_state_dict``).  Surface mirrored from baseline/avse1/model.py:
+  forward(dict{noisy_audio_spec, lip_images}) :114-128, training_step :130-133, cal_loss :164-168,
+  configure_optimizers :170-178 (Adam; the plateau scheduler is the harness's business).
+MI355X specifics:
+  * the STFT front-end that the reference runs on CPU in its DataLoader
+    (dataset.py:112-118, librosa) and the iSTFT of test.py:85-88 run as HIP kernels
+    (libavse_hip.so: framing + radix-4 FFT-512 per wave) — ``features_from_waves`` / ``enhance``;
+  * convolutions / BatchNorm / LSTM / GEMMs are MIOpen / hipBLASLt MFMA kernels (fp32, exact
+    f32 MFMA on gfx950 — no TF32 shortcut exists), channels-first like the reference.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import kernels as K
+
+STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
+
+
+def _prelu(c):
+    return nn.PReLU(c)
+
+
+class _BasicBlock(nn.Module):            # utils/resnet.py:26-67 (relu_type='prelu')
+    def __init__(self, cin, cout, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.relu1, self.relu2 = _prelu(cout), _prelu(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.downsample = downsample
+
+    def forward(self, x):
+        y = self.bn2(self.conv2(self.relu1(self.bn1(self.conv1(x)))))
+        return self.relu2(y + (x if self.downsample is None else self.downsample(x)))
+
+
+class _ResNet18(nn.Module):              # utils/resnet.py:70-124
+    def __init__(self):
+        super().__init__()
+        chans, cin = (64, 128, 256, 512), 64
+        for i, c in enumerate(chans):
+            s = 1 if i == 0 else 2
+            ds = None if (s == 1 and cin == c) else nn.Sequential(nn.Conv2d(cin, c, 1, s, bias=False), nn.BatchNorm2d(c))
+            setattr(self, f"layer{i + 1}", nn.Sequential(_BasicBlock(cin, c, s, ds), _BasicBlock(c, c)))
+            cin = c
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+
+    def forward(self, x):
+        for i in range(1, 5):
+            x = getattr(self, f"layer{i}")(x)
+        return self.avgpool(x).flatten(1)
+
+
+class _Chomp(nn.Module):
+    def __init__(self, n):
+        super().__init__()
+        self.n = n
+
+    def forward(self, x):
+        return x[:, :, self.n // 2: x.shape[-1] - self.n // 2]
+
+
+class _TemporalBlock(nn.Module):          # utils/tcn.py:144-243 (dwpw=False, symm_chomp=True)
+    def __init__(self, c, k, dil, p_drop):
+        super().__init__()
+        pad = (k - 1) * dil
+        self.conv1 = nn.Conv1d(c, c, k, padding=pad, dilation=dil)
+        self.batchnorm1 = nn.BatchNorm1d(c)
+        self.chomp1 = _Chomp(pad)
+        self.relu1 = _prelu(c)
+        self.dropout1 = nn.Dropout(p_drop)
+        self.conv2 = nn.Conv1d(c, c, k, padding=pad, dilation=dil)
+        self.batchnorm2 = nn.BatchNorm1d(c)
+        self.chomp2 = _Chomp(pad)
+        self.relu2 = _prelu(c)
+        self.dropout2 = nn.Dropout(p_drop)
+        self.net = nn.Sequential(self.conv1, self.batchnorm1, self.chomp1, self.relu1, self.dropout1,
+                                 self.conv2, self.batchnorm2, self.chomp2, self.relu2, self.dropout2)
+        self.downsample = None
+        self.relu = _prelu(c)
+
+    def forward(self, x):
+        return self.relu(self.net(x) + x)
+
+
+class _TCNTrunk(nn.Module):
+    def __init__(self, c=512, levels=4, k=3, p_drop=0.2):
+        super().__init__()
+        self.network = nn.Sequential(*[_TemporalBlock(c, k, 2 ** i, p_drop) for i in range(levels)])
+
+    def forward(self, x):
+        return self.network(x)
+
+
+class _TCN(nn.Module):                    # utils/nn.py:106-128 (extract_feats=True)
+    def __init__(self):
+        super().__init__()
+        self.tcn_trunk = _TCNTrunk()
+        self.tcn_output = nn.Linear(512, 500)   # present in checkpoints, unused on the feature path
+
+    def forward(self, x):
+        return self.tcn_trunk(x.transpose(1, 2))
+
+
+class VisualFeatNet(nn.Module):           # model.py:17-58
+    def __init__(self):
+        super().__init__()
+        self.trunk = _ResNet18()
+        self.frontend3D = nn.Sequential(
+            nn.Conv3d(3, 64, (5, 7, 7), (1, 2, 2), (2, 3, 3), bias=False), nn.BatchNorm3d(64), _prelu(64),
+            nn.MaxPool3d((1, 3, 3), (1, 2, 2), (0, 1, 1)))
+        self.tcn = _TCN()
+
+    def forward(self, lips):              # (B, 3, T, H, W) raw 0..255 float -> (B, T, 512)
+        Bn = lips.shape[0]
+        x = self.frontend3D(lips)
+        Tn = x.shape[2]
+        x = x.transpose(1, 2).reshape(Bn * Tn, x.shape[1], x.shape[3], x.shape[4])
+        x = self.trunk(x).view(Bn, Tn, -1)
+        return self.tcn(x).transpose(1, 2)
+
+
+class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 convs + 1x1 -> 4)
+    def __init__(self, num_conv=5, k=5, filters=64, last_filter=4):
+        super().__init__()
+        self.num_conv, self.last_filter = num_conv, last_filter
+        self.bn0 = nn.BatchNorm2d(1)
+        for i in range(num_conv):
+            dil = 2 ** i
+            setattr(self, f"conv{i + 1}", nn.Conv2d(1 if i == 0 else filters, filters, k, padding=(k - 1) * dil // 2,
+                                                    dilation=dil))
+            setattr(self, f"bn{i + 1}", nn.BatchNorm2d(filters))
+        self.convf = nn.Conv2d(filters, last_filter, 1)
+        self.bn_last = nn.BatchNorm2d(last_filter)
+
+    def forward(self, spec):              # (B, 1, T, F) -> (B, T, 4F)
+        T, Fb = spec.shape[2], spec.shape[3]
+        x = self.bn0(spec)
+        for i in range(1, self.num_conv + 1):
+            x = F.relu(getattr(self, f"bn{i}")(getattr(self, f"conv{i}")(x)))
+        x = F.relu(self.bn_last(self.convf(x)))
+        return x.permute(0, 2, 1, 3).reshape(-1, T, Fb * self.last_filter)
+
+
+class FusionNet(nn.Module):               # model.py:81-96
+    def __init__(self, a_only=False):
+        super().__init__()
+        self.lstm_conv = nn.LSTM((0 if a_only else 512) + 4 * STFT_BINS, STFT_BINS, num_layers=1, batch_first=True)
+        self.time_distributed_1 = nn.Linear(STFT_BINS, STFT_BINS)
+
+    def forward(self, x):
+        return torch.sigmoid(self.time_distributed_1(self.lstm_conv(x)[0]))
+
+
+class AVNet(nn.Module):
+    """LightningModule surface of baseline/avse1/model.py:AVNet (forward / training_step / cal_loss)."""
+
+    def __init__(self, a_only=False, loss="l1", lr=0.00158):
+        super().__init__()
+        self.a_only = a_only
+        self.net_visualfeat = None if a_only else VisualFeatNet()
+        self.net_audiofeat = AudioFeatNet()
+        self.net_fusion = FusionNet(a_only)
+        if loss.lower() == "l1":
+            self.loss = F.l1_loss
+        elif loss.lower() == "l2":
+            self.loss = F.mse_loss
+        else:
+            raise NotImplementedError(f"{loss} is currently unavailable as loss function. Select one of l1, l2")
+        self.lr = lr
+
+    def forward(self, inp):
+        spec = inp["noisy_audio_spec"]
+        T = spec.shape[2]
+        audio = self.net_audiofeat(spec)
+        if self.a_only:
+            comb = audio
+        else:
+            vis = self.net_visualfeat(inp["lip_images"].float())              # (B, 75, 512)
+            # F.interpolate(nearest, size=(T, 512)) on (B, 1, 75, 512) == gather of rows floor(t*75/T)
+            idx = torch.div(torch.arange(T, device=spec.device) * vis.shape[1], T, rounding_mode="floor")
+            comb = torch.cat((vis.index_select(1, idx), audio), dim=-1)
+        mask = self.net_fusion(comb)
+        return spec * mask.unsqueeze(1)
+
+    def cal_loss(self, batch):
+        return self.loss(self(batch), batch["mask"])
+
+    def training_step(self, batch, batch_idx=0):
+        return self.cal_loss(batch)
+
+    def validation_step(self, batch, batch_idx=0):
+        return self.cal_loss(batch)
+
+    def configure_optimizers(self):
+        return torch.optim.Adam(self.parameters(), lr=self.lr)
+
+    # ---- HIP front-end / back-end (what the reference does on CPU with librosa)
+    @staticmethod
+    def features_from_waves(noisy, clean=None):
+        """(B, 48000) waveforms -> batch dict of |STFT|.T features (dataset.py:112-118, 154-157)."""
+        out = {"noisy_audio_spec": K.stft(noisy).unsqueeze(1)}
+        if clean is not None:
+            out["mask"] = K.stft(clean).unsqueeze(1)
+        return out
+
+    @torch.no_grad()
+    def enhance(self, noisy_wave, lip_images, length=None):
+        """test.py:79-89: predicted magnitude x noisy phase -> iSTFT (all on the GPU)."""
+        mag, spec = K.stft(noisy_wave, return_complex=True)
+        pred = self({"noisy_audio_spec": mag.unsqueeze(1), "lip_images": lip_images})[:, 0]
+        return K.istft(pred, spec, noisy_wave.shape[-1] if length is None else length)
+
+
+def load_lightning_state_dict(model, ckpt_state_dict):
+    """Load a Lightning ``.ckpt['state_dict']`` (keys already match: net_visualfeat.*, net_audiofeat.*, ...)."""
+    return model.load_state_dict(ckpt_state_dict, strict=True)

@@ -1,0 +1,218 @@
+// Depthwise causal conv1d (width <= 4, optional SiLU) forward / backward for gfx950.
+//
+// Replaces causal_conv1d_cuda.causal_conv1d_fwd / causal_conv1d_bwd (causal-conv1d
+// 1.1.3.post1, un-vendored) called at
+// /root/reference/Mamba-TasNet/modules/mamba/selective_scan_interface.py:182,244,286.
+// Semantics pinned by the in-tree fallback bimamba.py:278-279:
+//   out[b,d,t] = act(bias[d] + sum_k w[d,k] * x[b,d,t-(W-1)+k]),  x[<0] = 0.
+// One workgroup per (b, d) row; the row is streamed in TILE-sized pieces through LDS with a
+// (W-1)-sample halo so every HBM byte is read once with lane-contiguous accesses (HBM-bound:
+// fwd 2*4 B/elem, bwd 3*4 B/elem).  The backward reduces dweight/dbias per row in LDS and a
+// second kernel sums the per-row partials over the batch (deterministic).
+#include <algorithm>
+
+#include "common.h"
+
+namespace avse {
+namespace cconv {
+
+constexpr int THREADS = 256;
+constexpr int PER = 8;                     // elements per thread per tile
+constexpr int TILE = THREADS * PER;        // 2048
+constexpr int MAXW = 4;
+
+template <int W, bool SILU, bool HAS_BIAS>
+__global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const float* __restrict__ x, int64_t x_bs,
+                                                      int64_t x_ds, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, float* __restrict__ out,
+                                                      int64_t o_bs, int64_t o_ds) {
+    __shared__ float s[TILE + MAXW];
+    const int row = blockIdx.x;
+    const int b = row / D, d = row % D;
+    const float* xr = x + b * x_bs + (int64_t)d * x_ds;
+    float* orow = out + b * o_bs + (int64_t)d * o_ds;
+    float wk[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
+    const float bv = HAS_BIAS ? bias[d] : 0.f;
+    for (int t0 = 0; t0 < L; t0 += TILE) {
+        __syncthreads();
+        // s[i] holds x[t0 - (W-1) + i]
+        for (int i = threadIdx.x; i < TILE + W - 1; i += THREADS) {
+            const int t = t0 - (W - 1) + i;
+            s[i] = (t >= 0 && t < L) ? xr[t] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            const int i = threadIdx.x + p * THREADS, t = t0 + i;
+            if (t < L) {
+                float acc = bv;
+#pragma unroll
+                for (int k = 0; k < W; ++k) acc += wk[k] * s[i + k];
+                orow[t] = SILU ? siluf_(acc) : acc;
+            }
+        }
+    }
+}
+
+template <int W, bool SILU, bool HAS_BIAS>
+__global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const float* __restrict__ x, int64_t x_bs,
+                                                      int64_t x_ds, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, const float* __restrict__ dout,
+                                                      int64_t g_bs, int64_t g_ds, float* __restrict__ dx,
+                                                      int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws) {
+    __shared__ float sx[TILE + 2 * MAXW];
+    __shared__ float sg[TILE + MAXW];
+    __shared__ float sred[THREADS / 64][MAXW + 1];
+    const int row = blockIdx.x;
+    const int b = row / D, d = row % D;
+    const float* xr = x + b * x_bs + (int64_t)d * x_ds;
+    const float* gr = dout + b * g_bs + (int64_t)d * g_ds;
+    float* dxr = dx + b * dx_bs + (int64_t)d * dx_ds;
+    float wk[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
+    const float bv = HAS_BIAS ? bias[d] : 0.f;
+    float dw[W], db = 0.f;
+#pragma unroll
+    for (int k = 0; k < W; ++k) dw[k] = 0.f;
+
+    for (int t0 = 0; t0 < L; t0 += TILE) {
+        __syncthreads();
+        // sx[i] = x[t0 - (W-1) + i], i in [0, TILE + 2(W-1)) ; sg[i] = dpre[t0 + i], i in [0, TILE + W - 1)
+        for (int i = threadIdx.x; i < TILE + 2 * (W - 1); i += THREADS) {
+            const int t = t0 - (W - 1) + i;
+            sx[i] = (t >= 0 && t < L) ? xr[t] : 0.f;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < TILE + W - 1; i += THREADS) {
+            const int t = t0 + i;
+            float g = 0.f;
+            if (t < L) {
+                g = gr[t];
+                if (SILU) {
+                    float pre = bv;
+#pragma unroll
+                    for (int k = 0; k < W; ++k) pre += wk[k] * sx[i + k];
+                    const float sgm = sigmoidf_(pre);
+                    g *= sgm * (1.f + pre * (1.f - sgm));
+                }
+            }
+            sg[i] = g;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            const int i = threadIdx.x + p * THREADS, t = t0 + i;
+            if (t < L) {
+                // dx[t] = sum_k w[k] * dpre[t + (W-1) - k]
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < W; ++k) acc += wk[k] * sg[i + (W - 1) - k];
+                dxr[t] = acc;
+                const float g = sg[i];
+                db += g;
+#pragma unroll
+                for (int k = 0; k < W; ++k) dw[k] += g * sx[i + k];
+            }
+        }
+    }
+    // block reduce dw, db
+#pragma unroll
+    for (int k = 0; k <= W; ++k) {
+        float v = (k < W) ? dw[k] : db;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+        if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x <= W) {
+        float v = 0.f;
+        for (int i = 0; i < THREADS / 64; ++i) v += sred[i][threadIdx.x];
+        ws[(int64_t)row * (MAXW + 1) + threadIdx.x] = v;
+    }
+}
+
+__global__ void reduce_kernel(const float* ws, int batch, int D, int W, float* dw, float* db) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= D * (W + 1)) return;
+    const int d = i / (W + 1), k = i % (W + 1);
+    float v = 0.f;
+    for (int b = 0; b < batch; ++b) v += ws[((int64_t)b * D + d) * (MAXW + 1) + (k < W ? k : MAXW)];
+    if (k < W) dw[d * W + k] = v;
+    else if (db) db[d] = v;
+}
+
+}  // namespace cconv
+}  // namespace avse
+
+using namespace avse::cconv;
+
+extern "C" {
+
+int64_t avse_cconv_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t width) {
+    (void)width;
+    return 4 * batch * dim * (MAXW + 1);
+}
+
+int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const float* x, int64_t x_bs,
+                   int64_t x_ds, const float* weight, const float* bias, float* out, int64_t out_bs, int64_t out_ds,
+                   int32_t silu, avse_stream_t stream) {
+    if (!x || !weight || !out) return AVSE_EINVAL;
+    if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
+    if (batch * dim > (1LL << 31) - 1) return AVSE_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid((unsigned)(batch * dim)), block(THREADS);
+    switch ((int)width) {
+#define CASE(WW)                                                                                               \
+    case WW:                                                                                                   \
+        if (silu) {                                                                                            \
+            if (bias) hipLaunchKernelGGL((fwd_kernel<WW, true, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds); \
+            else hipLaunchKernelGGL((fwd_kernel<WW, true, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds); \
+        } else {                                                                                               \
+            if (bias) hipLaunchKernelGGL((fwd_kernel<WW, false, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds); \
+            else hipLaunchKernelGGL((fwd_kernel<WW, false, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds); \
+        }                                                                                                      \
+        break;
+        CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+        default: return AVSE_ESHAPE;
+    }
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const float* x, int64_t x_bs,
+                   int64_t x_ds, const float* weight, const float* bias, const float* dout, int64_t dout_bs,
+                   int64_t dout_ds, float* dx, int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias,
+                   int32_t silu, float* workspace, avse_stream_t stream) {
+    if (!x || !weight || !dout || !dx || !dweight || !workspace) return AVSE_EINVAL;
+    if (bias && !dbias) return AVSE_EINVAL;
+    if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid((unsigned)(batch * dim)), block(THREADS);
+    switch ((int)width) {
+#define CASE(WW)                                                                                               \
+    case WW:                                                                                                   \
+        if (silu) {                                                                                            \
+            if (bias) hipLaunchKernelGGL((bwd_kernel<WW, true, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace); \
+            else hipLaunchKernelGGL((bwd_kernel<WW, true, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace); \
+        } else {                                                                                               \
+            if (bias) hipLaunchKernelGGL((bwd_kernel<WW, false, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace); \
+            else hipLaunchKernelGGL((bwd_kernel<WW, false, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace); \
+        }                                                                                                      \
+        break;
+        CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+        default: return AVSE_ESHAPE;
+    }
+    AVSE_CHECK_LAUNCH();
+    const int n = (int)(dim * (width + 1));
+    hipLaunchKernelGGL(reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, st, workspace, (int)batch, (int)dim,
+                       (int)width, dweight, dbias);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+}  // extern "C"

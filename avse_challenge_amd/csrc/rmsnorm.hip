@@ -1,0 +1,178 @@
+// Fused residual-add + RMSNorm forward / backward for gfx950.
+//
+// Replaces the Block pre-norm of /root/reference/Mamba-TasNet/modules/mamba/bimamba.py:447-451
+// (residual = hidden + residual; norm(residual)) with the mamba-ssm Triton RMSNorm
+// (x * rsqrt(mean(x^2) + eps) * w, un-vendored) and MambaBlocksSequential.norm_f
+// (mamba_blocks.py:195-197).  One wave per row (n <= 1024, n % 4 == 0), float4 accesses,
+// the sum of squares reduced in registers with cross-lane adds: one HBM pass each way.
+// dweight is reduced per workgroup (grid-stride over rows) and summed by a second kernel.
+#include "common.h"
+
+namespace avse {
+namespace rms {
+
+constexpr int THREADS = 256;
+constexpr int WPB = THREADS / 64;
+constexpr int MAXV = 4;  // float4 per lane -> n <= 1024
+
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(THREADS) void fwd_kernel(int rows, int n, const float* __restrict__ h,
+                                                      const float* __restrict__ res_in, const float* __restrict__ w,
+                                                      float eps, float* __restrict__ y, float* __restrict__ res_out,
+                                                      float* __restrict__ rstd_out) {
+    const int lane = threadIdx.x & 63;
+    const int nv = n / 4;
+    for (int row = blockIdx.x * WPB + (threadIdx.x >> 6); row < rows; row += gridDim.x * WPB) {
+        const float4* hr = reinterpret_cast<const float4*>(h + (int64_t)row * n);
+        const float4* rr = res_in ? reinterpret_cast<const float4*>(res_in + (int64_t)row * n) : nullptr;
+        float4 v[MAXV];
+        float ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < MAXV; ++i) {
+            const int c = lane + i * 64;
+            if (c < nv) {
+                float4 a = hr[c];
+                if (rr) {
+                    const float4 r = rr[c];
+                    a.x += r.x; a.y += r.y; a.z += r.z; a.w += r.w;
+                }
+                v[i] = a;
+                ss += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+            }
+        }
+        ss = wave_sum(ss);
+        const float rs = rsqrtf(ss / n + eps);
+        float4* yr = reinterpret_cast<float4*>(y + (int64_t)row * n);
+        float4* ro = reinterpret_cast<float4*>(res_out + (int64_t)row * n);
+        const float4* wv = reinterpret_cast<const float4*>(w);
+#pragma unroll
+        for (int i = 0; i < MAXV; ++i) {
+            const int c = lane + i * 64;
+            if (c < nv) {
+                const float4 ww = wv[c];
+                const float4 a = v[i];
+                ro[c] = a;
+                yr[c] = make_float4(a.x * rs * ww.x, a.y * rs * ww.y, a.z * rs * ww.z, a.w * rs * ww.w);
+            }
+        }
+        if (lane == 0) rstd_out[row] = rs;
+    }
+}
+
+// dx = rstd * (dy*w - xhat * mean(dy*w*xhat)) + dres_out ; dw_partial = sum_rows dy * xhat
+__global__ __launch_bounds__(THREADS) void bwd_kernel(int rows, int n, const float* __restrict__ dy,
+                                                      const float* __restrict__ dres, const float* __restrict__ x,
+                                                      const float* __restrict__ w, const float* __restrict__ rstd,
+                                                      float* __restrict__ dx, float* __restrict__ ws) {
+    __shared__ float4 sdw[WPB][256];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nv = n / 4;
+    float4 dwacc[MAXV];
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) dwacc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* wv = reinterpret_cast<const float4*>(w);
+    for (int row = blockIdx.x * WPB + wid; row < rows; row += gridDim.x * WPB) {
+        const float4* dyr = reinterpret_cast<const float4*>(dy + (int64_t)row * n);
+        const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)row * n);
+        const float rs = rstd[row];
+        float4 g[MAXV], xh[MAXV];
+        float dot = 0.f;
+#pragma unroll
+        for (int i = 0; i < MAXV; ++i) {
+            const int c = lane + i * 64;
+            if (c < nv) {
+                const float4 a = xr[c], d = dyr[c], ww = wv[c];
+                xh[i] = make_float4(a.x * rs, a.y * rs, a.z * rs, a.w * rs);
+                g[i] = make_float4(d.x * ww.x, d.y * ww.y, d.z * ww.z, d.w * ww.w);
+                dot += g[i].x * xh[i].x + g[i].y * xh[i].y + g[i].z * xh[i].z + g[i].w * xh[i].w;
+                dwacc[i].x += d.x * xh[i].x; dwacc[i].y += d.y * xh[i].y;
+                dwacc[i].z += d.z * xh[i].z; dwacc[i].w += d.w * xh[i].w;
+            }
+        }
+        dot = wave_sum(dot) / n;
+        float4* dxr = reinterpret_cast<float4*>(dx + (int64_t)row * n);
+        const float4* drr = dres ? reinterpret_cast<const float4*>(dres + (int64_t)row * n) : nullptr;
+#pragma unroll
+        for (int i = 0; i < MAXV; ++i) {
+            const int c = lane + i * 64;
+            if (c < nv) {
+                float4 o = make_float4(rs * (g[i].x - xh[i].x * dot), rs * (g[i].y - xh[i].y * dot),
+                                       rs * (g[i].z - xh[i].z * dot), rs * (g[i].w - xh[i].w * dot));
+                if (drr) {
+                    const float4 r = drr[c];
+                    o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+                }
+                dxr[c] = o;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+        const int c = lane + i * 64;
+        if (c < nv) sdw[wid][c] = dwacc[i];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < nv; c += THREADS) {
+        float4 s = sdw[0][c];
+        for (int k = 1; k < WPB; ++k) {
+            const float4 t = sdw[k][c];
+            s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+        }
+        reinterpret_cast<float4*>(ws + (int64_t)blockIdx.x * n)[c] = s;
+    }
+}
+
+__global__ void reduce_kernel(const float* ws, int nblocks, int n, float* dw) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    float v = 0.f;
+    for (int b = 0; b < nblocks; ++b) v += ws[(int64_t)b * n + c];
+    dw[c] = v;
+}
+
+inline int nblocks_for(int64_t rows) {
+    int64_t nb = (rows + WPB - 1) / WPB;
+    return (int)(nb < 1024 ? nb : 1024);
+}
+
+}  // namespace rms
+}  // namespace avse
+
+using namespace avse::rms;
+
+extern "C" {
+
+int avse_add_rmsnorm_fwd(int64_t rows, int64_t n, const float* h, const float* res_in, const float* weight, float eps,
+                         float* y, float* res_out, float* rstd, avse_stream_t stream) {
+    if (!h || !weight || !y || !res_out || !rstd) return AVSE_EINVAL;
+    if (rows <= 0 || n <= 0 || n % 4 || n > 64 * 4 * MAXV || rows > (1LL << 31) - 1) return AVSE_ESHAPE;
+    hipLaunchKernelGGL(fwd_kernel, dim3(nblocks_for(rows)), dim3(THREADS), 0, (hipStream_t)stream, (int)rows, (int)n,
+                       h, res_in, weight, eps, y, res_out, rstd);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int64_t avse_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t n) { return 4 * (int64_t)nblocks_for(rows) * n; }
+
+int avse_rmsnorm_bwd(int64_t rows, int64_t n, const float* dy, const float* dres_out, const float* res_out,
+                     const float* weight, const float* rstd, float* dx, float* dweight, float* workspace,
+                     avse_stream_t stream) {
+    if (!dy || !res_out || !weight || !rstd || !dx || !dweight || !workspace) return AVSE_EINVAL;
+    if (rows <= 0 || n <= 0 || n % 4 || n > 64 * 4 * MAXV || rows > (1LL << 31) - 1) return AVSE_ESHAPE;
+    const int nb = nblocks_for(rows);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(bwd_kernel, dim3(nb), dim3(THREADS), 0, st, (int)rows, (int)n, dy, dres_out, res_out, weight,
+                       rstd, dx, workspace);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, nb, (int)n,
+                       dweight);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+}  // extern "C"

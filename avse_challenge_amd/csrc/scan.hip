@@ -1,0 +1,553 @@
+// Selective-scan forward / backward for gfx950 (MI355X).
+//
+// Replaces selective_scan_cuda.fwd/bwd (mamba-ssm 1.1.3.post1, un-vendored) as called at
+// /root/reference/Mamba-TasNet/modules/mamba/selective_scan_interface.py:42,67,218,252.
+// Semantics: selective_scan_ref (:91-157) with real A, n_groups == 1, dstate 16.
+//
+// Decomposition (channel-parallel, sequential in time — no inter-chunk scan needed):
+//   * workgroup = 256 threads = 4 waves; one batch row b and CPB = 64 channels d.
+//   * a channel's 16 states are split over G = 4 ADJACENT lanes (4 states each), so the
+//     per-step reduction y = sum_n C_n h_n is two DPP quad_perm adds (no LDS);
+//   * time is processed in chunks of TC = 64 steps staged in LDS: u and dt (softplus
+//     applied once per element at load time) interleaved as float2 rows (one ds_read_b64
+//     per step), B and C transposed to [t][B0..15 C0..15] rows (two ds_read_b128 per step,
+//     broadcast to the 16 channels of a wave), all HBM traffic lane-contiguous;
+//   * the forward stores the state at every chunk end into the x intermediates, which is
+//     what lets the backward restart every chunk without a second recompute pass.
+// Backward per chunk (reverse order): recompute the chunk forward keeping the state at
+// each 16-step sub-chunk start, then per sub-chunk (reverse) recompute 16 steps into
+// registers and run the adjoint (lambda) recurrence backwards.  dB/dC (sums over d) are
+// reduced reduce-scatter style across the wave's 16 channels (8 shuffles/step), across the
+// 4 waves in LDS, and written as per-workgroup partial slabs summed by a second kernel —
+// deterministic, no float atomics.
+#include <algorithm>
+
+#include "common.h"
+
+namespace avse {
+namespace scan {
+
+constexpr int NSTATE = 16;
+constexpr int NS = 4;            // states per lane
+constexpr int G = NSTATE / NS;   // lanes per channel
+constexpr int THREADS = 256;
+constexpr int CPW = 64 / G;      // channels per wave
+constexpr int CPB = 4 * CPW;     // channels per block (64)
+constexpr int TC = 64;           // chunk (checkpoint) length
+constexpr int TS = 16;           // backward sub-chunk
+constexpr int UD_STRIDE = 2 * TC + 2;   // float2 rows, 16 channels of a wave -> distinct banks
+constexpr int Z_STRIDE = 2 * TC + 2;
+constexpr int BC_STRIDE = 2 * NSTATE + 4;  // 36 floats: 16-B aligned rows, 4-way write conflicts
+
+struct Lane {
+    int wave, lane, c, g;
+};
+__device__ inline Lane lane_ids() {
+    Lane L;
+    L.wave = threadIdx.x >> 6;
+    L.lane = threadIdx.x & 63;
+    L.c = L.wave * CPW + (L.lane >> 2);
+    L.g = L.lane & 3;
+    return L;
+}
+
+// ------------------------------------------------------------------------------- loaders
+template <typename Tin, bool SOFTPLUS, bool HAS_BIAS>
+__device__ inline void load_u_dt(float* s_ud, const Tin* u, int64_t u_bs, int64_t u_ds, const Tin* dl,
+                                 int64_t d_bs, int64_t d_ds, const float* bias, int b, int d0, int D,
+                                 int t0, int tn) {
+    for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
+        int r = idx / TC, t = idx % TC, d = d0 + r;
+        float uu = 0.f, dt = 0.f;
+        if (d < D && t < tn) {
+            uu = io<Tin>::ld(u + b * u_bs + (int64_t)d * u_ds + t0 + t);
+            dt = io<Tin>::ld(dl + b * d_bs + (int64_t)d * d_ds + t0 + t);
+            if (HAS_BIAS) dt += bias[d];
+            if (SOFTPLUS) dt = softplus(dt);
+        }
+        *reinterpret_cast<float2*>(&s_ud[r * UD_STRIDE + 2 * t]) = make_float2(uu, dt);
+    }
+}
+
+template <typename Tin>
+__device__ inline void load_bc(float* s_bc, const Tin* B, int64_t B_bs, int64_t B_ns, const Tin* C,
+                               int64_t C_bs, int64_t C_ns, int b, int t0, int tn) {
+    for (int idx = threadIdx.x; idx < NSTATE * TC; idx += THREADS) {
+        int n = idx / TC, t = idx % TC;
+        float bv = 0.f, cv = 0.f;
+        if (t < tn) {
+            bv = io<Tin>::ld(B + b * B_bs + n * B_ns + t0 + t);
+            cv = io<Tin>::ld(C + b * C_bs + n * C_ns + t0 + t);
+        }
+        s_bc[t * BC_STRIDE + n] = bv;
+        s_bc[t * BC_STRIDE + NSTATE + n] = cv;
+    }
+}
+
+// ------------------------------------------------------------------------------- forward
+template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS>
+__global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int nblk_d) {
+    __shared__ __attribute__((aligned(16))) float s_ud[CPB * UD_STRIDE];
+    __shared__ __attribute__((aligned(16))) float s_z[HAS_Z ? CPB * (TC + 1) : 2];
+    __shared__ __attribute__((aligned(16))) float s_bc[TC * BC_STRIDE];
+
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int b = bid / nblk_d, d0 = (bid % nblk_d) * CPB;
+    const int D = (int)a.dim, L = (int)a.seqlen;
+    const Lane id = lane_ids();
+    const int d = d0 + id.c;
+    const bool dvalid = d < D;
+
+    float A2[NS], h[NS], asum[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        A2[j] = dvalid ? a.A[(int64_t)d * NSTATE + id.g * NS + j] * AVSE_LOG2E : 0.f;
+        h[j] = 0.f;
+        asum[j] = 0.f;
+    }
+    const float Dv = (HAS_D && dvalid) ? a.D[d] : 0.f;
+
+    const Tin* u = (const Tin*)a.u;
+    const Tin* dl = (const Tin*)a.delta;
+    const Tin* z = (const Tin*)a.z;
+    const int nck = (L + TC - 1) / TC;
+
+    for (int k = 0; k < nck; ++k) {
+        const int t0 = k * TC, tn = min(TC, L - t0);
+        __syncthreads();
+        load_u_dt<Tin, SOFTPLUS, HAS_BIAS>(s_ud, u, a.u_bs, a.u_ds, dl, a.delta_bs, a.delta_ds, a.delta_bias, b,
+                                           d0, D, t0, tn);
+        load_bc<Tin>(s_bc, (const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t0, tn);
+        if (HAS_Z) {
+            for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
+                int r = idx / TC, t = idx % TC, dd = d0 + r;
+                float zz = (dd < D && t < tn) ? io<Tin>::ld(z + b * a.z_bs + (int64_t)dd * a.z_ds + t0 + t) : 0.f;
+                s_z[r * (TC + 1) + t] = siluf_(zz);
+            }
+        }
+        __syncthreads();
+
+        float* my_ud = &s_ud[id.c * UD_STRIDE];
+#pragma unroll 4
+        for (int t = 0; t < tn; ++t) {
+            const float2 ud = *reinterpret_cast<const float2*>(&my_ud[2 * t]);
+            const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
+            const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
+            const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
+            const float cc[4] = {cq.x, cq.y, cq.z, cq.w};
+            const float dt = ud.y, dtu = ud.y * ud.x;
+            float y = 0.f;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                const float e = dt * A2[j];
+                h[j] = fast_exp2(e) * h[j] + dtu * bb[j];
+                asum[j] += e;
+                y += h[j] * cc[j];
+            }
+            y = group_sum<G>(y);
+            const float out = y + Dv * ud.x;
+            if (id.g == 0) {
+                my_ud[2 * t] = out;                                    // u slot <- out
+                if (HAS_Z) s_z[id.c * (TC + 1) + t] *= out;          // silu(z) slot <- out_z
+            }
+        }
+        __syncthreads();
+        Tin* out = (Tin*)a.out;
+        Tin* outz = (Tin*)a.out_z;
+        for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
+            int r = idx / TC, t = idx % TC, dd = d0 + r;
+            if (dd < D && t < tn) {
+                io<Tin>::st(out + b * a.out_bs + (int64_t)dd * a.out_ds + t0 + t, s_ud[r * UD_STRIDE + 2 * t]);
+                if (HAS_Z) io<Tin>::st(outz + b * a.out_z_bs + (int64_t)dd * a.out_z_ds + t0 + t, s_z[r * (TC + 1) + t]);
+            }
+        }
+        if (dvalid) {
+            float* xp = a.x + (((int64_t)b * D + d) * nck + k) * (2 * NSTATE) + 2 * id.g * NS;
+            float4 v0 = make_float4(fast_exp2(asum[0]), h[0], fast_exp2(asum[1]), h[1]);
+            float4 v1 = make_float4(fast_exp2(asum[2]), h[2], fast_exp2(asum[3]), h[3]);
+            reinterpret_cast<float4*>(xp)[0] = v0;
+            reinterpret_cast<float4*>(xp)[1] = v1;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------- backward
+// reduce-scatter of 8 values over the 16 channel lanes (lane bits 2..5) of a wave; returns
+// the full sum of value index vi = 4*b2 + 2*b3 + b4 (b_k = bit k of the lane id).
+__device__ inline float rs8(float v[8], int lane) {
+    const bool b2 = lane & 4, b3 = lane & 8, b4 = lane & 16;
+    float w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float send = b2 ? v[i] : v[i + 4];
+        float keep = b2 ? v[i + 4] : v[i];
+        w[i] = keep + swz_xor<4>(send);
+    }
+    float x2[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        float send = b3 ? w[i] : w[i + 2];
+        float keep = b3 ? w[i + 2] : w[i];
+        x2[i] = keep + swz_xor<8>(send);
+    }
+    float send = b4 ? x2[0] : x2[1];
+    float keep = b4 ? x2[1] : x2[0];
+    float r = keep + swz_xor<16>(send);
+    return r + xor32(r);
+}
+
+template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS>
+__global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int nblk_d) {
+    __shared__ __attribute__((aligned(16))) float s_ud[CPB * UD_STRIDE];   // (u, dt) -> (du, ddelta)
+    __shared__ __attribute__((aligned(16))) float s_zg[CPB * Z_STRIDE];    // (z, dout) -> (dz, g)
+    __shared__ __attribute__((aligned(16))) float s_bc[TC * BC_STRIDE];
+    __shared__ float s_red[4 * TS * 2 * NSTATE];
+    __shared__ float s_oz[CPB * (TC + 1)];                               // recomputed out_z (optional)
+
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int b = bid / nblk_d, cb = bid % nblk_d, d0 = cb * CPB;
+    const int D = (int)a.dim, L = (int)a.seqlen;
+    const Lane id = lane_ids();
+    const int d = d0 + id.c;
+    const bool dvalid = d < D;
+    const int nck = (L + TC - 1) / TC;
+
+    float A[NS], A2[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        A[j] = dvalid ? a.A[(int64_t)d * NSTATE + id.g * NS + j] : 0.f;
+        A2[j] = A[j] * AVSE_LOG2E;
+    }
+    const float Dv = (HAS_D && dvalid) ? a.D[d] : 0.f;
+
+    float lam[NS], dAn[NS], dA_acc[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) { lam[j] = 0.f; dAn[j] = 0.f; dA_acc[j] = 0.f; }
+    float dD_acc = 0.f, dbias_acc = 0.f;
+
+    const Tin* u = (const Tin*)a.u;
+    const Tin* dl = (const Tin*)a.delta;
+    const Tin* z = (const Tin*)a.z;
+    const Tin* dout = (const Tin*)a.dout;
+    float* ws_bc = a.workspace;                                    // (b, nblk_d, 32, L)
+    const int64_t slab = (int64_t)2 * NSTATE * L;
+
+    for (int k = nck - 1; k >= 0; --k) {
+        const int t0 = k * TC, tn = min(TC, L - t0);
+        __syncthreads();
+        load_u_dt<Tin, SOFTPLUS, HAS_BIAS>(s_ud, u, a.u_bs, a.u_ds, dl, a.delta_bs, a.delta_ds, a.delta_bias, b,
+                                           d0, D, t0, tn);
+        load_bc<Tin>(s_bc, (const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t0, tn);
+        for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
+            int r = idx / TC, t = idx % TC, dd = d0 + r;
+            float zz = 0.f, go = 0.f;
+            if (dd < D && t < tn) {
+                if (HAS_Z) zz = io<Tin>::ld(z + b * a.z_bs + (int64_t)dd * a.z_ds + t0 + t);
+                go = io<Tin>::ld(dout + b * a.dout_bs + (int64_t)dd * a.dout_ds + t0 + t);
+            }
+            *reinterpret_cast<float2*>(&s_zg[r * Z_STRIDE + 2 * t]) = make_float2(zz, go);
+        }
+        __syncthreads();
+
+        // pass 1: state at every sub-chunk start
+        float hs[TC / TS][NS];
+        {
+            float h[NS];
+            if (k > 0 && dvalid) {
+                const float* xp = a.x + (((int64_t)b * D + d) * nck + (k - 1)) * (2 * NSTATE) + 2 * id.g * NS;
+#pragma unroll
+                for (int j = 0; j < NS; ++j) h[j] = xp[2 * j + 1];
+            } else {
+#pragma unroll
+                for (int j = 0; j < NS; ++j) h[j] = 0.f;
+            }
+#pragma unroll
+            for (int s = 0; s < TC / TS; ++s) {
+#pragma unroll
+                for (int j = 0; j < NS; ++j) hs[s][j] = h[j];
+                if (s == TC / TS - 1) break;
+#pragma unroll 4
+                for (int i = 0; i < TS; ++i) {
+                    const int t = s * TS + i;
+                    if (t >= tn) break;
+                    const float2 ud = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * t]);
+                    const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
+                    const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
+                    const float dtu = ud.y * ud.x;
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) h[j] = fast_exp2(ud.y * A2[j]) * h[j] + dtu * bb[j];
+                }
+            }
+        }
+
+        // pass 2: sub-chunks in reverse
+#pragma unroll
+        for (int s = TC / TS - 1; s >= 0; --s) {
+            const int ts = s * TS;
+            if (ts < tn) {
+                float hist[TS][NS];
+                // recompute 16 steps; produce g = dout*silu(z), dz, (out_z)
+                {
+                    float h[NS];
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) h[j] = hs[s][j];
+#pragma unroll
+                    for (int i = 0; i < TS; ++i) {
+                        const int t = ts + i;
+                        if (t < tn) {
+                            float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
+                            const float2 ud = *reinterpret_cast<const float2*>(ud_p);
+                            const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
+                            const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
+                            const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
+                            const float cc[4] = {cq.x, cq.y, cq.z, cq.w};
+                            const float dtu = ud.y * ud.x;
+                            float y = 0.f;
+#pragma unroll
+                            for (int j = 0; j < NS; ++j) {
+                                h[j] = fast_exp2(ud.y * A2[j]) * h[j] + dtu * bb[j];
+                                hist[i][j] = h[j];
+                                y += h[j] * cc[j];
+                            }
+                            y = group_sum<G>(y);
+                            const float out = y + Dv * ud.x;
+                            float* zg_p = &s_zg[id.c * Z_STRIDE + 2 * t];
+                            const float2 zg = *reinterpret_cast<const float2*>(zg_p);
+                            float gv, dzv = 0.f, oz = out;
+                            if (HAS_Z) {
+                                const float sg = sigmoidf_(zg.x);
+                                const float sl = zg.x * sg;
+                                gv = zg.y * sl;
+                                dzv = zg.y * out * sg * (1.f + zg.x * (1.f - sg));
+                                oz = out * sl;
+                            } else {
+                                gv = zg.y;
+                            }
+                            if (id.g == 0) {
+                                *reinterpret_cast<float2*>(zg_p) = make_float2(dzv, gv);
+                                if (a.recompute_out_z) s_oz[id.c * (TC + 1) + t] = oz;
+                            }
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < NS; ++j) hist[i][j] = 0.f;
+                        }
+                    }
+                }
+                // adjoint sweep
+#pragma unroll
+                for (int i = TS - 1; i >= 0; --i) {
+                    const int t = ts + i;
+                    float part[8];
+                    if (t < tn) {
+                        float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
+                        const float2 ud = *reinterpret_cast<const float2*>(ud_p);
+                        const float gv = s_zg[id.c * Z_STRIDE + 2 * t + 1];
+                        const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
+                        const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
+                        const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
+                        const float cc[4] = {cq.x, cq.y, cq.z, cq.w};
+                        const float dt = ud.y, uu = ud.x;
+                        float ddt = 0.f, dus = 0.f;
+#pragma unroll
+                        for (int j = 0; j < NS; ++j) {
+                            const float hp = (i == 0) ? hs[s][j] : hist[i > 0 ? i - 1 : 0][j];
+                            const float dA = fast_exp2(dt * A2[j]);
+                            lam[j] = lam[j] * dAn[j] + gv * cc[j];
+                            const float lhp = lam[j] * dA * hp;
+                            ddt += A[j] * lhp + lam[j] * bb[j] * uu;
+                            dus += lam[j] * bb[j];
+                            dA_acc[j] += dt * lhp;
+                            part[j] = lam[j] * dt * uu;
+                            part[4 + j] = gv * hist[i][j];
+                            dAn[j] = dA;
+                        }
+                        ddt = group_sum<G>(ddt);
+                        dus = group_sum<G>(dus);
+                        const float du = dus * dt + gv * Dv;
+                        const float sig = SOFTPLUS ? (1.f - fast_exp(-dt)) : 1.f;
+                        const float ddr = ddt * sig;
+                        dD_acc += gv * uu;
+                        dbias_acc += ddr;
+                        if (id.g == 0) *reinterpret_cast<float2*>(ud_p) = make_float2(du, ddr);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) part[j] = 0.f;
+                    }
+                    const float r = rs8(part, id.lane);
+                    if (id.lane < 32) {
+                        const int vi = ((id.lane >> 2) & 1) * 4 + ((id.lane >> 3) & 1) * 2 + ((id.lane >> 4) & 1);
+                        const int slot = (vi < 4 ? 0 : NSTATE) + id.g * NS + (vi & 3);
+                        s_red[(id.wave * TS + i) * 2 * NSTATE + slot] = r;
+                    }
+                }
+                __syncthreads();
+                // cross-wave sum -> partial slab
+                for (int idx = threadIdx.x; idx < TS * 2 * NSTATE; idx += THREADS) {
+                    const int slot = idx / TS, i = idx % TS, t = ts + i;
+                    if (t < tn) {
+                        float v = 0.f;
+#pragma unroll
+                        for (int w = 0; w < 4; ++w) v += s_red[(w * TS + i) * 2 * NSTATE + slot];
+                        ws_bc[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + t0 + t] = v;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        __syncthreads();
+        // write du, ddelta, dz (+ out_z) tiles
+        Tin* du = (Tin*)a.du;
+        Tin* dd_ = (Tin*)a.ddelta;
+        Tin* dz = (Tin*)a.dz;
+        Tin* oz = (Tin*)a.out_z;
+        for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
+            int r = idx / TC, t = idx % TC, dd = d0 + r;
+            if (dd < D && t < tn) {
+                const float2 v = *reinterpret_cast<const float2*>(&s_ud[r * UD_STRIDE + 2 * t]);
+                io<Tin>::st(du + b * a.du_bs + (int64_t)dd * a.du_ds + t0 + t, v.x);
+                io<Tin>::st(dd_ + b * a.ddelta_bs + (int64_t)dd * a.ddelta_ds + t0 + t, v.y);
+                if (HAS_Z) io<Tin>::st(dz + b * a.dz_bs + (int64_t)dd * a.dz_ds + t0 + t, s_zg[r * Z_STRIDE + 2 * t]);
+                if (a.recompute_out_z)
+                    io<Tin>::st(oz + b * a.out_z_bs + (int64_t)dd * a.out_z_ds + t0 + t, s_oz[r * (TC + 1) + t]);
+            }
+        }
+    }
+    // per-(b, d) partials of dA, dD, ddelta_bias
+    float* ws_d = ws_bc + (int64_t)a.batch * nblk_d * slab;       // (b, D, 18)
+    if (dvalid) {
+        float* p = ws_d + ((int64_t)b * D + d) * (NSTATE + 2);
+#pragma unroll
+        for (int j = 0; j < NS; ++j) p[id.g * NS + j] = dA_acc[j];
+        if (id.g == 0) {
+            p[NSTATE] = dD_acc;
+            p[NSTATE + 1] = dbias_acc;
+        }
+    }
+}
+
+// dB/dC: sum partial slabs over channel blocks
+__global__ void reduce_bc_kernel(const float* ws, int nblk_d, int L, int batch, float* dB, int64_t dB_bs,
+                                 int64_t dB_ns, float* dC, int64_t dC_bs, int64_t dC_ns) {
+    const int64_t slab = (int64_t)2 * NSTATE * L;
+    const int64_t total = (int64_t)batch * 2 * NSTATE * L;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int t = (int)(i % L);
+        const int slot = (int)((i / L) % (2 * NSTATE));
+        const int b = (int)(i / ((int64_t)L * 2 * NSTATE));
+        float v = 0.f;
+        for (int cb = 0; cb < nblk_d; ++cb) v += ws[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + t];
+        if (slot < NSTATE) dB[b * dB_bs + slot * dB_ns + t] = v;
+        else dC[b * dC_bs + (slot - NSTATE) * dC_ns + t] = v;
+    }
+}
+
+// dA (d, n), dD (d), ddelta_bias (d): sum over batch
+__global__ void reduce_d_kernel(const float* ws_d, int batch, int D, float* dA, float* dD, float* dbias) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;     // over D * 18
+    if (i >= D * (NSTATE + 2)) return;
+    const int d = i / (NSTATE + 2), c = i % (NSTATE + 2);
+    float v = 0.f;
+    for (int b = 0; b < batch; ++b) v += ws_d[((int64_t)b * D + d) * (NSTATE + 2) + c];
+    if (c < NSTATE) dA[(int64_t)d * NSTATE + c] = v;
+    else if (c == NSTATE) { if (dD) dD[d] = v; }
+    else if (dbias) dbias[d] = v;
+}
+
+template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS>
+static void launch_fwd(const avse_scan_fwd_args& a, int nblk_d, int nblocks, hipStream_t st) {
+    if (a.delta_softplus)
+        hipLaunchKernelGGL((fwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, true>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
+    else
+        hipLaunchKernelGGL((fwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, false>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
+}
+
+template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS>
+static void launch_bwd(const avse_scan_bwd_args& a, int nblk_d, int nblocks, hipStream_t st) {
+    if (a.delta_softplus)
+        hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, true>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
+    else
+        hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, false>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
+}
+
+}  // namespace scan
+}  // namespace avse
+
+using namespace avse;
+using namespace avse::scan;
+
+#define AVSE_DISPATCH_FLAGS(LAUNCH, T, ARGS, ...)                                                   \
+    do {                                                                                           \
+        const bool hz = ARGS.z != nullptr, hd = ARGS.D != nullptr, hb = ARGS.delta_bias != nullptr; \
+        if (hz && hd && hb) LAUNCH<T, true, true, true>(ARGS, __VA_ARGS__);                        \
+        else if (hz && hd) LAUNCH<T, true, true, false>(ARGS, __VA_ARGS__);                        \
+        else if (hz && hb) LAUNCH<T, true, false, true>(ARGS, __VA_ARGS__);                        \
+        else if (hz) LAUNCH<T, true, false, false>(ARGS, __VA_ARGS__);                             \
+        else if (hd && hb) LAUNCH<T, false, true, true>(ARGS, __VA_ARGS__);                        \
+        else if (hd) LAUNCH<T, false, true, false>(ARGS, __VA_ARGS__);                             \
+        else if (hb) LAUNCH<T, false, false, true>(ARGS, __VA_ARGS__);                             \
+        else LAUNCH<T, false, false, false>(ARGS, __VA_ARGS__);                                    \
+    } while (0)
+
+extern "C" {
+
+int64_t avse_scan_n_chunks(int64_t seqlen) { return (seqlen + TC - 1) / TC; }
+
+int64_t avse_scan_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t seqlen, int64_t dstate) {
+    (void)dstate;
+    const int64_t nblk_d = (dim + CPB - 1) / CPB;
+    return 4 * (batch * nblk_d * 2 * NSTATE * seqlen + batch * dim * (NSTATE + 2));
+}
+
+static int check_common(int64_t batch, int64_t dim, int64_t seqlen, int64_t dstate, int32_t dtype) {
+    if (batch <= 0 || dim <= 0 || seqlen <= 0) return AVSE_ESHAPE;
+    if (dstate != NSTATE) return AVSE_ESHAPE;
+    if (dtype != AVSE_F32 && dtype != AVSE_BF16) return AVSE_EDTYPE;
+    if (batch * ((dim + CPB - 1) / CPB) > (1LL << 30)) return AVSE_ESHAPE;
+    return AVSE_OK;
+}
+
+int avse_scan_fwd(const avse_scan_fwd_args* a, avse_stream_t stream) {
+    if (!a || !a->u || !a->delta || !a->A || !a->B || !a->C || !a->out || !a->x) return AVSE_EINVAL;
+    if (a->z && !a->out_z) return AVSE_EINVAL;
+    int rc = check_common(a->batch, a->dim, a->seqlen, a->dstate, a->in_dtype);
+    if (rc) return rc;
+    const int nblk_d = (int)((a->dim + CPB - 1) / CPB);
+    const int nblocks = (int)(a->batch * nblk_d);
+    hipStream_t st = (hipStream_t)stream;
+    if (a->in_dtype == AVSE_F32) AVSE_DISPATCH_FLAGS(launch_fwd, float, (*a), nblk_d, nblocks, st);
+    else AVSE_DISPATCH_FLAGS(launch_fwd, bf16_t, (*a), nblk_d, nblocks, st);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_scan_bwd(const avse_scan_bwd_args* a, avse_stream_t stream) {
+    if (!a || !a->u || !a->delta || !a->A || !a->B || !a->C || !a->dout || !a->x || !a->du || !a->ddelta ||
+        !a->dA || !a->dB || !a->dC || !a->workspace)
+        return AVSE_EINVAL;
+    if (a->z && !a->dz) return AVSE_EINVAL;
+    if (a->recompute_out_z && (!a->z || !a->out_z)) return AVSE_EINVAL;
+    if (a->D && !a->dD) return AVSE_EINVAL;
+    if (a->delta_bias && !a->ddelta_bias) return AVSE_EINVAL;
+    int rc = check_common(a->batch, a->dim, a->seqlen, a->dstate, a->in_dtype);
+    if (rc) return rc;
+    const int nblk_d = (int)((a->dim + CPB - 1) / CPB);
+    const int nblocks = (int)(a->batch * nblk_d);
+    hipStream_t st = (hipStream_t)stream;
+    if (a->in_dtype == AVSE_F32) AVSE_DISPATCH_FLAGS(launch_bwd, float, (*a), nblk_d, nblocks, st);
+    else AVSE_DISPATCH_FLAGS(launch_bwd, bf16_t, (*a), nblk_d, nblocks, st);
+    AVSE_CHECK_LAUNCH();
+    const int64_t slab = 2 * NSTATE * a->seqlen;
+    const float* ws_d = a->workspace + a->batch * nblk_d * slab;
+    const int64_t tot = a->batch * 2 * NSTATE * a->seqlen;
+    const int rb = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+    hipLaunchKernelGGL(reduce_bc_kernel, dim3(rb), dim3(256), 0, st, a->workspace, nblk_d, (int)a->seqlen,
+                       (int)a->batch, (float*)a->dB, a->dB_bs, a->dB_ns, (float*)a->dC, a->dC_bs, a->dC_ns);
+    AVSE_CHECK_LAUNCH();
+    const int nd = (int)(a->dim * (NSTATE + 2));
+    hipLaunchKernelGGL(reduce_d_kernel, dim3((nd + 255) / 256), dim3(256), 0, st, ws_d, (int)a->batch,
+                       (int)a->dim, a->dA, a->dD, a->ddelta_bias);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,258 @@
+"""torch-facing wrappers over the C ABI (include/avse_hip.h).  GPU tensors only; no fallback.
+
+Each wrapper validates shapes/dtypes/strides, allocates its outputs and workspace with torch
+(caching allocator, stream-ordered) and enqueues the HIP kernels on torch's current stream.
+"""
+import torch
+
+from . import _lib
+from ._lib import AVSE_BF16, AVSE_F32, ScanBwdArgs, ScanFwdArgs, check, ptr, stream_ptr
+
+NSTATE = 16
+
+
+def _need_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("avse_challenge_amd kernels run on the GPU only (got a CPU tensor); "
+                               "the CPU restatement lives in oracle/ and is test infrastructure")
+
+
+def _dtype_code(dt):
+    if dt == torch.float32:
+        return AVSE_F32
+    if dt == torch.bfloat16:
+        return AVSE_BF16
+    raise RuntimeError(f"unsupported dtype {dt} (fp32 or bf16)")
+
+
+def _last_contig(t):
+    return t if t.stride(-1) == 1 else t.contiguous()
+
+
+def _bc4(M, dtype):
+    M = M.to(dtype)
+    if M.dim() == 3:
+        M = M.unsqueeze(1)
+    if M.shape[1] != 1:
+        raise RuntimeError("only n_groups == 1 B/C are supported (the reference path uses 1)")
+    return _last_contig(M)
+
+
+# ------------------------------------------------------------------------ selective scan
+
+def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False):
+    """Returns (out, x, out_z|None) — the selective_scan_cuda.fwd contract."""
+    _need_gpu(u, delta, A, B, C, D, z, delta_bias)
+    u = _last_contig(u)
+    dt = u.dtype
+    delta = _last_contig(delta.to(dt))
+    z = None if z is None else _last_contig(z.to(dt))
+    B, C = _bc4(B, dt), _bc4(C, dt)
+    b, d, l = u.shape
+    if A.shape != (d, NSTATE):
+        raise RuntimeError(f"A must be ({d}, {NSTATE}), got {tuple(A.shape)}")
+    A = A.float().contiguous()
+    D = None if D is None else D.float().contiguous()
+    delta_bias = None if delta_bias is None else delta_bias.float().contiguous()
+    L = _lib.lib()
+    nck = L.avse_scan_n_chunks(l)
+    out = torch.empty((b, d, l), device=u.device, dtype=dt)
+    x = torch.empty((b, d, nck, 2 * NSTATE), device=u.device, dtype=torch.float32)
+    out_z = torch.empty((b, d, l), device=u.device, dtype=dt) if z is not None else None
+    a = ScanFwdArgs()
+    a.batch, a.dim, a.seqlen, a.dstate = b, d, l, NSTATE
+    a.in_dtype, a.delta_softplus = _dtype_code(dt), int(bool(delta_softplus))
+    a.u, a.u_bs, a.u_ds = u.data_ptr(), u.stride(0), u.stride(1)
+    a.delta, a.delta_bs, a.delta_ds = delta.data_ptr(), delta.stride(0), delta.stride(1)
+    a.A = A.data_ptr()
+    a.B, a.B_bs, a.B_ns = B.data_ptr(), B.stride(0), B.stride(2)
+    a.C, a.C_bs, a.C_ns = C.data_ptr(), C.stride(0), C.stride(2)
+    a.D = D.data_ptr() if D is not None else None
+    if z is not None:
+        a.z, a.z_bs, a.z_ds = z.data_ptr(), z.stride(0), z.stride(1)
+        a.out_z, a.out_z_bs, a.out_z_ds = out_z.data_ptr(), out_z.stride(0), out_z.stride(1)
+    a.delta_bias = delta_bias.data_ptr() if delta_bias is not None else None
+    a.out, a.out_bs, a.out_ds = out.data_ptr(), out.stride(0), out.stride(1)
+    a.x = x.data_ptr()
+    check(L.avse_scan_fwd(a, stream_ptr(u.device)), "avse_scan_fwd")
+    return out, x, out_z
+
+
+def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, dz=None,
+                       delta_softplus=False, recompute_out_z=False):
+    """Returns [du, ddelta, dA, dB, dC, dD, ddelta_bias, dz, out_z] — selective_scan_cuda.bwd contract.
+    dB, dC are fp32 shaped (b, 1, n, l); a passed-in ``dz`` view is written in place."""
+    _need_gpu(u, delta, A, B, C, D, z, delta_bias, dout, x)
+    u = _last_contig(u)
+    dt = u.dtype
+    delta = _last_contig(delta.to(dt))
+    dout = _last_contig(dout.to(dt))
+    z = None if z is None else _last_contig(z.to(dt))
+    B, C = _bc4(B, dt), _bc4(C, dt)
+    b, d, l = u.shape
+    A = A.float().contiguous()
+    D = None if D is None else D.float().contiguous()
+    delta_bias = None if delta_bias is None else delta_bias.float().contiguous()
+    x = x.float().contiguous()
+    L = _lib.lib()
+    if x.shape != (b, d, L.avse_scan_n_chunks(l), 2 * NSTATE):
+        raise RuntimeError(f"scan intermediates have shape {tuple(x.shape)}; expected avse layout")
+    dev = u.device
+    du = torch.empty((b, d, l), device=dev, dtype=dt)
+    ddelta = torch.empty((b, d, l), device=dev, dtype=dt)
+    dA = torch.empty((d, NSTATE), device=dev, dtype=torch.float32)
+    dB = torch.empty((b, 1, NSTATE, l), device=dev, dtype=torch.float32)
+    dC = torch.empty((b, 1, NSTATE, l), device=dev, dtype=torch.float32)
+    dD = torch.empty((d,), device=dev, dtype=torch.float32) if D is not None else None
+    dbias = torch.empty((d,), device=dev, dtype=torch.float32) if delta_bias is not None else None
+    if z is not None:
+        if dz is None:
+            dz = torch.empty((b, d, l), device=dev, dtype=dt)
+        elif dz.stride(-1) != 1 or dz.dtype != dt or tuple(dz.shape) != (b, d, l):
+            raise RuntimeError("dz must be a (b, d, l) view with unit last stride and the input dtype")
+    else:
+        dz = None
+    out_z = torch.empty((b, d, l), device=dev, dtype=dt) if (recompute_out_z and z is not None) else None
+    ws = torch.empty((L.avse_scan_bwd_workspace_bytes(b, d, l, NSTATE) + 3) // 4, device=dev, dtype=torch.float32)
+    a = ScanBwdArgs()
+    a.batch, a.dim, a.seqlen, a.dstate = b, d, l, NSTATE
+    a.in_dtype, a.delta_softplus = _dtype_code(dt), int(bool(delta_softplus))
+    a.recompute_out_z = int(out_z is not None)
+    a.u, a.u_bs, a.u_ds = u.data_ptr(), u.stride(0), u.stride(1)
+    a.delta, a.delta_bs, a.delta_ds = delta.data_ptr(), delta.stride(0), delta.stride(1)
+    a.A = A.data_ptr()
+    a.B, a.B_bs, a.B_ns = B.data_ptr(), B.stride(0), B.stride(2)
+    a.C, a.C_bs, a.C_ns = C.data_ptr(), C.stride(0), C.stride(2)
+    a.D = D.data_ptr() if D is not None else None
+    if z is not None:
+        a.z, a.z_bs, a.z_ds = z.data_ptr(), z.stride(0), z.stride(1)
+        a.dz, a.dz_bs, a.dz_ds = dz.data_ptr(), dz.stride(0), dz.stride(1)
+    if out_z is not None:
+        a.out_z, a.out_z_bs, a.out_z_ds = out_z.data_ptr(), out_z.stride(0), out_z.stride(1)
+    a.delta_bias = delta_bias.data_ptr() if delta_bias is not None else None
+    a.dout, a.dout_bs, a.dout_ds = dout.data_ptr(), dout.stride(0), dout.stride(1)
+    a.x = x.data_ptr()
+    a.du, a.du_bs, a.du_ds = du.data_ptr(), du.stride(0), du.stride(1)
+    a.ddelta, a.ddelta_bs, a.ddelta_ds = ddelta.data_ptr(), ddelta.stride(0), ddelta.stride(1)
+    a.dA = dA.data_ptr()
+    a.dB, a.dB_bs, a.dB_ns = dB.data_ptr(), dB.stride(0), dB.stride(2)
+    a.dC, a.dC_bs, a.dC_ns = dC.data_ptr(), dC.stride(0), dC.stride(2)
+    a.dD = dD.data_ptr() if dD is not None else None
+    a.ddelta_bias = dbias.data_ptr() if dbias is not None else None
+    a.workspace = ws.data_ptr()
+    check(L.avse_scan_bwd(a, stream_ptr(dev)), "avse_scan_bwd")
+    return [du, ddelta, dA, dB, dC, dD, dbias, dz, out_z]
+
+
+# ------------------------------------------------------------------------ causal conv1d
+
+def causal_conv1d_fwd(x, weight, bias=None, silu=False):
+    _need_gpu(x, weight, bias)
+    in_dtype = x.dtype
+    x = _last_contig(x.float())
+    if weight.dim() == 3:
+        weight = weight.reshape(weight.shape[0], -1)
+    weight = weight.float().contiguous()
+    bias = None if bias is None else bias.float().contiguous()
+    b, d, l = x.shape
+    w = weight.shape[1]
+    out = torch.empty((b, d, l), device=x.device, dtype=torch.float32)
+    check(_lib.lib().avse_cconv_fwd(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(out),
+                                    out.stride(0), out.stride(1), int(bool(silu)), stream_ptr(x.device)),
+          "avse_cconv_fwd")
+    return out if in_dtype == torch.float32 else out.to(in_dtype)
+
+
+def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False):
+    _need_gpu(x, weight, bias, dout)
+    x = _last_contig(x.float())
+    wshape = weight.shape
+    weight = weight.reshape(wshape[0], -1).float().contiguous()
+    bias = None if bias is None else bias.float().contiguous()
+    dout = _last_contig(dout.float())
+    b, d, l = x.shape
+    w = weight.shape[1]
+    dx_ret = dx
+    if dx is None or dx.dtype != torch.float32 or dx.stride(-1) != 1:
+        dx = torch.empty((b, d, l), device=x.device, dtype=torch.float32)
+    dweight = torch.empty((d, w), device=x.device, dtype=torch.float32)
+    dbias = torch.empty((d,), device=x.device, dtype=torch.float32) if bias is not None else None
+    ws = torch.empty((_lib.lib().avse_cconv_bwd_workspace_bytes(b, d, w) + 3) // 4, device=x.device,
+                     dtype=torch.float32)
+    check(_lib.lib().avse_cconv_bwd(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(dout),
+                                    dout.stride(0), dout.stride(1), ptr(dx), dx.stride(0), dx.stride(1), ptr(dweight),
+                                    ptr(dbias), int(bool(silu)), ptr(ws), stream_ptr(x.device)), "avse_cconv_bwd")
+    if dx_ret is not None and dx_ret is not dx:
+        dx_ret.copy_(dx)
+        dx = dx_ret
+    return [dx, dweight, dbias]
+
+
+# ------------------------------------------------------------------------ add + RMSNorm
+
+def add_rmsnorm_fwd(h, res, weight, eps=1e-5):
+    """(norm(h + res) * w, h + res, rstd) over the last dim; res may be None."""
+    _need_gpu(h, res, weight)
+    n = h.shape[-1]
+    h2 = h.float().contiguous().view(-1, n)
+    r2 = None if res is None else res.float().contiguous().view(-1, n)
+    w = weight.float().contiguous()
+    rows = h2.shape[0]
+    y = torch.empty_like(h2)
+    res_out = torch.empty_like(h2)
+    rstd = torch.empty((rows,), device=h.device, dtype=torch.float32)
+    check(_lib.lib().avse_add_rmsnorm_fwd(rows, n, ptr(h2), ptr(r2), ptr(w), float(eps), ptr(y), ptr(res_out),
+                                          ptr(rstd), stream_ptr(h.device)), "avse_add_rmsnorm_fwd")
+    return y.view(h.shape), res_out.view(h.shape), rstd
+
+
+def rmsnorm_bwd(dy, dres_out, res_out, weight, rstd):
+    _need_gpu(dy, dres_out, res_out, weight, rstd)
+    n = res_out.shape[-1]
+    dy2 = dy.float().contiguous().view(-1, n)
+    dr2 = None if dres_out is None else dres_out.float().contiguous().view(-1, n)
+    x2 = res_out.float().contiguous().view(-1, n)
+    rows = x2.shape[0]
+    dx = torch.empty_like(x2)
+    dw = torch.empty((n,), device=dy.device, dtype=torch.float32)
+    ws = torch.empty((_lib.lib().avse_rmsnorm_bwd_workspace_bytes(rows, n) + 3) // 4, device=dy.device,
+                     dtype=torch.float32)
+    check(_lib.lib().avse_rmsnorm_bwd(rows, n, ptr(dy2), ptr(dr2), ptr(x2), ptr(weight.float().contiguous()),
+                                      ptr(rstd), ptr(dx), ptr(dw), ptr(ws), stream_ptr(dy.device)), "avse_rmsnorm_bwd")
+    return dx.view(res_out.shape), dw
+
+
+# ------------------------------------------------------------------------ STFT / iSTFT
+
+def stft_frames(T):
+    return int(_lib.lib().avse_stft_frames(T))
+
+
+def stft(wave, return_complex=False):
+    """wave (B, T) fp32 -> |STFT|.T (B, frames, 257) [and complex (B, frames, 257)]; librosa 0.8.1 semantics."""
+    _need_gpu(wave)
+    wave = wave.float().contiguous()
+    Bn, T = wave.shape
+    F = stft_frames(T)
+    mag = torch.empty((Bn, F, 257), device=wave.device, dtype=torch.float32)
+    spec = torch.empty((Bn, F, 257, 2), device=wave.device, dtype=torch.float32) if return_complex else None
+    check(_lib.lib().avse_stft_fwd(Bn, T, ptr(wave), ptr(mag), ptr(spec), stream_ptr(wave.device)), "avse_stft_fwd")
+    if return_complex:
+        return mag, torch.view_as_complex(spec)
+    return mag
+
+
+def istft(mag, phase_spec, length):
+    """mag (B, frames, 257) and the complex spectrum whose angle is used (B, frames, 257) -> (B, length)."""
+    _need_gpu(mag, phase_spec)
+    mag = mag.float().contiguous()
+    ps = torch.view_as_real(phase_spec.to(torch.complex64)).contiguous()
+    Bn, F, nb = mag.shape
+    if nb != 257 or tuple(ps.shape[:3]) != (Bn, F, 257):
+        raise RuntimeError("istft expects (B, frames, 257) magnitude and matching complex phase spectrum")
+    fbuf = torch.empty((Bn, F, 512), device=mag.device, dtype=torch.float32)
+    out = torch.empty((Bn, length), device=mag.device, dtype=torch.float32)
+    check(_lib.lib().avse_istft(Bn, F, length, ptr(mag), ptr(ps), ptr(fbuf), ptr(out), stream_ptr(mag.device)),
+          "avse_istft")
+    return out

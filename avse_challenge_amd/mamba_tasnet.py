@@ -1,0 +1,235 @@
+"""Mamba-TasNet separator on the MI355X kernels (drop-in for the reference modules).
+
+Mirrors, with identical parameter names / state_dict keys (checkpoints load unchanged):
+  MambaInnerNoOutProj  Mamba-TasNet/modules/mamba/selective_scan_interface.py:160-294
+  BiMambaV2            modules/mamba/bimamba.py:39-174 (params), :176-253 (v2 forward)
+  Block                modules/mamba/bimamba.py:409-462 (Add -> RMSNorm -> mixer)
+  MambaBlocksSequential modules/mamba_blocks.py:87-212
+  MaskNet              modules/mamba_masknet.py:13-139
+  Encoder / Decoder    speechbrain dual_path Encoder/Decoder (hparams mambatasnet_*.yaml)
+  MambaTasNet.forward  train_wsj0mix.py:86-111 compute_forward
+The scan, the causal conv and the add+RMSNorm run in libavse_hip.so; the dense projections
+are GEMMs (torch.matmul -> hipBLASLt MFMA).  No CPU fallback: CPU tensors raise.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import kernels as K
+
+NSTATE = 16
+
+
+class MambaInnerNoOutProj(torch.autograd.Function):
+    """Conv1d(k4)+SiLU -> x_proj -> dt_proj -> selective scan (z-gated); checkpoint_lvl 1."""
+
+    @staticmethod
+    def forward(ctx, xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias):
+        R = dt_proj_w.shape[1]
+        x, z = xz.chunk(2, dim=1)
+        conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True)             # (b, d, l)
+        x_dbl = torch.matmul(conv_out.transpose(1, 2), x_proj_w.t())             # (b, l, R + 2n)
+        delta = torch.matmul(dt_proj_w, x_dbl[..., :R].transpose(1, 2))          # (b, d, l)
+        Bm = x_dbl[..., R:R + NSTATE].transpose(1, 2).contiguous()               # (b, n, l)
+        Cm = x_dbl[..., R + NSTATE:].transpose(1, 2).contiguous()
+        out, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, dt_bias, True)
+        ctx.save_for_backward(xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck, out)
+        return out_z
+
+    @staticmethod
+    def backward(ctx, dout):
+        xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck, out = ctx.saved_tensors
+        R = dt_proj_w.shape[1]
+        x, z = xz.chunk(2, dim=1)
+        conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True)
+        delta = torch.matmul(dt_proj_w, x_dbl[..., :R].transpose(1, 2))
+        dxz = torch.empty_like(xz)
+        dx, dz = dxz.chunk(2, dim=1)
+        dconv, ddelta, dA, dB, dC, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
+            conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, out, dz, True, False)
+        dx_dbl = torch.empty_like(x_dbl)
+        dx_dbl[..., R:R + NSTATE] = dB[:, 0].transpose(1, 2)
+        dx_dbl[..., R + NSTATE:] = dC[:, 0].transpose(1, 2)
+        ddt_proj_w = torch.einsum("bdl,blr->dr", ddelta, x_dbl[..., :R])
+        dx_dbl[..., :R] = torch.matmul(ddelta.transpose(1, 2), dt_proj_w)
+        dx_proj_w = torch.einsum("blk,bdl->kd", dx_dbl, conv_out)
+        dconv = dconv + torch.matmul(x_proj_w.t(), dx_dbl.transpose(1, 2))
+        _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True)
+        return (dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias)
+
+
+class AddRMSNorm(torch.autograd.Function):
+    """(RMSNorm(h + res) * w, h + res) — bimamba.py:447-451 with mamba-ssm RMSNorm (eps 1e-5)."""
+
+    @staticmethod
+    def forward(ctx, h, res, weight, eps):
+        y, res_out, rstd = K.add_rmsnorm_fwd(h, res, weight, eps)
+        ctx.has_res = res is not None
+        ctx.save_for_backward(res_out, weight, rstd)
+        return y, res_out
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        res_out, weight, rstd = ctx.saved_tensors
+        dx, dw = K.rmsnorm_bwd(dy, dres, res_out, weight, rstd)
+        return dx, (dx if ctx.has_res else None), dw, None
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, hidden_size, eps=1e-5, device=None, dtype=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(hidden_size, device=device))
+
+    def forward(self, x, residual=None):
+        return AddRMSNorm.apply(x, residual, self.weight, self.eps)[0]
+
+
+class BiMambaV2(nn.Module):
+    """bimamba.Mamba(bimamba_type='v2', if_devide_out=True): same parameters and init."""
+
+    def __init__(self, d_model, d_state=16, d_conv=4, expand=2, dt_min=0.001, dt_max=0.1, dt_init_floor=1e-4):
+        super().__init__()
+        assert d_state == NSTATE, "the HIP scan is built for d_state 16 (all reference configs)"
+        self.d_model, self.d_state, self.d_conv = d_model, d_state, d_conv
+        self.d_inner = expand * d_model
+        self.dt_rank = math.ceil(d_model / 16)
+        di, r, n = self.d_inner, self.dt_rank, d_state
+        self.in_proj = nn.Linear(d_model, 2 * di, bias=False)
+        self.conv1d = nn.Conv1d(di, di, d_conv, groups=di, padding=d_conv - 1, bias=True)
+        self.x_proj = nn.Linear(di, r + 2 * n, bias=False)
+        self.dt_proj = nn.Linear(r, di, bias=True)
+        self.A_log = nn.Parameter(torch.log(torch.arange(1, n + 1, dtype=torch.float32)).repeat(di, 1))
+        self.D = nn.Parameter(torch.ones(di))
+        self.A_b_log = nn.Parameter(torch.log(torch.arange(1, n + 1, dtype=torch.float32)).repeat(di, 1))
+        self.conv1d_b = nn.Conv1d(di, di, d_conv, groups=di, padding=d_conv - 1, bias=True)
+        self.x_proj_b = nn.Linear(di, r + 2 * n, bias=False)
+        self.dt_proj_b = nn.Linear(r, di, bias=True)
+        self.D_b = nn.Parameter(torch.ones(di))
+        self.out_proj = nn.Linear(di, d_model, bias=False)
+        # dt init as bimamba.py:101-120
+        std = self.dt_rank ** -0.5
+        with torch.no_grad():
+            for proj in (self.dt_proj, self.dt_proj_b):
+                nn.init.uniform_(proj.weight, -std, std)
+                dt = torch.exp(torch.rand(di) * (math.log(dt_max) - math.log(dt_min)) + math.log(dt_min))
+                dt = dt.clamp(min=dt_init_floor)
+                proj.bias.copy_(dt + torch.log(-torch.expm1(-dt)))
+
+    def forward(self, h):                                        # (b, l, d_model)
+        xz = torch.matmul(self.in_proj.weight, h.transpose(1, 2))                # (b, 2di, l)
+        A = -torch.exp(self.A_log.float())
+        A_b = -torch.exp(self.A_b_log.float())
+        f = MambaInnerNoOutProj.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
+                                      self.dt_proj.weight, A, self.D.float(), self.dt_proj.bias.float())
+        bk = MambaInnerNoOutProj.apply(xz.flip(-1), self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
+                                       self.dt_proj_b.weight, A_b, self.D_b.float(), self.dt_proj_b.bias.float())
+        y = 0.5 * f + 0.5 * bk.flip(-1)
+        return F.linear(y.transpose(1, 2), self.out_proj.weight)
+
+
+class Block(nn.Module):
+    def __init__(self, d_model, mixer, eps=1e-5):
+        super().__init__()
+        self.mixer = mixer
+        self.norm = RMSNorm(d_model, eps)
+
+    def forward(self, h, residual=None):
+        y, residual = AddRMSNorm.apply(h, residual, self.norm.weight, self.norm.eps)
+        return self.mixer(y), residual
+
+
+class MambaBlocksSequential(nn.Module):
+    def __init__(self, n_mamba, d_model, d_state=16, expand=2, d_conv=4, eps=1e-5):
+        super().__init__()
+        self.layers = nn.Sequential(*[Block(d_model, BiMambaV2(d_model, d_state, d_conv, expand), eps)
+                                      for _ in range(n_mamba)])
+        self.norm_f = RMSNorm(d_model, eps)
+
+    def forward(self, x):
+        h, res = x, None
+        for layer in self.layers:
+            h, res = layer(h, res)
+        return AddRMSNorm.apply(h, res, self.norm_f.weight, self.norm_f.eps)[0]
+
+
+class ChannelwiseLayerNorm(nn.Module):
+    """speechbrain conv_tasnet.ChannelwiseLayerNorm (EPS 1e-8, biased var over channels)."""
+
+    def __init__(self, channels, eps=1e-8):
+        super().__init__()
+        self.eps = eps
+        self.gamma = nn.Parameter(torch.ones(1, 1, channels))
+        self.beta = nn.Parameter(torch.zeros(1, 1, channels))
+
+    def forward(self, y):
+        var, mean = torch.var_mean(y, dim=2, keepdim=True, unbiased=False)
+        return self.gamma * (y - mean) * torch.rsqrt(var + self.eps) + self.beta
+
+
+class Conv1x1(nn.Module):
+    """speechbrain nnet.CNN.Conv1d(kernel_size=1, bias=False) on (B, L, C); key conv.weight."""
+
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv = nn.Conv1d(cin, cout, 1, bias=False)
+
+    def forward(self, x):
+        return F.linear(x, self.conv.weight[:, :, 0])
+
+
+class MaskNet(nn.Module):
+    def __init__(self, enc_dim, bot_dim, n_spk=2, n_mamba=16, d_model=256, d_state=16, expand=2, d_conv=4):
+        super().__init__()
+        self.n_spk = n_spk
+        self.layer_norm = ChannelwiseLayerNorm(enc_dim)
+        self.bottleneck_conv1x1 = Conv1x1(enc_dim, bot_dim)
+        self.mamba_net = MambaBlocksSequential(n_mamba, d_model, d_state, expand, d_conv)
+        self.mask_conv1x1 = Conv1x1(bot_dim, n_spk * enc_dim)
+
+    def forward(self, mixture_w):                      # (M, N, K) -> (n_spk, M, N, K)
+        x = mixture_w.permute(0, 2, 1)
+        Bn, L, D = x.shape
+        y = self.mask_conv1x1(self.mamba_net(self.bottleneck_conv1x1(self.layer_norm(x))))
+        return F.relu(y.reshape(Bn, L, self.n_spk, D).permute(2, 0, 3, 1))
+
+
+class Encoder(nn.Module):
+    def __init__(self, kernel_size=16, out_channels=512):
+        super().__init__()
+        self.conv1d = nn.Conv1d(1, out_channels, kernel_size, stride=kernel_size // 2, bias=False)
+
+    def forward(self, x):
+        return F.relu(self.conv1d(x[:, None, :]))
+
+
+class Decoder(nn.ConvTranspose1d):
+    def forward(self, x):
+        return super().forward(x).squeeze(1)
+
+
+class MambaTasNet(nn.Module):
+    """Encoder / MaskNet / Decoder with compute_forward semantics (train_wsj0mix.py:86-111)."""
+
+    def __init__(self, N=512, kernel_size=16, n_mamba=32, n_spk=2, d_state=16, expand=2, d_conv=4):
+        super().__init__()
+        self.num_spks = n_spk
+        self.encoder = Encoder(kernel_size, N)
+        self.masknet = MaskNet(N, N, n_spk, n_mamba, N, d_state, expand, d_conv)
+        self.decoder = Decoder(N, 1, kernel_size, stride=kernel_size // 2, bias=False)
+
+    def forward(self, mix):                            # (B, T) -> (B, T, n_spk)
+        mix_w = self.encoder(mix)
+        est_mask = self.masknet(mix_w)
+        sep_h = mix_w.unsqueeze(0) * est_mask
+        est = torch.stack([self.decoder(sep_h[i]) for i in range(self.num_spks)], dim=-1)
+        T = mix.shape[1]
+        if T > est.shape[1]:
+            return F.pad(est, (0, 0, 0, T - est.shape[1]))
+        return est[:, :T, :]
+
+
+MAMBA_TASNET_SIZES = {"XS": dict(N=128, n_mamba=16), "S": dict(N=256, n_mamba=16),
+                      "M": dict(N=256, n_mamba=32), "L": dict(N=512, n_mamba=32)}

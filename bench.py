@@ -1,0 +1,271 @@
+"""Throughput bench: utterances/s of the avse1 AV training step on MI355X (BASELINE configs[1]).
+
+python bench.py [--gpus N --steps K --warmup W --workload avse1|mamba]
+For N > 1 launch under torch.distributed.run (one rank per GPU, RCCL); every rank trains on
+its own synthetic batch (weak scaling, DDP gradient all-reduce overlapped with backward).
+
+A step = one pass of the hot path over one batch, inputs already resident in HBM:
+  avse1 (default, C2): HIP STFT of the noisy + clean waveforms (B x 48000 @ 16 kHz)
+          -> AVNet forward (75 lip frames 96x96 uint8) -> L1 loss -> backward -> Adam.
+  mamba (C3):  Mamba-TasNet (XS/S/M/L) on B x 4 s @ 8 kHz mixtures -> PIT SI-SNR -> bwd -> Adam.
+Rank 0 prints ONE JSON line (plus "roofline" for the dominant kernel, timed live with HIP
+events on torch's current stream, and "cpu_baseline": the oracle restatement on host cores).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "utterances/sec (3s@16kHz + 75 lip frames)"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+FP32_PEAK_TFS = 157.3          # FP32 matrix (= vector) peak, spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba"])
+    p.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the BASELINE config's)")
+    p.add_argument("--size", default="L", choices=["XS", "S", "M", "L"], help="Mamba-TasNet size")
+    p.add_argument("--lip-hw", type=int, default=96)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-roofline", action="store_true")
+    return p.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+# ------------------------------------------------------------------------------ workloads
+
+class Avse1Step:
+    unit_desc = "3s@16kHz utterance + 75 lip frames"
+
+    def __init__(self, B, dev, rank, world, lip_hw):
+        from avse_challenge_amd import avse1, data
+        self.B, self.lip_hw = B, lip_hw
+        self.model = avse1.AVNet().to(dev).train()
+        self.ddp = self.model
+        if world > 1:
+            self.ddp = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=[dev.index],
+                                                                 bucket_cap_mb=64, gradient_as_bucket_view=True)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=self.model.lr)
+        self.noisy, self.clean, self.lips = data.avse1_batch(B, dev, 1234 + rank, lip_hw)
+        self.avse1 = avse1
+
+    def __call__(self):
+        batch = self.avse1.AVNet.features_from_waves(self.noisy, self.clean)
+        batch["lip_images"] = self.lips
+        pred = self.ddp(batch)
+        loss = self.model.loss(pred, batch["mask"])
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        self.opt.step()
+        return loss
+
+    def config(self, world):
+        return {"workload": "avse1 AV baseline train step (BASELINE configs[1]): HIP STFT front-end + AVNet "
+                            "(ResNet18 lip enc + TCN, dilated Conv2d audio net, LSTM fusion) fwd/bwd + Adam",
+                "global_batch": self.B * world, "per_gpu_batch": self.B, "seq_len": 48000,
+                "stft_frames": 376, "lip_frames": 75, "lip_hw": self.lip_hw, "parallelism": f"dp{world}"}
+
+    def roofline(self, dev):
+        """Dominant kernel class of the step: the 64->64 5x5 dilated Conv2d of AudioFeatNet (MFMA-bound).
+        Times conv3 (dilation 4) forward at the step's shape with HIP events; FLOPs = 2*B*64*64*25*376*257."""
+        conv = self.model.net_audiofeat.conv3
+        x = torch.randn(self.B, 64, 376, 257, device=dev)
+        with torch.no_grad():
+            for _ in range(3):
+                conv(x)
+            torch.cuda.synchronize()
+            n = 10
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(n):
+                conv(x)
+            e1.record()
+            torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / n
+        flops = 2.0 * self.B * 64 * 64 * 25 * 376 * 257
+        ach = flops / (ms * 1e-3) / 1e12
+        return {"kernel": "AudioFeatNet.conv3 fwd (Conv2d 64->64 5x5 dil 4, MIOpen)", "bound": "mfma",
+                "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFS, 4),
+                "traffic": None, "avg_ms": round(ms, 4), "algorithmic_flops_per_launch": flops}
+
+    def cpu_baseline(self):
+        from oracle import avse1_ref, stft_ref
+        nthreads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+        torch.set_num_threads(max(1, min(nthreads, 64)))
+        B = 2
+        m = avse1_ref.AVNet().train()
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        g = torch.Generator().manual_seed(0)
+        noisy = 0.1 * torch.randn(B, 48000, generator=g)
+        clean = 0.1 * torch.randn(B, 48000, generator=g)
+        lips = torch.randint(0, 256, (B, 3, 75, self.lip_hw, self.lip_hw), generator=g, dtype=torch.uint8)
+
+        def step():
+            batch = {"noisy_audio_spec": torch.from_numpy(stft_ref.stft_mag_T(noisy.numpy()))[:, None],
+                     "mask": torch.from_numpy(stft_ref.stft_mag_T(clean.numpy()))[:, None], "lip_images": lips}
+            loss = m.cal_loss(batch)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        step()
+        t0 = time.perf_counter()
+        iters = 0
+        while iters < 2 or (time.perf_counter() - t0 < 10.0 and iters < 6):
+            step()
+            iters += 1
+        dt = time.perf_counter() - t0
+        return {"value": round(B * iters / dt, 4), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
+                "sample": f"oracle/avse1_ref AVNet train step (numpy librosa-0.8.1 STFT + fwd + bwd + Adam), "
+                          f"batch {B}, {iters} steps after 1 warm-up, lips {self.lip_hw}x{self.lip_hw}"}
+
+
+class MambaStep:
+    unit_desc = "4s@8kHz WSJ0-2mix utterance"
+
+    def __init__(self, B, dev, rank, world, size):
+        from avse_challenge_amd import data, losses, mamba_tasnet
+        self.B, self.size = B, size
+        self.model = mamba_tasnet.MambaTasNet(**mamba_tasnet.MAMBA_TASNET_SIZES[size]).to(dev).train()
+        self.ddp = self.model
+        if world > 1:
+            self.ddp = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=[dev.index],
+                                                                 bucket_cap_mb=64, gradient_as_bucket_view=True)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=1.5e-4)
+        self.mix, self.tgt = data.wsj0mix_batch(B, dev, 4321 + rank)
+        self.losses = losses
+
+    def __call__(self):
+        est = self.ddp(self.mix)
+        loss = self.losses.si_snr_pit(self.tgt, est).mean()
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.model.parameters(), 5.0)
+        self.opt.step()
+        return loss
+
+    def config(self, world):
+        return {"workload": f"Mamba-TasNet-{self.size} train step (BASELINE configs[2])", "global_batch": self.B * world,
+                "per_gpu_batch": self.B, "seq_len": 32000, "frames": 3999, "parallelism": f"dp{world}"}
+
+    def roofline(self, dev):
+        from avse_challenge_amd import kernels as K
+        d = 2 * self.model.masknet.mamba_net.layers[0].mixer.d_model
+        b, l = self.B, 3999
+        u = torch.randn(b, d, l, device=dev)
+        dl = 0.1 * torch.randn(b, d, l, device=dev)
+        z = torch.randn(b, d, l, device=dev)
+        A = -torch.rand(d, 16, device=dev) - 0.5
+        Bm, Cm = torch.randn(b, 16, l, device=dev), torch.randn(b, 16, l, device=dev)
+        D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
+        for _ in range(2):
+            K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = 5
+        e0.record()
+        for _ in range(n):
+            K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / n
+        byts = 4.0 * b * l * (5 * d + 2 * 16)     # u, delta, z read; out, out_z written; B, C
+        ach = byts / (ms * 1e-3) / 1e9
+        return {"kernel": "avse_scan_fwd (selective scan, fp32, training fwd writes out + out_z)", "bound": "hbm",
+                "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": None, "avg_ms": round(ms, 4), "algorithmic_bytes_per_launch": byts}
+
+    def cpu_baseline(self):
+        from oracle import losses_ref, mamba_ref
+        torch.set_num_threads(max(1, min(len(os.sched_getaffinity(0)), 64)))
+        m = mamba_ref.MambaTasNet(**mamba_ref.MAMBA_TASNET_SIZES[self.size], n_spk=2)
+        m.masknet.mamba_net.layers = m.masknet.mamba_net.layers[:1]      # 1 of n layers, scaled below
+        n_layers = mamba_ref.MAMBA_TASNET_SIZES[self.size]["n_mamba"]
+        g = torch.Generator().manual_seed(0)
+        mix = 0.1 * torch.randn(1, 32000, generator=g)
+        tgt = 0.1 * torch.randn(1, 32000, 2, generator=g)
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            m(mix)
+        dt = (time.perf_counter() - t0) * n_layers      # forward only, 1 layer timed, scaled to all layers
+        return {"value": round(1.0 / dt, 6), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
+                "sample": f"oracle/mamba_ref forward of 1 of {n_layers} BiMamba layers on one 4 s utterance, "
+                          f"scaled x{n_layers} (forward only; the training step is >=3x slower)"}
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist()
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cudnn.benchmark = True            # as the reference trainers (avse1 train.py:11)
+    if args.workload == "avse1":
+        B = args.batch or 32
+        step = Avse1Step(B, dev, rank, world, args.lip_hw)
+    else:
+        B = args.batch or 64
+        step = MambaStep(B, dev, rank, world, args.size)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    if not torch.isfinite(loss.detach()).all():
+        raise RuntimeError("non-finite loss in the timed region")
+
+    roof = None if args.no_roofline or rank != 0 else step.roofline(dev)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = step.cpu_baseline()
+    if rank == 0:
+        value = world * B * args.steps / dt
+        rec = {"metric": METRIC if args.workload == "avse1" else "utterances/sec (4s@8kHz WSJ0-2mix, Mamba-TasNet)",
+               "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "data": "synthetic (speech-like noise with 4 Hz envelope at SNR {0,3,6,9} dB, uint8 lips; "
+                       "random-init weights)",
+               "config": step.config(world), "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

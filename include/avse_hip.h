@@ -1,0 +1,143 @@
+/*
+ * avse_hip.h — C ABI of the MI355X (gfx950) hot-path kernels of avse_challenge_amd.
+ *
+ * Plain pointers + sizes + strides; no torch types.  Every entry point:
+ *   - enqueues on the given hipStream_t only (NULL = default stream), never synchronises,
+ *     never allocates: outputs and workspaces are caller-owned (graph-capture safe);
+ *   - returns AVSE_OK (0) or a negative error code (see avse_strerror) after validating
+ *     shapes / strides / alignment on the host, BEFORE any launch;
+ *   - is stateless and thread-safe.
+ * Element strides are in ELEMENTS of the tensor's dtype; the innermost (seqlen / time)
+ * dimension must be contiguous (stride 1), as the reference kernels require
+ * (Mamba-TasNet/modules/mamba/selective_scan_interface.py:23-35, :171-173).
+ *
+ * Which reference interface each entry replaces is cited per function; the reference-side
+ * binding a maintainer would add is shown in INTEGRATION.md.
+ */
+#ifndef AVSE_HIP_H
+#define AVSE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* avse_stream_t; /* a hipStream_t */
+
+enum { AVSE_OK = 0, AVSE_EINVAL = -1, AVSE_ESHAPE = -2, AVSE_EDTYPE = -3, AVSE_ELAUNCH = -4, AVSE_EALIGN = -5 };
+enum { AVSE_F32 = 0, AVSE_BF16 = 1 };
+
+const char* avse_strerror(int code);
+int avse_abi_version(void);
+
+/* ---------------------------------------------------------------- selective scan ------
+ * Replaces selective_scan_cuda.fwd / .bwd of mamba-ssm 1.1.3.post1 as called at
+ * Mamba-TasNet/modules/mamba/selective_scan_interface.py:42,67 (SelectiveScanFn) and
+ * :218,252 (MambaInnerFnNoOutProj).  Semantics: selective_scan_ref (:91-157), real A,
+ * B/C "variable" with n_groups == 1 (B, C: (b, 1, n, l)).  dstate n must be 16.
+ *
+ * x (scan intermediates) layout: (b, d, n_chunks, 2*n) fp32 with n_chunks =
+ * avse_scan_n_chunks(l); x[..., k, 2i+1] = state i after chunk k (so x[..., -1, 1::2] is
+ * the last state, as SelectiveScanFn reads at :45); x[..., k, 2i] = prod of exp(dt*A_i)
+ * up to that point.  The backward restarts each chunk from these checkpoints.
+ */
+typedef struct {
+    int64_t batch, dim, seqlen, dstate;
+    int32_t in_dtype;          /* AVSE_F32 or AVSE_BF16: dtype of u, delta, z, B, C, out, out_z */
+    int32_t delta_softplus;
+    const void* u;      int64_t u_bs, u_ds;          /* batch / dim strides */
+    const void* delta;  int64_t delta_bs, delta_ds;
+    const float* A;                                  /* (d, n) contiguous */
+    const void* B;      int64_t B_bs, B_ns;          /* (b, 1, n, l): batch / state strides */
+    const void* C;      int64_t C_bs, C_ns;
+    const float* D;                                  /* (d) or NULL */
+    const void* z;      int64_t z_bs, z_ds;          /* NULL = no gating */
+    const float* delta_bias;                         /* (d) or NULL */
+    void* out;          int64_t out_bs, out_ds;      /* y + D*u (before gating) */
+    float* x;                                        /* (b, d, n_chunks, 2n) contiguous */
+    void* out_z;        int64_t out_z_bs, out_z_ds;  /* out * silu(z); ignored when z == NULL */
+} avse_scan_fwd_args;
+
+typedef struct {
+    int64_t batch, dim, seqlen, dstate;
+    int32_t in_dtype, delta_softplus;
+    int32_t recompute_out_z;
+    const void* u;      int64_t u_bs, u_ds;
+    const void* delta;  int64_t delta_bs, delta_ds;
+    const float* A;
+    const void* B;      int64_t B_bs, B_ns;
+    const void* C;      int64_t C_bs, C_ns;
+    const float* D;
+    const void* z;      int64_t z_bs, z_ds;
+    const float* delta_bias;
+    const void* dout;   int64_t dout_bs, dout_ds;
+    const float* x;                                  /* forward checkpoints */
+    /* outputs */
+    void* du;           int64_t du_bs, du_ds;
+    void* ddelta;       int64_t ddelta_bs, ddelta_ds;
+    float* dA;                                       /* (d, n) */
+    float* dB;          int64_t dB_bs, dB_ns;        /* (b, 1, n, l) fp32 (as mamba-ssm) */
+    float* dC;          int64_t dC_bs, dC_ns;
+    float* dD;                                       /* (d) or NULL when D == NULL */
+    float* ddelta_bias;                              /* (d) or NULL when delta_bias == NULL */
+    void* dz;           int64_t dz_bs, dz_ds;        /* written when z != NULL */
+    void* out_z;        int64_t out_z_bs, out_z_ds;  /* written when recompute_out_z */
+    float* workspace;                                /* avse_scan_bwd_workspace_bytes() */
+} avse_scan_bwd_args;
+
+int64_t avse_scan_n_chunks(int64_t seqlen);
+int64_t avse_scan_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t seqlen, int64_t dstate);
+int avse_scan_fwd(const avse_scan_fwd_args* a, avse_stream_t stream);
+int avse_scan_bwd(const avse_scan_bwd_args* a, avse_stream_t stream);
+
+/* ---------------------------------------------------------------- causal conv1d -------
+ * Replaces causal_conv1d_cuda.causal_conv1d_fwd / causal_conv1d_bwd (causal-conv1d
+ * 1.1.3.post1) as called at selective_scan_interface.py:182,244 and :286.  Depthwise,
+ * width w <= 4, left zero-padding w-1, optional SiLU; x: (b, d, l) with l contiguous.
+ * Semantics pinned by bimamba.py:278-279 (act(conv1d(x)[..., :seqlen])).
+ */
+int64_t avse_cconv_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t width);
+int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
+                   const float* x, int64_t x_bs, int64_t x_ds,
+                   const float* weight /* (d, w) */, const float* bias /* (d) or NULL */,
+                   float* out, int64_t out_bs, int64_t out_ds, int32_t silu, avse_stream_t stream);
+int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
+                   const float* x, int64_t x_bs, int64_t x_ds,
+                   const float* weight, const float* bias,
+                   const float* dout, int64_t dout_bs, int64_t dout_ds,
+                   float* dx, int64_t dx_bs, int64_t dx_ds,
+                   float* dweight /* (d, w) */, float* dbias /* (d) or NULL */,
+                   int32_t silu, float* workspace, avse_stream_t stream);
+
+/* ---------------------------------------------------------------- add + RMSNorm -------
+ * Replaces the Block pre-norm of Mamba-TasNet/modules/mamba/bimamba.py:447-451
+ * (residual = h + residual; RMSNorm(residual), mamba-ssm Triton RMSNorm, eps 1e-5) and
+ * MambaBlocksSequential's final norm_f (mamba_blocks.py:195-197).  Rows of width n.
+ */
+int avse_add_rmsnorm_fwd(int64_t rows, int64_t n, const float* h, const float* res_in /* or NULL */,
+                         const float* weight, float eps, float* y, float* res_out, float* rstd,
+                         avse_stream_t stream);
+int64_t avse_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t n);
+int avse_rmsnorm_bwd(int64_t rows, int64_t n, const float* dy, const float* dres_out /* or NULL */,
+                     const float* res_out, const float* weight, const float* rstd,
+                     float* dx, float* dweight, float* workspace, avse_stream_t stream);
+
+/* ---------------------------------------------------------------- STFT / iSTFT --------
+ * Replaces the CPU librosa 0.8.1 calls of baseline/avse1/dataset.py:112-118 (stft, n_fft
+ * 512, hop 128, periodic Hann, center=True reflect padding, |.|, transposed to
+ * (frames, 257)) and baseline/avse1/test.py:85-88 (istft with the noisy phase, length).
+ * wave: (b, T) fp32 contiguous.  mag: (b, frames, 257).  spec (optional): interleaved
+ * complex (b, frames, 257, 2).  frames = 1 + T / 128 (T >= 257 for reflect padding).
+ */
+int64_t avse_stft_frames(int64_t T);
+int avse_stft_fwd(int64_t batch, int64_t T, const float* wave, float* mag, float* spec_or_null,
+                  avse_stream_t stream);
+/* iSTFT of mag * exp(i*angle(phase_spec)); frames_buf: workspace (b, frames, 512) fp32 */
+int avse_istft(int64_t batch, int64_t frames, int64_t length, const float* mag, const float* phase_spec,
+               float* frames_buf, float* wave_out, avse_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVSE_HIP_H */

@@ -1,0 +1,107 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads, exports every symbol the
+header declares, validates arguments on the host, and the product never routes through oracle/."""
+import ast
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "avse_hip.h")
+PKG = os.path.join(REPO, "avse_challenge_amd")
+LIB = os.path.join(PKG, "libavse_hip.so")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(avse_[a-z0-9_]+)\s*\(", src)))
+
+
+needs_lib = pytest.mark.skipif(not os.path.exists(LIB), reason="libavse_hip.so not built (run __graft_entry__.build)")
+
+
+@needs_lib
+def test_library_exports_every_declared_symbol():
+    from avse_challenge_amd import _lib
+    L = _lib.lib()
+    decl = declared_functions()
+    assert len(decl) >= 15
+    for name in decl:
+        assert hasattr(L, name), name
+        assert name in _lib.SIGNATURES, f"{name} not bound in _lib.SIGNATURES"
+
+
+@needs_lib
+def test_host_side_validation_without_gpu():
+    from avse_challenge_amd import _lib
+    L = _lib.lib()
+    assert L.avse_abi_version() == 1
+    assert L.avse_scan_n_chunks(3999) == 63 and L.avse_scan_n_chunks(64) == 1
+    assert L.avse_stft_frames(48000) == 376           # baseline/avse1/config.py:19
+    a = _lib.ScanFwdArgs()
+    assert L.avse_scan_fwd(a, None) == -1             # null pointers -> EINVAL before any launch
+    dummy = ctypes.c_void_p(16)
+    for f in ("u", "delta", "A", "B", "C", "out", "x"):
+        setattr(a, f, dummy)
+    a.batch, a.dim, a.seqlen, a.dstate = 1, 64, 10, 8
+    assert L.avse_scan_fwd(a, None) == -2             # dstate != 16 -> ESHAPE
+    a.dstate, a.in_dtype = 16, 7
+    assert L.avse_scan_fwd(a, None) == -3             # dtype -> EDTYPE
+    assert L.avse_cconv_fwd(1, 1, 10, 5, dummy, 10, 10, dummy, None, dummy, 10, 10, 0, None) == -2   # width > 4
+    assert L.avse_add_rmsnorm_fwd(4, 6, dummy, None, dummy, 1e-5, dummy, dummy, dummy, None) == -2   # n % 4
+    assert b"shape" in L.avse_strerror(-2)
+    ws = L.avse_scan_bwd_workspace_bytes(2, 128, 100, 16)
+    assert ws == 4 * (2 * 2 * 32 * 100 + 2 * 128 * 18)
+
+
+def test_product_never_imports_oracle():
+    for root, _, files in os.walk(PKG):
+        for f in files:
+            if f.endswith(".py"):
+                tree = ast.parse(open(os.path.join(root, f)).read())
+                for node in ast.walk(tree):
+                    if isinstance(node, ast.Import):
+                        names = [a.name for a in node.names]
+                    elif isinstance(node, ast.ImportFrom):
+                        names = [node.module or ""]
+                    else:
+                        continue
+                    assert not any(n == "oracle" or n.startswith("oracle.") for n in names), (f, names)
+
+
+def test_kernels_fail_loudly_without_gpu():
+    import torch
+    from avse_challenge_amd import kernels
+    with pytest.raises(RuntimeError):
+        kernels.selective_scan_fwd(*(torch.zeros(1, 64, 8),) * 2, torch.zeros(64, 16), torch.zeros(1, 16, 8),
+                                   torch.zeros(1, 16, 8))
+
+
+def test_missing_library_raises(monkeypatch, tmp_path):
+    from avse_challenge_amd import _lib
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.HipLibraryError):
+        _lib.lib()
+
+
+def test_dropin_modules_resolve_reference_import_names():
+    import importlib
+    import sys
+    from avse_challenge_amd import dropin
+    path = dropin.install()
+    try:
+        for name in ("selective_scan_cuda", "causal_conv1d_cuda", "causal_conv1d", "mamba_ssm",
+                     "mamba_ssm.ops.triton.layernorm", "mamba_ssm.ops.triton.selective_state_update"):
+            m = importlib.import_module(name)
+            assert m.__file__.startswith(path), (name, m.__file__)
+        ssc = importlib.import_module("selective_scan_cuda")
+        assert callable(ssc.fwd) and callable(ssc.bwd)
+        cc = importlib.import_module("causal_conv1d")
+        assert callable(cc.causal_conv1d_fn)
+        ln = importlib.import_module("mamba_ssm.ops.triton.layernorm")
+        assert ln.RMSNorm(8, eps=1e-5).weight.shape == (8,)
+    finally:
+        sys.path.remove(path)

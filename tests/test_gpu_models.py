@@ -1,0 +1,120 @@
+"""GPU parity of the model-level drop-ins (same state_dict keys, det_init weights) vs the goldens."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import avse1_ref, mamba_ref
+from oracle.det_init import det_init_, det_input
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+T = lambda a: torch.from_numpy(np.asarray(a)).to(DEV)
+
+
+def close(a, b, atol, rtol=0.0, what=""):
+    a = a.detach().double().cpu().numpy()
+    np.testing.assert_allclose(a, np.asarray(b, np.float64), atol=atol, rtol=rtol, err_msg=what)
+
+
+@pytest.fixture(autouse=True)
+def _fp32_exact():
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    yield
+
+
+def test_bimamba_block_fwd_bwd_golden():
+    from avse_challenge_amd import mamba_tasnet as M
+    g = load_golden("bimamba_block")
+    blk = det_init_(M.Block(32, M.BiMambaV2(32)), 12).to(DEV)
+    hs = T(g["hidden"]).requires_grad_(True)
+    res = T(g["residual"]).requires_grad_(True)
+    oh, orr = blk(hs, res)
+    close(oh, g["out_hidden"], 2e-5, 1e-5, "hidden")
+    close(orr, g["out_residual"], 1e-6, 0, "residual")
+    (oh * T(g["gout"])).sum().backward()
+    close(hs.grad, g["g_hidden"], 5e-5, 1e-4, "g_hidden")
+    close(res.grad, g["g_residual"], 5e-5, 1e-4, "g_residual")
+    for k, p in blk.named_parameters():
+        ref = g["g_" + k.replace(".", "__")]
+        scale = max(1.0, float(np.abs(ref).max()))
+        close(p.grad, ref, 1e-4 * scale, 1e-4, k)
+
+
+def test_masknet_golden():
+    from avse_challenge_amd import mamba_tasnet as M
+    g = load_golden("masknet_small")
+    mn = det_init_(M.MaskNet(64, 64, 2, 2, 64), 13).to(DEV)
+    with torch.no_grad():
+        close(mn(T(g["mixture_w"])), g["est_mask"], 2e-5, 1e-5)
+
+
+def test_mamba_tasnet_xs_train_step_vs_oracle():
+    """Whole separator (XS widths, 2 layers) fwd + grads vs the CPU oracle on identical weights."""
+    from avse_challenge_amd import losses as PL
+    from avse_challenge_amd import mamba_tasnet as M
+    from oracle import losses_ref
+    ours = det_init_(M.MambaTasNet(N=128, n_mamba=2), 21).to(DEV)
+    ref = det_init_(mamba_ref.MambaTasNet(N=128, n_mamba=2), 21).double()
+    mix = 0.1 * det_input((2, 1600), 601)
+    tgt = 0.1 * det_input((2, 1600, 2), 602)
+    est = ours(mix.to(DEV))
+    est_r = ref(mix.double())
+    close(est, est_r, 5e-5, 1e-4, "separated")
+    loss = PL.si_snr_pit(tgt.to(DEV), est).mean()
+    loss_r = losses_ref.si_snr_pit(tgt.double(), est_r).mean()
+    loss.backward()
+    loss_r.backward()
+    assert abs(float(loss) - float(loss_r)) < 1e-3
+    rp = dict(ref.named_parameters())
+    for k, p in ours.named_parameters():
+        r = rp[k].grad
+        scale = max(1e-3, float(r.abs().max()))
+        close(p.grad, r, 2e-3 * scale, 2e-3, k)
+
+
+def test_avse1_full_golden_eval():
+    from avse_challenge_amd import avse1
+    g = load_golden("avse1_full")
+    net = det_init_(avse1.AVNet(), 54).to(DEV).eval()
+    batch = {"noisy_audio_spec": det_input((1, 1, 376, 257), 505).abs().to(DEV),
+             "lip_images": det_input((1, 3, 75, 96, 96), 506, "uint8").to(DEV),
+             "mask": det_input((1, 1, 376, 257), 507).abs().to(DEV)}
+    with torch.no_grad():
+        pred = net(batch)
+        close(pred, g["pred"], 1e-4, 1e-4, "pred")
+        close(net.cal_loss(batch), g["loss"], 1e-5, 1e-5, "loss")
+
+
+def test_avse1_wave_frontend_and_train_step_vs_oracle():
+    """HIP STFT front-end + train step (train-mode BN, dropout off) vs the oracle on CPU."""
+    from avse_challenge_amd import avse1
+    from oracle import stft_ref
+    ours = det_init_(avse1.AVNet(), 55).to(DEV).train()
+    ref = det_init_(avse1_ref.AVNet(), 55).train()
+    for m in list(ours.modules()) + list(ref.modules()):
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    noisy = 0.1 * det_input((2, 48000), 603)
+    clean = 0.1 * det_input((2, 48000), 604)
+    lips = det_input((2, 3, 75, 64, 64), 605, "uint8")
+    batch = avse1.AVNet.features_from_waves(noisy.to(DEV), clean.to(DEV))
+    batch["lip_images"] = lips.to(DEV)
+    rb = {"noisy_audio_spec": torch.from_numpy(stft_ref.stft_mag_T(noisy.numpy()))[:, None],
+          "mask": torch.from_numpy(stft_ref.stft_mag_T(clean.numpy()))[:, None], "lip_images": lips}
+    close(batch["noisy_audio_spec"], rb["noisy_audio_spec"], 2e-5, 1e-5, "stft features")
+    loss = ours.training_step(batch)
+    loss_r = ref.cal_loss(rb)
+    assert abs(float(loss) - float(loss_r)) < 1e-5 * max(1.0, abs(float(loss_r)))
+    loss.backward()
+    loss_r.backward()
+    rp = dict(ref.named_parameters())
+    worst = 0.0
+    for k, p in ours.named_parameters():
+        if p.grad is None:
+            continue
+        r = rp[k].grad
+        err = float((p.grad.cpu() - r).abs().max()) / max(1e-6, float(r.abs().max()))
+        worst = max(worst, err)
+    assert worst < 1e-3, worst
