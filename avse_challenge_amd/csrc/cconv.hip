@@ -139,7 +139,7 @@ __global__ void reduce_kernel(const float* ws, int batch, int D, int W, float* d
     if (i >= D * (W + 1)) return;
     const int d = i / (W + 1), k = i % (W + 1);
     float v = 0.f;
-    for (int b = 0; b < batch; ++b) v += ws[((int64_t)b * D + d) * (MAXW + 1) + (k < W ? k : MAXW)];
+    for (int b = 0; b < batch; ++b) v += ws[((int64_t)b * D + d) * (MAXW + 1) + k];
     if (k < W) dw[d * W + k] = v;
     else if (db) db[d] = v;
 }

@@ -14,7 +14,8 @@ T = lambda a: torch.from_numpy(np.asarray(a)).to(DEV)
 
 def close(a, b, atol, rtol=0.0, what=""):
     a = a.detach().double().cpu().numpy()
-    np.testing.assert_allclose(a, np.asarray(b, np.float64), atol=atol, rtol=rtol, err_msg=what)
+    b = b.detach().double().cpu().numpy() if torch.is_tensor(b) else np.asarray(b, np.float64)
+    np.testing.assert_allclose(a, b, atol=atol, rtol=rtol, err_msg=what)
 
 
 @pytest.fixture(autouse=True)
@@ -88,12 +89,17 @@ def test_avse1_full_golden_eval():
 
 
 def test_avse1_wave_frontend_and_train_step_vs_oracle():
-    """HIP STFT front-end + train step (train-mode BN, dropout off) vs the oracle on CPU."""
+    """HIP STFT front-end + train step (train-mode BN, dropout off) vs the oracle.
+
+    Gradient tolerance is calibrated, not guessed: the fp64 oracle is the truth, and the GPU fp32
+    gradients must be within 4x (+1e-5) of the error the fp32 CPU oracle itself makes against it
+    (five stacked train-mode BatchNorms amplify summation-order differences)."""
     from avse_challenge_amd import avse1
     from oracle import stft_ref
     ours = det_init_(avse1.AVNet(), 55).to(DEV).train()
-    ref = det_init_(avse1_ref.AVNet(), 55).train()
-    for m in list(ours.modules()) + list(ref.modules()):
+    ref32 = det_init_(avse1_ref.AVNet(), 55).train()
+    ref64 = det_init_(avse1_ref.AVNet(), 55).double().train()
+    for m in list(ours.modules()) + list(ref32.modules()) + list(ref64.modules()):
         if isinstance(m, torch.nn.Dropout):
             m.p = 0.0
     noisy = 0.1 * det_input((2, 48000), 603)
@@ -104,17 +110,19 @@ def test_avse1_wave_frontend_and_train_step_vs_oracle():
     rb = {"noisy_audio_spec": torch.from_numpy(stft_ref.stft_mag_T(noisy.numpy()))[:, None],
           "mask": torch.from_numpy(stft_ref.stft_mag_T(clean.numpy()))[:, None], "lip_images": lips}
     close(batch["noisy_audio_spec"], rb["noisy_audio_spec"], 2e-5, 1e-5, "stft features")
+    rb64 = {k: (v.double() if v.dtype == torch.float32 else v) for k, v in rb.items()}
     loss = ours.training_step(batch)
-    loss_r = ref.cal_loss(rb)
-    assert abs(float(loss) - float(loss_r)) < 1e-5 * max(1.0, abs(float(loss_r)))
-    loss.backward()
-    loss_r.backward()
-    rp = dict(ref.named_parameters())
-    worst = 0.0
+    loss32 = ref32.cal_loss(rb)
+    loss64 = ref64.cal_loss(rb64)
+    assert abs(float(loss) - float(loss64)) < 1e-5 * max(1.0, abs(float(loss64)))
+    for l_ in (loss, loss32, loss64):
+        l_.backward()
+    p32, p64 = dict(ref32.named_parameters()), dict(ref64.named_parameters())
     for k, p in ours.named_parameters():
         if p.grad is None:
             continue
-        r = rp[k].grad
-        err = float((p.grad.cpu() - r).abs().max()) / max(1e-6, float(r.abs().max()))
-        worst = max(worst, err)
-    assert worst < 1e-3, worst
+        truth = p64[k].grad
+        scale = max(1e-12, float(truth.abs().max()))
+        e_gpu = float((p.grad.cpu().double() - truth).abs().max()) / scale
+        e_cpu = float((p32[k].grad.double() - truth).abs().max()) / scale
+        assert e_gpu <= 4 * e_cpu + 1e-5, (k, e_gpu, e_cpu)
