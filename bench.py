@@ -222,7 +222,9 @@ def main():
     world, rank, dev = setup_dist()
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
-    torch.backends.cudnn.benchmark = True            # as the reference trainers (avse1 train.py:11)
+    # MIOpen immediate mode: find mode (benchmark=True, as avse1 train.py:11 sets for cuDNN) JIT-compiles
+    # every candidate solver on a fresh box (minutes); immediate mode compiles only the chosen one.
+    torch.backends.cudnn.benchmark = bool(int(os.environ.get("AVSE_MIOPEN_FIND", "0")))
     if args.workload == "avse1":
         B = args.batch or 32
         step = Avse1Step(B, dev, rank, world, args.lip_hw)
@@ -230,8 +232,12 @@ def main():
         B = args.batch or 64
         step = MambaStep(B, dev, rank, world, args.size)
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        t = time.perf_counter()
         step()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup {i + 1}/{args.warmup}: {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()

@@ -179,7 +179,9 @@ class AVNet(nn.Module):
         if self.a_only:
             comb = self.net_audiofeat(spec)
         else:
-            vis = self.net_visualfeat(inp["lip_images"].float()).unsqueeze(1)
+            # model.py:122 casts the uint8 lips with .float(); the fp64 oracle run casts to its own dtype
+            lips = inp["lip_images"].to(self.net_audiofeat.conv1.weight.dtype)
+            vis = self.net_visualfeat(lips).unsqueeze(1)
             vis = F.interpolate(vis, size=(T, 512)).reshape(-1, T, 512)
             comb = torch.cat((vis, self.net_audiofeat(spec)), dim=-1)
         mask = self.net_fusion(comb)
