@@ -217,9 +217,22 @@ class MambaStep:
                           f"scaled x{n_layers} (forward only; the training step is >=3x slower)"}
 
 
+def heartbeat(rank, period=60.0):
+    """Progress line every minute: the first step JIT-compiles MIOpen kernels on a fresh box (minutes)."""
+    import threading
+
+    def run():
+        t0 = time.time()
+        while True:
+            time.sleep(period)
+            print(f"[bench] rank {rank} alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist()
+    heartbeat(rank)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
     # MIOpen immediate mode: find mode (benchmark=True, as avse1 train.py:11 sets for cuDNN) JIT-compiles
