@@ -81,6 +81,11 @@ SIGNATURES = {
     "avse_stft_frames": (c_i64, [c_i64]),
     "avse_stft_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_istft": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_conv3d_wgrad_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
+    "avse_conv3d_wgrad": (c_i32, [c_i64] * 11 + [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
+    "avse_prelu_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "avse_prelu_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "avse_prelu_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

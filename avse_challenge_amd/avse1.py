@@ -8,20 +8,23 @@ MI355X specifics:
   * the STFT front-end that the reference runs on CPU in its DataLoader
     (dataset.py:112-118, librosa) and the iSTFT of test.py:85-88 run as HIP kernels
     (libavse_hip.so: framing + radix-4 FFT-512 per wave) — ``features_from_waves`` / ``enhance``;
-  * convolutions / BatchNorm / LSTM / GEMMs are MIOpen / hipBLASLt MFMA kernels (fp32, exact
-    f32 MFMA on gfx950 — no TF32 shortcut exists), channels-first like the reference.
+  * the lip front-end Conv3d weight gradient runs on the HIP MFMA implicit-GEMM kernel and every
+    PReLU on the HIP fwd / fused-bwd kernels (layers.py);
+  * the remaining convolutions / BatchNorm / LSTM / GEMMs are MIOpen / hipBLASLt MFMA kernels (fp32,
+    exact f32 MFMA on gfx950 — no TF32 shortcut exists), channels-first like the reference.
 """
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
+from .layers import LipConv3d, PReLU
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
 
 def _prelu(c):
-    return nn.PReLU(c)
+    return PReLU(c)          # HIP fwd + fused dx / slope-gradient bwd (layers.py)
 
 
 class _BasicBlock(nn.Module):            # utils/resnet.py:26-67 (relu_type='prelu')
@@ -112,7 +115,7 @@ class VisualFeatNet(nn.Module):           # model.py:17-58
         super().__init__()
         self.trunk = _ResNet18()
         self.frontend3D = nn.Sequential(
-            nn.Conv3d(3, 64, (5, 7, 7), (1, 2, 2), (2, 3, 3), bias=False), nn.BatchNorm3d(64), _prelu(64),
+            LipConv3d(3, 64, (5, 7, 7), (1, 2, 2), (2, 3, 3)), nn.BatchNorm3d(64), _prelu(64),
             nn.MaxPool3d((1, 3, 3), (1, 2, 2), (0, 1, 1)))
         self.tcn = _TCN()
 

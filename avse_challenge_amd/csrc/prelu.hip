@@ -1,0 +1,131 @@
+// PReLU forward / backward (per-channel or single slope) for gfx950.
+//
+// Replaces nn.PReLU in the avse1 lip stream (frontend3D / ResNet BasicBlock / TCN:
+// /root/reference/baseline/avse1/model.py:29-34, utils/resnet.py:45-46, utils/tcn.py:170-196)
+// and the avse4 TCN (baseline/avse4/model.py:260,282).  torch's prelu_backward is a
+// TensorIterator two-output reduction that took 2 ms on average and 20.9 ms on the
+// (32,64,75,48,48) front-end activation (rocprofv3, profiles/).  Here: one workgroup per
+// (n, c) row of the (N, C, S) view, float4 streaming, the slope gradient reduced in registers /
+// LDS per row and summed over n by a second tiny kernel (deterministic).  HBM-bound:
+// fwd 8 B/elem, bwd 12 B/elem.
+#include "common.h"
+
+namespace avse {
+namespace prelu {
+
+constexpr int THREADS = 256;
+
+__global__ __launch_bounds__(THREADS) void fwd_kernel(int C, int64_t S, int per_channel, const float* __restrict__ x,
+                                                      const float* __restrict__ a, float* __restrict__ y) {
+    const int64_t row = blockIdx.x;
+    const float av = a[per_channel ? (int)(row % C) : 0];
+    const float* xr = x + row * S;
+    float* yr = y + row * S;
+    if ((S & 3) == 0) {
+        const float4* x4 = reinterpret_cast<const float4*>(xr);
+        float4* y4 = reinterpret_cast<float4*>(yr);
+        for (int64_t i = threadIdx.x; i < S / 4; i += THREADS) {
+            float4 v = x4[i];
+            v.x = v.x > 0.f ? v.x : av * v.x;
+            v.y = v.y > 0.f ? v.y : av * v.y;
+            v.z = v.z > 0.f ? v.z : av * v.z;
+            v.w = v.w > 0.f ? v.w : av * v.w;
+            y4[i] = v;
+        }
+    } else {
+        for (int64_t i = threadIdx.x; i < S; i += THREADS) {
+            const float v = xr[i];
+            yr[i] = v > 0.f ? v : av * v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(THREADS) void bwd_kernel(int C, int64_t S, int per_channel, const float* __restrict__ x,
+                                                      const float* __restrict__ a, const float* __restrict__ dy,
+                                                      float* __restrict__ dx, float* __restrict__ ws) {
+    __shared__ float red[THREADS / 64];
+    const int64_t row = blockIdx.x;
+    const float av = a[per_channel ? (int)(row % C) : 0];
+    const float* xr = x + row * S;
+    const float* gr = dy + row * S;
+    float* dr = dx + row * S;
+    float da = 0.f;
+    if ((S & 3) == 0) {
+        const float4* x4 = reinterpret_cast<const float4*>(xr);
+        const float4* g4 = reinterpret_cast<const float4*>(gr);
+        float4* d4 = reinterpret_cast<float4*>(dr);
+        for (int64_t i = threadIdx.x; i < S / 4; i += THREADS) {
+            const float4 v = x4[i], g = g4[i];
+            float4 o;
+            o.x = v.x > 0.f ? g.x : av * g.x; da += v.x > 0.f ? 0.f : g.x * v.x;
+            o.y = v.y > 0.f ? g.y : av * g.y; da += v.y > 0.f ? 0.f : g.y * v.y;
+            o.z = v.z > 0.f ? g.z : av * g.z; da += v.z > 0.f ? 0.f : g.z * v.z;
+            o.w = v.w > 0.f ? g.w : av * g.w; da += v.w > 0.f ? 0.f : g.w * v.w;
+            d4[i] = o;
+        }
+    } else {
+        for (int64_t i = threadIdx.x; i < S; i += THREADS) {
+            const float v = xr[i], g = gr[i];
+            dr[i] = v > 0.f ? g : av * g;
+            da += v > 0.f ? 0.f : g * v;
+        }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) da += __shfl_xor(da, m, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = da;
+    __syncthreads();
+    if (threadIdx.x == 0) ws[row] = red[0] + red[1] + red[2] + red[3];
+}
+
+// da[c] = sum_n ws[n*C + c]  (per_channel) or sum over all rows (single slope)
+__global__ void reduce_kernel(const float* __restrict__ ws, int64_t N, int C, int per_channel, float* __restrict__ da) {
+    __shared__ float red[256 / 64];
+    const int c = blockIdx.x;
+    float v = 0.f;
+    if (per_channel) {
+        for (int64_t n = threadIdx.x; n < N; n += blockDim.x) v += ws[n * C + c];
+    } else {
+        for (int64_t i = threadIdx.x; i < N * C; i += blockDim.x) v += ws[i];
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) da[c] = red[0] + red[1] + red[2] + red[3];
+}
+
+}  // namespace prelu
+}  // namespace avse
+
+using namespace avse::prelu;
+
+extern "C" {
+
+int avse_prelu_fwd(int64_t N, int64_t C, int64_t S, int32_t num_params, const float* x, const float* a, float* y,
+                   avse_stream_t stream) {
+    if (!x || !a || !y) return AVSE_EINVAL;
+    if (N <= 0 || C <= 0 || S <= 0 || (num_params != 1 && num_params != C) || N * C > (1LL << 31) - 1) return AVSE_ESHAPE;
+    if (((uintptr_t)x | (uintptr_t)y) & 15) return AVSE_EALIGN;
+    hipLaunchKernelGGL(fwd_kernel, dim3((unsigned)(N * C)), dim3(THREADS), 0, (hipStream_t)stream, (int)C, S,
+                       (int)(num_params > 1), x, a, y);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int64_t avse_prelu_bwd_workspace_bytes(int64_t N, int64_t C) { return 4 * N * C; }
+
+int avse_prelu_bwd(int64_t N, int64_t C, int64_t S, int32_t num_params, const float* x, const float* a, const float* dy,
+                   float* dx, float* da, float* workspace, avse_stream_t stream) {
+    if (!x || !a || !dy || !dx || !da || !workspace) return AVSE_EINVAL;
+    if (N <= 0 || C <= 0 || S <= 0 || (num_params != 1 && num_params != C) || N * C > (1LL << 31) - 1) return AVSE_ESHAPE;
+    if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) return AVSE_EALIGN;
+    hipStream_t st = (hipStream_t)stream;
+    const int pc = num_params > 1;
+    hipLaunchKernelGGL(bwd_kernel, dim3((unsigned)(N * C)), dim3(THREADS), 0, st, (int)C, S, pc, x, a, dy, dx, workspace);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(reduce_kernel, dim3(pc ? (unsigned)C : 1u), dim3(256), 0, st, workspace, N, (int)C, pc, da);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+}  // extern "C"

@@ -256,3 +256,59 @@ def istft(mag, phase_spec, length):
     check(_lib.lib().avse_istft(Bn, F, length, ptr(mag), ptr(ps), ptr(fbuf), ptr(out), stream_ptr(mag.device)),
           "avse_istft")
     return out
+
+
+# ------------------------------------------------------------------------ lip front-end Conv3d dW
+
+def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
+    """dW of Conv3d(Cin, 64, kernel_size, stride (1,2,2), padding, bias=False) -> (64, Cin, KT, KH, KW)."""
+    _need_gpu(x, dy)
+    x = x.float().contiguous()
+    dy = dy.float().contiguous()
+    Bn, Cin, Tn, H, W = x.shape
+    KT, KH, KW = kernel_size
+    PT, PH, PW = padding
+    if dy.shape[1] != 64:
+        raise RuntimeError("conv3d_wgrad is built for 64 output channels (the lip front-ends)")
+    N = Cin * KT * KH * KW
+    if out is None:
+        out = torch.empty((64, Cin, KT, KH, KW), device=x.device, dtype=torch.float32)
+        accumulate = False
+    L = _lib.lib()
+    ws = torch.empty((L.avse_conv3d_wgrad_workspace_bytes(Bn, dy.shape[2], dy.shape[3], N) + 3) // 4,
+                     device=x.device, dtype=torch.float32)
+    check(L.avse_conv3d_wgrad(Bn, Cin, Tn, H, W, KT, KH, KW, PT, PH, PW, ptr(x), ptr(dy), ptr(out),
+                              int(bool(accumulate)), ptr(ws), stream_ptr(x.device)), "avse_conv3d_wgrad")
+    return out
+
+
+# ------------------------------------------------------------------------ PReLU
+
+def _ncs(x):
+    N, C = x.shape[0], x.shape[1]
+    S = x.numel() // max(1, N * C)
+    return N, C, S
+
+
+def prelu_fwd(x, a):
+    _need_gpu(x, a)
+    x = x.contiguous()
+    if x.dtype != torch.float32:
+        raise RuntimeError("prelu kernels are fp32")
+    N, C, S = _ncs(x)
+    y = torch.empty_like(x)
+    check(_lib.lib().avse_prelu_fwd(N, C, S, a.numel(), ptr(x), ptr(a.contiguous()), ptr(y), stream_ptr(x.device)),
+          "avse_prelu_fwd")
+    return y
+
+
+def prelu_bwd(x, a, dy):
+    _need_gpu(x, a, dy)
+    x, dy = x.contiguous(), dy.contiguous().float()
+    N, C, S = _ncs(x)
+    dx = torch.empty_like(x)
+    da = torch.empty((a.numel(),), device=x.device, dtype=torch.float32)
+    ws = torch.empty((N * C,), device=x.device, dtype=torch.float32)
+    check(_lib.lib().avse_prelu_bwd(N, C, S, a.numel(), ptr(x), ptr(a.contiguous()), ptr(dy), ptr(dx), ptr(da), ptr(ws),
+                                    stream_ptr(x.device)), "avse_prelu_bwd")
+    return dx, da.view_as(a)

@@ -1,0 +1,64 @@
+"""nn.Module drop-ins whose hot halves run in libavse_hip.so (same parameter names as torch's).
+
+PReLU        nn.PReLU(num_parameters): fwd + fused dx / slope-gradient bwd kernels
+LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip front-ends:
+             forward on MIOpen, weight gradient on the MFMA implicit-GEMM kernel (the lips are
+             data: no input gradient is needed on the reference path; if one is requested it is
+             computed with the library transposed conv).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import kernels as K
+
+
+class _PReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, a):
+        ctx.save_for_backward(x, a)
+        return K.prelu_fwd(x, a)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, a = ctx.saved_tensors
+        dx, da = K.prelu_bwd(x, a, dy)
+        return dx, da
+
+
+class PReLU(nn.Module):
+    def __init__(self, num_parameters=1, init=0.25):
+        super().__init__()
+        self.num_parameters = num_parameters
+        self.weight = nn.Parameter(torch.full((num_parameters,), init))
+
+    def forward(self, x):
+        if not x.is_cuda:
+            raise RuntimeError("PReLU runs on the GPU kernels only")
+        return _PReLUFn.apply(x, self.weight)
+
+
+class _LipConv3dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, padding):
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.padding = stride, padding
+        return F.conv3d(x, w, None, stride, padding)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.nn.grad.conv3d_input(x.shape, w, dy, ctx.stride, ctx.padding)
+        dw = K.conv3d_wgrad(x, dy, tuple(w.shape[2:]), ctx.padding) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None
+
+
+class LipConv3d(nn.Conv3d):
+    def __init__(self, cin, cout, kernel_size, stride=(1, 2, 2), padding=(2, 3, 3), bias=False):
+        super().__init__(cin, cout, kernel_size, stride=stride, padding=padding, bias=bias)
+        assert tuple(self.stride) == (1, 2, 2) and cout == 64 and not bias
+
+    def forward(self, x):
+        return _LipConv3dFn.apply(x, self.weight, tuple(self.stride), tuple(self.padding))

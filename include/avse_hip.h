@@ -137,6 +137,28 @@ int avse_stft_fwd(int64_t batch, int64_t T, const float* wave, float* mag, float
 int avse_istft(int64_t batch, int64_t frames, int64_t length, const float* mag, const float* phase_spec,
                float* frames_buf, float* wave_out, avse_stream_t stream);
 
+/* ---------------------------------------------------------------- lip front-end Conv3d dW
+ * Weight gradient of nn.Conv3d(CIN, 64, (KT,KH,KW), stride (1,2,2), pad (PT,PH,PW), bias=False)
+ * — baseline/avse1/model.py:29-34 (CIN 3, (5,7,7), pad (2,3,3)); baseline/avse4/utils.py:100-106
+ * (CIN 1).  x: (B, CIN, T, H, W), dy: (B, 64, TO, HO, WO) contiguous fp32; dw: (64, CIN, KT, KH, KW).
+ * accumulate != 0 adds into dw.  Exact-fp32 MFMA implicit GEMM; WO <= 64.
+ */
+int64_t avse_conv3d_wgrad_workspace_bytes(int64_t B, int64_t TO, int64_t HO, int64_t N);
+int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,
+                      int64_t PT, int64_t PH, int64_t PW, const float* x, const float* dy, float* dw,
+                      int32_t accumulate, float* workspace, avse_stream_t stream);
+
+/* ---------------------------------------------------------------- PReLU -----------------
+ * nn.PReLU(num_parameters in {1, C}) on an (N, C, S) contiguous view — avse1 lip stream
+ * (model.py:32, utils/resnet.py:45-46, utils/tcn.py) and avse4 TCN (model.py:260,282).
+ * Pointers 16-byte aligned.  bwd writes dx and the slope gradient da (num_params).
+ */
+int avse_prelu_fwd(int64_t N, int64_t C, int64_t S, int32_t num_params, const float* x, const float* a, float* y,
+                   avse_stream_t stream);
+int64_t avse_prelu_bwd_workspace_bytes(int64_t N, int64_t C);
+int avse_prelu_bwd(int64_t N, int64_t C, int64_t S, int32_t num_params, const float* x, const float* a,
+                   const float* dy, float* dx, float* da, float* workspace, avse_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

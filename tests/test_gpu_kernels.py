@@ -233,3 +233,51 @@ def test_istft_vs_oracle_and_roundtrip():
 def test_kernels_reject_cpu_tensors():
     with pytest.raises(RuntimeError):
         K().stft(torch.zeros(1, 1000))
+
+
+# ------------------------------------------------------------------ lip front-end Conv3d weight gradient
+
+@pytest.mark.parametrize("cin,T,H,W", [(3, 6, 20, 18), (1, 5, 16, 16), (3, 3, 96, 96)])
+def test_conv3d_wgrad_vs_fp64(cin, T, H, W):
+    x = det_input((2, cin, T, H, W), 700 + cin, "uniform", 255.0)
+    w = det_input((64, cin, 5, 7, 7), 701) / 50
+    y = torch.nn.functional.conv3d(x.double(), w.double(), None, (1, 2, 2), (2, 3, 3))
+    dy = det_input(tuple(y.shape), 702)
+    ref = torch.nn.grad.conv3d_weight(x.double(), w.shape, dy.double(), (1, 2, 2), (2, 3, 3))
+    got = K().conv3d_wgrad(x.to(DEV), dy.to(DEV), (5, 7, 7), (2, 3, 3))
+    scale = float(ref.abs().max())
+    close(got, ref, 2e-6 * scale * (1 + x.numel() / 1e5) ** 0.5, 0, "dW")
+    got2 = K().conv3d_wgrad(x.to(DEV), dy.to(DEV), (5, 7, 7), (2, 3, 3), out=got.clone(), accumulate=True)
+    close(got2, 2 * ref, 4e-6 * scale * (1 + x.numel() / 1e5) ** 0.5, 0, "dW accumulate")
+
+
+def test_lip_conv3d_module_grad():
+    from avse_challenge_amd.layers import LipConv3d
+    m = LipConv3d(3, 64, (5, 7, 7)).to(DEV)
+    x = det_input((2, 3, 4, 24, 24), 710, "uniform", 255.0).to(DEV)
+    y = m(x)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    ref = torch.nn.grad.conv3d_weight(x.double().cpu(), m.weight.shape, gy.double().cpu(), (1, 2, 2), (2, 3, 3))
+    close(m.weight.grad, ref, 1e-5 * float(ref.abs().max()), 0)
+
+
+# ------------------------------------------------------------------ PReLU
+
+@pytest.mark.parametrize("shape,npar", [((4, 64, 10, 12), 64), ((3, 512, 75), 512), ((2, 8, 7), 1), ((5, 16, 33), 16)])
+def test_prelu_vs_torch(shape, npar):
+    from avse_challenge_amd.layers import PReLU
+    x = det_input(shape, 720).double().requires_grad_(True)
+    a = (0.1 + torch.rand(npar, generator=torch.Generator().manual_seed(1))).double().requires_grad_(True)
+    y = torch.nn.functional.prelu(x, a)
+    gy = det_input(shape, 721).double()
+    y.backward(gy)
+    m = PReLU(npar).to(DEV)
+    with torch.no_grad():
+        m.weight.copy_(a.detach().float())
+    xg = x.detach().float().to(DEV).requires_grad_(True)
+    yg = m(xg)
+    close(yg, y, 1e-6, 1e-6, "y")
+    yg.backward(gy.float().to(DEV))
+    close(xg.grad, x.grad, 1e-6, 1e-6, "dx")
+    close(m.weight.grad, a.grad, 1e-4, 1e-5, "da")
