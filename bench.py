@@ -280,7 +280,8 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (speech-like noise with 4 Hz envelope at SNR {0,3,6,9} dB, uint8 lips; "
                        "random-init weights)",
-               "config": step.config(world), "roofline": roof, "cpu_baseline": cpu}
+               "config": {**step.config(world), "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)},
+               "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
