@@ -20,7 +20,7 @@ AVSE_F32, AVSE_BF16 = 0, 1
 class ScanFwdArgs(ctypes.Structure):
     _fields_ = [
         ("batch", c_i64), ("dim", c_i64), ("seqlen", c_i64), ("dstate", c_i64),
-        ("in_dtype", c_i32), ("delta_softplus", c_i32),
+        ("in_dtype", c_i32), ("delta_softplus", c_i32), ("reverse", c_i32),
         ("u", c_vp), ("u_bs", c_i64), ("u_ds", c_i64),
         ("delta", c_vp), ("delta_bs", c_i64), ("delta_ds", c_i64),
         ("A", c_vp),
@@ -38,7 +38,7 @@ class ScanFwdArgs(ctypes.Structure):
 class ScanBwdArgs(ctypes.Structure):
     _fields_ = [
         ("batch", c_i64), ("dim", c_i64), ("seqlen", c_i64), ("dstate", c_i64),
-        ("in_dtype", c_i32), ("delta_softplus", c_i32), ("recompute_out_z", c_i32),
+        ("in_dtype", c_i32), ("delta_softplus", c_i32), ("recompute_out_z", c_i32), ("reverse", c_i32),
         ("u", c_vp), ("u_bs", c_i64), ("u_ds", c_i64),
         ("delta", c_vp), ("delta_bs", c_i64), ("delta_ds", c_i64),
         ("A", c_vp),
@@ -72,9 +72,9 @@ SIGNATURES = {
     "avse_scan_bwd": (c_i32, [ctypes.POINTER(ScanBwdArgs), c_vp]),
     "avse_cconv_bwd_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "avse_cconv_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
-                               c_i32, c_vp]),
+                               c_i32, c_i32, c_vp]),
     "avse_cconv_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
-                               c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp]),
+                               c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "avse_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
     "avse_rmsnorm_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

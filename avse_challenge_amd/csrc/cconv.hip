@@ -25,7 +25,7 @@ template <int W, bool SILU, bool HAS_BIAS>
 __global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const float* __restrict__ x, int64_t x_bs,
                                                       int64_t x_ds, const float* __restrict__ w,
                                                       const float* __restrict__ bias, float* __restrict__ out,
-                                                      int64_t o_bs, int64_t o_ds) {
+                                                      int64_t o_bs, int64_t o_ds, int rev) {
     __shared__ float s[TILE + MAXW];
     const int row = blockIdx.x;
     const int b = row / D, d = row % D;
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const float*
         // s[i] holds x[t0 - (W-1) + i]
         for (int i = threadIdx.x; i < TILE + W - 1; i += THREADS) {
             const int t = t0 - (W - 1) + i;
-            s[i] = (t >= 0 && t < L) ? xr[t] : 0.f;
+            s[i] = (t >= 0 && t < L) ? xr[rev ? L - 1 - t : t] : 0.f;
         }
         __syncthreads();
 #pragma unroll
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const float*
                 float acc = bv;
 #pragma unroll
                 for (int k = 0; k < W; ++k) acc += wk[k] * s[i + k];
-                orow[t] = SILU ? siluf_(acc) : acc;
+                orow[rev ? L - 1 - t : t] = SILU ? siluf_(acc) : acc;
             }
         }
     }
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const float*
                                                       int64_t x_ds, const float* __restrict__ w,
                                                       const float* __restrict__ bias, const float* __restrict__ dout,
                                                       int64_t g_bs, int64_t g_ds, float* __restrict__ dx,
-                                                      int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws) {
+                                                      int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws, int rev) {
     __shared__ float sx[TILE + 2 * MAXW];
     __shared__ float sg[TILE + MAXW];
     __shared__ float sred[THREADS / 64][MAXW + 1];
@@ -83,14 +83,14 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const float*
         // sx[i] = x[t0 - (W-1) + i], i in [0, TILE + 2(W-1)) ; sg[i] = dpre[t0 + i], i in [0, TILE + W - 1)
         for (int i = threadIdx.x; i < TILE + 2 * (W - 1); i += THREADS) {
             const int t = t0 - (W - 1) + i;
-            sx[i] = (t >= 0 && t < L) ? xr[t] : 0.f;
+            sx[i] = (t >= 0 && t < L) ? xr[rev ? L - 1 - t : t] : 0.f;
         }
         __syncthreads();
         for (int i = threadIdx.x; i < TILE + W - 1; i += THREADS) {
             const int t = t0 + i;
             float g = 0.f;
             if (t < L) {
-                g = gr[t];
+                g = gr[rev ? L - 1 - t : t];
                 if (SILU) {
                     float pre = bv;
 #pragma unroll
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const float*
                 float acc = 0.f;
 #pragma unroll
                 for (int k = 0; k < W; ++k) acc += wk[k] * sg[i + (W - 1) - k];
-                dxr[t] = acc;
+                dxr[rev ? L - 1 - t : t] = acc;
                 const float g = sg[i];
                 db += g;
 #pragma unroll
@@ -158,7 +158,7 @@ int64_t avse_cconv_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t width
 
 int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const float* x, int64_t x_bs,
                    int64_t x_ds, const float* weight, const float* bias, float* out, int64_t out_bs, int64_t out_ds,
-                   int32_t silu, avse_stream_t stream) {
+                   int32_t silu, int32_t reverse, avse_stream_t stream) {
     if (!x || !weight || !out) return AVSE_EINVAL;
     if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
     if (batch * dim > (1LL << 31) - 1) return AVSE_ESHAPE;
@@ -168,11 +168,11 @@ int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, co
 #define CASE(WW)                                                                                               \
     case WW:                                                                                                   \
         if (silu) {                                                                                            \
-            if (bias) hipLaunchKernelGGL((fwd_kernel<WW, true, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds); \
-            else hipLaunchKernelGGL((fwd_kernel<WW, true, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds); \
+            if (bias) hipLaunchKernelGGL((fwd_kernel<WW, true, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
+            else hipLaunchKernelGGL((fwd_kernel<WW, true, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
         } else {                                                                                               \
-            if (bias) hipLaunchKernelGGL((fwd_kernel<WW, false, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds); \
-            else hipLaunchKernelGGL((fwd_kernel<WW, false, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds); \
+            if (bias) hipLaunchKernelGGL((fwd_kernel<WW, false, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
+            else hipLaunchKernelGGL((fwd_kernel<WW, false, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
         }                                                                                                      \
         break;
         CASE(1) CASE(2) CASE(3) CASE(4)
@@ -186,7 +186,7 @@ int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, co
 int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const float* x, int64_t x_bs,
                    int64_t x_ds, const float* weight, const float* bias, const float* dout, int64_t dout_bs,
                    int64_t dout_ds, float* dx, int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias,
-                   int32_t silu, float* workspace, avse_stream_t stream) {
+                   int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream) {
     if (!x || !weight || !dout || !dx || !dweight || !workspace) return AVSE_EINVAL;
     if (bias && !dbias) return AVSE_EINVAL;
     if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
@@ -196,11 +196,11 @@ int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, co
 #define CASE(WW)                                                                                               \
     case WW:                                                                                                   \
         if (silu) {                                                                                            \
-            if (bias) hipLaunchKernelGGL((bwd_kernel<WW, true, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace); \
-            else hipLaunchKernelGGL((bwd_kernel<WW, true, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace); \
+            if (bias) hipLaunchKernelGGL((bwd_kernel<WW, true, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
+            else hipLaunchKernelGGL((bwd_kernel<WW, true, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
         } else {                                                                                               \
-            if (bias) hipLaunchKernelGGL((bwd_kernel<WW, false, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace); \
-            else hipLaunchKernelGGL((bwd_kernel<WW, false, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace); \
+            if (bias) hipLaunchKernelGGL((bwd_kernel<WW, false, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
+            else hipLaunchKernelGGL((bwd_kernel<WW, false, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
         }                                                                                                      \
         break;
         CASE(1) CASE(2) CASE(3) CASE(4)

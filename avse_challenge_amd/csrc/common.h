@@ -39,6 +39,41 @@ template <> struct io<bf16_t> {
     }
 };
 
+// Raw buffer loads: 32-bit per-lane voffset + wave-uniform soffset (an SGPR), hardware range check
+// (out-of-range reads return 0).  Used for the strided row gathers of the scan so that 16 rows
+// per tensor cost ONE address VGPR (the row step goes in soffset), not 16 64-bit pointers.
+template <typename T> struct bufld;
+template <> struct bufld<float> {
+    __device__ static inline float ld(__amdgpu_buffer_rsrc_t r, int voff_elems, int soff_elems) {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff_elems * 4, soff_elems * 4, 0));
+    }
+};
+template <> struct bufld<bf16_t> {
+    __device__ static inline float ld(__amdgpu_buffer_rsrc_t r, int voff_elems, int soff_elems) {
+        const unsigned short v = __builtin_amdgcn_raw_buffer_load_b16(r, voff_elems * 2, soff_elems * 2, 0);
+        return __uint_as_float(((uint32_t)v) << 16);
+    }
+};
+template <typename T> struct bufst;
+template <> struct bufst<float> {
+    __device__ static inline void st(__amdgpu_buffer_rsrc_t r, int voff_elems, int soff_elems, float v) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff_elems * 4, soff_elems * 4, 0);
+    }
+};
+template <> struct bufst<bf16_t> {
+    __device__ static inline void st(__amdgpu_buffer_rsrc_t r, int voff_elems, int soff_elems, float v) {
+        bf16_t h;
+        io<bf16_t>::st(&h, v);
+        __builtin_amdgcn_raw_buffer_store_b16(h.x, r, voff_elems * 2, soff_elems * 2, 0);
+    }
+};
+template <typename T>
+__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const T* base, int64_t n_elems) {
+    int64_t bytes = n_elems * (int64_t)sizeof(T);
+    if (bytes > 0x7FFFFFFFLL) bytes = 0x7FFFFFFFLL;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+
 __device__ inline float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ inline float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * AVSE_LOG2E); }
 

@@ -52,35 +52,73 @@ __device__ inline Lane lane_ids() {
 }
 
 // ------------------------------------------------------------------------------- loaders
-template <typename Tin, bool SOFTPLUS, bool HAS_BIAS>
-__device__ inline void load_u_dt(float* s_ud, const Tin* u, int64_t u_bs, int64_t u_ds, const Tin* dl,
-                                 int64_t d_bs, int64_t d_ds, const float* bias, int b, int d0, int D,
-                                 int t0, int tn) {
-    for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
-        int r = idx / TC, t = idx % TC, d = d0 + r;
-        float uu = 0.f, dt = 0.f;
-        if (d < D && t < tn) {
-            uu = io<Tin>::ld(u + b * u_bs + (int64_t)d * u_ds + t0 + t);
-            dt = io<Tin>::ld(dl + b * d_bs + (int64_t)d * d_ds + t0 + t);
-            if (HAS_BIAS) dt += bias[d];
-            if (SOFTPLUS) dt = softplus(dt);
-        }
-        *reinterpret_cast<float2*>(&s_ud[r * UD_STRIDE + 2 * t]) = make_float2(uu, dt);
-    }
-}
+// Every thread owns tile column t = lane (one time step) and rows wave + 4*i; all the chunk's
+// global loads are issued into registers first (several KB in flight per wave) and written to
+// LDS afterwards, so a chunk load costs ~one HBM round trip instead of one per element.  The
+// logical step t of chunk k lives at memory position pos = t0 + t, or L-1-(t0+t) when reversed.
+constexpr int RPT = CPB * TC / THREADS;        // 16 rows per thread
+constexpr int BPT = NSTATE * TC / THREADS;     // 4 B (and C) rows per thread
+
+__device__ inline int tpos(int t, int L, bool rev) { return rev ? L - 1 - t : t; }
 
 template <typename Tin>
-__device__ inline void load_bc(float* s_bc, const Tin* B, int64_t B_bs, int64_t B_ns, const Tin* C,
-                               int64_t C_bs, int64_t C_ns, int b, int t0, int tn) {
-    for (int idx = threadIdx.x; idx < NSTATE * TC; idx += THREADS) {
-        int n = idx / TC, t = idx % TC;
-        float bv = 0.f, cv = 0.f;
-        if (t < tn) {
-            bv = io<Tin>::ld(B + b * B_bs + n * B_ns + t0 + t);
-            cv = io<Tin>::ld(C + b * C_bs + n * C_ns + t0 + t);
+struct RowRegs {
+    float v[RPT];
+    __device__ inline void load(const Tin* p, int64_t bs, int64_t ds, int b, int d0, int D, int t0, int tn, int L,
+                                bool rev) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int nrow = min(CPB, D - d0);
+        const auto rs = make_rsrc(p + b * bs + (int64_t)d0 * ds, (int64_t)(nrow - 1) * ds + L);
+        const bool tv = lane < tn;
+        const int voff = wave * (int)ds + tpos(t0 + lane, L, rev);
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const float x = bufld<Tin>::ld(rs, voff, 4 * i * (int)ds);
+            v[i] = (tv && wave + 4 * i < nrow) ? x : 0.f;
         }
-        s_bc[t * BC_STRIDE + n] = bv;
-        s_bc[t * BC_STRIDE + NSTATE + n] = cv;
+    }
+};
+
+template <typename Tin>
+struct BCRegs {
+    float bv[BPT], cv[BPT];
+    __device__ inline void load(const Tin* B, int64_t B_bs, int64_t B_ns, const Tin* C, int64_t C_bs, int64_t C_ns,
+                                int b, int t0, int tn, int L, bool rev) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const bool tv = lane < tn;
+        const int pos = tpos(t0 + lane, L, rev);
+        const auto rb = make_rsrc(B + b * B_bs, (int64_t)(NSTATE - 1) * B_ns + L);
+        const auto rc = make_rsrc(C + b * C_bs, (int64_t)(NSTATE - 1) * C_ns + L);
+        const int vb = wave * (int)B_ns + pos, vc = wave * (int)C_ns + pos;
+#pragma unroll
+        for (int i = 0; i < BPT; ++i) {
+            const float x = bufld<Tin>::ld(rb, vb, 4 * i * (int)B_ns);
+            const float y = bufld<Tin>::ld(rc, vc, 4 * i * (int)C_ns);
+            bv[i] = tv ? x : 0.f;
+            cv[i] = tv ? y : 0.f;
+        }
+    }
+    __device__ inline void store(float* s_bc) const {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+        for (int i = 0; i < BPT; ++i) {
+            s_bc[lane * BC_STRIDE + wave + 4 * i] = bv[i];
+            s_bc[lane * BC_STRIDE + NSTATE + wave + 4 * i] = cv[i];
+        }
+    }
+};
+
+// (u, dt) rows: dt = softplus(delta + bias) applied once per element here
+template <bool SOFTPLUS, bool HAS_BIAS>
+__device__ inline void store_ud(float* s_ud, const float* u, const float* dl, const float* bias, int d0, int D) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        const int r = wave + 4 * i, d = d0 + r;
+        float dt = dl[i];
+        if (HAS_BIAS) dt += (d < D) ? bias[d] : 0.f;
+        if (SOFTPLUS) dt = softplus(dt);
+        *reinterpret_cast<float2*>(&s_ud[r * UD_STRIDE + 2 * lane]) = make_float2(u[i], dt);
     }
 }
 
@@ -94,17 +132,19 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int b = bid / nblk_d, d0 = (bid % nblk_d) * CPB;
     const int D = (int)a.dim, L = (int)a.seqlen;
+    const bool rev = a.reverse != 0;
     const Lane id = lane_ids();
     const int d = d0 + id.c;
     const bool dvalid = d < D;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
-    float A2[NS], h[NS], asum[NS];
+    float A2[NS], h[NS];
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
         A2[j] = dvalid ? a.A[(int64_t)d * NSTATE + id.g * NS + j] * AVSE_LOG2E : 0.f;
         h[j] = 0.f;
-        asum[j] = 0.f;
     }
+    float dtsum = 0.f;
     const float Dv = (HAS_D && dvalid) ? a.D[d] : 0.f;
 
     const Tin* u = (const Tin*)a.u;
@@ -112,23 +152,33 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     const Tin* z = (const Tin*)a.z;
     const int nck = (L + TC - 1) / TC;
 
+    RowRegs<Tin> ru, rd, rz;
+    BCRegs<Tin> rbc;
+    ru.load(u, a.u_bs, a.u_ds, b, d0, D, 0, min(TC, L), L, rev);
+    rd.load(dl, a.delta_bs, a.delta_ds, b, d0, D, 0, min(TC, L), L, rev);
+    if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, 0, min(TC, L), L, rev);
+    rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, 0, min(TC, L), L, rev);
+
     for (int k = 0; k < nck; ++k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
-        __syncthreads();
-        load_u_dt<Tin, SOFTPLUS, HAS_BIAS>(s_ud, u, a.u_bs, a.u_ds, dl, a.delta_bs, a.delta_ds, a.delta_bias, b,
-                                           d0, D, t0, tn);
-        load_bc<Tin>(s_bc, (const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t0, tn);
+        // registers -> LDS (chunk k)
+        store_ud<SOFTPLUS, HAS_BIAS>(s_ud, ru.v, rd.v, a.delta_bias, d0, D);
+        rbc.store(s_bc);
         if (HAS_Z) {
-            for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
-                int r = idx / TC, t = idx % TC, dd = d0 + r;
-                float zz = (dd < D && t < tn) ? io<Tin>::ld(z + b * a.z_bs + (int64_t)dd * a.z_ds + t0 + t) : 0.f;
-                s_z[r * (TC + 1) + t] = siluf_(zz);
-            }
+#pragma unroll
+            for (int i = 0; i < RPT; ++i) s_z[(wave + 4 * i) * (TC + 1) + lane] = siluf_(rz.v[i]);
         }
         __syncthreads();
+        // prefetch chunk k + 1 while chunk k computes
+        if (k + 1 < nck) {
+            const int t1 = t0 + TC, tn1 = min(TC, L - t1);
+            ru.load(u, a.u_bs, a.u_ds, b, d0, D, t1, tn1, L, rev);
+            rd.load(dl, a.delta_bs, a.delta_ds, b, d0, D, t1, tn1, L, rev);
+            if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t1, tn1, L, rev);
+            rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t1, tn1, L, rev);
+        }
 
         float* my_ud = &s_ud[id.c * UD_STRIDE];
-#pragma unroll 4
         for (int t = 0; t < tn; ++t) {
             const float2 ud = *reinterpret_cast<const float2*>(&my_ud[2 * t]);
             const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
@@ -136,38 +186,51 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
             const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
             const float cc[4] = {cq.x, cq.y, cq.z, cq.w};
             const float dt = ud.y, dtu = ud.y * ud.x;
+            dtsum += dt;
             float y = 0.f;
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
-                const float e = dt * A2[j];
-                h[j] = fast_exp2(e) * h[j] + dtu * bb[j];
-                asum[j] += e;
+                h[j] = fast_exp2(dt * A2[j]) * h[j] + dtu * bb[j];
                 y += h[j] * cc[j];
             }
             y = group_sum<G>(y);
             const float out = y + Dv * ud.x;
             if (id.g == 0) {
                 my_ud[2 * t] = out;                                    // u slot <- out
-                if (HAS_Z) s_z[id.c * (TC + 1) + t] *= out;          // silu(z) slot <- out_z
+                if (HAS_Z) s_z[id.c * (TC + 1) + t] *= out;           // silu(z) slot <- out_z
             }
         }
         __syncthreads();
-        Tin* out = (Tin*)a.out;
-        Tin* outz = (Tin*)a.out_z;
-        for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
-            int r = idx / TC, t = idx % TC, dd = d0 + r;
-            if (dd < D && t < tn) {
-                io<Tin>::st(out + b * a.out_bs + (int64_t)dd * a.out_ds + t0 + t, s_ud[r * UD_STRIDE + 2 * t]);
-                if (HAS_Z) io<Tin>::st(outz + b * a.out_z_bs + (int64_t)dd * a.out_z_ds + t0 + t, s_z[r * (TC + 1) + t]);
+        // flush chunk k outputs (lane = time column, rows wave + 4i): buffer stores, row step in soffset
+        {
+            const int nrow = min(CPB, D - d0);
+            const auto ro = make_rsrc((Tin*)a.out + b * a.out_bs + (int64_t)d0 * a.out_ds,
+                                      (int64_t)(nrow - 1) * a.out_ds + L);
+            const int vo = wave * (int)a.out_ds + tpos(t0 + lane, L, rev);
+            if (lane < tn) {
+#pragma unroll
+                for (int i = 0; i < RPT; ++i)
+                    if (wave + 4 * i < nrow) bufst<Tin>::st(ro, vo, 4 * i * (int)a.out_ds, s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]);
+            }
+            if (HAS_Z) {
+                const auto rz_ = make_rsrc((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d0 * a.out_z_ds,
+                                           (int64_t)(nrow - 1) * a.out_z_ds + L);
+                const int vz = wave * (int)a.out_z_ds + tpos(t0 + lane, L, rev);
+                if (lane < tn) {
+#pragma unroll
+                    for (int i = 0; i < RPT; ++i)
+                        if (wave + 4 * i < nrow) bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds, s_z[(wave + 4 * i) * (TC + 1) + lane]);
+                }
             }
         }
         if (dvalid) {
             float* xp = a.x + (((int64_t)b * D + d) * nck + k) * (2 * NSTATE) + 2 * id.g * NS;
-            float4 v0 = make_float4(fast_exp2(asum[0]), h[0], fast_exp2(asum[1]), h[1]);
-            float4 v1 = make_float4(fast_exp2(asum[2]), h[2], fast_exp2(asum[3]), h[3]);
+            float4 v0 = make_float4(fast_exp2(dtsum * A2[0]), h[0], fast_exp2(dtsum * A2[1]), h[1]);
+            float4 v1 = make_float4(fast_exp2(dtsum * A2[2]), h[2], fast_exp2(dtsum * A2[3]), h[3]);
             reinterpret_cast<float4*>(xp)[0] = v0;
             reinterpret_cast<float4*>(xp)[1] = v1;
         }
+        __syncthreads();
     }
 }
 
@@ -232,20 +295,27 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     float* ws_bc = a.workspace;                                    // (b, nblk_d, 32, L)
     const int64_t slab = (int64_t)2 * NSTATE * L;
 
+    const bool rev = a.reverse != 0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
     for (int k = nck - 1; k >= 0; --k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
-        __syncthreads();
-        load_u_dt<Tin, SOFTPLUS, HAS_BIAS>(s_ud, u, a.u_bs, a.u_ds, dl, a.delta_bs, a.delta_ds, a.delta_bias, b,
-                                           d0, D, t0, tn);
-        load_bc<Tin>(s_bc, (const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t0, tn);
-        for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
-            int r = idx / TC, t = idx % TC, dd = d0 + r;
-            float zz = 0.f, go = 0.f;
-            if (dd < D && t < tn) {
-                if (HAS_Z) zz = io<Tin>::ld(z + b * a.z_bs + (int64_t)dd * a.z_ds + t0 + t);
-                go = io<Tin>::ld(dout + b * a.dout_bs + (int64_t)dd * a.dout_ds + t0 + t);
-            }
-            *reinterpret_cast<float2*>(&s_zg[r * Z_STRIDE + 2 * t]) = make_float2(zz, go);
+        {
+            // all global loads of the chunk in flight before any LDS store
+            RowRegs<Tin> ru, rd, rz, rg;
+            BCRegs<Tin> rbc;
+            ru.load(u, a.u_bs, a.u_ds, b, d0, D, t0, tn, L, rev);
+            rd.load(dl, a.delta_bs, a.delta_ds, b, d0, D, t0, tn, L, rev);
+            if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t0, tn, L, rev);
+            rg.load(dout, a.dout_bs, a.dout_ds, b, d0, D, t0, tn, L, rev);
+            rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t0, tn, L, rev);
+            __syncthreads();
+            store_ud<SOFTPLUS, HAS_BIAS>(s_ud, ru.v, rd.v, a.delta_bias, d0, D);
+            rbc.store(s_bc);
+#pragma unroll
+            for (int i = 0; i < RPT; ++i)
+                *reinterpret_cast<float2*>(&s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane]) =
+                    make_float2(HAS_Z ? rz.v[i] : 0.f, rg.v[i]);
         }
         __syncthreads();
 
@@ -388,29 +458,54 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
                         float v = 0.f;
 #pragma unroll
                         for (int w = 0; w < 4; ++w) v += s_red[(w * TS + i) * 2 * NSTATE + slot];
-                        ws_bc[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + t0 + t] = v;
+                        ws_bc[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + tpos(t0 + t, L, rev)] = v;
                     }
                 }
                 __syncthreads();
             }
         }
         __syncthreads();
-        // write du, ddelta, dz (+ out_z) tiles
-        Tin* du = (Tin*)a.du;
-        Tin* dd_ = (Tin*)a.ddelta;
-        Tin* dz = (Tin*)a.dz;
-        Tin* oz = (Tin*)a.out_z;
-        for (int idx = threadIdx.x; idx < CPB * TC; idx += THREADS) {
-            int r = idx / TC, t = idx % TC, dd = d0 + r;
-            if (dd < D && t < tn) {
-                const float2 v = *reinterpret_cast<const float2*>(&s_ud[r * UD_STRIDE + 2 * t]);
-                io<Tin>::st(du + b * a.du_bs + (int64_t)dd * a.du_ds + t0 + t, v.x);
-                io<Tin>::st(dd_ + b * a.ddelta_bs + (int64_t)dd * a.ddelta_ds + t0 + t, v.y);
-                if (HAS_Z) io<Tin>::st(dz + b * a.dz_bs + (int64_t)dd * a.dz_ds + t0 + t, s_zg[r * Z_STRIDE + 2 * t]);
-                if (a.recompute_out_z)
-                    io<Tin>::st(oz + b * a.out_z_bs + (int64_t)dd * a.out_z_ds + t0 + t, s_oz[r * (TC + 1) + t]);
+        // write du, ddelta, dz (+ out_z) tiles (lane = time column): buffer stores, row step in soffset
+        {
+            const int nrow = min(CPB, D - d0);
+            const int pos = tpos(t0 + lane, L, rev);
+            const auto r_du = make_rsrc((Tin*)a.du + b * a.du_bs + (int64_t)d0 * a.du_ds, (int64_t)(nrow - 1) * a.du_ds + L);
+            const auto r_dd = make_rsrc((Tin*)a.ddelta + b * a.ddelta_bs + (int64_t)d0 * a.ddelta_ds,
+                                        (int64_t)(nrow - 1) * a.ddelta_ds + L);
+            const int v_du = wave * (int)a.du_ds + pos, v_dd = wave * (int)a.ddelta_ds + pos;
+            if (lane < tn) {
+#pragma unroll
+                for (int i = 0; i < RPT; ++i) {
+                    if (wave + 4 * i < nrow) {
+                        const float2 v = *reinterpret_cast<const float2*>(&s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]);
+                        bufst<Tin>::st(r_du, v_du, 4 * i * (int)a.du_ds, v.x);
+                        bufst<Tin>::st(r_dd, v_dd, 4 * i * (int)a.ddelta_ds, v.y);
+                    }
+                }
+            }
+            if (HAS_Z) {
+                const auto r_dz = make_rsrc((Tin*)a.dz + b * a.dz_bs + (int64_t)d0 * a.dz_ds, (int64_t)(nrow - 1) * a.dz_ds + L);
+                const int v_dz = wave * (int)a.dz_ds + pos;
+                if (lane < tn) {
+#pragma unroll
+                    for (int i = 0; i < RPT; ++i)
+                        if (wave + 4 * i < nrow)
+                            bufst<Tin>::st(r_dz, v_dz, 4 * i * (int)a.dz_ds, s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane]);
+                }
+            }
+            if (a.recompute_out_z) {
+                const auto r_oz = make_rsrc((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d0 * a.out_z_ds,
+                                            (int64_t)(nrow - 1) * a.out_z_ds + L);
+                const int v_oz = wave * (int)a.out_z_ds + pos;
+                if (lane < tn) {
+#pragma unroll
+                    for (int i = 0; i < RPT; ++i)
+                        if (wave + 4 * i < nrow)
+                            bufst<Tin>::st(r_oz, v_oz, 4 * i * (int)a.out_z_ds, s_oz[(wave + 4 * i) * (TC + 1) + lane]);
+                }
             }
         }
+        __syncthreads();
     }
     // per-(b, d) partials of dA, dD, ddelta_bias
     float* ws_d = ws_bc + (int64_t)a.batch * nblk_d * slab;       // (b, D, 18)

@@ -41,8 +41,9 @@ def _bc4(M, dtype):
 
 # ------------------------------------------------------------------------ selective scan
 
-def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False):
-    """Returns (out, x, out_z|None) — the selective_scan_cuda.fwd contract."""
+def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False, reverse=False):
+    """Returns (out, x, out_z|None) — the selective_scan_cuda.fwd contract.
+    reverse=True scans time backwards (== flip(scan(flip(inputs))) with no flip copies)."""
     _need_gpu(u, delta, A, B, C, D, z, delta_bias)
     u = _last_contig(u)
     dt = u.dtype
@@ -62,7 +63,7 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
     out_z = torch.empty((b, d, l), device=u.device, dtype=dt) if z is not None else None
     a = ScanFwdArgs()
     a.batch, a.dim, a.seqlen, a.dstate = b, d, l, NSTATE
-    a.in_dtype, a.delta_softplus = _dtype_code(dt), int(bool(delta_softplus))
+    a.in_dtype, a.delta_softplus, a.reverse = _dtype_code(dt), int(bool(delta_softplus)), int(bool(reverse))
     a.u, a.u_bs, a.u_ds = u.data_ptr(), u.stride(0), u.stride(1)
     a.delta, a.delta_bs, a.delta_ds = delta.data_ptr(), delta.stride(0), delta.stride(1)
     a.A = A.data_ptr()
@@ -80,7 +81,7 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
 
 
 def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, dz=None,
-                       delta_softplus=False, recompute_out_z=False):
+                       delta_softplus=False, recompute_out_z=False, reverse=False):
     """Returns [du, ddelta, dA, dB, dC, dD, ddelta_bias, dz, out_z] — selective_scan_cuda.bwd contract.
     dB, dC are fp32 shaped (b, 1, n, l); a passed-in ``dz`` view is written in place."""
     _need_gpu(u, delta, A, B, C, D, z, delta_bias, dout, x)
@@ -119,6 +120,7 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
     a.batch, a.dim, a.seqlen, a.dstate = b, d, l, NSTATE
     a.in_dtype, a.delta_softplus = _dtype_code(dt), int(bool(delta_softplus))
     a.recompute_out_z = int(out_z is not None)
+    a.reverse = int(bool(reverse))
     a.u, a.u_bs, a.u_ds = u.data_ptr(), u.stride(0), u.stride(1)
     a.delta, a.delta_bs, a.delta_ds = delta.data_ptr(), delta.stride(0), delta.stride(1)
     a.A = A.data_ptr()
@@ -147,7 +149,7 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
 
 # ------------------------------------------------------------------------ causal conv1d
 
-def causal_conv1d_fwd(x, weight, bias=None, silu=False):
+def causal_conv1d_fwd(x, weight, bias=None, silu=False, reverse=False):
     _need_gpu(x, weight, bias)
     in_dtype = x.dtype
     x = _last_contig(x.float())
@@ -159,12 +161,12 @@ def causal_conv1d_fwd(x, weight, bias=None, silu=False):
     w = weight.shape[1]
     out = torch.empty((b, d, l), device=x.device, dtype=torch.float32)
     check(_lib.lib().avse_cconv_fwd(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(out),
-                                    out.stride(0), out.stride(1), int(bool(silu)), stream_ptr(x.device)),
-          "avse_cconv_fwd")
+                                    out.stride(0), out.stride(1), int(bool(silu)), int(bool(reverse)),
+                                    stream_ptr(x.device)), "avse_cconv_fwd")
     return out if in_dtype == torch.float32 else out.to(in_dtype)
 
 
-def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False):
+def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False):
     _need_gpu(x, weight, bias, dout)
     x = _last_contig(x.float())
     wshape = weight.shape
@@ -182,7 +184,8 @@ def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False):
                      dtype=torch.float32)
     check(_lib.lib().avse_cconv_bwd(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(dout),
                                     dout.stride(0), dout.stride(1), ptr(dx), dx.stride(0), dx.stride(1), ptr(dweight),
-                                    ptr(dbias), int(bool(silu)), ptr(ws), stream_ptr(x.device)), "avse_cconv_bwd")
+                                    ptr(dbias), int(bool(silu)), int(bool(reverse)), ptr(ws), stream_ptr(x.device)),
+          "avse_cconv_bwd")
     if dx_ret is not None and dx_ret is not dx:
         dx_ret.copy_(dx)
         dx = dx_ret

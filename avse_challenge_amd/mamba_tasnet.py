@@ -23,32 +23,38 @@ NSTATE = 16
 
 
 class MambaInnerNoOutProj(torch.autograd.Function):
-    """Conv1d(k4)+SiLU -> x_proj -> dt_proj -> selective scan (z-gated); checkpoint_lvl 1."""
+    """Conv1d(k4)+SiLU -> x_proj -> dt_proj -> selective scan (z-gated); checkpoint_lvl 1.
+
+    ``reverse=True`` is the v2 backward direction WITHOUT the two flip copies of bimamba.py:236,253:
+    the conv and the scan walk time backwards by index, so the result is already the reference's
+    ``out_b.flip(-1)`` in natural time order (x_dbl / delta / B / C stay in natural order too)."""
 
     @staticmethod
-    def forward(ctx, xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias):
+    def forward(ctx, xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias, reverse=False):
         R = dt_proj_w.shape[1]
         x, z = xz.chunk(2, dim=1)
-        conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True)             # (b, d, l)
+        conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=reverse)     # (b, d, l)
         x_dbl = torch.matmul(conv_out.transpose(1, 2), x_proj_w.t())             # (b, l, R + 2n)
         delta = torch.matmul(dt_proj_w, x_dbl[..., :R].transpose(1, 2))          # (b, d, l)
         Bm = x_dbl[..., R:R + NSTATE].transpose(1, 2).contiguous()               # (b, n, l)
         Cm = x_dbl[..., R + NSTATE:].transpose(1, 2).contiguous()
-        out, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, dt_bias, True)
+        out, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, dt_bias, True, reverse=reverse)
         ctx.save_for_backward(xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck, out)
+        ctx.reverse = reverse
         return out_z
 
     @staticmethod
     def backward(ctx, dout):
         xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck, out = ctx.saved_tensors
+        rev = ctx.reverse
         R = dt_proj_w.shape[1]
         x, z = xz.chunk(2, dim=1)
-        conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True)
+        conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=rev)
         delta = torch.matmul(dt_proj_w, x_dbl[..., :R].transpose(1, 2))
         dxz = torch.empty_like(xz)
         dx, dz = dxz.chunk(2, dim=1)
         dconv, ddelta, dA, dB, dC, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
-            conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, out, dz, True, False)
+            conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, out, dz, True, False, reverse=rev)
         dx_dbl = torch.empty_like(x_dbl)
         dx_dbl[..., R:R + NSTATE] = dB[:, 0].transpose(1, 2)
         dx_dbl[..., R + NSTATE:] = dC[:, 0].transpose(1, 2)
@@ -56,8 +62,8 @@ class MambaInnerNoOutProj(torch.autograd.Function):
         dx_dbl[..., :R] = torch.matmul(ddelta.transpose(1, 2), dt_proj_w)
         dx_proj_w = torch.einsum("blk,bdl->kd", dx_dbl, conv_out)
         dconv = dconv + torch.matmul(x_proj_w.t(), dx_dbl.transpose(1, 2))
-        _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True)
-        return (dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias)
+        _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True, reverse=rev)
+        return (dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias, None)
 
 
 class AddRMSNorm(torch.autograd.Function):
@@ -124,9 +130,9 @@ class BiMambaV2(nn.Module):
         A_b = -torch.exp(self.A_b_log.float())
         f = MambaInnerNoOutProj.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
                                       self.dt_proj.weight, A, self.D.float(), self.dt_proj.bias.float())
-        bk = MambaInnerNoOutProj.apply(xz.flip(-1), self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
-                                       self.dt_proj_b.weight, A_b, self.D_b.float(), self.dt_proj_b.bias.float())
-        y = 0.5 * f + 0.5 * bk.flip(-1)
+        bk = MambaInnerNoOutProj.apply(xz, self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
+                                       self.dt_proj_b.weight, A_b, self.D_b.float(), self.dt_proj_b.bias.float(), True)
+        y = 0.5 * (f + bk)          # == 0.5*out + 0.5*out_b.flip(-1) of bimamba.py:253, flip-free
         return F.linear(y.transpose(1, 2), self.out_proj.weight)
 
 
@@ -197,17 +203,28 @@ class MaskNet(nn.Module):
 
 
 class Encoder(nn.Module):
+    """Conv1d(1, N, k, stride k/2) + ReLU as framing + GEMM (MIOpen's pick for this shape is a naive
+    direct kernel: 270 ms per backward call at B=16, profiles/)."""
+
     def __init__(self, kernel_size=16, out_channels=512):
         super().__init__()
         self.conv1d = nn.Conv1d(1, out_channels, kernel_size, stride=kernel_size // 2, bias=False)
 
-    def forward(self, x):
-        return F.relu(self.conv1d(x[:, None, :]))
+    def forward(self, x):                                      # (B, T) -> (B, N, L)
+        k = self.conv1d.kernel_size[0]
+        frames = x.unfold(-1, k, self.conv1d.stride[0])        # (B, L, k) view
+        return F.relu(torch.matmul(self.conv1d.weight[:, 0, :], frames.transpose(1, 2)))
 
 
 class Decoder(nn.ConvTranspose1d):
-    def forward(self, x):
-        return super().forward(x).squeeze(1)
+    """ConvTranspose1d(N, 1, k, stride k/2) as GEMM + overlap-add (F.fold)."""
+
+    def forward(self, x):                                      # (B, N, L) -> (B, T')
+        k, s = self.kernel_size[0], self.stride[0]
+        L = x.shape[-1]
+        frames = torch.matmul(self.weight[:, 0, :].t(), x)     # (B, k, L)
+        T = (L - 1) * s + k
+        return F.fold(frames, (1, T), (1, k), stride=(1, s))[:, 0, 0, :]
 
 
 class MambaTasNet(nn.Module):

@@ -46,6 +46,8 @@ typedef struct {
     int64_t batch, dim, seqlen, dstate;
     int32_t in_dtype;          /* AVSE_F32 or AVSE_BF16: dtype of u, delta, z, B, C, out, out_z */
     int32_t delta_softplus;
+    int32_t reverse;           /* 1: scan over time backwards, i.e. flip(scan(flip(.))) without copies
+                                  (the BiMamba v2 backward direction, bimamba.py:236-253) */
     const void* u;      int64_t u_bs, u_ds;          /* batch / dim strides */
     const void* delta;  int64_t delta_bs, delta_ds;
     const float* A;                                  /* (d, n) contiguous */
@@ -63,6 +65,7 @@ typedef struct {
     int64_t batch, dim, seqlen, dstate;
     int32_t in_dtype, delta_softplus;
     int32_t recompute_out_z;
+    int32_t reverse;
     const void* u;      int64_t u_bs, u_ds;
     const void* delta;  int64_t delta_bs, delta_ds;
     const float* A;
@@ -95,20 +98,22 @@ int avse_scan_bwd(const avse_scan_bwd_args* a, avse_stream_t stream);
  * Replaces causal_conv1d_cuda.causal_conv1d_fwd / causal_conv1d_bwd (causal-conv1d
  * 1.1.3.post1) as called at selective_scan_interface.py:182,244 and :286.  Depthwise,
  * width w <= 4, left zero-padding w-1, optional SiLU; x: (b, d, l) with l contiguous.
- * Semantics pinned by bimamba.py:278-279 (act(conv1d(x)[..., :seqlen])).
+ * Semantics pinned by bimamba.py:278-279 (act(conv1d(x)[..., :seqlen])).  reverse = 1 computes
+ * flip(conv(flip(x))) (anti-causal) in place of the xz.flip(-1) copy of bimamba.py:236.
  */
 int64_t avse_cconv_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t width);
 int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
                    const float* x, int64_t x_bs, int64_t x_ds,
                    const float* weight /* (d, w) */, const float* bias /* (d) or NULL */,
-                   float* out, int64_t out_bs, int64_t out_ds, int32_t silu, avse_stream_t stream);
+                   float* out, int64_t out_bs, int64_t out_ds, int32_t silu, int32_t reverse,
+                   avse_stream_t stream);
 int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
                    const float* x, int64_t x_bs, int64_t x_ds,
                    const float* weight, const float* bias,
                    const float* dout, int64_t dout_bs, int64_t dout_ds,
                    float* dx, int64_t dx_bs, int64_t dx_ds,
                    float* dweight /* (d, w) */, float* dbias /* (d) or NULL */,
-                   int32_t silu, float* workspace, avse_stream_t stream);
+                   int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- add + RMSNorm -------
  * Replaces the Block pre-norm of Mamba-TasNet/modules/mamba/bimamba.py:447-451

@@ -281,3 +281,56 @@ def test_prelu_vs_torch(shape, npar):
     yg.backward(gy.float().to(DEV))
     close(xg.grad, x.grad, 1e-6, 1e-6, "dx")
     close(m.weight.grad, a.grad, 1e-4, 1e-5, "da")
+
+
+# ------------------------------------------------------------------ flip-by-index (BiMamba v2 backward direction)
+
+@pytest.mark.parametrize("l", [1, 64, 150, 257])
+def test_scan_and_cconv_reverse_equal_flipped(l):
+    b, d = 2, 64
+    u = det_input((b, d, l), 800 + l).to(DEV)
+    delta = (0.5 * det_input((b, d, l), 801)).to(DEV)
+    A = (-torch.exp(0.5 * det_input((d, 16), 802))).to(DEV)
+    Bm, Cm = det_input((b, 1, 16, l), 803).to(DEV), det_input((b, 1, 16, l), 804).to(DEV)
+    D = det_input((d,), 805).to(DEV)
+    z = det_input((b, d, l), 806).to(DEV)
+    bias = (0.3 * det_input((d,), 807)).to(DEV)
+    f = lambda t: t.flip(-1)
+    out_r, x_r, oz_r = K().selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, reverse=True)
+    out_f, x_f, oz_f = K().selective_scan_fwd(f(u), f(delta), A, f(Bm), f(Cm), D, f(z), bias, True)
+    close(oz_r, f(oz_f), 1e-6, 1e-6, "scan fwd reverse")
+    close(x_r, x_f, 1e-6, 1e-6, "checkpoints")
+    g = det_input((b, d, l), 808).to(DEV)
+    gr = K().selective_scan_bwd(u, delta, A, Bm, Cm, D, z, bias, g, x_r, out_r, None, True, False, reverse=True)
+    gf = K().selective_scan_bwd(f(u), f(delta), A, f(Bm), f(Cm), D, f(z), bias, f(g), x_f, out_f, None, True, False)
+    for i, name in enumerate(["du", "ddelta", "dA", "dB", "dC", "dD", "dbias", "dz"]):
+        flipped = gf[i].flip(-1) if name in ("du", "ddelta", "dB", "dC", "dz") else gf[i]
+        close(gr[i], flipped, 1e-5, 1e-5, name)
+    w, cb = det_input((d, 4), 809).to(DEV), det_input((d,), 810).to(DEV)
+    co_r = K().causal_conv1d_fwd(u, w, cb, True, reverse=True)
+    close(co_r, f(K().causal_conv1d_fwd(f(u), w, cb, True)), 1e-6, 1e-6, "cconv fwd reverse")
+    dr = K().causal_conv1d_bwd(u, w, cb, g, silu=True, reverse=True)
+    df = K().causal_conv1d_bwd(f(u), w, cb, f(g), silu=True)
+    close(dr[0], f(df[0]), 1e-5, 1e-5, "cconv dx")
+    close(dr[1], df[1], 1e-4, 1e-5, "cconv dw")
+    close(dr[2], df[2], 1e-4, 1e-5, "cconv db")
+
+
+def test_encoder_decoder_framing_gemm_vs_golden():
+    from avse_challenge_amd import mamba_tasnet as M
+    from oracle.det_init import det_init_
+    g = load_golden("encdec")
+    enc = det_init_(M.Encoder(16, 64), 14).to(DEV)
+    dec = det_init_(M.Decoder(64, 1, 16, stride=8, bias=False), 15).to(DEV)
+    mix = g2t(g["mix"]).requires_grad_(True)
+    w = enc(mix)
+    close(w, g["mix_w"], 1e-5, 1e-5, "encoder")
+    y = dec(w)
+    close(y, g["dec"], 1e-5, 1e-5, "decoder")
+    # gradients vs torch's reference conv ops in fp64 on CPU
+    y.sum().backward()
+    mix64 = torch.from_numpy(g["mix"]).double().requires_grad_(True)
+    w64 = torch.relu(torch.nn.functional.conv1d(mix64[:, None], enc.conv1d.weight.detach().cpu().double(), stride=8))
+    y64 = torch.nn.functional.conv_transpose1d(w64, dec.weight.detach().cpu().double(), stride=8)
+    y64.sum().backward()
+    close(mix.grad, mix64.grad, 1e-4, 1e-5, "d mix")
