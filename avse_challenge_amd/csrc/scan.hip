@@ -21,6 +21,7 @@
 // 4 waves in LDS, and written as per-workgroup partial slabs summed by a second kernel —
 // deterministic, no float atomics.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -179,27 +180,43 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
         }
 
         float* my_ud = &s_ud[id.c * UD_STRIDE];
-        for (int t = 0; t < tn; ++t) {
-            const float2 ud = *reinterpret_cast<const float2*>(&my_ud[2 * t]);
-            const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
-            const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
-            const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
-            const float cc[4] = {cq.x, cq.y, cq.z, cq.w};
-            const float dt = ud.y, dtu = ud.y * ud.x;
-            dtsum += dt;
-            float y = 0.f;
+        float* my_z = &s_z[HAS_Z ? id.c * (TC + 1) : 0];
+        // 8 steps per iteration: the LDS reads of all 8 issue together and the 8 cross-lane
+        // y reductions (DPP) are independent, so one wave per SIMD still keeps its pipes busy.
+        constexpr int U = 8;
+        auto steps = [&](int t, auto UNR) {
+            constexpr int NU = decltype(UNR)::value;
+            float yv[NU], uv[NU];
 #pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                h[j] = fast_exp2(dt * A2[j]) * h[j] + dtu * bb[j];
-                y += h[j] * cc[j];
+            for (int q = 0; q < NU; ++q) {
+                const float2 ud = *reinterpret_cast<const float2*>(&my_ud[2 * (t + q)]);
+                const float4 bq = *reinterpret_cast<const float4*>(&s_bc[(t + q) * BC_STRIDE + id.g * NS]);
+                const float4 cq = *reinterpret_cast<const float4*>(&s_bc[(t + q) * BC_STRIDE + NSTATE + id.g * NS]);
+                const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
+                const float cc[4] = {cq.x, cq.y, cq.z, cq.w};
+                const float dt = ud.y, dtu = ud.y * ud.x;
+                dtsum += dt;
+                float y = 0.f;
+#pragma unroll
+                for (int j = 0; j < NS; ++j) {
+                    h[j] = fast_exp2(dt * A2[j]) * h[j] + dtu * bb[j];
+                    y += h[j] * cc[j];
+                }
+                yv[q] = y;
+                uv[q] = ud.x;
             }
-            y = group_sum<G>(y);
-            const float out = y + Dv * ud.x;
-            if (id.g == 0) {
-                my_ud[2 * t] = out;                                    // u slot <- out
-                if (HAS_Z) s_z[id.c * (TC + 1) + t] *= out;           // silu(z) slot <- out_z
+#pragma unroll
+            for (int q = 0; q < NU; ++q) {
+                const float out = group_sum<G>(yv[q]) + Dv * uv[q];
+                if (id.g == 0) {
+                    my_ud[2 * (t + q)] = out;                          // u slot <- out
+                    if (HAS_Z) my_z[t + q] *= out;                     // silu(z) slot <- out_z
+                }
             }
-        }
+        };
+        int t = 0;
+        for (; t + U <= tn; t += U) steps(t, std::integral_constant<int, U>());
+        for (; t < tn; ++t) steps(t, std::integral_constant<int, 1>());
         __syncthreads();
         // flush chunk k outputs (lane = time column, rows wave + 4i): buffer stores, row step in soffset
         {
