@@ -70,13 +70,15 @@ struct RowRegs {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         const int nrow = min(CPB, D - d0);
         const auto rs = make_rsrc(p + b * bs + (int64_t)d0 * ds, (int64_t)(nrow - 1) * ds + L);
-        const bool tv = lane < tn;
         const int voff = wave * (int)ds + tpos(t0 + lane, L, rev);
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-            const float x = bufld<Tin>::ld(rs, voff, 4 * i * (int)ds);
-            v[i] = (tv && wave + 4 * i < nrow) ? x : 0.f;
-        }
+        for (int i = 0; i < RPT; ++i) v[i] = bufld<Tin>::ld(rs, voff, 4 * i * (int)ds);   // raw: masked at use
+    }
+    // element i is real data iff the lane's step is inside the chunk and the row exists; the
+    // select happens when the registers are consumed, so no wait is forced at load time
+    __device__ inline float get(int i, int tn, int nrow) const {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        return (lane < tn && wave + 4 * i < nrow) ? v[i] : 0.f;
     }
 };
 
@@ -86,41 +88,49 @@ struct BCRegs {
     __device__ inline void load(const Tin* B, int64_t B_bs, int64_t B_ns, const Tin* C, int64_t C_bs, int64_t C_ns,
                                 int b, int t0, int tn, int L, bool rev) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        const bool tv = lane < tn;
         const int pos = tpos(t0 + lane, L, rev);
         const auto rb = make_rsrc(B + b * B_bs, (int64_t)(NSTATE - 1) * B_ns + L);
         const auto rc = make_rsrc(C + b * C_bs, (int64_t)(NSTATE - 1) * C_ns + L);
         const int vb = wave * (int)B_ns + pos, vc = wave * (int)C_ns + pos;
 #pragma unroll
         for (int i = 0; i < BPT; ++i) {
-            const float x = bufld<Tin>::ld(rb, vb, 4 * i * (int)B_ns);
-            const float y = bufld<Tin>::ld(rc, vc, 4 * i * (int)C_ns);
-            bv[i] = tv ? x : 0.f;
-            cv[i] = tv ? y : 0.f;
+            bv[i] = bufld<Tin>::ld(rb, vb, 4 * i * (int)B_ns);
+            cv[i] = bufld<Tin>::ld(rc, vc, 4 * i * (int)C_ns);
         }
     }
-    __device__ inline void store(float* s_bc) const {
+    __device__ inline void store(float* s_bc, int tn) const {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const bool tv = lane < tn;
 #pragma unroll
         for (int i = 0; i < BPT; ++i) {
-            s_bc[lane * BC_STRIDE + wave + 4 * i] = bv[i];
-            s_bc[lane * BC_STRIDE + NSTATE + wave + 4 * i] = cv[i];
+            s_bc[lane * BC_STRIDE + wave + 4 * i] = tv ? bv[i] : 0.f;
+            s_bc[lane * BC_STRIDE + NSTATE + wave + 4 * i] = tv ? cv[i] : 0.f;
         }
     }
 };
 
-// (u, dt) rows: dt = softplus(delta + bias) applied once per element here
-template <bool SOFTPLUS, bool HAS_BIAS>
-__device__ inline void store_ud(float* s_ud, const float* u, const float* dl, const float* bias, int d0, int D) {
+// (u, dt) rows: dt = softplus(delta + bias) applied once per element here; bias_r holds the
+// thread's 16 row biases (loaded once per kernel, so no global load sits in the chunk loop)
+template <typename Tin, bool SOFTPLUS, bool HAS_BIAS>
+__device__ inline void store_ud(float* s_ud, const RowRegs<Tin>& ru, const RowRegs<Tin>& rd, const float* bias_r,
+                                int tn, int nrow) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-        const int r = wave + 4 * i, d = d0 + r;
-        float dt = dl[i];
-        if (HAS_BIAS) dt += (d < D) ? bias[d] : 0.f;
+        const bool ok = lane < tn && wave + 4 * i < nrow;
+        float dt = rd.v[i];
+        if (HAS_BIAS) dt += bias_r[i];
         if (SOFTPLUS) dt = softplus(dt);
-        *reinterpret_cast<float2*>(&s_ud[r * UD_STRIDE + 2 * lane]) = make_float2(u[i], dt);
+        *reinterpret_cast<float2*>(&s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]) =
+            make_float2(ok ? ru.v[i] : 0.f, ok ? dt : 0.f);
     }
+}
+
+template <bool HAS_BIAS>
+__device__ inline void load_bias_rows(float* bias_r, const float* bias, int d0, int D) {
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) bias_r[i] = (HAS_BIAS && d0 + wave + 4 * i < D) ? bias[d0 + wave + 4 * i] : 0.f;
 }
 
 // ------------------------------------------------------------------------------- forward
@@ -153,6 +163,9 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     const Tin* z = (const Tin*)a.z;
     const int nck = (L + TC - 1) / TC;
 
+    const int nrow = min(CPB, D - d0);
+    float bias_r[RPT];
+    load_bias_rows<HAS_BIAS>(bias_r, a.delta_bias, d0, D);
     RowRegs<Tin> ru, rd, rz;
     BCRegs<Tin> rbc;
     ru.load(u, a.u_bs, a.u_ds, b, d0, D, 0, min(TC, L), L, rev);
@@ -163,11 +176,11 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     for (int k = 0; k < nck; ++k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
         // registers -> LDS (chunk k)
-        store_ud<SOFTPLUS, HAS_BIAS>(s_ud, ru.v, rd.v, a.delta_bias, d0, D);
-        rbc.store(s_bc);
+        store_ud<Tin, SOFTPLUS, HAS_BIAS>(s_ud, ru, rd, bias_r, tn, nrow);
+        rbc.store(s_bc, tn);
         if (HAS_Z) {
 #pragma unroll
-            for (int i = 0; i < RPT; ++i) s_z[(wave + 4 * i) * (TC + 1) + lane] = siluf_(rz.v[i]);
+            for (int i = 0; i < RPT; ++i) s_z[(wave + 4 * i) * (TC + 1) + lane] = siluf_(rz.get(i, tn, nrow));
         }
         __syncthreads();
         // prefetch chunk k + 1 while chunk k computes
@@ -255,7 +268,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
 // reduce-scatter of 8 values over the 16 channel lanes (lane bits 2..5) of a wave; returns
 // the full sum of value index vi = 4*b2 + 2*b3 + b4 (b_k = bit k of the lane id).
 __device__ inline float rs8(float v[8], int lane) {
-    const bool b2 = lane & 4, b3 = lane & 8, b4 = lane & 16;
+    const bool b2 = lane & 4, b3 = lane & 8;
     float w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -270,19 +283,22 @@ __device__ inline float rs8(float v[8], int lane) {
         float keep = b3 ? w[i + 2] : w[i];
         x2[i] = keep + swz_xor<8>(send);
     }
-    float send = b4 ? x2[0] : x2[1];
-    float keep = b4 ? x2[1] : x2[0];
-    float r = keep + swz_xor<16>(send);
-    return r + xor32(r);
+    // xor-16 level as one VALU permlane16_swap: (r0 + r1) keeps x2[0] on even rows and x2[1] on
+    // odd rows, each summed with the partner row's copy; xor-32 the same with permlane32_swap.
+    auto p16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x2[0]), __float_as_uint(x2[1]), false, false);
+    const float r = __uint_as_float(p16[0]) + __uint_as_float(p16[1]);
+    auto p32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+    return __uint_as_float(p32[0]) + __uint_as_float(p32[1]);
 }
+
+constexpr int RED = 8;   // adjoint steps buffered per cross-wave dB/dC flush
 
 template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS>
 __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int nblk_d) {
     __shared__ __attribute__((aligned(16))) float s_ud[CPB * UD_STRIDE];   // (u, dt) -> (du, ddelta)
     __shared__ __attribute__((aligned(16))) float s_zg[CPB * Z_STRIDE];    // (z, dout) -> (dz, g)
     __shared__ __attribute__((aligned(16))) float s_bc[TC * BC_STRIDE];
-    __shared__ float s_red[4 * TS * 2 * NSTATE];
-    __shared__ float s_oz[CPB * (TC + 1)];                               // recomputed out_z (optional)
+    __shared__ float s_red[4 * RED * 2 * NSTATE];
 
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int b = bid / nblk_d, cb = bid % nblk_d, d0 = cb * CPB;
@@ -314,6 +330,9 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
 
     const bool rev = a.reverse != 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nrow_b = min(CPB, D - d0);
+    float bias_r[RPT];
+    load_bias_rows<HAS_BIAS>(bias_r, a.delta_bias, d0, D);
 
     for (int k = nck - 1; k >= 0; --k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
@@ -327,12 +346,12 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
             rg.load(dout, a.dout_bs, a.dout_ds, b, d0, D, t0, tn, L, rev);
             rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t0, tn, L, rev);
             __syncthreads();
-            store_ud<SOFTPLUS, HAS_BIAS>(s_ud, ru.v, rd.v, a.delta_bias, d0, D);
-            rbc.store(s_bc);
+            store_ud<Tin, SOFTPLUS, HAS_BIAS>(s_ud, ru, rd, bias_r, tn, nrow_b);
+            rbc.store(s_bc, tn);
 #pragma unroll
             for (int i = 0; i < RPT; ++i)
                 *reinterpret_cast<float2*>(&s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane]) =
-                    make_float2(HAS_Z ? rz.v[i] : 0.f, rg.v[i]);
+                    make_float2(HAS_Z ? rz.get(i, tn, nrow_b) : 0.f, rg.get(i, tn, nrow_b));
         }
         __syncthreads();
 
@@ -412,7 +431,9 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
                             }
                             if (id.g == 0) {
                                 *reinterpret_cast<float2*>(zg_p) = make_float2(dzv, gv);
-                                if (a.recompute_out_z) s_oz[id.c * (TC + 1) + t] = oz;
+                                if (a.recompute_out_z)   // rare path: direct (uncoalesced) store
+                                    io<Tin>::st((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d * a.out_z_ds +
+                                                    tpos(t0 + t, L, rev), oz);
                             }
                         } else {
 #pragma unroll
@@ -464,21 +485,23 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
                     if (id.lane < 32) {
                         const int vi = ((id.lane >> 2) & 1) * 4 + ((id.lane >> 3) & 1) * 2 + ((id.lane >> 4) & 1);
                         const int slot = (vi < 4 ? 0 : NSTATE) + id.g * NS + (vi & 3);
-                        s_red[(id.wave * TS + i) * 2 * NSTATE + slot] = r;
+                        s_red[(id.wave * RED + (i & (RED - 1))) * 2 * NSTATE + slot] = r;
                     }
-                }
-                __syncthreads();
-                // cross-wave sum -> partial slab
-                for (int idx = threadIdx.x; idx < TS * 2 * NSTATE; idx += THREADS) {
-                    const int slot = idx / TS, i = idx % TS, t = ts + i;
-                    if (t < tn) {
-                        float v = 0.f;
+                    if ((i & (RED - 1)) == 0) {
+                        // cross-wave sum of steps ts+i .. ts+i+RED-1 -> partial slab
+                        __syncthreads();
+                        for (int idx = threadIdx.x; idx < RED * 2 * NSTATE; idx += THREADS) {
+                            const int slot = idx / RED, ii = idx % RED, tt = ts + i + ii;
+                            if (tt < tn) {
+                                float v = 0.f;
 #pragma unroll
-                        for (int w = 0; w < 4; ++w) v += s_red[(w * TS + i) * 2 * NSTATE + slot];
-                        ws_bc[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + tpos(t0 + t, L, rev)] = v;
+                                for (int w = 0; w < 4; ++w) v += s_red[(w * RED + ii) * 2 * NSTATE + slot];
+                                ws_bc[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + tpos(t0 + tt, L, rev)] = v;
+                            }
+                        }
+                        __syncthreads();
                     }
                 }
-                __syncthreads();
             }
         }
         __syncthreads();
@@ -508,17 +531,6 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
                     for (int i = 0; i < RPT; ++i)
                         if (wave + 4 * i < nrow)
                             bufst<Tin>::st(r_dz, v_dz, 4 * i * (int)a.dz_ds, s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane]);
-                }
-            }
-            if (a.recompute_out_z) {
-                const auto r_oz = make_rsrc((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d0 * a.out_z_ds,
-                                            (int64_t)(nrow - 1) * a.out_z_ds + L);
-                const int v_oz = wave * (int)a.out_z_ds + pos;
-                if (lane < tn) {
-#pragma unroll
-                    for (int i = 0; i < RPT; ++i)
-                        if (wave + 4 * i < nrow)
-                            bufst<Tin>::st(r_oz, v_oz, 4 * i * (int)a.out_z_ds, s_oz[(wave + 4 * i) * (TC + 1) + lane]);
                 }
             }
         }
