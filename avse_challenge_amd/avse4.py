@@ -1,0 +1,248 @@
+"""avse4 binaural AV enhancement baseline on MI355X (drop-in for baseline/avse4/model.py).
+
+Same module tree / state_dict keys as the reference (AVSE4BaselineModule -> model
+(avse4_separator) + visual_frontend), so its Lightning checkpoints load unchanged.  Citations are
+relative to /root/reference/baseline/avse4:
+  overlap_and_add :19-66 -> F.fold        Encoder :97-109 -> framing GEMM     Decoder :112-123
+  TemporalConvNet :126-182                TemporalBlock :255-269              DepthwiseSeparableConv :272-293
+  GlobalLayerNorm :225-252                VisualConv1D :184-205               VisualFrontend utils.py:97-118
+  AVSE4BaselineModule :295-393 (forward :316-321, training_step :323, enhance :335-352, cal_loss :374-383)
+MI355X specifics: every (PReLU -> gLN) pair runs as the fused HIP prelu_gln kernels, every
+depthwise dilated conv1d as the HIP dwconv kernels, the lip Conv3d weight gradient on the HIP
+MFMA implicit GEMM; all 1x1 convolutions / the encoder / the decoder basis are hipBLASLt GEMMs.
+"""
+import copy
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import losses
+from .layers import LipConv3d, _PReLUFn, dwconv1d, prelu_gln
+
+NORM_MEAN, NORM_STD = 0.4161, 0.1688
+
+
+def _pw(conv, x):
+    """1x1 Conv1d without bias as a GEMM: (Cout, Cin) @ (B, Cin, K)."""
+    return torch.matmul(conv.weight[:, :, 0], x)
+
+
+class GlobalLayerNorm(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.gamma = nn.Parameter(torch.ones(1, c, 1))
+        self.beta = nn.Parameter(torch.zeros(1, c, 1))
+
+
+class ChannelWiseLayerNorm(nn.LayerNorm):
+    def forward(self, x):
+        return super().forward(x.transpose(1, 2)).transpose(1, 2)
+
+
+class DepthwiseSeparableConv(nn.Module):
+    def __init__(self, cin, cout, k, stride, padding, dilation):
+        super().__init__()
+        assert stride == 1 and padding == (k - 1) * dilation // 2
+        self.dilation = dilation
+        self.net = nn.Sequential(nn.Conv1d(cin, cin, k, stride=stride, padding=padding, dilation=dilation,
+                                           groups=cin, bias=False),
+                                 nn.PReLU(), GlobalLayerNorm(cin), nn.Conv1d(cin, cout, 1, bias=False))
+
+    def forward(self, x):
+        dw, pr, nm, pw = self.net
+        y = dwconv1d(x, dw.weight, self.dilation)
+        y = prelu_gln(y, pr.weight, nm.gamma, nm.beta)
+        return _pw(pw, y)
+
+
+class TemporalBlock(nn.Module):
+    def __init__(self, cin, cout, k, stride, padding, dilation):
+        super().__init__()
+        self.net = nn.Sequential(nn.Conv1d(cin, cout, 1, bias=False), nn.PReLU(), GlobalLayerNorm(cout),
+                                 DepthwiseSeparableConv(cout, cin, k, stride, padding, dilation))
+
+    def forward(self, x):
+        c1, pr, nm, ds = self.net
+        y = prelu_gln(_pw(c1, x), pr.weight, nm.gamma, nm.beta)
+        return ds(y) + x
+
+
+class VisualConv1D(nn.Module):
+    def __init__(self, c=512):
+        super().__init__()
+        self.net = nn.Sequential(nn.ReLU(), nn.BatchNorm1d(c),
+                                 nn.Conv1d(c, c, 3, padding=1, groups=c, bias=False), nn.PReLU(),
+                                 nn.BatchNorm1d(c), nn.Conv1d(c, c, 1, bias=False))
+
+    def forward(self, x):
+        _, bn1, dw, pr, bn2, pw = self.net
+        y = dwconv1d(bn1(F.relu(x)), dw.weight, 1)
+        y = bn2(_PReLUFn.apply(y, pr.weight))
+        return _pw(pw, y) + x
+
+
+class TemporalConvNet(nn.Module):
+    def __init__(self, N, B, H, P, X, R, C, num_channels=2, vis_dim=512, up=32):
+        super().__init__()
+        self.num_channels, self.C, self.up = num_channels, C, up
+        self.layer_norm = ChannelWiseLayerNorm(N)
+        self.bottleneck_conv1x1 = nn.Conv1d(N, B, 1, bias=False)
+        blocks = [nn.Conv1d(2 * B, B, 1, bias=False)]
+        for x in range(X):
+            d = 2 ** x
+            blocks.append(TemporalBlock(B, H, P, 1, (P - 1) * d // 2, d))
+        self.tcn = nn.ModuleList([copy.deepcopy(nn.Sequential(*blocks)) for _ in range(R)])
+        self.visual_conv = nn.Sequential(*[VisualConv1D(vis_dim) for _ in range(5)])
+        self.ve_conv1x1 = nn.ModuleList([copy.deepcopy(nn.Conv1d(vis_dim, B, 1, bias=False)) for _ in range(R)])
+        self.mask_conv1x1 = nn.Conv1d(B, N * num_channels, 1, bias=False)
+
+    def forward(self, x, visual):
+        visual = self.visual_conv(visual.transpose(1, 2))
+        x = _pw(self.bottleneck_conv1x1, self.layer_norm(x))
+        bsz, Bc, K = x.shape
+        for i in range(len(self.tcn)):
+            v = _pw(self.ve_conv1x1[i], visual)
+            v = F.interpolate(v, self.up * v.shape[-1], mode="linear")
+            v = F.pad(v, (0, K - v.shape[-1]))
+            seq = self.tcn[i]
+            x = _pw(seq[0], torch.cat((x, v), 1))
+            for blk in list(seq)[1:]:
+                x = blk(x)
+        x = F.relu(_pw(self.mask_conv1x1, x))
+        return x.reshape(bsz, self.num_channels, Bc, K)
+
+
+class Encoder(nn.Module):
+    def __init__(self, L, N, num_channels=2):
+        super().__init__()
+        self.L = L
+        self.conv1d_U = nn.Conv1d(num_channels, N, L, stride=L // 2, bias=False)
+
+    def forward(self, m):                                   # (B, C, T) -> (B, N, K)
+        frames = m.unfold(-1, self.L, self.L // 2)          # (B, C, K, L)
+        Bn, C, K, L = frames.shape
+        f = frames.permute(0, 2, 1, 3).reshape(Bn, K, C * L)
+        return F.relu(torch.matmul(self.conv1d_U.weight.reshape(self.conv1d_U.weight.shape[0], -1), f.transpose(1, 2)))
+
+
+class Decoder(nn.Module):
+    def __init__(self, N, L):
+        super().__init__()
+        self.L = L
+        self.basis_signals = nn.Linear(N, L, bias=False)
+
+    def forward(self, mixture_w, est_mask):                  # -> (B, C, 20*(K-1)+40)
+        est = mixture_w[:, None] * est_mask                  # (B, C, N, K)
+        Bn, C, N, K = est.shape
+        frames = torch.matmul(self.basis_signals.weight, est.reshape(Bn * C, N, K))     # (B*C, L, K)
+        T = (K - 1) * (self.L // 2) + self.L
+        out = F.fold(frames, (1, T), (1, self.L), stride=(1, self.L // 2))
+        return out.reshape(Bn, C, T)
+
+
+class Separator(nn.Module):
+    """avse4_separator (model.py:73-94)."""
+
+    def __init__(self, N=256, L=40, B=256, H=512, P=3, X=8, R=4, C=2, num_channels=2):
+        super().__init__()
+        self.encoder = Encoder(L, N, num_channels)
+        self.separator = TemporalConvNet(N, B, H, P, X, R, C, num_channels)
+        self.decoder = Decoder(N, L)
+        for p in self.parameters():
+            if p.dim() > 1:
+                nn.init.xavier_normal_(p)
+
+    def forward(self, mixture, visual):
+        w = self.encoder(mixture)
+        est = self.decoder(w, self.separator(w, visual))
+        return F.pad(est, (0, mixture.shape[-1] - est.shape[-1]))
+
+
+class ResNetLayer(nn.Module):
+    def __init__(self, cin, cout, stride):
+        super().__init__()
+        bn = dict(momentum=0.01, eps=0.001)
+        self.conv1a = nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
+        self.bn1a = nn.BatchNorm2d(cout, **bn)
+        self.conv2a = nn.Conv2d(cout, cout, 3, padding=1, bias=False)
+        self.stride = stride
+        self.downsample = nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+        self.outbna = nn.BatchNorm2d(cout, **bn)
+        self.conv1b = nn.Conv2d(cout, cout, 3, padding=1, bias=False)
+        self.bn1b = nn.BatchNorm2d(cout, **bn)
+        self.conv2b = nn.Conv2d(cout, cout, 3, padding=1, bias=False)
+        self.outbnb = nn.BatchNorm2d(cout, **bn)
+
+    def forward(self, x):
+        y = self.conv2a(F.relu(self.bn1a(self.conv1a(x))))
+        y = y + (x if self.stride == 1 else self.downsample(x))
+        mid = y
+        y = F.relu(self.outbna(y))
+        y = self.conv2b(F.relu(self.bn1b(self.conv1b(y)))) + mid
+        return F.relu(self.outbnb(y))
+
+
+class ResNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.layer1 = ResNetLayer(64, 64, 1)
+        self.layer2 = ResNetLayer(64, 128, 2)
+        self.layer3 = ResNetLayer(128, 256, 2)
+        self.layer4 = ResNetLayer(256, 512, 2)
+        self.avgpool = nn.AvgPool2d(4, stride=1)
+
+    def forward(self, x):
+        return self.avgpool(self.layer4(self.layer3(self.layer2(self.layer1(x)))))
+
+
+class VisualFrontend(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.frontend3D = nn.Sequential(
+            LipConv3d(1, 64, (5, 7, 7), (1, 2, 2), (2, 3, 3)), nn.BatchNorm3d(64, momentum=0.01, eps=0.001), nn.ReLU(),
+            nn.MaxPool3d((1, 3, 3), stride=(1, 2, 2), padding=(0, 1, 1)))
+        self.resnet = ResNet()
+
+    def forward(self, x):                                   # (B, 1, T, 112, 112) -> (B, T, 512)
+        bsz = x.shape[0]
+        y = self.frontend3D((x - NORM_MEAN) / NORM_STD).transpose(1, 2)
+        y = y.reshape(y.shape[0] * y.shape[1], y.shape[2], y.shape[3], y.shape[4])
+        return self.resnet(y).reshape(bsz, -1, 512)
+
+
+class AVSE4BaselineModule(nn.Module):
+    """LightningModule surface of AVSE4BaselineModule (forward / training_step / enhance / cal_loss)."""
+
+    def __init__(self, lr=0.0001, a_only=False, num_channels=2, **sep_kwargs):
+        super().__init__()
+        assert num_channels in [1, 2], "Only mono and binaural audio are supported"
+        self.lr, self.a_only, self.num_channels = lr, a_only, num_channels
+        self.model = Separator(num_channels=num_channels, **sep_kwargs)
+        self.visual_frontend = VisualFrontend()
+
+    def forward(self, data):
+        return self.model(data["noisy_audio"].float(), self.visual_frontend(data["vis_feat"].float()))
+
+    def cal_loss(self, batch):
+        return losses.avse4_loss(batch["clean"], self(batch))
+
+    def training_step(self, batch, batch_idx=0):
+        return self.cal_loss(batch)
+
+    def validation_step(self, batch, batch_idx=0):
+        return self.cal_loss(batch)
+
+    def configure_optimizers(self):
+        return torch.optim.Adam(self.parameters(), lr=self.lr)
+
+    @torch.no_grad()
+    def enhance(self, data):
+        """model.py:335-352: forward one utterance and peak-normalise (returns numpy arrays)."""
+        dev = next(self.parameters()).device
+        inputs = {"noisy_audio": torch.as_tensor(np.asarray(data["noisy_audio"]))[None].to(dev),
+                  "vis_feat": torch.as_tensor(np.asarray(data["vis_feat"]))[None].to(dev)}
+        est = self(inputs)[0].cpu().numpy()
+        est /= np.max(np.abs(est))
+        return np.asarray(data["clean"]), np.asarray(data["noisy_audio"]), est

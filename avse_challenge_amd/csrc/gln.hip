@@ -1,0 +1,251 @@
+// Fused PReLU -> GlobalLayerNorm forward / backward for gfx950 (avse4 TCN hot path).
+//
+// Replaces the (nn.PReLU(), GlobalLayerNorm) pairs of /root/reference/baseline/avse4/model.py:
+//   TemporalBlock.net          :259-266  conv1x1 -> PReLU -> gLN -> ...
+//   DepthwiseSeparableConv.net :284-292  dwconv  -> PReLU -> gLN -> conv1x1
+// gLN (model.py:225-252): per sample mean/var over (C, K), EPS 1e-8 inside pow(var + EPS, .5),
+// biased variance; y = gamma_c (p - mean) / sqrt(var + EPS) + beta_c with p = PReLU(x) (one slope).
+//
+// Layout (B, C, K), K contiguous.  Every kernel is one pass over rows (b, c) with one 256-thread
+// workgroup per row (lane-contiguous loads); per-row partial sums go to small workspaces that tiny
+// finalize kernels reduce (deterministic, double accumulation across rows).  Statistics use sums
+// shifted by the sample's first element, which removes the E[x^2]-E[x]^2 cancellation.
+// HBM: fwd = 2 reads + 1 write of x, bwd = 2 reads of (x, dy) + 1 write of dx.
+#include "common.h"
+
+namespace avse {
+namespace gln {
+
+constexpr int THREADS = 256;
+
+__device__ inline float prelu(float x, float a) { return x > 0.f ? x : a * x; }
+
+template <typename T>
+__device__ inline T block_sum(T v, T* red) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+// row partials of shifted sums: ws[row] = (sum(p - s), sum((p - s)^2)), s = p(x[b, 0, 0])
+__global__ __launch_bounds__(THREADS) void stats_kernel(int C, int K, const float* __restrict__ x,
+                                                        const float* __restrict__ alpha, float2* __restrict__ ws) {
+    __shared__ float red[4];
+    const int row = blockIdx.x, b = row / C;
+    const float a = alpha[0];
+    const float shift = prelu(x[(int64_t)b * C * K], a);
+    const float* xr = x + (int64_t)row * K;
+    float s1 = 0.f, s2 = 0.f;
+    for (int t = threadIdx.x; t < K; t += THREADS) {
+        const float v = prelu(xr[t], a) - shift;
+        s1 += v;
+        s2 += v * v;
+    }
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+    if (threadIdx.x == 0) ws[row] = make_float2(s1, s2);
+}
+
+// per sample: mean, rstd = 1/sqrt(var + EPS)
+__global__ void stats_finalize(int B, int C, int K, const float* __restrict__ x, const float* __restrict__ alpha,
+                               const float2* __restrict__ ws, float eps, float2* __restrict__ stats) {
+    __shared__ double red1[4], red2[4];
+    const int b = blockIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const float2 v = ws[(int64_t)b * C + c];
+        s1 += v.x;
+        s2 += v.y;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        s1 += __shfl_xor(s1, m, 64);
+        s2 += __shfl_xor(s2, m, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red1[threadIdx.x >> 6] = s1;
+        red2[threadIdx.x >> 6] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double n = (double)C * K;
+        const double m1 = (red1[0] + red1[1] + red1[2] + red1[3]) / n;
+        const double m2 = (red2[0] + red2[1] + red2[2] + red2[3]) / n;
+        const double var = fmax(m2 - m1 * m1, 0.0);
+        const float shift = prelu(x[(int64_t)b * C * K], alpha[0]);
+        stats[b] = make_float2((float)(m1 + shift), (float)(1.0 / sqrt(var + (double)eps)));
+    }
+}
+
+__global__ __launch_bounds__(THREADS) void apply_kernel(int C, int K, const float* __restrict__ x,
+                                                        const float* __restrict__ alpha, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, const float2* __restrict__ stats,
+                                                        float* __restrict__ y) {
+    const int row = blockIdx.x, b = row / C, c = row % C;
+    const float a = alpha[0];
+    const float2 st = stats[b];
+    const float g = gamma[c] * st.y, o = beta[c] - gamma[c] * st.y * st.x;
+    const float* xr = x + (int64_t)row * K;
+    float* yr = y + (int64_t)row * K;
+    for (int t = threadIdx.x; t < K; t += THREADS) yr[t] = g * prelu(xr[t], a) + o;
+}
+
+// backward pass 1: per row S1 = sum dy, S2 = sum dy * xhat
+__global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int C, int K, const float* __restrict__ x,
+                                                             const float* __restrict__ alpha, const float2* __restrict__ stats,
+                                                             const float* __restrict__ dy, float2* __restrict__ ws) {
+    __shared__ float red[4];
+    const int row = blockIdx.x, b = row / C;
+    const float a = alpha[0];
+    const float2 st = stats[b];
+    const float* xr = x + (int64_t)row * K;
+    const float* gr = dy + (int64_t)row * K;
+    float s1 = 0.f, s2 = 0.f;
+    for (int t = threadIdx.x; t < K; t += THREADS) {
+        const float g = gr[t];
+        const float xh = (prelu(xr[t], a) - st.x) * st.y;
+        s1 += g;
+        s2 += g * xh;
+    }
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+    if (threadIdx.x == 0) ws[row] = make_float2(s1, s2);
+}
+
+// per sample: (mean_g, mean_gxh) over (C, K) with g = dy * gamma; per channel dgamma, dbeta (sum over b)
+__global__ void bwd_finalize(int B, int C, int K, const float2* __restrict__ ws, const float* __restrict__ gamma,
+                             float2* __restrict__ smeans, float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    __shared__ double red1[4], red2[4];
+    const int blk = blockIdx.x;
+    if (blk < B) {
+        const int b = blk;
+        double s1 = 0.0, s2 = 0.0;
+        for (int c = threadIdx.x; c < C; c += blockDim.x) {
+            const float2 v = ws[(int64_t)b * C + c];
+            s1 += (double)gamma[c] * v.x;
+            s2 += (double)gamma[c] * v.y;
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            s1 += __shfl_xor(s1, m, 64);
+            s2 += __shfl_xor(s2, m, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            red1[threadIdx.x >> 6] = s1;
+            red2[threadIdx.x >> 6] = s2;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const double n = (double)C * K;
+            smeans[b] = make_float2((float)((red1[0] + red1[1] + red1[2] + red1[3]) / n),
+                                    (float)((red2[0] + red2[1] + red2[2] + red2[3]) / n));
+        }
+    } else {
+        const int c0 = (blk - B) * blockDim.x;
+        const int c = c0 + threadIdx.x;
+        if (c < C) {
+            double g = 0.0, bt = 0.0;
+            for (int b = 0; b < B; ++b) {
+                const float2 v = ws[(int64_t)b * C + c];
+                bt += v.x;
+                g += v.y;
+            }
+            dgamma[c] = (float)g;
+            dbeta[c] = (float)bt;
+        }
+    }
+}
+
+// backward pass 2: dx = (x > 0 ? 1 : a) * rstd * (dy*gamma - mean_g - xhat*mean_gxh); dalpha row partial
+__global__ __launch_bounds__(THREADS) void bwd_apply_kernel(int C, int K, const float* __restrict__ x,
+                                                            const float* __restrict__ alpha, const float* __restrict__ gamma,
+                                                            const float2* __restrict__ stats, const float2* __restrict__ smeans,
+                                                            const float* __restrict__ dy, float* __restrict__ dx,
+                                                            float* __restrict__ ws_alpha) {
+    __shared__ float red[4];
+    const int row = blockIdx.x, b = row / C, c = row % C;
+    const float a = alpha[0];
+    const float2 st = stats[b], sm = smeans[b];
+    const float gm = gamma[c];
+    const float* xr = x + (int64_t)row * K;
+    const float* gr = dy + (int64_t)row * K;
+    float* dr = dx + (int64_t)row * K;
+    float da = 0.f;
+    for (int t = threadIdx.x; t < K; t += THREADS) {
+        const float xv = xr[t];
+        const float xh = (prelu(xv, a) - st.x) * st.y;
+        const float dp = st.y * (gr[t] * gm - sm.x - xh * sm.y);
+        dr[t] = xv > 0.f ? dp : a * dp;
+        da += xv > 0.f ? 0.f : dp * xv;
+    }
+    da = block_sum(da, red);
+    if (threadIdx.x == 0) ws_alpha[row] = da;
+}
+
+__global__ void alpha_finalize(int rows, const float* __restrict__ ws_alpha, float* __restrict__ dalpha) {
+    __shared__ double red[4];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < rows; i += blockDim.x) s += ws_alpha[i];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) dalpha[0] = (float)(red[0] + red[1] + red[2] + red[3]);
+}
+
+}  // namespace gln
+}  // namespace avse
+
+using namespace avse::gln;
+
+extern "C" {
+
+int64_t avse_prelu_gln_workspace_bytes(int64_t B, int64_t C) { return 8 * B * C + 4 * B * C + 16 * B; }
+
+int avse_prelu_gln_fwd(int64_t B, int64_t C, int64_t K, const float* x, const float* alpha, const float* gamma,
+                       const float* beta, float eps, float* y, float* stats, float* workspace, avse_stream_t stream) {
+    if (!x || !alpha || !gamma || !beta || !y || !stats || !workspace) return AVSE_EINVAL;
+    if (B <= 0 || C <= 0 || K <= 0 || B * C > (1LL << 31) - 1) return AVSE_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned rows = (unsigned)(B * C);
+    float2* ws = (float2*)workspace;
+    hipLaunchKernelGGL(stats_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, x, alpha, ws);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(stats_finalize, dim3((unsigned)B), dim3(256), 0, st, (int)B, (int)C, (int)K, x, alpha, ws, eps,
+                       (float2*)stats);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(apply_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, x, alpha, gamma, beta,
+                       (const float2*)stats, y);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const float* alpha, const float* gamma,
+                       const float* stats, const float* dy, float* dx, float* dalpha, float* dgamma, float* dbeta,
+                       float* workspace, avse_stream_t stream) {
+    if (!x || !alpha || !gamma || !stats || !dy || !dx || !dalpha || !dgamma || !dbeta || !workspace) return AVSE_EINVAL;
+    if (B <= 0 || C <= 0 || K <= 0 || B * C > (1LL << 31) - 1) return AVSE_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned rows = (unsigned)(B * C);
+    float2* ws = (float2*)workspace;
+    float* ws_a = (float*)(ws + B * C);
+    float2* smeans = (float2*)(ws_a + B * C);
+    hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, x, alpha,
+                       (const float2*)stats, dy, ws);
+    AVSE_CHECK_LAUNCH();
+    const unsigned cblocks = (unsigned)((C + 255) / 256);
+    hipLaunchKernelGGL(bwd_finalize, dim3((unsigned)B + cblocks), dim3(256), 0, st, (int)B, (int)C, (int)K, ws, gamma,
+                       smeans, dgamma, dbeta);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bwd_apply_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, x, alpha, gamma,
+                       (const float2*)stats, smeans, dy, dx, ws_a);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(alpha_finalize, dim3(1), dim3(256), 0, st, (int)rows, ws_a, dalpha);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+}  // extern "C"

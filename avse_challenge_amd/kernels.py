@@ -315,3 +315,64 @@ def prelu_bwd(x, a, dy):
     check(_lib.lib().avse_prelu_bwd(N, C, S, a.numel(), ptr(x), ptr(a.contiguous()), ptr(dy), ptr(dx), ptr(da), ptr(ws),
                                     stream_ptr(x.device)), "avse_prelu_bwd")
     return dx, da.view_as(a)
+
+
+# ------------------------------------------------------------------------ PReLU -> gLN (avse4)
+
+def prelu_gln_fwd(x, alpha, gamma, beta, eps=1e-8):
+    """gLN(PReLU(x)) on (B, C, K); returns (y, stats (B, 2) = mean, rstd)."""
+    _need_gpu(x, alpha, gamma, beta)
+    x = x.float().contiguous()
+    Bn, C, Kn = x.shape
+    y = torch.empty_like(x)
+    stats = torch.empty((Bn, 2), device=x.device, dtype=torch.float32)
+    L = _lib.lib()
+    ws = torch.empty((L.avse_prelu_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    check(L.avse_prelu_gln_fwd(Bn, C, Kn, ptr(x), ptr(alpha.float().contiguous()), ptr(gamma.float().contiguous()),
+                               ptr(beta.float().contiguous()), float(eps), ptr(y), ptr(stats), ptr(ws),
+                               stream_ptr(x.device)), "avse_prelu_gln_fwd")
+    return y, stats
+
+
+def prelu_gln_bwd(x, alpha, gamma, stats, dy):
+    _need_gpu(x, alpha, gamma, stats, dy)
+    x, dy = x.float().contiguous(), dy.float().contiguous()
+    Bn, C, Kn = x.shape
+    dx = torch.empty_like(x)
+    dalpha = torch.empty((1,), device=x.device, dtype=torch.float32)
+    dgamma = torch.empty((C,), device=x.device, dtype=torch.float32)
+    dbeta = torch.empty((C,), device=x.device, dtype=torch.float32)
+    L = _lib.lib()
+    ws = torch.empty((L.avse_prelu_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    check(L.avse_prelu_gln_bwd(Bn, C, Kn, ptr(x), ptr(alpha.float().contiguous()), ptr(gamma.float().contiguous()),
+                               ptr(stats), ptr(dy), ptr(dx), ptr(dalpha), ptr(dgamma), ptr(dbeta), ptr(ws),
+                               stream_ptr(x.device)), "avse_prelu_gln_bwd")
+    return dx, dalpha, dgamma, dbeta
+
+
+# ------------------------------------------------------------------------ depthwise dilated conv1d
+
+def dwconv_fwd(x, w, dilation):
+    _need_gpu(x, w)
+    x = x.float().contiguous()
+    Bn, C, Kn = x.shape
+    w2 = w.reshape(C, -1).float().contiguous()
+    y = torch.empty_like(x)
+    check(_lib.lib().avse_dwconv_fwd(Bn, C, Kn, w2.shape[1], int(dilation), ptr(x), ptr(w2), ptr(y),
+                                     stream_ptr(x.device)), "avse_dwconv_fwd")
+    return y
+
+
+def dwconv_bwd(x, w, dy, dilation):
+    _need_gpu(x, w, dy)
+    x, dy = x.float().contiguous(), dy.float().contiguous()
+    Bn, C, Kn = x.shape
+    w2 = w.reshape(C, -1).float().contiguous()
+    P = w2.shape[1]
+    dx = torch.empty_like(x)
+    dw = torch.empty((C, P), device=x.device, dtype=torch.float32)
+    L = _lib.lib()
+    ws = torch.empty((L.avse_dwconv_bwd_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    check(L.avse_dwconv_bwd(Bn, C, Kn, P, int(dilation), ptr(x), ptr(w2), ptr(dy), ptr(dx), ptr(dw), ptr(ws),
+                            stream_ptr(x.device)), "avse_dwconv_bwd")
+    return dx, dw.view_as(w)

@@ -1,5 +1,8 @@
 """nn.Module drop-ins whose hot halves run in libavse_hip.so (same parameter names as torch's).
 
+prelu_gln    fused PReLU -> GlobalLayerNorm (avse4 TCN) autograd op
+dwconv1d     depthwise dilated "same" conv1d autograd op (avse4 TCN / VisualConv1D)
+
 PReLU        nn.PReLU(num_parameters): fwd + fused dx / slope-gradient bwd kernels
 LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip front-ends:
              forward on MIOpen, weight gradient on the MFMA implicit-GEMM kernel (the lips are
@@ -62,3 +65,45 @@ class LipConv3d(nn.Conv3d):
 
     def forward(self, x):
         return _LipConv3dFn.apply(x, self.weight, tuple(self.stride), tuple(self.padding))
+
+
+class _PReluGLNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, alpha, gamma, beta, eps):
+        y, stats = K.prelu_gln_fwd(x, alpha, gamma.reshape(-1), beta.reshape(-1), eps)
+        ctx.save_for_backward(x, alpha, gamma, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, alpha, gamma, stats = ctx.saved_tensors
+        dx, da, dg, db = K.prelu_gln_bwd(x, alpha, gamma.reshape(-1), stats, dy)
+        return dx, da.view_as(alpha), dg.view_as(gamma), db.view_as(gamma), None
+
+
+def prelu_gln(x, alpha, gamma, beta, eps=1e-8):
+    """GlobalLayerNorm(PReLU(x)) for (B, C, K) fp32 GPU tensors (one PReLU slope)."""
+    if not x.is_cuda:
+        raise RuntimeError("prelu_gln runs on the GPU kernels only")
+    return _PReluGLNFn.apply(x, alpha, gamma, beta, eps)
+
+
+class _DWConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, dilation):
+        ctx.save_for_backward(x, w)
+        ctx.dilation = dilation
+        return K.dwconv_fwd(x, w, dilation)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx, dw = K.dwconv_bwd(x, w, dy, ctx.dilation)
+        return dx, dw, None
+
+
+def dwconv1d(x, w, dilation):
+    """Depthwise 'same' conv1d: w (C, 1, P), padding (P-1)/2*dilation, no bias."""
+    if not x.is_cuda:
+        raise RuntimeError("dwconv1d runs on the GPU kernels only")
+    return _DWConvFn.apply(x, w, dilation)

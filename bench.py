@@ -8,6 +8,8 @@ A step = one pass of the hot path over one batch, inputs already resident in HBM
   avse1 (default, C2): HIP STFT of the noisy + clean waveforms (B x 48000 @ 16 kHz)
           -> AVNet forward (75 lip frames 96x96 uint8) -> L1 loss -> backward -> Adam.
   mamba (C3):  Mamba-TasNet (XS/S/M/L) on B x 4 s @ 8 kHz mixtures -> PIT SI-SNR -> bwd -> Adam.
+  avse4 (C4):  binaural AVSE4BaselineModule on B x 2ch x 5 s @ 16 kHz + 125 lip frames 112x112
+               -> SI-SNR loss -> bwd -> Adam (C4 = global batch 16 over dp8 = 2 per GPU).
 Rank 0 prints ONE JSON line (plus "roofline" for the dominant kernel, timed live with HIP
 events on torch's current stream, and "cpu_baseline": the oracle restatement on host cores).
 """
@@ -33,7 +35,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba"])
+    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba", "avse4"])
     p.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the BASELINE config's)")
     p.add_argument("--size", default="L", choices=["XS", "S", "M", "L"], help="Mamba-TasNet size")
     p.add_argument("--lip-hw", type=int, default=96)
@@ -217,6 +219,87 @@ class MambaStep:
                           f"scaled x{n_layers} (forward only; the training step is >=3x slower)"}
 
 
+class Avse4Step:
+    unit_desc = "5s@16kHz binaural utterance + 125 lip frames"
+
+    def __init__(self, B, dev, rank, world):
+        from avse_challenge_amd import avse4, data
+        self.B = B
+        self.model = avse4.AVSE4BaselineModule(num_channels=2).to(dev).train()
+        self.ddp = self.model
+        if world > 1:
+            self.ddp = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=[dev.index],
+                                                                 bucket_cap_mb=64, gradient_as_bucket_view=True)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=self.model.lr)
+        self.batch = data.avse4_batch(B, dev, 777 + rank)
+        from avse_challenge_amd import losses
+        self.losses = losses
+
+    def __call__(self):
+        loss = self.losses.avse4_loss(self.batch["clean"], self.ddp(self.batch))
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        self.opt.step()
+        return loss
+
+    def config(self, world):
+        return {"workload": "avse4 binaural AV baseline train step (BASELINE configs[3]): ResNet18 lip encoder + "
+                            "Conv-TasNet TCN (8x4 blocks, fused PReLU/gLN, depthwise dilated conv) fwd/bwd + Adam",
+                "global_batch": self.B * world, "per_gpu_batch": self.B, "seq_len": 80000, "channels": 2,
+                "frames": 3999, "lip_frames": 125, "lip_hw": 112, "parallelism": f"dp{world}"}
+
+    def roofline(self, dev):
+        """HBM-bound TCN kernel at the step's shape: depthwise dilated conv1d fwd on (B, 512, 3999), dil 128.
+        Algorithmic bytes = read x + write y = 8 B per element."""
+        from avse_challenge_amd import kernels as K
+        x = torch.randn(self.B, 512, 3999, device=dev)
+        w = torch.randn(512, 1, 3, device=dev)
+        return _time_hbm(lambda: K.dwconv_fwd(x, w, 128), 8.0 * x.numel(),
+                         "avse_dwconv_fwd (depthwise dilated conv1d, H=512, K=3999, dil 128)")
+
+    def cpu_baseline(self):
+        from oracle import avse4_ref
+        torch.set_num_threads(max(1, min(len(os.sched_getaffinity(0)), 64)))
+        m = avse4_ref.AVSE4BaselineModule(num_channels=2).train()
+        opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+        g = torch.Generator().manual_seed(0)
+        batch = {"noisy_audio": 0.1 * torch.randn(1, 2, 80000, generator=g),
+                 "clean": 0.1 * torch.randn(1, 2, 80000, generator=g),
+                 "vis_feat": torch.rand(1, 1, 125, 112, 112, generator=g)}
+
+        def step():
+            loss = m.cal_loss(batch)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        step()
+        t0 = time.perf_counter()
+        iters = 0
+        while iters < 1 or (time.perf_counter() - t0 < 10.0 and iters < 4):
+            step()
+            iters += 1
+        dt = time.perf_counter() - t0
+        return {"value": round(iters / dt, 4), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
+                "sample": f"oracle/avse4_ref train step (fwd + bwd + Adam), batch 1, {iters} steps after 1 warm-up"}
+
+
+def _time_hbm(fn, byts, name, n=10):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    ach = byts / (ms * 1e-3) / 1e9
+    return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_ms": round(ms, 4),
+            "algorithmic_bytes_per_launch": byts}
+
+
 def heartbeat(rank, period=60.0):
     """Progress line every minute: the first step JIT-compiles MIOpen kernels on a fresh box (minutes)."""
     import threading
@@ -241,6 +324,9 @@ def main():
     if args.workload == "avse1":
         B = args.batch or 32
         step = Avse1Step(B, dev, rank, world, args.lip_hw)
+    elif args.workload == "avse4":
+        B = args.batch or 2
+        step = Avse4Step(B, dev, rank, world)
     else:
         B = args.batch or 64
         step = MambaStep(B, dev, rank, world, args.size)
@@ -274,7 +360,8 @@ def main():
         cpu = step.cpu_baseline()
     if rank == 0:
         value = world * B * args.steps / dt
-        rec = {"metric": METRIC if args.workload == "avse1" else "utterances/sec (4s@8kHz WSJ0-2mix, Mamba-TasNet)",
+        rec = {"metric": {"avse1": METRIC, "mamba": "utterances/sec (4s@8kHz WSJ0-2mix, Mamba-TasNet)",
+                          "avse4": "utterances/sec (5s@16kHz binaural + 125 lip frames, avse4)"}[args.workload],
                "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "fp32",

@@ -164,6 +164,28 @@ int64_t avse_prelu_bwd_workspace_bytes(int64_t N, int64_t C);
 int avse_prelu_bwd(int64_t N, int64_t C, int64_t S, int32_t num_params, const float* x, const float* a,
                    const float* dy, float* dx, float* da, float* workspace, avse_stream_t stream);
 
+/* ---------------------------------------------------------------- PReLU -> gLN (avse4) ----
+ * y = gLN(PReLU(x)) of baseline/avse4/model.py:259-266,284-292 (PReLU with one slope; gLN
+ * :225-252, EPS inside the sqrt).  x, y: (B, C, K) contiguous; gamma, beta: (C); stats: (B, 2)
+ * = (mean, rstd) written by fwd and read by bwd.  workspace: avse_prelu_gln_workspace_bytes.
+ */
+int64_t avse_prelu_gln_workspace_bytes(int64_t B, int64_t C);
+int avse_prelu_gln_fwd(int64_t B, int64_t C, int64_t K, const float* x, const float* alpha, const float* gamma,
+                       const float* beta, float eps, float* y, float* stats, float* workspace, avse_stream_t stream);
+int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const float* alpha, const float* gamma,
+                       const float* stats, const float* dy, float* dx, float* dalpha, float* dgamma, float* dbeta,
+                       float* workspace, avse_stream_t stream);
+
+/* ---------------------------------------------------------------- depthwise dilated conv1d --
+ * nn.Conv1d(C, C, P, padding=(P-1)/2*dil, dilation=dil, groups=C, bias=False) — avse4
+ * model.py:278-285 (TCN, dil 2^x) and :191-198 (VisualConv1D).  P in {1,3,5,7}, halo <= 512.
+ */
+int64_t avse_dwconv_bwd_workspace_bytes(int64_t B, int64_t C);
+int avse_dwconv_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w, float* y,
+                    avse_stream_t stream);
+int avse_dwconv_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
+                    const float* dy, float* dx, float* dw, float* workspace, avse_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

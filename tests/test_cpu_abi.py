@@ -105,3 +105,13 @@ def test_dropin_modules_resolve_reference_import_names():
         assert ln.RMSNorm(8, eps=1e-5).weight.shape == (8,)
     finally:
         sys.path.remove(path)
+
+
+def test_avse4_dropin_keys_match_oracle():
+    """The product avse4 module tree loads the reference's state_dict unchanged (keys and shapes)."""
+    from avse_challenge_amd import avse4
+    from oracle import avse4_ref
+    a = avse4.AVSE4BaselineModule(num_channels=2).state_dict()
+    b = avse4_ref.AVSE4BaselineModule(num_channels=2).state_dict()
+    assert list(a) == list(b)
+    assert all(a[k].shape == b[k].shape for k in a)

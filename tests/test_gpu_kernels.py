@@ -334,3 +334,55 @@ def test_encoder_decoder_framing_gemm_vs_golden():
     y64 = torch.nn.functional.conv_transpose1d(w64, dec.weight.detach().cpu().double(), stride=8)
     y64.sum().backward()
     close(mix.grad, mix64.grad, 1e-4, 1e-5, "d mix")
+
+
+# ------------------------------------------------------------------ avse4 TCN: fused PReLU->gLN, depthwise dilated conv1d
+
+@pytest.mark.parametrize("shape", [(2, 256, 300), (1, 512, 4001), (3, 8, 1), (2, 64, 2049)])
+def test_prelu_gln_vs_fp64(shape):
+    """gLN(PReLU(x)) of baseline/avse4/model.py:225-252 (eps 1e-8) vs the fp64 oracle; fwd + all grads."""
+    from avse_challenge_amd.layers import prelu_gln
+    from oracle.avse4_ref import GlobalLayerNorm
+    C = shape[1]
+    x = (1.5 * det_input(shape, 900) + 0.3).double().requires_grad_(True)
+    a = torch.tensor([0.25], dtype=torch.float64, requires_grad=True)
+    gln = GlobalLayerNorm(C).double()
+    with torch.no_grad():
+        gln.gamma.copy_(0.5 + torch.rand(1, C, 1, generator=torch.Generator().manual_seed(3)))
+        gln.beta.copy_(0.1 * det_input((1, C, 1), 901))
+    y = gln(torch.nn.functional.prelu(x, a))
+    gy = det_input(shape, 902).double()
+    y.backward(gy)
+    xg = x.detach().float().to(DEV).requires_grad_(True)
+    ag = a.detach().float().to(DEV).requires_grad_(True)
+    gg = gln.gamma.detach().float().to(DEV).requires_grad_(True)
+    bg = gln.beta.detach().float().to(DEV).requires_grad_(True)
+    yg = prelu_gln(xg, ag, gg, bg)
+    close(yg, y, 2e-5, 1e-5, "y")
+    yg.backward(gy.float().to(DEV))
+    n = shape[0] * shape[1] * shape[2]
+    close(xg.grad, x.grad, 2e-5 * max(1.0, float(x.grad.abs().max())), 1e-4, "dx")
+    close(ag.grad, a.grad, 1e-4 * max(1.0, float(a.grad.abs().max())) + 1e-7 * n, 1e-4, "dalpha")
+    close(gg.grad, gln.gamma.grad, 1e-4 * max(1.0, float(gln.gamma.grad.abs().max())), 1e-4, "dgamma")
+    close(bg.grad, gln.beta.grad, 1e-4 * max(1.0, float(gln.beta.grad.abs().max())), 1e-4, "dbeta")
+
+
+@pytest.mark.parametrize("B,C,Kn,P,dil", [(2, 256, 300, 3, 4), (1, 512, 4001, 3, 128), (2, 16, 5, 3, 8),
+                                           (3, 512, 75, 3, 1), (1, 7, 2500, 5, 3), (2, 4, 1, 7, 1),
+                                           (1, 64, 2048, 3, 1), (2, 32, 4099, 1, 1)])
+def test_dwconv_vs_fp64(B, C, Kn, P, dil):
+    """Depthwise dilated 'same' conv1d (model.py:278-285, :191-198) vs torch fp64 conv1d; fwd, dx, dw.
+    Covers K < halo, K = 1, K a multiple / non-multiple of the LDS tile, P in {1,3,5,7}."""
+    from avse_challenge_amd.layers import dwconv1d
+    x = det_input((B, C, Kn), 910).double().requires_grad_(True)
+    w = det_input((C, 1, P), 911).double().requires_grad_(True)
+    y = torch.nn.functional.conv1d(x, w, None, 1, (P - 1) // 2 * dil, dil, C)
+    gy = det_input((B, C, Kn), 912).double()
+    y.backward(gy)
+    xg = x.detach().float().to(DEV).requires_grad_(True)
+    wg = w.detach().float().to(DEV).requires_grad_(True)
+    yg = dwconv1d(xg, wg, dil)
+    close(yg, y, 1e-5, 1e-6, "y")
+    yg.backward(gy.float().to(DEV))
+    close(xg.grad, x.grad, 1e-5, 1e-6, "dx")
+    close(wg.grad, w.grad, 1e-6 * B * Kn + 1e-5, 1e-5, "dw")
