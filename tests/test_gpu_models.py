@@ -194,23 +194,63 @@ def test_avse4_full_golden():
         close(m.cal_loss(batch), g["loss"], 1e-3)
 
 
-def test_avse4_train_step_vs_oracle():
-    """Reduced avse4 (N=B=64, H=128, X=3, R=2) + visual front-end: loss and every gradient vs fp64 oracle."""
+def test_avse4_separator_train_step_vs_fp64():
+    """Reduced avse4 separator (N=B=64, H=128, X=3, R=2; every HIP op of the TCN) with a fixed visual
+    embedding: loss and every parameter gradient vs the fp64 oracle.  Tolerance per parameter: max error
+    relative to the fp64 gradient's max within 10x what the fp32 CPU oracle makes (floor 5e-4), cosine
+    > 1 - 1e-6.  (The visual front-end is MIOpen fp32; its own error is covered by the next test.)"""
+    from avse_challenge_amd import avse4
+    from avse_challenge_amd.losses import avse4_loss as loss_gpu
+    from oracle import avse4_ref
+    from oracle.losses_ref import avse4_loss
+    kw = dict(N=64, L=40, B=64, H=128, P=3, X=3, R=2, C=2, num_channels=2)
+    ours = det_init_(avse4.Separator(**kw), 62).to(DEV).train()
+    ref64 = det_init_(avse4_ref.Separator(**kw), 62).double().train()
+    ref32 = det_init_(avse4_ref.Separator(**kw), 62).train()
+    noisy, clean = 0.1 * det_input((2, 2, 8000), 621), 0.1 * det_input((2, 2, 8000), 622)
+    vis = det_input((2, 13, 512), 623)
+    loss = loss_gpu(clean.to(DEV), ours(noisy.to(DEV), vis.to(DEV)))
+    l64 = avse4_loss(clean.double(), ref64(noisy.double(), vis.double()))
+    l32 = avse4_loss(clean, ref32(noisy, vis))
+    close(loss, l64, 1e-4, 1e-5, "loss")
+    for l in (loss, l64, l32):
+        l.backward()
+    for (k, p), (_, q), (_, r) in zip(ours.named_parameters(), ref64.named_parameters(), ref32.named_parameters()):
+        scale = max(1e-6, float(q.grad.abs().max()))
+        e_gpu = float((p.grad.double().cpu() - q.grad).abs().max()) / scale
+        e_cpu = float((r.grad.double() - q.grad).abs().max()) / scale
+        cos = torch.nn.functional.cosine_similarity(p.grad.double().cpu().reshape(-1), q.grad.reshape(-1), 0)
+        assert e_gpu <= max(10 * e_cpu, 5e-4) and cos > 1 - 1e-6, (k, e_gpu, e_cpu, float(cos))
+
+
+def test_avse4_full_train_step_vs_oracle():
+    """Whole reduced AVSE4BaselineModule incl. the lip front-end: loss vs fp64; every gradient within the
+    error band of the stock PyTorch-ROCm fp32 run of the oracle on the same GPU (MIOpen convs of the
+    ResNet front-end dominate it): max rel error <= max(3x torch-GPU's, 1e-2), cosine > 1 - 1e-4."""
     from avse_challenge_amd import avse4
     from oracle import avse4_ref
+    from oracle.losses_ref import avse4_loss
     kw = dict(N=64, L=40, B=64, H=128, P=3, X=3, R=2, C=2)
     ours = det_init_(avse4.AVSE4BaselineModule(num_channels=2, **kw), 61).to(DEV).train()
-    ref = det_init_(avse4_ref.AVSE4BaselineModule(num_channels=2, **kw), 61).double().train()
-    assert list(dict(ours.named_parameters())) == list(dict(ref.named_parameters()))
+    tg = det_init_(avse4_ref.AVSE4BaselineModule(num_channels=2, **kw), 61).to(DEV).train()
+    ref64 = det_init_(avse4_ref.AVSE4BaselineModule(num_channels=2, **kw), 61).double().train()
+    assert list(dict(ours.named_parameters())) == list(dict(ref64.named_parameters()))
     batch = {"noisy_audio": 0.1 * det_input((2, 2, 8000), 611), "vis_feat": det_input((2, 1, 13, 112, 112), 612, "uniform"),
              "clean": 0.1 * det_input((2, 2, 8000), 613)}
-    loss = ours.training_step({k: v.to(DEV) for k, v in batch.items()})
-    lref = ref.cal_loss({k: v.double() for k, v in batch.items()})
-    close(loss, lref, 1e-3, 1e-4, "loss")
-    loss.backward()
-    lref.backward()
-    for (k, p), (_, q) in zip(ours.named_parameters(), ref.named_parameters()):
-        scale = max(1e-3, float(q.grad.abs().max()))
-        err = float((p.grad.double().cpu() - q.grad).abs().max()) / scale
+    bg = {k: v.to(DEV) for k, v in batch.items()}
+    loss = ours.training_step(bg)
+    lt = tg.cal_loss(bg)
+    b64 = {k: v.double() for k, v in batch.items()}      # forward() casts to fp32: call the parts in fp64
+    l64 = avse4_loss(b64["clean"], ref64.model(b64["noisy_audio"], ref64.visual_frontend(b64["vis_feat"])))
+    close(loss, l64, 1e-3, 1e-4, "loss")
+    for l in (loss, lt, l64):
+        l.backward()
+    for (k, p), (_, t), (_, q) in zip(ours.named_parameters(), tg.named_parameters(), ref64.named_parameters()):
+        if q.grad is None:                        # layer1.downsample: unused at stride 1 (utils.py:62)
+            assert p.grad is None, k
+            continue
+        scale = max(1e-6, float(q.grad.abs().max()))
+        e_gpu = float((p.grad.double().cpu() - q.grad).abs().max()) / scale
+        e_torch = float((t.grad.double().cpu() - q.grad).abs().max()) / scale
         cos = torch.nn.functional.cosine_similarity(p.grad.double().cpu().reshape(-1), q.grad.reshape(-1), 0)
-        assert err < 5e-3 and cos > 1 - 1e-5, (k, err, float(cos))
+        assert e_gpu <= max(3 * e_torch, 1e-2) and cos > 1 - 1e-4, (k, e_gpu, e_torch, float(cos))
