@@ -24,9 +24,51 @@ from .layers import LipConv3d, _PReLUFn, dwconv1d, prelu_gln
 NORM_MEAN, NORM_STD = 0.4161, 0.1688
 
 
+class _PointwiseFn(torch.autograd.Function):
+    """1x1 Conv1d without bias as batched GEMMs on the (B, C, K) layout, no layout copies:
+    y_b = W x_b;  dx_b = W^T dy_b;  dW = sum_b dy_b x_b^T (batched GEMM + a (B, Cout, Cin) sum)."""
+
+    @staticmethod
+    def forward(ctx, w, x):
+        ctx.save_for_backward(w, x)
+        return torch.bmm(w.expand(x.shape[0], *w.shape), x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        w, x = ctx.saved_tensors
+        dw = dx = None
+        if ctx.needs_input_grad[0]:
+            dw = torch.bmm(dy, x.transpose(1, 2)).sum(0)
+        if ctx.needs_input_grad[1]:
+            dx = torch.bmm(w.t().expand(dy.shape[0], w.shape[1], w.shape[0]), dy)
+        return dw, dx
+
+
 def _pw(conv, x):
-    """1x1 Conv1d without bias as a GEMM: (Cout, Cin) @ (B, Cin, K)."""
-    return torch.matmul(conv.weight[:, :, 0], x)
+    """1x1 Conv1d without bias: (Cout, Cin) @ (B, Cin, K)."""
+    return _PointwiseFn.apply(conv.weight[:, :, 0], x)
+
+
+_INTERP = {}
+
+
+def _upsample_matrix(n_in, up, n_out, device):
+    """(n_in, n_out) matrix M with v @ M == F.pad(F.interpolate(v, up * n_in, mode='linear'), (0, n_out - up*n_in)):
+    align_corners=False source coordinate (j + 0.5) / up - 0.5 clamped at 0 (model.py:166-168).  Two non-zeros
+    per column whose weights are multiples of 1/up, so the GEMM reproduces the interpolation exactly."""
+    key = (n_in, up, n_out, device)
+    if key not in _INTERP:
+        m = torch.zeros(n_in, n_out, dtype=torch.float64)
+        j = torch.arange(min(n_out, up * n_in), dtype=torch.float64)
+        src = ((j + 0.5) / up - 0.5).clamp(min=0.0)
+        i0 = src.floor().long()
+        lam = src - i0
+        i1 = (i0 + 1).clamp(max=n_in - 1)
+        cols = j.long()
+        m.index_put_((i0, cols), 1.0 - lam, accumulate=True)
+        m.index_put_((i1, cols), lam, accumulate=True)
+        _INTERP[key] = m.float().to(device)
+    return _INTERP[key]
 
 
 class GlobalLayerNorm(nn.Module):
@@ -104,8 +146,7 @@ class TemporalConvNet(nn.Module):
         bsz, Bc, K = x.shape
         for i in range(len(self.tcn)):
             v = _pw(self.ve_conv1x1[i], visual)
-            v = F.interpolate(v, self.up * v.shape[-1], mode="linear")
-            v = F.pad(v, (0, K - v.shape[-1]))
+            v = torch.matmul(v, _upsample_matrix(v.shape[-1], self.up, K, v.device))   # interpolate x32 + pad
             seq = self.tcn[i]
             x = _pw(seq[0], torch.cat((x, v), 1))
             for blk in list(seq)[1:]:

@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--lip-hw", type=int, default=96)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-graph", action="store_true", help="eager launches instead of captured HIP graphs")
     return p.parse_args()
 
 
@@ -68,23 +69,14 @@ class Avse1Step:
         from avse_challenge_amd import avse1, data
         self.B, self.lip_hw = B, lip_hw
         self.model = avse1.AVNet().to(dev).train()
-        self.ddp = self.model
-        if world > 1:
-            self.ddp = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=[dev.index],
-                                                                 bucket_cap_mb=64, gradient_as_bucket_view=True)
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=self.model.lr)
+        self.lr, self.clip = self.model.lr, None
         self.noisy, self.clean, self.lips = data.avse1_batch(B, dev, 1234 + rank, lip_hw)
         self.avse1 = avse1
 
-    def __call__(self):
+    def loss(self):
         batch = self.avse1.AVNet.features_from_waves(self.noisy, self.clean)
         batch["lip_images"] = self.lips
-        pred = self.ddp(batch)
-        loss = self.model.loss(pred, batch["mask"])
-        self.opt.zero_grad(set_to_none=True)
-        loss.backward()
-        self.opt.step()
-        return loss
+        return self.model.loss(self.model(batch), batch["mask"])
 
     def config(self, world):
         return {"workload": "avse1 AV baseline train step (BASELINE configs[1]): HIP STFT front-end + AVNet "
@@ -153,22 +145,12 @@ class MambaStep:
         from avse_challenge_amd import data, losses, mamba_tasnet
         self.B, self.size = B, size
         self.model = mamba_tasnet.MambaTasNet(**mamba_tasnet.MAMBA_TASNET_SIZES[size]).to(dev).train()
-        self.ddp = self.model
-        if world > 1:
-            self.ddp = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=[dev.index],
-                                                                 bucket_cap_mb=64, gradient_as_bucket_view=True)
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=1.5e-4)
+        self.lr, self.clip = 1.5e-4, 5.0
         self.mix, self.tgt = data.wsj0mix_batch(B, dev, 4321 + rank)
         self.losses = losses
 
-    def __call__(self):
-        est = self.ddp(self.mix)
-        loss = self.losses.si_snr_pit(self.tgt, est).mean()
-        self.opt.zero_grad(set_to_none=True)
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(self.model.parameters(), 5.0)
-        self.opt.step()
-        return loss
+    def loss(self):
+        return self.losses.si_snr_pit(self.tgt, self.model(self.mix)).mean()
 
     def config(self, world):
         return {"workload": f"Mamba-TasNet-{self.size} train step (BASELINE configs[2])", "global_batch": self.B * world,
@@ -226,21 +208,11 @@ class Avse4Step:
         from avse_challenge_amd import avse4, data
         self.B = B
         self.model = avse4.AVSE4BaselineModule(num_channels=2).to(dev).train()
-        self.ddp = self.model
-        if world > 1:
-            self.ddp = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=[dev.index],
-                                                                 bucket_cap_mb=64, gradient_as_bucket_view=True)
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=self.model.lr)
+        self.lr, self.clip = self.model.lr, None
         self.batch = data.avse4_batch(B, dev, 777 + rank)
-        from avse_challenge_amd import losses
-        self.losses = losses
 
-    def __call__(self):
-        loss = self.losses.avse4_loss(self.batch["clean"], self.ddp(self.batch))
-        self.opt.zero_grad(set_to_none=True)
-        loss.backward()
-        self.opt.step()
-        return loss
+    def loss(self):
+        return self.model.training_step(self.batch)
 
     def config(self, world):
         return {"workload": "avse4 binaural AV baseline train step (BASELINE configs[3]): ResNet18 lip encoder + "
@@ -281,6 +253,77 @@ class Avse4Step:
         dt = time.perf_counter() - t0
         return {"value": round(iters / dt, 4), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
                 "sample": f"oracle/avse4_ref train step (fwd + bwd + Adam), batch 1, {iters} steps after 1 warm-up"}
+
+
+class Trainer:
+    """One training step = forward + loss + backward (+ gradient all-reduce over RCCL when N > 1)
+    + optional grad-norm clip + Adam.  Gradients live in ONE flat fp32 buffer (param.grad are views):
+    the data-parallel exchange is a single large all-reduce of it (ring over xGMI), and with
+    --graph (default) the launch-bound forward/backward and the optimizer are each replayed as a
+    captured HIP graph; the collective stays outside the graphs."""
+
+    def __init__(self, step, world, dev, use_graph):
+        self.step, self.world, self.use_graph = step, world, use_graph
+        self.params = [p for p in step.model.parameters() if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(n, device=dev)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        if world > 1:                      # identical initial weights on every rank (DDP semantics)
+            for p in step.model.parameters():
+                dist.broadcast(p.data, 0)
+            for b in step.model.buffers():
+                dist.broadcast(b, 0)
+        self.opt = torch.optim.Adam(self.params, lr=step.lr, capturable=use_graph, foreach=True)
+        self.g_fb = self.g_opt = None
+        self.loss = None
+
+    def _fwd_bwd(self):
+        self.flat.zero_()
+        loss = self.step.loss()
+        loss.backward()
+        return loss.detach()
+
+    def _opt(self):
+        if self.world > 1:
+            self.flat.mul_(1.0 / self.world)
+        if self.step.clip is not None:
+            torch.nn.utils.clip_grad_norm_(self.params, self.step.clip, foreach=True)
+        self.opt.step()
+
+    def _allreduce(self):
+        if self.world > 1:
+            dist.all_reduce(self.flat)
+
+    def eager(self):
+        self.loss = self._fwd_bwd()
+        self._allreduce()
+        self._opt()
+        return self.loss
+
+    def capture(self):
+        """Capture after eager warm-up (lazy MIOpen / hipBLASLt / Adam-state init done)."""
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.g_fb, self.g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_fb, stream=s):
+                self.loss = self._fwd_bwd()
+            with torch.cuda.graph(self.g_opt, stream=s):
+                self._opt()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+
+    def __call__(self):
+        if self.g_fb is None:
+            return self.eager()
+        self.g_fb.replay()
+        self._allreduce()
+        self.g_opt.replay()
+        return self.loss
 
 
 def _time_hbm(fn, byts, name, n=10):
@@ -331,18 +374,37 @@ def main():
         B = args.batch or 64
         step = MambaStep(B, dev, rank, world, args.size)
 
-    for i in range(args.warmup):
+    work = step
+    step = Trainer(work, world, dev, use_graph=not args.no_graph)
+    for i in range(max(args.warmup, 1 if not args.no_graph else 0)):
         t = time.perf_counter()
         step()
         torch.cuda.synchronize()
         if rank == 0:
             print(f"[bench] warmup {i + 1}/{args.warmup}: {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
+    graph = False
+    if not args.no_graph:
+        try:
+            step.capture()
+            step()
+            torch.cuda.synchronize()
+            graph = True
+        except Exception as e:      # noqa: BLE001 - report and fall back to eager launches
+            print(f"[bench] HIP graph capture failed ({type(e).__name__}: {e}); eager launches", file=sys.stderr,
+                  flush=True)
+            step.g_fb = step.g_opt = None
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
+    mark = bool(int(os.environ.get("AVSE_PROFILE_MARK", "0")))   # tools/ktrace_window.py brackets the timed steps
+    if mark:
+        torch.cuda._sleep(1000)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+    if mark:
+        torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -354,10 +416,10 @@ def main():
     if not torch.isfinite(loss.detach()).all():
         raise RuntimeError("non-finite loss in the timed region")
 
-    roof = None if args.no_roofline or rank != 0 else step.roofline(dev)
+    roof = None if args.no_roofline or rank != 0 else work.roofline(dev)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = step.cpu_baseline()
+        cpu = work.cpu_baseline()
     if rank == 0:
         value = world * B * args.steps / dt
         rec = {"metric": {"avse1": METRIC, "mamba": "utterances/sec (4s@8kHz WSJ0-2mix, Mamba-TasNet)",
@@ -367,7 +429,7 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (speech-like noise with 4 Hz envelope at SNR {0,3,6,9} dB, uint8 lips; "
                        "random-init weights)",
-               "config": {**step.config(world), "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)},
+               "config": {**work.config(world), "hip_graph": graph, "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)},
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(rec), flush=True)
     if world > 1:

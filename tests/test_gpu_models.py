@@ -254,3 +254,37 @@ def test_avse4_full_train_step_vs_oracle():
         e_torch = float((t.grad.double().cpu() - q.grad).abs().max()) / scale
         cos = torch.nn.functional.cosine_similarity(p.grad.double().cpu().reshape(-1), q.grad.reshape(-1), 0)
         assert e_gpu <= max(3 * e_torch, 1e-2) and cos > 1 - 1e-4, (k, e_gpu, e_torch, float(cos))
+
+
+def test_bench_trainer_graph_replay_equals_eager():
+    """bench.Trainer: a step replayed from the captured HIP graphs == the same step launched eagerly."""
+    import bench
+    from avse_challenge_amd import avse4
+    from avse_challenge_amd.losses import avse4_loss
+
+    class Step:
+        def __init__(self):
+            kw = dict(N=64, L=40, B=64, H=128, P=3, X=3, R=2, C=2, num_channels=2)
+            self.model = det_init_(avse4.Separator(**kw), 71).to(DEV).train()
+            self.lr, self.clip = 1e-3, 5.0
+            self.noisy = (0.1 * det_input((2, 2, 8000), 711)).to(DEV)
+            self.clean = (0.1 * det_input((2, 2, 8000), 712)).to(DEV)
+            self.vis = det_input((2, 13, 512), 713).to(DEV)
+
+        def loss(self):
+            return avse4_loss(self.clean, self.model(self.noisy, self.vis))
+
+    runs = []
+    for graph in (False, True):
+        st = Step()
+        tr = bench.Trainer(st, 1, torch.device(DEV), use_graph=True)
+        losses = [float(tr())]                    # eager warm-up step (lazy init)
+        if graph:
+            tr.capture()
+        for _ in range(3):
+            losses.append(float(tr()))
+        runs.append((losses, [p.detach().clone() for p in st.model.parameters()]))
+    (l0, p0), (l1, p1) = runs
+    np.testing.assert_allclose(l1, l0, rtol=1e-5, atol=1e-6)
+    for a, b in zip(p0, p1):
+        close(b, a, 1e-5, 1e-5)
