@@ -2,10 +2,23 @@
 
 Hand-written gfx950 HIP kernels (libavse_hip.so, C ABI in include/avse_hip.h) behind the
 reference's operator / module surfaces:
-  kernels        torch wrappers of the C ABI (selective scan, causal conv1d, add+RMSNorm, STFT/iSTFT)
+  kernels        torch wrappers of the C ABI (selective scan, causal conv1d, add+RMSNorm, STFT/iSTFT,
+                 lip Conv3d weight gradient, PReLU, fused PReLU+gLN, depthwise dilated conv1d)
+  layers         autograd modules over those kernels (PReLU, LipConv3d, prelu_gln, dwconv1d)
   dropin         importable stand-ins for selective_scan_cuda / causal_conv1d(_cuda) / mamba_ssm
   mamba_tasnet   Mamba-TasNet separator (Encoder, MaskNet of BiMamba v2 blocks, Decoder)
   avse1          avse1 AVNet with the STFT front-end / iSTFT back-end on the GPU
+  avse4          avse4 binaural AVSE4BaselineModule (TCN on the fused HIP kernels)
   losses, data   SI-SNR / PIT objectives; synthetic GPU-resident batches
+
+miopen_db/ holds MIOpen find-db records (plain text, measured on MI355X with this image's MIOpen) for
+the library convolutions the models keep on MIOpen.  Without them MIOpen's immediate mode evaluates
+every candidate solver, naive ones included, on the first call of each shape: ~280 s for the avse1
+B=32 step on a fresh box, vs ~8 s with the records.
 """
+import os
+
+MIOPEN_DB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
+os.environ.setdefault("MIOPEN_USER_DB_PATH", MIOPEN_DB)     # read by MIOpen at handle creation
+
 __version__ = "0.1.0"

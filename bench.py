@@ -24,6 +24,7 @@ import torch.distributed as dist
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
+import avse_challenge_amd  # noqa: E402,F401  (sets MIOPEN_USER_DB_PATH before the first convolution)
 
 METRIC = "utterances/sec (3s@16kHz + 75 lip frames)"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
@@ -64,6 +65,9 @@ def barrier(world):
 
 class Avse1Step:
     unit_desc = "3s@16kHz utterance + 75 lip frames"
+    # MIOpen's LSTM (FusionNet) issues hipBLASLt calls that are illegal under stream capture, and the
+    # step is kernel-bound at B=32 anyway: avse1 runs with eager launches.
+    graph_ok = False
 
     def __init__(self, B, dev, rank, world, lip_hw):
         from avse_challenge_amd import avse1, data
@@ -140,6 +144,7 @@ class Avse1Step:
 
 class MambaStep:
     unit_desc = "4s@8kHz WSJ0-2mix utterance"
+    graph_ok = True
 
     def __init__(self, B, dev, rank, world, size):
         from avse_challenge_amd import data, losses, mamba_tasnet
@@ -203,6 +208,7 @@ class MambaStep:
 
 class Avse4Step:
     unit_desc = "5s@16kHz binaural utterance + 125 lip frames"
+    graph_ok = True
 
     def __init__(self, B, dev, rank, world):
         from avse_challenge_amd import avse4, data
@@ -375,15 +381,16 @@ def main():
         step = MambaStep(B, dev, rank, world, args.size)
 
     work = step
-    step = Trainer(work, world, dev, use_graph=not args.no_graph)
-    for i in range(max(args.warmup, 1 if not args.no_graph else 0)):
+    use_graph = work.graph_ok and not args.no_graph
+    step = Trainer(work, world, dev, use_graph=use_graph)
+    for i in range(max(args.warmup, 1 if use_graph else 0)):
         t = time.perf_counter()
         step()
         torch.cuda.synchronize()
         if rank == 0:
             print(f"[bench] warmup {i + 1}/{args.warmup}: {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
     graph = False
-    if not args.no_graph:
+    if use_graph:
         try:
             step.capture()
             step()

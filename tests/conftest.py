@@ -7,6 +7,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
+import avse_challenge_amd  # noqa: E402,F401  (MIOpen find-db path, before any convolution)
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
