@@ -237,7 +237,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
             const auto ro = make_rsrc((Tin*)a.out + b * a.out_bs + (int64_t)d0 * a.out_ds,
                                       (int64_t)(nrow - 1) * a.out_ds + L);
             const int vo = wave * (int)a.out_ds + tpos(t0 + lane, L, rev);
-            if (lane < tn) {
+            if (a.out && lane < tn) {      // out is optional when z is given (training fwd: the bwd recomputes it)
 #pragma unroll
                 for (int i = 0; i < RPT; ++i)
                     if (wave + 4 * i < nrow) bufst<Tin>::st(ro, vo, 4 * i * (int)a.out_ds, s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]);
@@ -631,8 +631,8 @@ static int check_common(int64_t batch, int64_t dim, int64_t seqlen, int64_t dsta
 }
 
 int avse_scan_fwd(const avse_scan_fwd_args* a, avse_stream_t stream) {
-    if (!a || !a->u || !a->delta || !a->A || !a->B || !a->C || !a->out || !a->x) return AVSE_EINVAL;
-    if (a->z && !a->out_z) return AVSE_EINVAL;
+    if (!a || !a->u || !a->delta || !a->A || !a->B || !a->C || !a->x) return AVSE_EINVAL;
+    if (a->z ? !a->out_z : !a->out) return AVSE_EINVAL;
     int rc = check_common(a->batch, a->dim, a->seqlen, a->dstate, a->in_dtype);
     if (rc) return rc;
     const int nblk_d = (int)((a->dim + CPB - 1) / CPB);

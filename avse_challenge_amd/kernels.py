@@ -41,9 +41,12 @@ def _bc4(M, dtype):
 
 # ------------------------------------------------------------------------ selective scan
 
-def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False, reverse=False):
+def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False, reverse=False,
+                       return_out=True):
     """Returns (out, x, out_z|None) — the selective_scan_cuda.fwd contract.
-    reverse=True scans time backwards (== flip(scan(flip(inputs))) with no flip copies)."""
+    reverse=True scans time backwards (== flip(scan(flip(inputs))) with no flip copies).
+    return_out=False (only with z): skip writing the pre-gate ``out`` (returned as None); the
+    backward recomputes it, so training saves one (b, d, l) write and its activation memory."""
     _need_gpu(u, delta, A, B, C, D, z, delta_bias)
     u = _last_contig(u)
     dt = u.dtype
@@ -58,7 +61,9 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
     delta_bias = None if delta_bias is None else delta_bias.float().contiguous()
     L = _lib.lib()
     nck = L.avse_scan_n_chunks(l)
-    out = torch.empty((b, d, l), device=u.device, dtype=dt)
+    if not return_out and z is None:
+        raise RuntimeError("return_out=False needs z (the gated output is then the only result)")
+    out = torch.empty((b, d, l), device=u.device, dtype=dt) if return_out else None
     x = torch.empty((b, d, nck, 2 * NSTATE), device=u.device, dtype=torch.float32)
     out_z = torch.empty((b, d, l), device=u.device, dtype=dt) if z is not None else None
     a = ScanFwdArgs()
@@ -74,7 +79,8 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
         a.z, a.z_bs, a.z_ds = z.data_ptr(), z.stride(0), z.stride(1)
         a.out_z, a.out_z_bs, a.out_z_ds = out_z.data_ptr(), out_z.stride(0), out_z.stride(1)
     a.delta_bias = delta_bias.data_ptr() if delta_bias is not None else None
-    a.out, a.out_bs, a.out_ds = out.data_ptr(), out.stride(0), out.stride(1)
+    if out is not None:
+        a.out, a.out_bs, a.out_ds = out.data_ptr(), out.stride(0), out.stride(1)
     a.x = x.data_ptr()
     check(L.avse_scan_fwd(a, stream_ptr(u.device)), "avse_scan_fwd")
     return out, x, out_z

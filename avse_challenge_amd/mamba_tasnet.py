@@ -38,14 +38,17 @@ class MambaInnerNoOutProj(torch.autograd.Function):
         delta = torch.matmul(dt_proj_w, x_dbl[..., :R].transpose(1, 2))          # (b, d, l)
         Bm = x_dbl[..., R:R + NSTATE].transpose(1, 2).contiguous()               # (b, n, l)
         Cm = x_dbl[..., R + NSTATE:].transpose(1, 2).contiguous()
-        out, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, dt_bias, True, reverse=reverse)
-        ctx.save_for_backward(xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck, out)
+        # the pre-gate `out` is neither written nor saved (the reference saves it, :212): the scan
+        # backward recomputes y + D u per step anyway, so it only cost HBM traffic and memory
+        _, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, dt_bias, True, reverse=reverse,
+                                             return_out=False)
+        ctx.save_for_backward(xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck)
         ctx.reverse = reverse
         return out_z
 
     @staticmethod
     def backward(ctx, dout):
-        xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck, out = ctx.saved_tensors
+        xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck = ctx.saved_tensors
         rev = ctx.reverse
         R = dt_proj_w.shape[1]
         x, z = xz.chunk(2, dim=1)
@@ -54,7 +57,7 @@ class MambaInnerNoOutProj(torch.autograd.Function):
         dxz = torch.empty_like(xz)
         dx, dz = dxz.chunk(2, dim=1)
         dconv, ddelta, dA, dB, dC, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
-            conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, out, dz, True, False, reverse=rev)
+            conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, None, dz, True, False, reverse=rev)
         dx_dbl = torch.empty_like(x_dbl)
         dx_dbl[..., R:R + NSTATE] = dB[:, 0].transpose(1, 2)
         dx_dbl[..., R + NSTATE:] = dC[:, 0].transpose(1, 2)

@@ -56,7 +56,7 @@ typedef struct {
     const float* D;                                  /* (d) or NULL */
     const void* z;      int64_t z_bs, z_ds;          /* NULL = no gating */
     const float* delta_bias;                         /* (d) or NULL */
-    void* out;          int64_t out_bs, out_ds;      /* y + D*u (before gating) */
+    void* out;          int64_t out_bs, out_ds;      /* y + D*u (before gating); may be NULL when z is given (bwd recomputes it) */
     float* x;                                        /* (b, d, n_chunks, 2n) contiguous */
     void* out_z;        int64_t out_z_bs, out_z_ds;  /* out * silu(z); ignored when z == NULL */
 } avse_scan_fwd_args;

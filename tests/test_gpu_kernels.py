@@ -386,3 +386,13 @@ def test_dwconv_vs_fp64(B, C, Kn, P, dil):
     yg.backward(gy.float().to(DEV))
     close(xg.grad, x.grad, 1e-5, 1e-6, "dx")
     close(wg.grad, w.grad, 1e-6 * B * Kn + 1e-5, 1e-5, "dw")
+
+
+def test_scan_fwd_without_out_matches():
+    """return_out=False (training fwd, pre-gate out not written) gives the same out_z / checkpoints."""
+    g = load_golden("scan_fp32")
+    ins = {k: g2t(g[k]) for k in ("u", "delta", "A", "B", "C", "D", "z", "delta_bias")}
+    out, x, oz = K().selective_scan_fwd(**ins, delta_softplus=True)
+    out2, x2, oz2 = K().selective_scan_fwd(**ins, delta_softplus=True, return_out=False)
+    assert out2 is None
+    assert torch.equal(oz, oz2) and torch.equal(x, x2)
