@@ -87,9 +87,11 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
 
 
 def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, dz=None,
-                       delta_softplus=False, recompute_out_z=False, reverse=False):
+                       delta_softplus=False, recompute_out_z=False, reverse=False, dB_out=None, dC_out=None):
     """Returns [du, ddelta, dA, dB, dC, dD, ddelta_bias, dz, out_z] — selective_scan_cuda.bwd contract.
-    dB, dC are fp32 shaped (b, 1, n, l); a passed-in ``dz`` view is written in place."""
+    dB, dC are fp32 shaped (b, 1, n, l); a passed-in ``dz`` view is written in place, and so are
+    ``dB_out`` / ``dC_out`` (fp32 (b, n, l) or (b, 1, n, l) views with unit last stride, e.g. rows of
+    the x_proj output gradient), which are then returned as dB / dC."""
     _need_gpu(u, delta, A, B, C, D, z, delta_bias, dout, x)
     u = _last_contig(u)
     dt = u.dtype
@@ -109,8 +111,14 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
     du = torch.empty((b, d, l), device=dev, dtype=dt)
     ddelta = torch.empty((b, d, l), device=dev, dtype=dt)
     dA = torch.empty((d, NSTATE), device=dev, dtype=torch.float32)
-    dB = torch.empty((b, 1, NSTATE, l), device=dev, dtype=torch.float32)
-    dC = torch.empty((b, 1, NSTATE, l), device=dev, dtype=torch.float32)
+    def _grad_bc(o):
+        if o is None:
+            return torch.empty((b, 1, NSTATE, l), device=dev, dtype=torch.float32)
+        o = o.unsqueeze(1) if o.dim() == 3 else o
+        if o.dtype != torch.float32 or o.stride(-1) != 1 or tuple(o.shape) != (b, 1, NSTATE, l):
+            raise RuntimeError("dB_out / dC_out must be fp32 (b, [1,] n, l) views with unit last stride")
+        return o
+    dB, dC = _grad_bc(dB_out), _grad_bc(dC_out)
     dD = torch.empty((d,), device=dev, dtype=torch.float32) if D is not None else None
     dbias = torch.empty((d,), device=dev, dtype=torch.float32) if delta_bias is not None else None
     if z is not None:

@@ -22,51 +22,98 @@ from . import kernels as K
 NSTATE = 16
 
 
+def _wbmm(w, x):
+    """(m, k) weight @ (b, k, n) -> (b, m, n) as one strided-batched GEMM (weight batch stride 0).
+    Keeping every projection in the scan's (b, channels, l) layout means no layout copies."""
+    return torch.bmm(w.expand(x.shape[0], *w.shape), x)
+
+
 class MambaInnerNoOutProj(torch.autograd.Function):
     """Conv1d(k4)+SiLU -> x_proj -> dt_proj -> selective scan (z-gated); checkpoint_lvl 1.
 
+    The x_proj output is kept transposed, x_dblT = W_x conv_out of shape (b, R + 2n, l): delta,
+    B and C are then row slices in the scan's layout (the reference builds x_dbl as (b*l, R+2n)
+    and rearranges, :180-197); every forward / backward GEMM is a strided-batched GEMM on the
+    (b, channels, l) layout, so no (b, d, l) tensor is ever transposed in memory.
+
     ``reverse=True`` is the v2 backward direction WITHOUT the two flip copies of bimamba.py:236,253:
     the conv and the scan walk time backwards by index, so the result is already the reference's
-    ``out_b.flip(-1)`` in natural time order (x_dbl / delta / B / C stay in natural order too)."""
+    ``out_b.flip(-1)`` in natural time order."""
 
     @staticmethod
     def forward(ctx, xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias, reverse=False):
         R = dt_proj_w.shape[1]
         x, z = xz.chunk(2, dim=1)
         conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=reverse)     # (b, d, l)
-        x_dbl = torch.matmul(conv_out.transpose(1, 2), x_proj_w.t())             # (b, l, R + 2n)
-        delta = torch.matmul(dt_proj_w, x_dbl[..., :R].transpose(1, 2))          # (b, d, l)
-        Bm = x_dbl[..., R:R + NSTATE].transpose(1, 2).contiguous()               # (b, n, l)
-        Cm = x_dbl[..., R + NSTATE:].transpose(1, 2).contiguous()
+        x_dblT = _wbmm(x_proj_w, conv_out)                                       # (b, R + 2n, l)
+        delta = _wbmm(dt_proj_w, x_dblT[:, :R])                                  # (b, d, l)
+        Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]                 # (b, n, l) views
         # the pre-gate `out` is neither written nor saved (the reference saves it, :212): the scan
         # backward recomputes y + D u per step anyway, so it only cost HBM traffic and memory
         _, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, dt_bias, True, reverse=reverse,
                                              return_out=False)
-        ctx.save_for_backward(xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck)
+        ctx.save_for_backward(xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck)
         ctx.reverse = reverse
         return out_z
 
     @staticmethod
     def backward(ctx, dout):
-        xz, conv_w, conv_b, x_dbl, x_proj_w, dt_proj_w, A, Bm, Cm, D, dt_bias, xck = ctx.saved_tensors
+        xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck = ctx.saved_tensors
         rev = ctx.reverse
         R = dt_proj_w.shape[1]
         x, z = xz.chunk(2, dim=1)
         conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=rev)
-        delta = torch.matmul(dt_proj_w, x_dbl[..., :R].transpose(1, 2))
+        delta = _wbmm(dt_proj_w, x_dblT[:, :R])
+        Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]
         dxz = torch.empty_like(xz)
         dx, dz = dxz.chunk(2, dim=1)
-        dconv, ddelta, dA, dB, dC, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
-            conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, None, dz, True, False, reverse=rev)
-        dx_dbl = torch.empty_like(x_dbl)
-        dx_dbl[..., R:R + NSTATE] = dB[:, 0].transpose(1, 2)
-        dx_dbl[..., R + NSTATE:] = dC[:, 0].transpose(1, 2)
-        ddt_proj_w = torch.einsum("bdl,blr->dr", ddelta, x_dbl[..., :R])
-        dx_dbl[..., :R] = torch.matmul(ddelta.transpose(1, 2), dt_proj_w)
-        dx_proj_w = torch.einsum("blk,bdl->kd", dx_dbl, conv_out)
-        dconv = dconv + torch.matmul(x_proj_w.t(), dx_dbl.transpose(1, 2))
+        dx_dblT = torch.empty_like(x_dblT)
+        dconv, ddelta, dA, _, _, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
+            conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, None, dz, True, False, reverse=rev,
+            dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:])
+        dx_dblT[:, :R] = _wbmm(dt_proj_w.t(), ddelta)
+        ddt_proj_w = torch.bmm(ddelta, x_dblT[:, :R].transpose(1, 2)).sum(0)     # (d, R)
+        dx_proj_w = torch.bmm(dx_dblT, conv_out.transpose(1, 2)).sum(0)          # (R + 2n, d)
+        dconv.baddbmm_(x_proj_w.t().expand(dconv.shape[0], *x_proj_w.t().shape), dx_dblT)
         _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True, reverse=rev)
         return (dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias, None)
+
+
+class _InProj(torch.autograd.Function):
+    """xz = W_in h^T: (b, l, d_model) -> (b, 2 d_inner, l) (bimamba.py:192-196); grads in the
+    layouts their consumers want: dh (b, l, d_model) contiguous, no transposed copies."""
+
+    @staticmethod
+    def forward(ctx, h, w):
+        ctx.save_for_backward(h, w)
+        return _wbmm(w, h.transpose(1, 2))
+
+    @staticmethod
+    def backward(ctx, dxz):
+        h, w = ctx.saved_tensors
+        dh = torch.bmm(dxz.transpose(1, 2), w.expand(dxz.shape[0], *w.shape))
+        dw = torch.bmm(dxz, h).sum(0)
+        return dh, dw
+
+
+class _BiOutProj(torch.autograd.Function):
+    """out = (0.5 f + 0.5 b)^T W_out^T for the two v2 directions (bimamba.py:253, flip-free):
+    (b, d_inner, l) x 2 -> (b, l, d_model).  One add in the forward; the backward hands the same
+    (b, d_inner, l) gradient to both directions (no 0.5-scaled copies)."""
+
+    @staticmethod
+    def forward(ctx, f, bk, w):
+        y = f + bk
+        ctx.save_for_backward(y, w)
+        wt = 0.5 * w.t()
+        return torch.bmm(y.transpose(1, 2), wt.expand(y.shape[0], *wt.shape))
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, w = ctx.saved_tensors
+        dy = _wbmm(0.5 * w.t(), dout.transpose(1, 2))                            # (b, d_inner, l)
+        dw = 0.5 * torch.bmm(dout.transpose(1, 2), y.transpose(1, 2)).sum(0)     # (d_model, d_inner)
+        return dy, dy, dw
 
 
 class AddRMSNorm(torch.autograd.Function):
@@ -128,15 +175,15 @@ class BiMambaV2(nn.Module):
                 proj.bias.copy_(dt + torch.log(-torch.expm1(-dt)))
 
     def forward(self, h):                                        # (b, l, d_model)
-        xz = torch.matmul(self.in_proj.weight, h.transpose(1, 2))                # (b, 2di, l)
+        xz = _InProj.apply(h, self.in_proj.weight)                               # (b, 2di, l), no copy
         A = -torch.exp(self.A_log.float())
         A_b = -torch.exp(self.A_b_log.float())
         f = MambaInnerNoOutProj.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
                                       self.dt_proj.weight, A, self.D.float(), self.dt_proj.bias.float())
         bk = MambaInnerNoOutProj.apply(xz, self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
                                        self.dt_proj_b.weight, A_b, self.D_b.float(), self.dt_proj_b.bias.float(), True)
-        y = 0.5 * (f + bk)          # == 0.5*out + 0.5*out_b.flip(-1) of bimamba.py:253, flip-free
-        return F.linear(y.transpose(1, 2), self.out_proj.weight)
+        # == out_proj(0.5*out + 0.5*out_b.flip(-1)) of bimamba.py:253, flip-free, one batched GEMM
+        return _BiOutProj.apply(f, bk, self.out_proj.weight)
 
 
 class Block(nn.Module):
