@@ -136,8 +136,10 @@ __device__ inline void load_bias_rows(float* bias_r, const float* bias, int d0, 
 // ------------------------------------------------------------------------------- forward
 template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS>
 __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int nblk_d) {
+    // z is not staged in LDS: the flush re-reads the chunk's z (L2 / Infinity-Cache resident: it was
+    // read one chunk earlier by a neighbouring workgroup or is still in flight) and applies silu
+    // there.  That keeps LDS at 42 KB and VGPRs under 168, i.e. 3 workgroups (12 waves) per CU.
     __shared__ __attribute__((aligned(16))) float s_ud[CPB * UD_STRIDE];
-    __shared__ __attribute__((aligned(16))) float s_z[HAS_Z ? CPB * (TC + 1) : 2];
     __shared__ __attribute__((aligned(16))) float s_bc[TC * BC_STRIDE];
 
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -149,11 +151,13 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     const bool dvalid = d < D;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
-    float A2[NS], h[NS];
+    // the lane's 4 states as 2 packed pairs: every state update is v_pk_mul / v_pk_fma on pairs
+    f2_t A2v[NS / 2], h2[NS / 2];
 #pragma unroll
-    for (int j = 0; j < NS; ++j) {
-        A2[j] = dvalid ? a.A[(int64_t)d * NSTATE + id.g * NS + j] * AVSE_LOG2E : 0.f;
-        h[j] = 0.f;
+    for (int p = 0; p < NS / 2; ++p) {
+        const int j = id.g * NS + 2 * p;
+        A2v[p] = dvalid ? f2_t{a.A[(int64_t)d * NSTATE + j], a.A[(int64_t)d * NSTATE + j + 1]} * AVSE_LOG2E : f2_t{0.f, 0.f};
+        h2[p] = f2_t{0.f, 0.f};
     }
     float dtsum = 0.f;
     const float Dv = (HAS_D && dvalid) ? a.D[d] : 0.f;
@@ -166,11 +170,10 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     const int nrow = min(CPB, D - d0);
     float bias_r[RPT];
     load_bias_rows<HAS_BIAS>(bias_r, a.delta_bias, d0, D);
-    RowRegs<Tin> ru, rd, rz;
+    RowRegs<Tin> ru, rd;
     BCRegs<Tin> rbc;
     ru.load(u, a.u_bs, a.u_ds, b, d0, D, 0, min(TC, L), L, rev);
     rd.load(dl, a.delta_bs, a.delta_ds, b, d0, D, 0, min(TC, L), L, rev);
-    if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, 0, min(TC, L), L, rev);
     rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, 0, min(TC, L), L, rev);
 
     for (int k = 0; k < nck; ++k) {
@@ -178,22 +181,20 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
         // registers -> LDS (chunk k)
         store_ud<Tin, SOFTPLUS, HAS_BIAS>(s_ud, ru, rd, bias_r, tn, nrow);
         rbc.store(s_bc, tn);
-        if (HAS_Z) {
-#pragma unroll
-            for (int i = 0; i < RPT; ++i) s_z[(wave + 4 * i) * (TC + 1) + lane] = siluf_(rz.get(i, tn, nrow));
-        }
         __syncthreads();
         // prefetch chunk k + 1 while chunk k computes
+#ifdef AVSE_EXP_NOLOAD
+        if (false) {
+#else
         if (k + 1 < nck) {
+#endif
             const int t1 = t0 + TC, tn1 = min(TC, L - t1);
             ru.load(u, a.u_bs, a.u_ds, b, d0, D, t1, tn1, L, rev);
             rd.load(dl, a.delta_bs, a.delta_ds, b, d0, D, t1, tn1, L, rev);
-            if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t1, tn1, L, rev);
             rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t1, tn1, L, rev);
         }
 
         float* my_ud = &s_ud[id.c * UD_STRIDE];
-        float* my_z = &s_z[HAS_Z ? id.c * (TC + 1) : 0];
         // 8 steps per iteration: the LDS reads of all 8 issue together and the 8 cross-lane
         // y reductions (DPP) are independent, so one wave per SIMD still keeps its pipes busy.
         constexpr int U = 8;
@@ -205,31 +206,37 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                 const float2 ud = *reinterpret_cast<const float2*>(&my_ud[2 * (t + q)]);
                 const float4 bq = *reinterpret_cast<const float4*>(&s_bc[(t + q) * BC_STRIDE + id.g * NS]);
                 const float4 cq = *reinterpret_cast<const float4*>(&s_bc[(t + q) * BC_STRIDE + NSTATE + id.g * NS]);
-                const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
-                const float cc[4] = {cq.x, cq.y, cq.z, cq.w};
+                const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
+                const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
                 const float dt = ud.y, dtu = ud.y * ud.x;
+                const f2_t dt2 = f2_t{dt, dt}, dtu2 = f2_t{dtu, dtu};
                 dtsum += dt;
-                float y = 0.f;
+                f2_t y2 = f2_t{0.f, 0.f};
 #pragma unroll
-                for (int j = 0; j < NS; ++j) {
-                    h[j] = fast_exp2(dt * A2[j]) * h[j] + dtu * bb[j];
-                    y += h[j] * cc[j];
+                for (int p = 0; p < NS / 2; ++p) {
+                    h2[p] = exp2_2(dt2 * A2v[p]) * h2[p] + dtu2 * bp[p];
+                    y2 += h2[p] * cp[p];
                 }
-                yv[q] = y;
+                yv[q] = y2.x + y2.y;
                 uv[q] = ud.x;
             }
 #pragma unroll
+            for (int q = 0; q < NU; ++q) yv[q] = group_sum<G>(yv[q]);
+            // every lane of the channel's quad holds the same sum and writes it to the same LDS word:
+            // no exec-mask branch per step, so the NU reductions and stores schedule together
+#pragma unroll
             for (int q = 0; q < NU; ++q) {
-                const float out = group_sum<G>(yv[q]) + Dv * uv[q];
-                if (id.g == 0) {
-                    my_ud[2 * (t + q)] = out;                          // u slot <- out
-                    if (HAS_Z) my_z[t + q] *= out;                     // silu(z) slot <- out_z
-                }
+                const float out = yv[q] + Dv * uv[q];
+                my_ud[2 * (t + q)] = out;                              // u slot <- out
             }
         };
         int t = 0;
+#ifndef AVSE_EXP_NOCOMPUTE
         for (; t + U <= tn; t += U) steps(t, std::integral_constant<int, U>());
         for (; t < tn; ++t) steps(t, std::integral_constant<int, 1>());
+#endif
+        RowRegs<Tin> rz;       // this chunk's z for the gate, issued before the barrier wait
+        if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t0, tn, L, rev);
         __syncthreads();
         // flush chunk k outputs (lane = time column, rows wave + 4i): buffer stores, row step in soffset
         {
@@ -249,14 +256,16 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                 if (lane < tn) {
 #pragma unroll
                     for (int i = 0; i < RPT; ++i)
-                        if (wave + 4 * i < nrow) bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds, s_z[(wave + 4 * i) * (TC + 1) + lane]);
+                        if (wave + 4 * i < nrow)
+                            bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds,
+                                           s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane] * siluf_(rz.v[i]));
                 }
             }
         }
         if (dvalid) {
             float* xp = a.x + (((int64_t)b * D + d) * nck + k) * (2 * NSTATE) + 2 * id.g * NS;
-            float4 v0 = make_float4(fast_exp2(dtsum * A2[0]), h[0], fast_exp2(dtsum * A2[1]), h[1]);
-            float4 v1 = make_float4(fast_exp2(dtsum * A2[2]), h[2], fast_exp2(dtsum * A2[3]), h[3]);
+            float4 v0 = make_float4(fast_exp2(dtsum * A2v[0].x), h2[0].x, fast_exp2(dtsum * A2v[0].y), h2[0].y);
+            float4 v1 = make_float4(fast_exp2(dtsum * A2v[1].x), h2[1].x, fast_exp2(dtsum * A2v[1].y), h2[1].y);
             reinterpret_cast<float4*>(xp)[0] = v0;
             reinterpret_cast<float4*>(xp)[1] = v1;
         }
@@ -308,17 +317,20 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     const bool dvalid = d < D;
     const int nck = (L + TC - 1) / TC;
 
-    float A[NS], A2[NS];
+    // the lane's 4 states as 2 packed pairs (v_pk_mul / v_pk_fma), as in the forward
+    constexpr int NP = NS / 2;
+    f2_t Av[NP], A2v[NP];
 #pragma unroll
-    for (int j = 0; j < NS; ++j) {
-        A[j] = dvalid ? a.A[(int64_t)d * NSTATE + id.g * NS + j] : 0.f;
-        A2[j] = A[j] * AVSE_LOG2E;
+    for (int p = 0; p < NP; ++p) {
+        const int j = id.g * NS + 2 * p;
+        Av[p] = dvalid ? f2_t{a.A[(int64_t)d * NSTATE + j], a.A[(int64_t)d * NSTATE + j + 1]} : f2_t{0.f, 0.f};
+        A2v[p] = Av[p] * AVSE_LOG2E;
     }
     const float Dv = (HAS_D && dvalid) ? a.D[d] : 0.f;
 
-    float lam[NS], dAn[NS], dA_acc[NS];
+    f2_t lam[NP], dAn[NP], dA_acc[NP];
 #pragma unroll
-    for (int j = 0; j < NS; ++j) { lam[j] = 0.f; dAn[j] = 0.f; dA_acc[j] = 0.f; }
+    for (int p = 0; p < NP; ++p) { lam[p] = f2_t{0.f, 0.f}; dAn[p] = f2_t{0.f, 0.f}; dA_acc[p] = f2_t{0.f, 0.f}; }
     float dD_acc = 0.f, dbias_acc = 0.f;
 
     const Tin* u = (const Tin*)a.u;
@@ -355,155 +367,164 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
         }
         __syncthreads();
 
-        // pass 1: state at every sub-chunk start
-        float hs[TC / TS][NS];
-        {
-            float h[NS];
-            if (k > 0 && dvalid) {
-                const float* xp = a.x + (((int64_t)b * D + d) * nck + (k - 1)) * (2 * NSTATE) + 2 * id.g * NS;
-#pragma unroll
-                for (int j = 0; j < NS; ++j) h[j] = xp[2 * j + 1];
-            } else {
-#pragma unroll
-                for (int j = 0; j < NS; ++j) h[j] = 0.f;
-            }
-#pragma unroll
-            for (int s = 0; s < TC / TS; ++s) {
-#pragma unroll
-                for (int j = 0; j < NS; ++j) hs[s][j] = h[j];
-                if (s == TC / TS - 1) break;
-#pragma unroll 4
-                for (int i = 0; i < TS; ++i) {
-                    const int t = s * TS + i;
-                    if (t >= tn) break;
-                    const float2 ud = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * t]);
-                    const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
-                    const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
-                    const float dtu = ud.y * ud.x;
-#pragma unroll
-                    for (int j = 0; j < NS; ++j) h[j] = fast_exp2(ud.y * A2[j]) * h[j] + dtu * bb[j];
+        // chunk body; FULL (tn == TC) would drop the per-step bounds tests
+        auto chunk_body = [&](auto FULLC) {
+            constexpr bool FULL = decltype(FULLC)::value;
+            // pass 1: state at every sub-chunk start
+            f2_t hs[TC / TS][NP];
+            {
+                f2_t h[NP];
+                if (k > 0 && dvalid) {
+                    const float* xp = a.x + (((int64_t)b * D + d) * nck + (k - 1)) * (2 * NSTATE) + 2 * id.g * NS;
+    #pragma unroll
+                    for (int p = 0; p < NP; ++p) h[p] = f2_t{xp[4 * p + 1], xp[4 * p + 3]};
+                } else {
+    #pragma unroll
+                    for (int p = 0; p < NP; ++p) h[p] = f2_t{0.f, 0.f};
+                }
+    #pragma unroll
+                for (int s = 0; s < TC / TS; ++s) {
+    #pragma unroll
+                    for (int p = 0; p < NP; ++p) hs[s][p] = h[p];
+                    if (s == TC / TS - 1) break;
+    #pragma unroll 4
+                    for (int i = 0; i < TS; ++i) {
+                        const int t = s * TS + i;
+                        if (!FULL && t >= tn) break;
+                        const float2 ud = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * t]);
+                        const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
+                        const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
+                        const f2_t dt2 = f2_t{ud.y, ud.y}, dtu2 = f2_t{ud.y * ud.x, ud.y * ud.x};
+    #pragma unroll
+                        for (int p = 0; p < NP; ++p) h[p] = exp2_2(dt2 * A2v[p]) * h[p] + dtu2 * bp[p];
+                    }
                 }
             }
-        }
 
-        // pass 2: sub-chunks in reverse
-#pragma unroll
-        for (int s = TC / TS - 1; s >= 0; --s) {
-            const int ts = s * TS;
-            if (ts < tn) {
-                float hist[TS][NS];
-                // recompute 16 steps; produce g = dout*silu(z), dz, (out_z)
-                {
-                    float h[NS];
-#pragma unroll
-                    for (int j = 0; j < NS; ++j) h[j] = hs[s][j];
-#pragma unroll
-                    for (int i = 0; i < TS; ++i) {
-                        const int t = ts + i;
-                        if (t < tn) {
-                            float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
-                            const float2 ud = *reinterpret_cast<const float2*>(ud_p);
-                            const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
-                            const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
-                            const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
-                            const float cc[4] = {cq.x, cq.y, cq.z, cq.w};
-                            const float dtu = ud.y * ud.x;
-                            float y = 0.f;
-#pragma unroll
-                            for (int j = 0; j < NS; ++j) {
-                                h[j] = fast_exp2(ud.y * A2[j]) * h[j] + dtu * bb[j];
-                                hist[i][j] = h[j];
-                                y += h[j] * cc[j];
-                            }
-                            y = group_sum<G>(y);
-                            const float out = y + Dv * ud.x;
-                            float* zg_p = &s_zg[id.c * Z_STRIDE + 2 * t];
-                            const float2 zg = *reinterpret_cast<const float2*>(zg_p);
-                            float gv, dzv = 0.f, oz = out;
-                            if (HAS_Z) {
-                                const float sg = sigmoidf_(zg.x);
-                                const float sl = zg.x * sg;
-                                gv = zg.y * sl;
-                                dzv = zg.y * out * sg * (1.f + zg.x * (1.f - sg));
-                                oz = out * sl;
-                            } else {
-                                gv = zg.y;
-                            }
-                            if (id.g == 0) {
-                                *reinterpret_cast<float2*>(zg_p) = make_float2(dzv, gv);
-                                if (a.recompute_out_z)   // rare path: direct (uncoalesced) store
+            // pass 2: sub-chunks in reverse
+    #pragma unroll
+            for (int s = TC / TS - 1; s >= 0; --s) {
+                const int ts = s * TS;
+                if (FULL || ts < tn) {
+                    f2_t hist[TS][NP];
+                    // recompute 16 steps; produce g = dout*silu(z), dz, (out_z)
+                    {
+                        f2_t h[NP];
+    #pragma unroll
+                        for (int p = 0; p < NP; ++p) h[p] = hs[s][p];
+    #pragma unroll
+                        for (int i = 0; i < TS; ++i) {
+                            const int t = ts + i;
+                            if (FULL || t < tn) {
+                                float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
+                                const float2 ud = *reinterpret_cast<const float2*>(ud_p);
+                                const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
+                                const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
+                                const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
+                                const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
+                                const f2_t dt2 = f2_t{ud.y, ud.y}, dtu2 = f2_t{ud.y * ud.x, ud.y * ud.x};
+                                f2_t y2 = f2_t{0.f, 0.f};
+    #pragma unroll
+                                for (int p = 0; p < NP; ++p) {
+                                    h[p] = exp2_2(dt2 * A2v[p]) * h[p] + dtu2 * bp[p];
+                                    hist[i][p] = h[p];
+                                    y2 += h[p] * cp[p];
+                                }
+                                float y = group_sum<G>(y2.x + y2.y);
+                                const float out = y + Dv * ud.x;
+                                float* zg_p = &s_zg[id.c * Z_STRIDE + 2 * t];
+                                const float2 zg = *reinterpret_cast<const float2*>(zg_p);
+                                float gv, dzv = 0.f, oz = out;
+                                if (HAS_Z) {
+                                    const float sg = sigmoidf_(zg.x);
+                                    const float sl = zg.x * sg;
+                                    gv = zg.y * sl;
+                                    dzv = zg.y * out * sg * (1.f + zg.x * (1.f - sg));
+                                    oz = out * sl;
+                                } else {
+                                    gv = zg.y;
+                                }
+                                *reinterpret_cast<float2*>(zg_p) = make_float2(dzv, gv);   // same value from the quad
+                                if (a.recompute_out_z && id.g == 0)   // rare path: direct (uncoalesced) store
                                     io<Tin>::st((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d * a.out_z_ds +
                                                     tpos(t0 + t, L, rev), oz);
+                            } else {
+    #pragma unroll
+                                for (int p = 0; p < NP; ++p) hist[i][p] = f2_t{0.f, 0.f};
                             }
+                        }
+                    }
+                    // adjoint sweep
+    #pragma unroll
+                    for (int i = TS - 1; i >= 0; --i) {
+                        const int t = ts + i;
+                        float part[8];
+                        if (FULL || t < tn) {
+                            float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
+                            const float2 ud = *reinterpret_cast<const float2*>(ud_p);
+                            const float gv = s_zg[id.c * Z_STRIDE + 2 * t + 1];
+                            const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
+                            const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
+                            const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
+                            const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
+                            const float dt = ud.y, uu = ud.x;
+                            const f2_t dt2 = f2_t{dt, dt}, uu2 = f2_t{uu, uu}, gv2 = f2_t{gv, gv};
+                            const f2_t dtu2 = dt2 * uu2;
+                            f2_t ddt2 = f2_t{0.f, 0.f}, dus2 = f2_t{0.f, 0.f};
+    #pragma unroll
+                            for (int p = 0; p < NP; ++p) {
+                                const f2_t hp = (i == 0) ? hs[s][p] : hist[i > 0 ? i - 1 : 0][p];
+                                const f2_t dA = exp2_2(dt2 * A2v[p]);
+                                lam[p] = lam[p] * dAn[p] + gv2 * cp[p];
+                                const f2_t lhp = lam[p] * dA * hp;
+                                const f2_t lb = lam[p] * bp[p];
+                                ddt2 += Av[p] * lhp + lb * uu2;
+                                dus2 += lb;
+                                dA_acc[p] += dt2 * lhp;
+                                const f2_t pb = lam[p] * dtu2, pc = gv2 * hist[i][p];
+                                part[2 * p] = pb.x;
+                                part[2 * p + 1] = pb.y;
+                                part[4 + 2 * p] = pc.x;
+                                part[4 + 2 * p + 1] = pc.y;
+                                dAn[p] = dA;
+                            }
+                            float ddt = group_sum<G>(ddt2.x + ddt2.y);
+                            float dus = group_sum<G>(dus2.x + dus2.y);
+                            const float du = dus * dt + gv * Dv;
+                            const float sig = SOFTPLUS ? (1.f - fast_exp(-dt)) : 1.f;
+                            const float ddr = ddt * sig;
+                            dD_acc += gv * uu;
+                            dbias_acc += ddr;
+                            *reinterpret_cast<float2*>(ud_p) = make_float2(du, ddr);   // same value from the quad
                         } else {
-#pragma unroll
-                            for (int j = 0; j < NS; ++j) hist[i][j] = 0.f;
+    #pragma unroll
+                            for (int j = 0; j < 8; ++j) part[j] = 0.f;
                         }
-                    }
-                }
-                // adjoint sweep
-#pragma unroll
-                for (int i = TS - 1; i >= 0; --i) {
-                    const int t = ts + i;
-                    float part[8];
-                    if (t < tn) {
-                        float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
-                        const float2 ud = *reinterpret_cast<const float2*>(ud_p);
-                        const float gv = s_zg[id.c * Z_STRIDE + 2 * t + 1];
-                        const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
-                        const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
-                        const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
-                        const float cc[4] = {cq.x, cq.y, cq.z, cq.w};
-                        const float dt = ud.y, uu = ud.x;
-                        float ddt = 0.f, dus = 0.f;
-#pragma unroll
-                        for (int j = 0; j < NS; ++j) {
-                            const float hp = (i == 0) ? hs[s][j] : hist[i > 0 ? i - 1 : 0][j];
-                            const float dA = fast_exp2(dt * A2[j]);
-                            lam[j] = lam[j] * dAn[j] + gv * cc[j];
-                            const float lhp = lam[j] * dA * hp;
-                            ddt += A[j] * lhp + lam[j] * bb[j] * uu;
-                            dus += lam[j] * bb[j];
-                            dA_acc[j] += dt * lhp;
-                            part[j] = lam[j] * dt * uu;
-                            part[4 + j] = gv * hist[i][j];
-                            dAn[j] = dA;
+                        const float r = rs8(part, id.lane);
+                        if (id.lane < 32) {
+                            const int vi = ((id.lane >> 2) & 1) * 4 + ((id.lane >> 3) & 1) * 2 + ((id.lane >> 4) & 1);
+                            const int slot = (vi < 4 ? 0 : NSTATE) + id.g * NS + (vi & 3);
+                            s_red[(id.wave * RED + (i & (RED - 1))) * 2 * NSTATE + slot] = r;
                         }
-                        ddt = group_sum<G>(ddt);
-                        dus = group_sum<G>(dus);
-                        const float du = dus * dt + gv * Dv;
-                        const float sig = SOFTPLUS ? (1.f - fast_exp(-dt)) : 1.f;
-                        const float ddr = ddt * sig;
-                        dD_acc += gv * uu;
-                        dbias_acc += ddr;
-                        if (id.g == 0) *reinterpret_cast<float2*>(ud_p) = make_float2(du, ddr);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) part[j] = 0.f;
-                    }
-                    const float r = rs8(part, id.lane);
-                    if (id.lane < 32) {
-                        const int vi = ((id.lane >> 2) & 1) * 4 + ((id.lane >> 3) & 1) * 2 + ((id.lane >> 4) & 1);
-                        const int slot = (vi < 4 ? 0 : NSTATE) + id.g * NS + (vi & 3);
-                        s_red[(id.wave * RED + (i & (RED - 1))) * 2 * NSTATE + slot] = r;
-                    }
-                    if ((i & (RED - 1)) == 0) {
-                        // cross-wave sum of steps ts+i .. ts+i+RED-1 -> partial slab
-                        __syncthreads();
-                        for (int idx = threadIdx.x; idx < RED * 2 * NSTATE; idx += THREADS) {
-                            const int slot = idx / RED, ii = idx % RED, tt = ts + i + ii;
-                            if (tt < tn) {
-                                float v = 0.f;
-#pragma unroll
-                                for (int w = 0; w < 4; ++w) v += s_red[(w * RED + ii) * 2 * NSTATE + slot];
-                                ws_bc[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + tpos(t0 + tt, L, rev)] = v;
+                        if ((i & (RED - 1)) == 0) {
+                            // cross-wave sum of steps ts+i .. ts+i+RED-1 -> partial slab
+                            __syncthreads();
+                            for (int idx = threadIdx.x; idx < RED * 2 * NSTATE; idx += THREADS) {
+                                const int slot = idx / RED, ii = idx % RED, tt = ts + i + ii;
+                                if (FULL || tt < tn) {
+                                    float v = 0.f;
+    #pragma unroll
+                                    for (int w = 0; w < 4; ++w) v += s_red[(w * RED + ii) * 2 * NSTATE + slot];
+                                    ws_bc[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + tpos(t0 + tt, L, rev)] = v;
+                                }
                             }
+                            __syncthreads();
                         }
-                        __syncthreads();
                     }
                 }
             }
-        }
+        };
+        chunk_body(std::false_type());   // a FULL (bounds-free) instantiation interleaved so far that it spilled
         __syncthreads();
         // write du, ddelta, dz (+ out_z) tiles (lane = time column): buffer stores, row step in soffset
         {
@@ -541,7 +562,10 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     if (dvalid) {
         float* p = ws_d + ((int64_t)b * D + d) * (NSTATE + 2);
 #pragma unroll
-        for (int j = 0; j < NS; ++j) p[id.g * NS + j] = dA_acc[j];
+        for (int q = 0; q < NP; ++q) {
+            p[id.g * NS + 2 * q] = dA_acc[q].x;
+            p[id.g * NS + 2 * q + 1] = dA_acc[q].y;
+        }
         if (id.g == 0) {
             p[NSTATE] = dD_acc;
             p[NSTATE + 1] = dbias_acc;

@@ -2,7 +2,7 @@
 
 python tools/scan_bench.py [--cfg B,D,L ...] [--iters N]
 Algorithmic bytes: scan fwd 4*L*(5*D + 2*16) per row of B (u, delta, z read; out,
-out_z written; B, C read); scan bwd 4*L*(9*D + 4*16); causal conv fwd 2*4*D*L, bwd 3*4*D*L.
+out_z written; B, C read), training fwd (no out) 4*L*(4*D + 2*16); scan bwd 4*L*(9*D + 4*16); causal conv fwd 2*4*D*L, bwd 3*4*D*L.
 """
 import argparse
 import json
@@ -53,6 +53,10 @@ def main():
             ms = timeit(lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, reverse=rev), args.iters)
             byts = es * b * l * (5 * d + 2 * 16)
             res[f"scan_fwd{'_rev' if rev else ''}"] = (ms, byts / ms / 1e6)
+            # training forward (what MambaInnerNoOutProj runs): out_z + checkpoints only, 4*D + 32 per step
+            ms = timeit(lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, reverse=rev,
+                                                     return_out=False), args.iters)
+            res[f"scan_fwd_train{'_rev' if rev else ''}"] = (ms, es * b * l * (4 * d + 2 * 16) / ms / 1e6)
             gout = torch.randn_like(u)
             ms = timeit(lambda: K.selective_scan_bwd(u, dl, A, Bm, Cm, D, z, bias, gout, x, out, None, True, False,
                                                      reverse=rev), max(2, args.iters // 2))
