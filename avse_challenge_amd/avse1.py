@@ -140,10 +140,20 @@ class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 conv
             setattr(self, f"bn{i + 1}", nn.BatchNorm2d(filters))
         self.convf = nn.Conv2d(filters, last_filter, 1)
         self.bn_last = nn.BatchNorm2d(last_filter)
+        self.channels_last = False
+
+    def use_channels_last(self, on=True):
+        """NHWC activations/weights: MIOpen's implicit-GEMM convs are NHWC kernels, so NCHW tensors
+        pay a transpose in and out of every conv (needs PYTORCH_MIOPEN_SUGGEST_NHWC=1)."""
+        self.channels_last = on
+        self.to(memory_format=torch.channels_last if on else torch.contiguous_format)
+        return self
 
     def forward(self, spec):              # (B, 1, T, F) -> (B, T, 4F)
         T, Fb = spec.shape[2], spec.shape[3]
         x = self.bn0(spec)
+        if self.channels_last:
+            x = x.contiguous(memory_format=torch.channels_last)
         for i in range(1, self.num_conv + 1):
             x = F.relu(getattr(self, f"bn{i}")(getattr(self, f"conv{i}")(x)))
         x = F.relu(self.bn_last(self.convf(x)))
