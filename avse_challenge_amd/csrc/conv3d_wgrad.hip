@@ -10,10 +10,12 @@
 //   dW[co][n] = sum_k dY[k][co] * Xcol[k][n],  n = ((ci*KT + kt)*KH + kh)*KW + kw,
 //   k = (b, t, ho, wo),  Xcol[k][n] = X[b][ci][t - PT + kt][2*ho - PH + kh][2*wo - PW + kw] (0 outside)
 //
-// One workgroup (4 waves) owns a strided set of output rows (b, t, ho); per row it stages the
-// CIN*KT*KH input rows it touches (width 2*(WO-1)+KW) and the 64 x WO gradient row in LDS, then
-// every wave runs WO/2 K-steps of 2 x NTW 32x32x2 MFMAs (M = 64 = 2 tiles, N split over waves).
+// One workgroup (4 waves) owns a strided set of output rows (b, t, ho) and a slice of N; per row it
+// stages the input rows its slice touches (width 2*(WO-1)+KW) and the 64 x WO gradient row in LDS,
+// then every wave runs WO/2 K-steps of 2 x NTW 32x32x2 MFMAs (M = 64 = 2 tiles, N split over waves).
 // Partial 64 x N tiles per workgroup go to a workspace; a second kernel sums them (deterministic).
+#include <algorithm>
+
 #include "common.h"
 
 namespace avse {
@@ -31,30 +33,33 @@ struct Shape {
     int N, rows, nparts;
 };
 
-template <int NTW>
-__global__ __launch_bounds__(THREADS) void wgrad_kernel(Shape s, const float* __restrict__ x, const float* __restrict__ dy,
-                                                        float* __restrict__ part) {
+// Per workgroup: a strided set of output rows (b, t, ho) and one N slice of 4*NTW 32-wide tiles
+// (blockIdx.y), so a slice stages only the input rows its columns touch.  Software pipelined:
+// the next row's input window and dY row are loaded into registers (raw buffer loads, out-of-range
+// -> 0, no waits at issue) while the MFMAs of the current row run out of LDS.
+template <int NTW, int RPW>
+__global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(Shape s, const float* __restrict__ x,
+                                                           const float* __restrict__ dy, float* __restrict__ part) {
     extern __shared__ float lds[];
     const int WIN = 2 * (s.WO - 1) + s.KW;
     const int WINP = WIN + 1;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: row math stays scalar
     const int nxrow = s.CIN * s.KT * s.KH;
-    float* xs = lds;                                  // [nxrow][WINP] + zero pad region
-    float* zero = xs + nxrow * WINP;                  // 2 * MAX_WO floats of zeros (N padding)
-    float* ys = zero + 2 * MAX_WO + 8;                // [64][YS]
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n_lo = blockIdx.y * 4 * NTW * 32;
+    const int n_hi = min(s.N, n_lo + 4 * NTW * 32);
+    const int r_lo = n_lo / s.KW, r_hi = min(nxrow, (n_hi + s.KW - 1) / s.KW);
+    const int nrs = r_hi - r_lo;                         // staged input rows (<= 4 * RPW)
+    float* xs = lds;                                     // [nrs][WINP]
+    float* zero = xs + nrs * WINP;                       // 2 * MAX_WO + 8 zeros (N padding)
+    float* ys = zero + 2 * MAX_WO + 8;                   // [64][YS]
     for (int i = threadIdx.x; i < 2 * MAX_WO + 8; i += THREADS) zero[i] = 0.f;
 
-    // per-lane B-operand base offsets for this wave's N tiles
     int boff[NTW];
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
-        const int n = (wave * NTW + j) * 32 + (lane & 31);
-        if (n < s.N) {
-            const int kw = n % s.KW, r = n / s.KW;     // r = (ci*KT + kt)*KH + kh
-            boff[j] = r * WINP + kw;
-        } else {
-            boff[j] = (int)(zero - xs);               // reads 0 (2*k stays inside the zero block)
-        }
+        const int n = n_lo + (wave * NTW + j) * 32 + (lane & 31);
+        boff[j] = n < n_hi ? (n / s.KW - r_lo) * WINP + n % s.KW : (int)(zero - xs);
     }
     floatx16 acc[2][NTW];
 #pragma unroll
@@ -66,28 +71,55 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(Shape s, const float* __
 
     const int64_t plane = (int64_t)s.H * s.W;
     const int64_t yplane = (int64_t)s.HO * s.WO;
-    for (int row = blockIdx.x; row < s.rows; row += gridDim.x) {
-        const int ho = row % s.HO;
-        const int t = (row / s.HO) % s.TO;
-        const int b = row / (s.HO * s.TO);
-        __syncthreads();
-        // stage input rows: xs[(ci*KT + kt)*KH + kh][c] = X[b][ci][t-PT+kt][2ho-PH+kh][c - PW]
-        for (int i = threadIdx.x; i < nxrow * WIN; i += THREADS) {
-            const int c = i % WIN, r = i / WIN;
+    const int nx = (int)((int64_t)s.B * s.CIN * s.T * plane);     // < 2^29 (checked at launch)
+    const int ny = (int)((int64_t)s.B * COUT * s.TO * yplane);
+    const auto rx = make_rsrc(x, nx);
+    const auto ry = make_rsrc(dy, ny);                    // element offset nx / ny is past num_records -> 0
+    float xr[RPW][2], yr[16];
+    const int wo2 = (s.WO + 1) & ~1;
+
+    auto prefetch = [&](int row) {
+        const int ho = row % s.HO, t = (row / s.HO) % s.TO, b = row / (s.HO * s.TO);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const int r = r_lo + wave + 4 * i;           // wave-uniform
             const int kh = r % s.KH, kt = (r / s.KH) % s.KT, ci = r / (s.KH * s.KT);
-            const int ti = t - s.PT + kt, hi = 2 * ho - s.PH + kh, wi = c - s.PW;
-            float v = 0.f;
-            if (ti >= 0 && ti < s.T && hi >= 0 && hi < s.H && wi >= 0 && wi < s.W)
-                v = x[(((int64_t)b * s.CIN + ci) * s.T + ti) * plane + (int64_t)hi * s.W + wi];
-            xs[r * WINP + c] = v;
+            const int ti = t - s.PT + kt, hi = 2 * ho - s.PH + kh;
+            const bool rowok = r < r_hi && ti >= 0 && ti < s.T && hi >= 0 && hi < s.H;
+            const int base = (int)(((int64_t)(b * s.CIN + ci) * s.T + ti) * plane + (int64_t)hi * s.W) - s.PW;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int c = lane + 64 * q, wi = c - s.PW;
+                const bool ok = rowok && c < WIN && wi >= 0 && wi < s.W;
+                xr[i][q] = bufld<float>::ld(rx, ok ? base + c : nx, 0);
+            }
         }
-        // stage dY row: ys[co][wo] = dY[b][co][t][ho][wo]; zero-pad to an even count
-        const int wo2 = (s.WO + 1) & ~1;
-        for (int i = threadIdx.x; i < COUT * wo2; i += THREADS) {
-            const int wo = i % wo2, co = i / wo2;
-            ys[co * YS + wo] = wo < s.WO ? dy[(((int64_t)b * COUT + co) * s.TO + t) * yplane + (int64_t)ho * s.WO + wo] : 0.f;
+        const int64_t yb = ((int64_t)b * COUT * s.TO + t) * yplane + (int64_t)ho * s.WO;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int co = wave + 4 * i;
+            const bool ok = lane < s.WO;
+            yr[i] = bufld<float>::ld(ry, ok ? (int)(yb + (int64_t)co * s.TO * yplane) + lane : ny, 0);
         }
+    };
+
+    int row = blockIdx.x;
+    if (row < s.rows) prefetch(row);
+    for (; row < s.rows; row += gridDim.x) {
+        __syncthreads();                                 // previous row's MFMAs are done with LDS
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const int rr = wave + 4 * i;
+            if (rr < nrs) {
+                if (lane < WIN) xs[rr * WINP + lane] = xr[i][0];          // lanes past the window would
+                if (lane + 64 < WIN) xs[rr * WINP + lane + 64] = xr[i][1];  // spill into the next row
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (lane < wo2) ys[(wave + 4 * i) * YS + lane] = lane < s.WO ? yr[i] : 0.f;
         __syncthreads();
+        if (row + (int)gridDim.x < s.rows) prefetch(row + gridDim.x);
         const int kh = lane >> 5;
         for (int k0 = 0; k0 < wo2; k0 += 2) {
             const int k = k0 + kh;
@@ -107,8 +139,8 @@ __global__ __launch_bounds__(THREADS) void wgrad_kernel(Shape s, const float* __
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
-            const int n = (wave * NTW + j) * 32 + (lane & 31);
-            if (n < s.N) {
+            const int n = n_lo + (wave * NTW + j) * 32 + (lane & 31);
+            if (n < n_hi) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int co = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -151,24 +183,29 @@ int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, i
     s.WO = (s.W + 2 * s.PW - s.KW) / 2 + 1;
     s.N = s.CIN * s.KT * s.KH * s.KW;
     if (B <= 0 || CIN <= 0 || s.TO <= 0 || s.HO <= 0 || s.WO <= 0 || s.WO > MAX_WO || s.KW > 8) return AVSE_ESHAPE;
+    constexpr int NTW = 3, RPW = 16;
     const int nt = (s.N + 31) / 32;
-    const int ntw = (nt + 3) / 4;
-    if (ntw > 6) return AVSE_ESHAPE;
+    const int nsplit = (nt + 4 * NTW - 1) / (4 * NTW);
     s.rows = s.B * s.TO * s.HO;
     s.nparts = nparts_for(s.rows);
     const int WIN = 2 * (s.WO - 1) + s.KW;
-    const size_t lds = 4 * ((size_t)s.CIN * s.KT * s.KH * (WIN + 1) + 2 * MAX_WO + 8 + COUT * YS);
-    if (lds > 160 * 1024) return AVSE_ESHAPE;
-    hipStream_t st = (hipStream_t)stream;
-    dim3 grid(s.nparts), block(THREADS);
-    switch (ntw) {
-        case 1: hipLaunchKernelGGL(wgrad_kernel<1>, grid, block, lds, st, s, x, dy, workspace); break;
-        case 2: hipLaunchKernelGGL(wgrad_kernel<2>, grid, block, lds, st, s, x, dy, workspace); break;
-        case 3: hipLaunchKernelGGL(wgrad_kernel<3>, grid, block, lds, st, s, x, dy, workspace); break;
-        case 4: hipLaunchKernelGGL(wgrad_kernel<4>, grid, block, lds, st, s, x, dy, workspace); break;
-        case 5: hipLaunchKernelGGL(wgrad_kernel<5>, grid, block, lds, st, s, x, dy, workspace); break;
-        default: hipLaunchKernelGGL(wgrad_kernel<6>, grid, block, lds, st, s, x, dy, workspace); break;
+    if (WIN > 128) return AVSE_ESHAPE;
+    // 32-bit buffer offsets: both tensors must stay under 2 GiB
+    if ((int64_t)s.B * s.CIN * s.T * s.H * s.W >= (1LL << 29) || (int64_t)s.B * COUT * s.TO * s.HO * s.WO >= (1LL << 29))
+        return AVSE_ESHAPE;
+    // staged rows of the widest slice must fit the RPW registers per wave
+    int max_nrs = 0;
+    for (int y = 0; y < nsplit; ++y) {
+        const int n_lo = y * 4 * NTW * 32, n_hi = std::min(s.N, n_lo + 4 * NTW * 32);
+        const int nrs = std::min(s.CIN * s.KT * s.KH, (n_hi + s.KW - 1) / s.KW) - n_lo / s.KW;
+        max_nrs = std::max(max_nrs, nrs);
     }
+    if (max_nrs > 4 * RPW) return AVSE_ESHAPE;
+    const size_t lds = 4 * ((size_t)max_nrs * (WIN + 1) + 2 * MAX_WO + 8 + COUT * YS);
+    if (lds > 64 * 1024) return AVSE_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid(s.nparts, nsplit), block(THREADS);
+    hipLaunchKernelGGL((wgrad_kernel<NTW, RPW>), grid, block, lds, st, s, x, dy, workspace);
     AVSE_CHECK_LAUNCH();
     const int total = COUT * s.N;
     hipLaunchKernelGGL(reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, workspace, s.nparts, total, dw,

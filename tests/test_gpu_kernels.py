@@ -237,7 +237,7 @@ def test_kernels_reject_cpu_tensors():
 
 # ------------------------------------------------------------------ lip front-end Conv3d weight gradient
 
-@pytest.mark.parametrize("cin,T,H,W", [(3, 6, 20, 18), (1, 5, 16, 16), (3, 3, 96, 96)])
+@pytest.mark.parametrize("cin,T,H,W", [(3, 6, 20, 18), (1, 5, 16, 16), (3, 3, 96, 96), (1, 3, 112, 112), (2, 2, 130, 40)])
 def test_conv3d_wgrad_vs_fp64(cin, T, H, W):
     x = det_input((2, cin, T, H, W), 700 + cin, "uniform", 255.0)
     w = det_input((64, cin, 5, 7, 7), 701) / 50
