@@ -261,7 +261,11 @@ def test_avse4_full_train_step_vs_oracle():
         e_gpu = float((p.grad.double().cpu() - q.grad).abs().max()) / scale
         e_torch = float((t.grad.double().cpu() - q.grad).abs().max()) / scale
         cos = torch.nn.functional.cosine_similarity(p.grad.double().cpu().reshape(-1), q.grad.reshape(-1), 0)
-        assert e_gpu <= max(3 * e_torch, 1e-2) and cos > 1 - 1e-4, (k, e_gpu, e_torch, float(cos))
+        # a scalar PReLU slope's gradient is one sum over B*C*K terms of both signs (cancellation), so its
+        # relative error swings with the upstream MIOpen error from process to process (measured 3e-3 ..
+        # 5e-2, tools/avse4_grad_diag.py); such 1-element parameters get a 1e-1 floor
+        floor = 1e-1 if p.numel() == 1 else 1e-2
+        assert e_gpu <= max(3 * e_torch, floor) and cos > 1 - 1e-4, (k, e_gpu, e_torch, float(cos))
 
 
 def test_bench_trainer_graph_replay_equals_eager():
