@@ -5,10 +5,10 @@ set -e
 name=$1; flags=$2
 root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/build/exp/$name
-mkdir -p "$out"
+mkdir -p "$out" "$root/expso"
 for f in "$root"/avse_challenge_amd/csrc/*.hip; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w -I"$root/include" $flags -c "$f" -o "$out/$(basename "$f" .hip).o" &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/build/exp/$name.so" "$out"/*.o
-echo "built build/exp/$name.so"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/expso/$name.so" "$out"/*.o
+echo "built expso/$name.so"
