@@ -32,6 +32,9 @@ os.environ.setdefault("PYTORCH_MIOPEN_SUGGEST_NHWC", "1")
 os.environ.setdefault("PYTORCH_MIOPEN_SUGGEST_NHWC_BATCHNORM", "1")
 
 METRIC = "utterances/sec (3s@16kHz + 75 lip frames)"
+# HBM bytes per launch of each roofline kernel, from rocprofv3 PMC passes (tools/pmc_traffic.sh:
+# FETCH_SIZE and WRITE_SIZE in separate passes, corrected as MI355X_MICROARCH.md prescribes)
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFS = 157.3          # FP32 matrix (= vector) peak, spec
 
@@ -100,6 +103,8 @@ class Avse1Step:
         Times conv3 (dilation 4) forward at the step's shape with HIP events; FLOPs = 2*B*64*64*25*376*257."""
         conv = self.model.net_audiofeat.conv3
         x = torch.randn(self.B, 64, 376, 257, device=dev)
+        if getattr(self.model.net_audiofeat, "channels_last", False):
+            x = x.to(memory_format=torch.channels_last)        # the layout the step runs the conv in
         with torch.no_grad():
             for _ in range(3):
                 conv(x)
@@ -114,9 +119,10 @@ class Avse1Step:
         ms = e0.elapsed_time(e1) / n
         flops = 2.0 * self.B * 64 * 64 * 25 * 376 * 257
         ach = flops / (ms * 1e-3) / 1e12
-        return {"kernel": "AudioFeatNet.conv3 fwd (Conv2d 64->64 5x5 dil 4, MIOpen)", "bound": "mfma",
-                "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFS, 4),
-                "traffic": None, "avg_ms": round(ms, 4), "algorithmic_flops_per_launch": flops}
+        return _with_traffic({"kernel": "AudioFeatNet.conv3 fwd (Conv2d 64->64 5x5 dil 4, MIOpen)", "bound": "mfma",
+                              "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
+                              "frac": round(ach / FP32_PEAK_TFS, 4), "traffic": None, "avg_ms": round(ms, 4),
+                              "algorithmic_flops_per_launch": flops}, "conv3" if self.B == 32 else "-")
 
     def cpu_baseline(self):
         from oracle import avse1_ref, stft_ref
@@ -191,9 +197,10 @@ class MambaStep:
         ms = e0.elapsed_time(e1) / n
         byts = 4.0 * b * l * (4 * d + 2 * 16)     # u, delta, z, B, C read; out_z written
         ach = byts / (ms * 1e-3) / 1e9
-        return {"kernel": "avse_scan_fwd (selective scan, fp32, training fwd: out_z + chunk states)", "bound": "hbm",
+        roof = {"kernel": "avse_scan_fwd (selective scan, fp32, training fwd: out_z + chunk states)", "bound": "hbm",
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                 "traffic": None, "avg_ms": round(ms, 4), "algorithmic_bytes_per_launch": byts}
+        return _with_traffic(roof, "scan") if b == 64 else roof
 
     def cpu_baseline(self):
         from oracle import losses_ref, mamba_ref
@@ -239,8 +246,9 @@ class Avse4Step:
         from avse_challenge_amd import kernels as K
         x = torch.randn(self.B, 512, 3999, device=dev)
         w = torch.randn(512, 1, 3, device=dev)
-        return _time_hbm(lambda: K.dwconv_fwd(x, w, 128), 8.0 * x.numel(),
+        roof = _time_hbm(lambda: K.dwconv_fwd(x, w, 128), 8.0 * x.numel(),
                          "avse_dwconv_fwd (depthwise dilated conv1d, H=512, K=3999, dil 128)")
+        return _with_traffic(roof, "dwconv") if self.B == 16 else roof
 
     def cpu_baseline(self):
         from oracle import avse4_ref
@@ -337,6 +345,23 @@ class Trainer:
         self._allreduce()
         self.g_opt.replay()
         return self.loss
+
+
+def pmc_traffic(phase):
+    """(bytes per launch, source) for a roofline kernel, or (None, reason) without a PMC summary."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            rec = json.load(f)[phase]
+        return rec["traffic_bytes"], f"{os.path.relpath(TRAFFIC_FILE, REPO)}[{phase}] ({rec['kernel'][:60]})"
+    except (OSError, KeyError, ValueError):
+        return None, "no PMC summary"
+
+
+def _with_traffic(roof, phase):
+    t, src = pmc_traffic(phase)
+    roof["traffic"] = t
+    roof["traffic_source"] = src
+    return roof
 
 
 def _time_hbm(fn, byts, name, n=10):

@@ -1,0 +1,63 @@
+"""Launch the bench's roofline kernels at the bench shapes (for rocprofv3 PMC passes: tools/pmc_traffic.sh).
+
+python tools/roofline_kernels.py PHASE [--n N]
+PHASE: scan (Mamba-L C3 training scan fwd, B=64), dwconv (avse4 C4 TCN dwconv fwd, B=16, dil 128),
+       cconv (causal conv fwd, B=64, D=1024: the dword-access calibration kernel, known bytes),
+       conv3 (avse1 C2 AudioFeatNet conv3 fwd, B=32, NHWC, MIOpen).
+Inputs are created before a device sync, then the kernel runs N times; the PMC summary counts only
+non-PyTorch kernels, so input generation does not enter the per-launch numbers.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from avse_challenge_amd import kernels as K  # noqa: E402
+
+SHAPES = {"scan": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999), "conv3": (32, 64, 376, 257)}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("phase", choices=sorted(SHAPES))
+    p.add_argument("--n", type=int, default=5)
+    a = p.parse_args()
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+    if a.phase == "scan":
+        b, d, l = SHAPES["scan"]
+        u, dl, z = (torch.randn(b, d, l, device=dev, generator=g) for _ in range(3))
+        dl.mul_(0.1)
+        A = -torch.rand(d, 16, device=dev, generator=g) - 0.5
+        Bm, Cm = torch.randn(b, 16, l, device=dev, generator=g), torch.randn(b, 16, l, device=dev, generator=g)
+        D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
+        fn = lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False)  # noqa: E731
+    elif a.phase == "dwconv":
+        x = torch.randn(*SHAPES["dwconv"], device=dev, generator=g)
+        w = torch.randn(512, 1, 3, device=dev, generator=g)
+        fn = lambda: K.dwconv_fwd(x, w, 128)  # noqa: E731
+    elif a.phase == "cconv":
+        b, d, l = SHAPES["cconv"]
+        x = torch.randn(b, d, l, device=dev, generator=g)
+        w, cb = torch.randn(d, 4, device=dev, generator=g), torch.randn(d, device=dev, generator=g)
+        fn = lambda: K.causal_conv1d_fwd(x, w, cb, True)  # noqa: E731
+    else:
+        from avse_challenge_amd import avse1
+        conv = avse1.AVNet().to(dev).net_audiofeat
+        conv.use_channels_last()
+        conv3 = conv.conv3
+        x = torch.randn(*SHAPES["conv3"], device=dev, generator=g).to(memory_format=torch.channels_last)
+        fn = lambda: conv3(x)  # noqa: E731
+    with torch.no_grad():
+        fn()
+        torch.cuda.synchronize()
+        for _ in range(a.n):
+            fn()
+        torch.cuda.synchronize()
+    print(f"{a.phase}: {a.n + 1} launches", flush=True)
+
+
+if __name__ == "__main__":
+    main()
