@@ -17,9 +17,9 @@
 // Backward per chunk (reverse order): recompute the chunk forward keeping the state at
 // each 16-step sub-chunk start, then per sub-chunk (reverse) recompute 16 steps into
 // registers and run the adjoint (lambda) recurrence backwards.  dB/dC (sums over d) are
-// reduced reduce-scatter style across the wave's 16 channels (8 shuffles/step), across the
-// 4 waves in LDS, and written as per-workgroup partial slabs summed by a second kernel —
-// deterministic, no float atomics.
+// reduced across the wave's 16 channels with permlane swaps and DPP rotations (no selects, no LDS
+// swizzles), across the 4 waves in LDS, and written as per-workgroup partial slabs summed by a
+// second kernel — deterministic, no float atomics.
 #include <algorithm>
 #include <type_traits>
 
@@ -274,30 +274,26 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
 }
 
 // ------------------------------------------------------------------------------- backward
-// reduce-scatter of 8 values over the 16 channel lanes (lane bits 2..5) of a wave; returns
-// the full sum of value index vi = 4*b2 + 2*b3 + b4 (b_k = bit k of the lane id).
-__device__ inline float rs8(float v[8], int lane) {
-    const bool b2 = lane & 4, b3 = lane & 8;
+// Sum of 8 values over the 16 channel lanes (lane bits 2..5) of a wave without selects: a
+// permlane32_swap + add per pair halves 8 -> 4 values (bit 5), permlane16_swap + add halves 4 -> 2
+// (bit 4), two DPP row rotations (ror 8, ror 4) finish bits 3 and 2.  Lane (b2, b3, b4, b5) then holds
+// the full sums of value indices vi = 4 b5 + 2 b4 + j in r[j], j = 0, 1, for its own state group
+// (bits 0-1); lanes with b2 = b3 = 0 carry the unique copy.  16 VALU, no LDS swizzles.
+__device__ inline void rs8_swap(const float v[8], float r[2]) {
     float w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        float send = b2 ? v[i] : v[i + 4];
-        float keep = b2 ? v[i + 4] : v[i];
-        w[i] = keep + swz_xor<4>(send);
+        auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 4]), false, false);
+        w[i] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
     }
-    float x2[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        float send = b3 ? w[i] : w[i + 2];
-        float keep = b3 ? w[i + 2] : w[i];
-        x2[i] = keep + swz_xor<8>(send);
+    for (int j = 0; j < 2; ++j) {
+        auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[j]), __float_as_uint(w[j + 2]), false, false);
+        float x = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+        x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, false));   // row_ror:8
+        x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, false));   // row_ror:4
+        r[j] = x;
     }
-    // xor-16 level as one VALU permlane16_swap: (r0 + r1) keeps x2[0] on even rows and x2[1] on
-    // odd rows, each summed with the partner row's copy; xor-32 the same with permlane32_swap.
-    auto p16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x2[0]), __float_as_uint(x2[1]), false, false);
-    const float r = __uint_as_float(p16[0]) + __uint_as_float(p16[1]);
-    auto p32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
-    return __uint_as_float(p32[0]) + __uint_as_float(p32[1]);
 }
 
 constexpr int RED = 8;   // adjoint steps buffered per cross-wave dB/dC flush
@@ -345,6 +341,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     const int nrow_b = min(CPB, D - d0);
     float bias_r[RPT];
     load_bias_rows<HAS_BIAS>(bias_r, a.delta_bias, d0, D);
+    const bool fold_gate = !a.recompute_out_z;
 
     for (int k = nck - 1; k >= 0; --k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
@@ -360,10 +357,19 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
             __syncthreads();
             store_ud<Tin, SOFTPLUS, HAS_BIAS>(s_ud, ru, rd, bias_r, tn, nrow_b);
             rbc.store(s_bc, tn);
+            // with z (and no out_z recompute) the gate is folded here, once per element instead of once
+            // per lane per step: s_zg = (F, g) with g = dout silu(z) and F = dout sg (1 + z (1 - sg)),
+            // so dz = out F in the replay; otherwise s_zg = (z, dout)
 #pragma unroll
-            for (int i = 0; i < RPT; ++i)
-                *reinterpret_cast<float2*>(&s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane]) =
-                    make_float2(HAS_Z ? rz.get(i, tn, nrow_b) : 0.f, rg.get(i, tn, nrow_b));
+            for (int i = 0; i < RPT; ++i) {
+                const float zv = HAS_Z ? rz.get(i, tn, nrow_b) : 0.f, gd = rg.get(i, tn, nrow_b);
+                float2 v = make_float2(zv, gd);
+                if (HAS_Z && fold_gate) {
+                    const float sg = sigmoidf_(zv);
+                    v = make_float2(gd * sg * (1.f + zv * (1.f - sg)), gd * zv * sg);
+                }
+                *reinterpret_cast<float2*>(&s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane]) = v;
+            }
         }
         __syncthreads();
 
@@ -435,7 +441,10 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
                                 float* zg_p = &s_zg[id.c * Z_STRIDE + 2 * t];
                                 const float2 zg = *reinterpret_cast<const float2*>(zg_p);
                                 float gv, dzv = 0.f, oz = out;
-                                if (HAS_Z) {
+                                if (HAS_Z && fold_gate) {
+                                    dzv = out * zg.x;
+                                    gv = zg.y;
+                                } else if (HAS_Z) {
                                     const float sg = sigmoidf_(zg.x);
                                     const float sl = zg.x * sg;
                                     gv = zg.y * sl;
@@ -478,7 +487,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
                                 lam[p] = lam[p] * dAn[p] + gv2 * cp[p];
                                 const f2_t lhp = lam[p] * dA * hp;
                                 const f2_t lb = lam[p] * bp[p];
-                                ddt2 += Av[p] * lhp + lb * uu2;
+                                ddt2 += Av[p] * lhp;            // + u * sum(lb) once per lane, below
                                 dus2 += lb;
                                 dA_acc[p] += dt2 * lhp;
                                 const f2_t pb = lam[p] * dtu2, pc = gv2 * hist[i][p];
@@ -488,8 +497,8 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
                                 part[4 + 2 * p + 1] = pc.y;
                                 dAn[p] = dA;
                             }
-                            float ddt = group_sum<G>(ddt2.x + ddt2.y);
-                            float dus = group_sum<G>(dus2.x + dus2.y);
+                            const float dus = group_sum<G>(dus2.x + dus2.y);
+                            const float ddt = group_sum<G>(ddt2.x + ddt2.y) + uu * dus;
                             const float du = dus * dt + gv * Dv;
                             const float sig = SOFTPLUS ? (1.f - fast_exp(-dt)) : 1.f;
                             const float ddr = ddt * sig;
@@ -500,11 +509,14 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     #pragma unroll
                             for (int j = 0; j < 8; ++j) part[j] = 0.f;
                         }
-                        const float r = rs8(part, id.lane);
-                        if (id.lane < 32) {
-                            const int vi = ((id.lane >> 2) & 1) * 4 + ((id.lane >> 3) & 1) * 2 + ((id.lane >> 4) & 1);
-                            const int slot = (vi < 4 ? 0 : NSTATE) + id.g * NS + (vi & 3);
-                            s_red[(id.wave * RED + (i & (RED - 1))) * 2 * NSTATE + slot] = r;
+                        float r2[2];
+                        rs8_swap(part, r2);
+                        if ((id.lane & 12) == 0) {
+                            // vi = 4 b5 + 2 b4 + j: slot = (b5 ? C : B) + g * 4 + 2 b4 + j
+                            const int slot = ((id.lane >> 5) & 1) * NSTATE + id.g * NS + ((id.lane >> 4) & 1) * 2;
+                            float* dst = &s_red[(id.wave * RED + (i & (RED - 1))) * 2 * NSTATE + slot];
+                            dst[0] = r2[0];
+                            dst[1] = r2[1];
                         }
                         if ((i & (RED - 1)) == 0) {
                             // cross-wave sum of steps ts+i .. ts+i+RED-1 -> partial slab
