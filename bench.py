@@ -44,9 +44,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba", "avse4"])
+    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba", "avse4", "dpmamba"])
     p.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the BASELINE config's)")
-    p.add_argument("--size", default="L", choices=["XS", "S", "M", "L"], help="Mamba-TasNet size")
+    p.add_argument("--size", default="L", choices=["XS", "S", "M", "L"], help="Mamba-TasNet / DPMamba size")
     p.add_argument("--lip-hw", type=int, default=96)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
@@ -218,6 +218,53 @@ class MambaStep:
         return {"value": round(1.0 / dt, 6), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
                 "sample": f"oracle/mamba_ref forward of 1 of {n_layers} BiMamba layers on one 4 s utterance, "
                           f"scaled x{n_layers} (forward only; the training step is >=3x slower)"}
+
+
+class DPMambaStep(MambaStep):
+    """DPMamba: the same BiMamba kernels on 250-frame chunks (intra) and across chunks
+    (inter); 4 s @ 8 kHz WSJ0-2mix-shaped mixtures, PIT SI-SNR, bwd, Adam."""
+
+    def __init__(self, B, dev, rank, world, size):
+        from avse_challenge_amd import data, dpmamba, losses
+        self.B, self.size = B, size
+        self.model = dpmamba.DPMambaTasNet(**dpmamba.DPMAMBA_SIZES[size]).to(dev).train()
+        self.lr, self.clip = 1.5e-4, 5.0
+        self.mix, self.tgt = data.wsj0mix_batch(B, dev, 4321 + rank)
+        self.losses = losses
+
+    def config(self, world):
+        return {"workload": f"DPMamba-{self.size} train step (SURVEY 8f row 2; dpmamba_{self.size}.yaml)",
+                "global_batch": self.B * world, "per_gpu_batch": self.B, "seq_len": 32000, "frames": 3999,
+                "chunk_size": 250, "chunks": 34, "parallelism": f"dp{world}"}
+
+    def roofline(self, dev):
+        """Intra-chunk selective scan fwd at the step's shape: (B*34 chunks, d_inner, 250)."""
+        from avse_challenge_amd import kernels as K
+        d = 2 * self.model.masknet.dual_mdl[0].intra_mdl.layers[0].mixer.d_model
+        b, l = self.B * 34, 250
+        u, dl, z = (torch.randn(b, d, l, device=dev) for _ in range(3))
+        dl.mul_(0.1)
+        A = -torch.rand(d, 16, device=dev) - 0.5
+        Bm, Cm = torch.randn(b, 16, l, device=dev), torch.randn(b, 16, l, device=dev)
+        D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
+        return _time_hbm(lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False),
+                         4.0 * b * l * (4 * d + 2 * 16), f"avse_scan_fwd (DPMamba intra, {b} x {d} x {l}, training fwd)")
+
+    def cpu_baseline(self):
+        from oracle import dpmamba_ref
+        torch.set_num_threads(max(1, min(len(os.sched_getaffinity(0)), 64)))
+        kw = dict(dpmamba_ref.DPMAMBA_SIZES[self.size])
+        n_dp = kw.pop("n_dp")
+        m = dpmamba_ref.DPMambaTasNet(n_dp=1, **kw)
+        g = torch.Generator().manual_seed(0)
+        mix = 0.1 * torch.randn(1, 32000, generator=g)
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            m(mix)
+        dt = (time.perf_counter() - t0) * n_dp
+        return {"value": round(1.0 / dt, 6), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
+                "sample": f"oracle/dpmamba_ref forward with 1 of {n_dp} dual-path layers on one 4 s utterance, "
+                          f"scaled x{n_dp} (forward only)"}
 
 
 class Avse4Step:
@@ -408,6 +455,9 @@ def main():
     elif args.workload == "avse4":
         B = args.batch or 16
         step = Avse4Step(B, dev, rank, world)
+    elif args.workload == "dpmamba":
+        B = args.batch or 32
+        step = DPMambaStep(B, dev, rank, world, args.size)
     else:
         B = args.batch or 64
         step = MambaStep(B, dev, rank, world, args.size)
@@ -462,7 +512,8 @@ def main():
     if rank == 0:
         value = world * B * args.steps / dt
         rec = {"metric": {"avse1": METRIC, "mamba": "utterances/sec (4s@8kHz WSJ0-2mix, Mamba-TasNet)",
-                          "avse4": "utterances/sec (5s@16kHz binaural + 125 lip frames, avse4)"}[args.workload],
+                          "avse4": "utterances/sec (5s@16kHz binaural + 125 lip frames, avse4)",
+                          "dpmamba": "utterances/sec (4s@8kHz WSJ0-2mix, DPMamba)"}[args.workload],
                "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "fp32",

@@ -13,3 +13,26 @@ def test_avse4_upsample_matrix_matches_interpolate_and_pad(n_in, K):
     ref = F.pad(F.interpolate(v, 32 * n_in, mode="linear"), (0, K - 32 * n_in))
     got = v @ _upsample_matrix(n_in, 32, K, v.device).double()
     assert torch.allclose(got, ref, atol=1e-12, rtol=0)
+
+
+@pytest.mark.parametrize("L,K", [(3999, 250), (499, 250), (250, 250), (7, 4)])
+def test_dpmamba_segmentation_overlap_add(L, K):
+    """Dual-path chunking (50 % overlap, zero padding) and its overlap-add: every frame lands in exactly two
+    chunks, so over_add(segment(x)) == 2 x; the chunk tensor equals the oracle's speechbrain restatement."""
+    from avse_challenge_amd.dpmamba import DualPathModel
+    from oracle.dpmamba_ref import Dual_Path_Model
+    x = torch.randn(2, 3, L, dtype=torch.float64)
+    seg, gap = DualPathModel._segmentation(x, K)
+    ref_mod = Dual_Path_Model.__new__(Dual_Path_Model)
+    seg_r, gap_r = ref_mod._Segmentation(x, K)
+    assert gap == gap_r and torch.equal(seg, seg_r)
+    assert torch.allclose(DualPathModel._over_add(seg, gap), 2 * x, atol=0, rtol=0)
+
+
+def test_dpmamba_state_dict_keys_match_oracle():
+    from avse_challenge_amd.dpmamba import DPMAMBA_SIZES, DPMambaTasNet
+    from oracle.dpmamba_ref import DPMambaTasNet as Ref
+    for kw in ({"N": 64, "n_dp": 2}, {**DPMAMBA_SIZES["XS"], "n_dp": 1}):
+        a = {k: tuple(v.shape) for k, v in DPMambaTasNet(**kw).state_dict().items()}
+        b = {k: tuple(v.shape) for k, v in Ref(**kw).state_dict().items()}
+        assert a == b
