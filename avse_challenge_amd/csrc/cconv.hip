@@ -134,14 +134,140 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const float*
     }
 }
 
-__global__ void reduce_kernel(const float* ws, int batch, int D, int W, float* dw, float* db) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= D * (W + 1)) return;
-    const int d = i / (W + 1), k = i % (W + 1);
-    float v = 0.f;
-    for (int b = 0; b < batch; ++b) v += ws[((int64_t)b * D + d) * (MAXW + 1) + k];
-    if (k < W) dw[d * W + k] = v;
-    else if (db) db[d] = v;
+// ---------------------------------------------------------------- short rows (L <= SHORT_L)
+// DPMamba's chunked sequences (intra L = 250, inter L = 34) would leave a 2048-wide row tile almost
+// empty: here each wave owns one row, held whole in a wave-private LDS line with its (W-1) halo; a
+// workgroup is 4 independent rows.
+constexpr int SHORT_L = 256;
+constexpr int SPAD = SHORT_L + 2 * MAXW;
+
+template <int W, bool SILU, bool HAS_BIAS>
+__global__ __launch_bounds__(THREADS) void fwd_short_kernel(int rows, int D, int L, const float* __restrict__ x,
+                                                            int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float* __restrict__ out,
+                                                            int64_t o_bs, int64_t o_ds, int rev) {
+    __shared__ float s[4][SPAD];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + wave;
+    if (row >= rows) return;                       // no workgroup barrier below: rows are wave-private
+    const int b = row / D, d = row % D;
+    const float* xr = x + b * x_bs + (int64_t)d * x_ds;
+    float* orow = out + b * o_bs + (int64_t)d * o_ds;
+    float* sw = s[wave];
+    for (int i = lane; i < L + W - 1; i += 64) {   // sw[i] = x[i - (W-1)]
+        const int t = i - (W - 1);
+        sw[i] = t >= 0 ? xr[rev ? L - 1 - t : t] : 0.f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float wk[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
+    const float bv = HAS_BIAS ? bias[d] : 0.f;
+    for (int t = lane; t < L; t += 64) {
+        float acc = bv;
+#pragma unroll
+        for (int k = 0; k < W; ++k) acc += wk[k] * sw[t + k];
+        orow[rev ? L - 1 - t : t] = SILU ? siluf_(acc) : acc;
+    }
+}
+
+template <int W, bool SILU, bool HAS_BIAS>
+__global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int L, const float* __restrict__ x,
+                                                            int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ dout, int64_t g_bs, int64_t g_ds,
+                                                            float* __restrict__ dx, int64_t dx_bs, int64_t dx_ds,
+                                                            float* __restrict__ ws, int rev) {
+    __shared__ float sx[4][SPAD];
+    __shared__ float sg[4][SPAD];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + wave;
+    if (row >= rows) return;
+    const int b = row / D, d = row % D;
+    const float* xr = x + b * x_bs + (int64_t)d * x_ds;
+    const float* gr = dout + b * g_bs + (int64_t)d * g_ds;
+    float* dxr = dx + b * dx_bs + (int64_t)d * dx_ds;
+    float wk[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
+    const float bv = HAS_BIAS ? bias[d] : 0.f;
+    float* px = sx[wave];
+    float* pg = sg[wave];
+    for (int i = lane; i < L + 2 * (W - 1); i += 64) {     // px[i] = x[i - (W-1)]
+        const int t = i - (W - 1);
+        px[i] = (t >= 0 && t < L) ? xr[rev ? L - 1 - t : t] : 0.f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int i = lane; i < L + W - 1; i += 64) {           // pg[i] = dpre[i]
+        float g = 0.f;
+        if (i < L) {
+            g = gr[rev ? L - 1 - i : i];
+            if (SILU) {
+                float pre = bv;
+#pragma unroll
+                for (int k = 0; k < W; ++k) pre += wk[k] * px[i + k];
+                const float sgm = sigmoidf_(pre);
+                g *= sgm * (1.f + pre * (1.f - sgm));
+            }
+        }
+        pg[i] = g;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float dw[W], db = 0.f;
+#pragma unroll
+    for (int k = 0; k < W; ++k) dw[k] = 0.f;
+    for (int t = lane; t < L; t += 64) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < W; ++k) acc += wk[k] * pg[t + (W - 1) - k];
+        dxr[rev ? L - 1 - t : t] = acc;
+        const float g = pg[t];
+        db += g;
+#pragma unroll
+        for (int k = 0; k < W; ++k) dw[k] += g * px[t + k];
+    }
+#pragma unroll
+    for (int k = 0; k <= W; ++k) {
+        float v = (k < W) ? dw[k] : db;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+        if (lane == 0) ws[(int64_t)row * (MAXW + 1) + k] = v;
+    }
+}
+
+// dweight / dbias: per-row partials summed over the batch, one workgroup per channel (deterministic:
+// fixed per-thread strides, then a fixed tree)
+__global__ __launch_bounds__(THREADS) void reduce_kernel(const float* ws, int batch, int D, int W, float* dw, float* db) {
+    __shared__ float red[THREADS / 64][MAXW + 1];
+    const int d = blockIdx.x;
+    float v[MAXW + 1];
+#pragma unroll
+    for (int k = 0; k <= MAXW; ++k) v[k] = 0.f;
+    for (int b = threadIdx.x; b < batch; b += THREADS) {
+        const float* p = ws + ((int64_t)b * D + d) * (MAXW + 1);
+#pragma unroll
+        for (int k = 0; k <= MAXW; ++k) v[k] += p[k];
+    }
+#pragma unroll
+    for (int k = 0; k <= MAXW; ++k) {
+        float t = v[k];
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][k] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x <= W) {
+        const int k = threadIdx.x;
+        const float t = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+        if (k < W) dw[d * W + k] = t;
+        else if (db) db[d] = t;
+    }
 }
 
 }  // namespace cconv
@@ -164,6 +290,27 @@ int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, co
     if (batch * dim > (1LL << 31) - 1) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)(batch * dim)), block(THREADS);
+    if (seqlen <= SHORT_L) {
+        const int rows = (int)(batch * dim);
+        dim3 g4((unsigned)((rows + 3) / 4));
+        switch ((int)width) {
+#define SCASE(WW)                                                                                              \
+    case WW:                                                                                                   \
+        if (silu) {                                                                                            \
+            if (bias) hipLaunchKernelGGL((fwd_short_kernel<WW, true, true>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
+            else hipLaunchKernelGGL((fwd_short_kernel<WW, true, false>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
+        } else {                                                                                               \
+            if (bias) hipLaunchKernelGGL((fwd_short_kernel<WW, false, true>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
+            else hipLaunchKernelGGL((fwd_short_kernel<WW, false, false>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
+        }                                                                                                      \
+        break;
+            SCASE(1) SCASE(2) SCASE(3) SCASE(4)
+#undef SCASE
+            default: return AVSE_ESHAPE;
+        }
+        AVSE_CHECK_LAUNCH();
+        return AVSE_OK;
+    }
     switch ((int)width) {
 #define CASE(WW)                                                                                               \
     case WW:                                                                                                   \
@@ -192,6 +339,25 @@ int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, co
     if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)(batch * dim)), block(THREADS);
+    if (seqlen <= SHORT_L) {
+        const int rows = (int)(batch * dim);
+        dim3 g4((unsigned)((rows + 3) / 4));
+        switch ((int)width) {
+#define SCASE(WW)                                                                                              \
+    case WW:                                                                                                   \
+        if (silu) {                                                                                            \
+            if (bias) hipLaunchKernelGGL((bwd_short_kernel<WW, true, true>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
+            else hipLaunchKernelGGL((bwd_short_kernel<WW, true, false>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
+        } else {                                                                                               \
+            if (bias) hipLaunchKernelGGL((bwd_short_kernel<WW, false, true>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
+            else hipLaunchKernelGGL((bwd_short_kernel<WW, false, false>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
+        }                                                                                                      \
+        break;
+            SCASE(1) SCASE(2) SCASE(3) SCASE(4)
+#undef SCASE
+            default: return AVSE_ESHAPE;
+        }
+    } else {
     switch ((int)width) {
 #define CASE(WW)                                                                                               \
     case WW:                                                                                                   \
@@ -207,9 +373,9 @@ int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, co
 #undef CASE
         default: return AVSE_ESHAPE;
     }
+    }
     AVSE_CHECK_LAUNCH();
-    const int n = (int)(dim * (width + 1));
-    hipLaunchKernelGGL(reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, st, workspace, (int)batch, (int)dim,
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)dim), dim3(THREADS), 0, st, workspace, (int)batch, (int)dim,
                        (int)width, dweight, dbias);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;

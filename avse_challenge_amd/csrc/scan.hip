@@ -601,16 +601,36 @@ __global__ void reduce_bc_kernel(const float* ws, int nblk_d, int L, int batch, 
     }
 }
 
-// dA (d, n), dD (d), ddelta_bias (d): sum over batch
-__global__ void reduce_d_kernel(const float* ws_d, int batch, int D, float* dA, float* dD, float* dbias) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;     // over D * 18
-    if (i >= D * (NSTATE + 2)) return;
-    const int d = i / (NSTATE + 2), c = i % (NSTATE + 2);
-    float v = 0.f;
-    for (int b = 0; b < batch; ++b) v += ws_d[((int64_t)b * D + d) * (NSTATE + 2) + c];
-    if (c < NSTATE) dA[(int64_t)d * NSTATE + c] = v;
-    else if (c == NSTATE) { if (dD) dD[d] = v; }
-    else if (dbias) dbias[d] = v;
+// dA (d, n), dD (d), ddelta_bias (d): sum over batch — one workgroup per channel d, threads striding
+// over the batch (DPMamba's inter pass runs thousands of sequences), then a fixed tree (deterministic)
+__global__ __launch_bounds__(THREADS) void reduce_d_kernel(const float* ws_d, int batch, int D, float* dA, float* dD,
+                                                           float* dbias) {
+    constexpr int NV = NSTATE + 2;
+    __shared__ float red[THREADS / 64][NV];
+    const int d = blockIdx.x;
+    float v[NV];
+#pragma unroll
+    for (int c = 0; c < NV; ++c) v[c] = 0.f;
+    for (int b = threadIdx.x; b < batch; b += THREADS) {
+        const float* p = ws_d + ((int64_t)b * D + d) * NV;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) v[c] += p[c];
+    }
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+        float t = v[c];
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][c] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        const int c = threadIdx.x;
+        const float t = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+        if (c < NSTATE) dA[(int64_t)d * NSTATE + c] = t;
+        else if (c == NSTATE) { if (dD) dD[d] = t; }
+        else if (dbias) dbias[d] = t;
+    }
 }
 
 template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS>
@@ -703,8 +723,7 @@ int avse_scan_bwd(const avse_scan_bwd_args* a, avse_stream_t stream) {
     hipLaunchKernelGGL(reduce_bc_kernel, dim3(rb), dim3(256), 0, st, a->workspace, nblk_d, (int)a->seqlen,
                        (int)a->batch, (float*)a->dB, a->dB_bs, a->dB_ns, (float*)a->dC, a->dC_bs, a->dC_ns);
     AVSE_CHECK_LAUNCH();
-    const int nd = (int)(a->dim * (NSTATE + 2));
-    hipLaunchKernelGGL(reduce_d_kernel, dim3((nd + 255) / 256), dim3(256), 0, st, ws_d, (int)a->batch,
+    hipLaunchKernelGGL(reduce_d_kernel, dim3((unsigned)a->dim), dim3(THREADS), 0, st, ws_d, (int)a->batch,
                        (int)a->dim, a->dA, a->dD, a->ddelta_bias);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;

@@ -161,7 +161,7 @@ def test_scan_full_size_properties():
 
 @pytest.mark.parametrize("w", [2, 3, 4])
 @pytest.mark.parametrize("silu", [False, True])
-@pytest.mark.parametrize("b,d,l", [(2, 64, 1), (2, 40, 300), (1, 8, 4100)])
+@pytest.mark.parametrize("b,d,l", [(2, 64, 1), (3, 70, 34), (2, 33, 250), (1, 5, 256), (1, 5, 257), (2, 40, 300), (1, 8, 4100)])
 def test_cconv_vs_oracle(b, d, l, w, silu):
     x = det_input((b, d, l), 300 + l).double().requires_grad_(True)
     wt = det_input((d, w), 301).double().requires_grad_(True)
