@@ -28,6 +28,18 @@ def _wbmm(w, x):
     return torch.bmm(w.expand(x.shape[0], *w.shape), x)
 
 
+def _bsum_mm(a, bt):
+    """sum_b a[b] @ bt[b] for a (b, m, l), bt (b, l, n): the weight gradient of a batched projection.
+    As one strided-batched GEMM + sum while the (b, m, n) partials are small (Mamba-TasNet: b = batch);
+    as ONE (m, b*l) x (b*l, n) GEMM when they are not (DPMamba's inter pass has b = B*250 sequences of
+    34 frames: the partials would take 33 GB, and each GEMM's depth would be 34)."""
+    nb, m, l = a.shape
+    n = bt.shape[2]
+    if nb * m * n <= (1 << 27):
+        return torch.bmm(a, bt).sum(0)
+    return a.transpose(0, 1).reshape(m, nb * l) @ bt.reshape(nb * l, n)
+
+
 class MambaInnerNoOutProj(torch.autograd.Function):
     """Conv1d(k4)+SiLU -> x_proj -> dt_proj -> selective scan (z-gated); checkpoint_lvl 1.
 
@@ -72,8 +84,8 @@ class MambaInnerNoOutProj(torch.autograd.Function):
             conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, None, dz, True, False, reverse=rev,
             dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:])
         dx_dblT[:, :R] = _wbmm(dt_proj_w.t(), ddelta)
-        ddt_proj_w = torch.bmm(ddelta, x_dblT[:, :R].transpose(1, 2)).sum(0)     # (d, R)
-        dx_proj_w = torch.bmm(dx_dblT, conv_out.transpose(1, 2)).sum(0)          # (R + 2n, d)
+        ddt_proj_w = _bsum_mm(ddelta, x_dblT[:, :R].transpose(1, 2))               # (d, R)
+        dx_proj_w = _bsum_mm(dx_dblT, conv_out.transpose(1, 2))                    # (R + 2n, d)
         dconv.baddbmm_(x_proj_w.t().expand(dconv.shape[0], *x_proj_w.t().shape), dx_dblT)
         _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True, reverse=rev)
         return (dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias, None)
@@ -92,7 +104,7 @@ class _InProj(torch.autograd.Function):
     def backward(ctx, dxz):
         h, w = ctx.saved_tensors
         dh = torch.bmm(dxz.transpose(1, 2), w.expand(dxz.shape[0], *w.shape))
-        dw = torch.bmm(dxz, h).sum(0)
+        dw = _bsum_mm(dxz, h)
         return dh, dw
 
 
@@ -112,7 +124,7 @@ class _BiOutProj(torch.autograd.Function):
     def backward(ctx, dout):
         y, w = ctx.saved_tensors
         dy = _wbmm(0.5 * w.t(), dout.transpose(1, 2))                            # (b, d_inner, l)
-        dw = 0.5 * torch.bmm(dout.transpose(1, 2), y.transpose(1, 2)).sum(0)     # (d_model, d_inner)
+        dw = 0.5 * _bsum_mm(dout.transpose(1, 2), y.transpose(1, 2))               # (d_model, d_inner)
         return dy, dy, dw
 
 
