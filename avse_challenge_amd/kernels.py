@@ -277,6 +277,9 @@ def istft(mag, phase_spec, length):
 
 # ------------------------------------------------------------------------ lip front-end Conv3d dW
 
+CONV3D_WGRAD_MAX_WO = 64      # output width the MFMA kernel stages per LDS row (conv3d_wgrad.hip MAX_WO)
+
+
 def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
     """dW of Conv3d(Cin, 64, kernel_size, stride (1,2,2), padding, bias=False) -> (64, Cin, KT, KH, KW)."""
     _need_gpu(x, dy)

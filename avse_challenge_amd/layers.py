@@ -54,7 +54,12 @@ class _LipConv3dFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.nn.grad.conv3d_input(x.shape, w, dy, ctx.stride, ctx.padding)
-        dw = K.conv3d_wgrad(x, dy, tuple(w.shape[2:]), ctx.padding) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if dy.shape[-1] <= K.CONV3D_WGRAD_MAX_WO:
+                dw = K.conv3d_wgrad(x, dy, tuple(w.shape[2:]), ctx.padding)
+            else:   # wider frames (avse2's 224x224 lips -> 112 output columns): the library's GPU kernel
+                dw = torch.nn.grad.conv3d_weight(x, w.shape, dy, ctx.stride, ctx.padding)
         return dx, dw, None, None
 
 

@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba", "avse4", "dpmamba"])
+    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba", "avse4", "dpmamba", "avse2"])
     p.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the BASELINE config's)")
     p.add_argument("--size", default="L", choices=["XS", "S", "M", "L"], help="Mamba-TasNet / DPMamba size")
     p.add_argument("--lip-hw", type=int, default=96)
@@ -267,6 +267,37 @@ class DPMambaStep(MambaStep):
                           f"scaled x{n_dp} (forward only)"}
 
 
+class Avse2Step:
+    """avse2: time-domain AV separator, 3 s @ 16 kHz + 75 gray lip frames 224x224
+    (baseline/avse2/config.py), DPRNN separator, SI-SNR loss, batch 16 (train.py:28)."""
+    unit_desc = "3s@16kHz utterance + 75 lip frames 224x224"
+    graph_ok = False            # MIOpen LSTM: not capturable (as avse1)
+
+    def __init__(self, B, dev, rank, world):
+        from avse_challenge_amd import avse2, data
+        self.B = B
+        self.model = avse2.AVSEModule().to(dev).train()
+        self.lr, self.clip = self.model.lr, None
+        g = torch.Generator(device=dev).manual_seed(555 + rank)
+        noisy, clean, _ = data.avse1_batch(B, dev, 555 + rank, lip_hw=8)
+        self.batch = {"noisy_audio": noisy, "clean": clean,
+                      "video_frames": torch.rand((B, 1, 75, 224, 224), device=dev, generator=g)}
+
+    def loss(self):
+        return self.model.cal_loss(self.batch)
+
+    def config(self, world):
+        return {"workload": "avse2 AV separator train step (SURVEY 8f row 3): Swish ResNet-18 lip encoder + DPRNN "
+                            "(bidirectional LSTMs, K=200) fwd/bwd + Adam", "global_batch": self.B * world,
+                "per_gpu_batch": self.B, "seq_len": 48000, "lip_frames": 75, "lip_hw": 224, "parallelism": f"dp{world}"}
+
+    def roofline(self, dev):
+        return None
+
+    def cpu_baseline(self):
+        return None
+
+
 class Avse4Step:
     unit_desc = "5s@16kHz binaural utterance + 125 lip frames"
     graph_ok = True
@@ -455,6 +486,9 @@ def main():
     elif args.workload == "avse4":
         B = args.batch or 16
         step = Avse4Step(B, dev, rank, world)
+    elif args.workload == "avse2":
+        B = args.batch or 16
+        step = Avse2Step(B, dev, rank, world)
     elif args.workload == "dpmamba":
         B = args.batch or 32
         step = DPMambaStep(B, dev, rank, world, args.size)
@@ -513,7 +547,8 @@ def main():
         value = world * B * args.steps / dt
         rec = {"metric": {"avse1": METRIC, "mamba": "utterances/sec (4s@8kHz WSJ0-2mix, Mamba-TasNet)",
                           "avse4": "utterances/sec (5s@16kHz binaural + 125 lip frames, avse4)",
-                          "dpmamba": "utterances/sec (4s@8kHz WSJ0-2mix, DPMamba)"}[args.workload],
+                          "dpmamba": "utterances/sec (4s@8kHz WSJ0-2mix, DPMamba)",
+                          "avse2": "utterances/sec (3s@16kHz + 75 lip frames 224x224, avse2)"}[args.workload],
                "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "fp32",

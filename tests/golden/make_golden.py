@@ -29,7 +29,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 sys.path.insert(0, REPO)
 
-from oracle import avse1_ref, avse4_ref, losses_ref, mamba_ref  # noqa: E402
+from oracle import avse1_ref, avse2_ref, avse4_ref, losses_ref, mamba_ref  # noqa: E402
 from oracle.det_init import det_init_, det_input  # noqa: E402
 
 torch.set_num_threads(8)
@@ -492,12 +492,61 @@ def gen_avse1():
           {"pred": _maxabs(bb, a), "loss": abs(float(la) - float(lb))})
 
 
+# ============================================================================ avse2
+
+def gen_avse2():
+    m2 = _import_from("baseline/avse2", "model")
+    # DPRNN separator block (bidirectional LSTMs, K=20 chunks x S=5) fwd + every gradient
+    sb_r, sb_o = m2.SeparatorBlock(64, 128, bidirectional=True), avse2_ref.SeparatorBlock(64, 128, True)
+    _same_keys(sb_r, sb_o)
+    det_init_(sb_r, 81)
+    det_init_(sb_o, 81)
+    x = det_input((2, 64, 20, 5), 801).requires_grad_(True)
+    gy = det_input((2, 64, 20, 5), 802)
+    y_r = sb_r(x)
+    (y_r * gy).sum().backward()
+    grads = {"g_" + k.replace(".", "__"): p.grad.clone() for k, p in sb_r.named_parameters()}
+    gx = x.grad.clone()
+    x2 = x.detach().clone().requires_grad_(True)
+    y_o = sb_o(x2)
+    (y_o * gy).sum().backward()
+    gmax = max(_maxabs(p.grad, grads["g_" + k.replace(".", "__")]) for k, p in sb_o.named_parameters())
+    _save("avse2_sepblock", dict(x=x.detach(), gy=gy, y=y_r.detach(), gx=gx, **grads),
+          "SeparatorBlock(64, 128, bidirectional) model.py:88-123 (DPRNN intra/inter LSTM + Linear + GroupNorm), "
+          "fwd + grads, det_init seed 81", {"y": _maxabs(y_o, y_r), "gx": _maxabs(x2.grad, gx), "param_grads": gmax})
+
+    # full AVSEModule: 1 s @ 16 kHz (1999 encoder frames -> 20 chunks of 200) + 25 lip frames 64x64, eval
+    full_r, full_o = m2.AVSEModule(), avse2_ref.AVSEModule()
+    _same_keys(full_r, full_o)
+    det_init_(full_r, 82)
+    det_init_(full_o, 82)
+    full_r.eval()
+    full_o.eval()
+    batch = {"noisy_audio": 0.1 * det_input((2, 16000), 803), "video_frames": det_input((2, 1, 25, 64, 64), 804, "uniform"),
+             "clean": 0.1 * det_input((2, 16000), 805)}
+    with torch.no_grad():
+        a = full_r(batch)
+        la = full_r.cal_loss({k: v.clone() for k, v in batch.items()})
+        bb = full_o(batch)
+        lb = full_o.cal_loss({k: v.clone() for k, v in batch.items()})
+    _save("avse2_full", dict(out=a, loss=la, vis_checksum=batch["video_frames"].double().sum()),
+          "AVSEModule eval forward + cal_loss (SI-SNR clamp -30) on (2,16000) audio + (2,1,25,64,64) lips; inputs "
+          "det_input seeds 803-805 regenerated in tests; det_init seed 82",
+          {"out": _maxabs(bb, a), "loss": abs(float(la) - float(lb))})
+
+
 def main():
+    """python make_golden.py [case ...]: all cases, or only the named ones (merged into manifest.json)."""
+    global MANIFEST
     avse2_dnn = _install_stubs()
-    gen_losses(avse2_dnn)
-    gen_mamba()
-    gen_avse4()
-    gen_avse1()
+    gens = {"losses": partial(gen_losses, avse2_dnn), "mamba": gen_mamba, "avse4": gen_avse4, "avse1": gen_avse1,
+            "avse2": gen_avse2}
+    only = sys.argv[1:] or list(gens)
+    if sys.argv[1:]:
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            MANIFEST = json.load(f)
+    for name in only:
+        gens[name]()
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(MANIFEST, f, indent=1, sort_keys=True)
     print("total bytes", sum(v["bytes"] for v in MANIFEST.values()))

@@ -187,3 +187,28 @@ def test_stft_frame_count_and_roundtrip():
     k = np.arange(257)[:, None]
     dft = (stft_ref.hann_periodic() * frame * np.exp(-2j * np.pi * k * np.arange(512) / 512)).sum(1)
     np.testing.assert_allclose(S[:, 1], dft, atol=1e-4)
+
+
+def test_avse2_sepblock_and_full():
+    from oracle import avse2_ref
+    g = load_golden("avse2_sepblock")
+    sb = det_init_(avse2_ref.SeparatorBlock(64, 128, True), 81)
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
+    y = sb(x)
+    _close(y, g["y"], 1e-6)
+    (y * torch.from_numpy(g["gy"])).sum().backward()
+    _close(x.grad, g["gx"], 1e-5)
+    for k, p in sb.named_parameters():
+        key = "g_" + k.replace(".", "__")
+        if key in g:
+            _close(p.grad, g[key], 1e-4)
+        else:
+            _close(p.grad.reshape(-1)[::97], g[key + "__sub97"], 1e-4)
+    g = load_golden("avse2_full")
+    m = det_init_(avse2_ref.AVSEModule(), 82).eval()
+    batch = {"noisy_audio": 0.1 * det_input((2, 16000), 803), "video_frames": det_input((2, 1, 25, 64, 64), 804, "uniform"),
+             "clean": 0.1 * det_input((2, 16000), 805)}
+    assert abs(batch["video_frames"].double().sum().item() - float(g["vis_checksum"])) < 1e-6
+    with torch.no_grad():
+        _close(m(batch), g["out"], 1e-6)
+        _close(m.cal_loss(batch), g["loss"], 1e-5)
