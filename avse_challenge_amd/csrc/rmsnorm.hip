@@ -127,12 +127,22 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int rows, int n, const flo
     }
 }
 
-__global__ void reduce_kernel(const float* ws, int nblocks, int n, float* dw) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;
+// dweight = sum of the per-workgroup partials: 64 channels per workgroup (lane = channel, coalesced),
+// 16 row groups striding over the partials, then a fixed LDS tree (deterministic)
+__global__ __launch_bounds__(1024) void reduce_kernel(const float* ws, int nblocks, int n, float* dw) {
+    __shared__ float red[16][65];
+    const int c = blockIdx.x * 64 + threadIdx.x, gy = threadIdx.y;
     float v = 0.f;
-    for (int b = 0; b < nblocks; ++b) v += ws[(int64_t)b * n + c];
-    dw[c] = v;
+    if (c < n)
+        for (int b = gy; b < nblocks; b += 16) v += ws[(int64_t)b * n + c];
+    red[gy][threadIdx.x] = v;
+    __syncthreads();
+    if (gy == 0 && c < n) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+        dw[c] = t;
+    }
 }
 
 inline int nblocks_for(int64_t rows) {
@@ -169,7 +179,7 @@ int avse_rmsnorm_bwd(int64_t rows, int64_t n, const float* dy, const float* dres
     hipLaunchKernelGGL(bwd_kernel, dim3(nb), dim3(THREADS), 0, st, (int)rows, (int)n, dy, dres_out, res_out, weight,
                        rstd, dx, workspace);
     AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, nb, (int)n,
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64, 16), 0, st, workspace, nb, (int)n,
                        dweight);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
