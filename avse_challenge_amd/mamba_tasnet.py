@@ -20,6 +20,11 @@ import torch.nn.functional as F
 from . import kernels as K
 
 NSTATE = 16
+# bf16 autocast (BASELINE configs[4]): the projections then run as bf16 GEMMs and the conv / scan on bf16
+# activations with fp32 state, as mamba-ssm's custom_fwd / custom_bwd functions do
+# (selective_scan_interface.py:170-176); the backward runs under the forward's autocast state.
+_FWD = torch.amp.custom_fwd(device_type="cuda")
+_BWD = torch.amp.custom_bwd(device_type="cuda")
 
 
 def _wbmm(w, x):
@@ -30,14 +35,15 @@ def _wbmm(w, x):
 
 def _bsum_mm(a, bt):
     """sum_b a[b] @ bt[b] for a (b, m, l), bt (b, l, n): the weight gradient of a batched projection.
+    The result is fp32 (under bf16 autocast the partials are bf16 GEMM outputs summed in fp32).
     As one strided-batched GEMM + sum while the (b, m, n) partials are small (Mamba-TasNet: b = batch);
     as ONE (m, b*l) x (b*l, n) GEMM when they are not (DPMamba's inter pass has b = B*250 sequences of
     34 frames: the partials would take 33 GB, and each GEMM's depth would be 34)."""
     nb, m, l = a.shape
     n = bt.shape[2]
     if nb * m * n <= (1 << 27):
-        return torch.bmm(a, bt).sum(0)
-    return a.transpose(0, 1).reshape(m, nb * l) @ bt.reshape(nb * l, n)
+        return torch.bmm(a, bt).float().sum(0)
+    return (a.transpose(0, 1).reshape(m, nb * l) @ bt.reshape(nb * l, n)).float()
 
 
 class MambaInnerNoOutProj(torch.autograd.Function):
@@ -53,6 +59,7 @@ class MambaInnerNoOutProj(torch.autograd.Function):
     ``out_b.flip(-1)`` in natural time order."""
 
     @staticmethod
+    @_FWD
     def forward(ctx, xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias, reverse=False):
         R = dt_proj_w.shape[1]
         x, z = xz.chunk(2, dim=1)
@@ -69,6 +76,7 @@ class MambaInnerNoOutProj(torch.autograd.Function):
         return out_z
 
     @staticmethod
+    @_BWD
     def backward(ctx, dout):
         xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck = ctx.saved_tensors
         rev = ctx.reverse
@@ -79,14 +87,15 @@ class MambaInnerNoOutProj(torch.autograd.Function):
         Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]
         dxz = torch.empty_like(xz)
         dx, dz = dxz.chunk(2, dim=1)
-        dx_dblT = torch.empty_like(x_dblT)
+        dx_dblT = torch.empty(x_dblT.shape, device=x_dblT.device, dtype=torch.float32)   # scan writes fp32 dB/dC
         dconv, ddelta, dA, _, _, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
             conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, None, dz, True, False, reverse=rev,
             dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:])
         dx_dblT[:, :R] = _wbmm(dt_proj_w.t(), ddelta)
         ddt_proj_w = _bsum_mm(ddelta, x_dblT[:, :R].transpose(1, 2))               # (d, R)
         dx_proj_w = _bsum_mm(dx_dblT, conv_out.transpose(1, 2))                    # (R + 2n, d)
-        dconv.baddbmm_(x_proj_w.t().expand(dconv.shape[0], *x_proj_w.t().shape), dx_dblT)
+        wxt = x_proj_w.t().to(dconv.dtype)
+        dconv.baddbmm_(wxt.expand(dconv.shape[0], *wxt.shape), dx_dblT.to(dconv.dtype))
         _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True, reverse=rev)
         return (dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias, None)
 
@@ -96,11 +105,13 @@ class _InProj(torch.autograd.Function):
     layouts their consumers want: dh (b, l, d_model) contiguous, no transposed copies."""
 
     @staticmethod
+    @_FWD
     def forward(ctx, h, w):
         ctx.save_for_backward(h, w)
         return _wbmm(w, h.transpose(1, 2))
 
     @staticmethod
+    @_BWD
     def backward(ctx, dxz):
         h, w = ctx.saved_tensors
         dh = torch.bmm(dxz.transpose(1, 2), w.expand(dxz.shape[0], *w.shape))
@@ -114,6 +125,7 @@ class _BiOutProj(torch.autograd.Function):
     (b, d_inner, l) gradient to both directions (no 0.5-scaled copies)."""
 
     @staticmethod
+    @_FWD
     def forward(ctx, f, bk, w):
         y = f + bk
         ctx.save_for_backward(y, w)
@@ -121,6 +133,7 @@ class _BiOutProj(torch.autograd.Function):
         return torch.bmm(y.transpose(1, 2), wt.expand(y.shape[0], *wt.shape))
 
     @staticmethod
+    @_BWD
     def backward(ctx, dout):
         y, w = ctx.saved_tensors
         dy = _wbmm(0.5 * w.t(), dout.transpose(1, 2))                            # (b, d_inner, l)

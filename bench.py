@@ -10,6 +10,8 @@ A step = one pass of the hot path over one batch, inputs already resident in HBM
   mamba (C3):  Mamba-TasNet (XS/S/M/L) on B x 4 s @ 8 kHz mixtures -> PIT SI-SNR -> bwd -> Adam.
   avse4 (C4):  binaural AVSE4BaselineModule on B x 2ch x 5 s @ 16 kHz + 125 lip frames 112x112
                -> SI-SNR loss -> bwd -> Adam (C4: 16 per GPU).
+  avmamba (C5): Mamba-TasNet-L + avse4 lip encoder, bf16 autocast, B x 3 s @ 16 kHz (L = 5999) + 75 lip
+               frames 112x112 -> SI-SNR loss -> bwd -> Adam (C5: 32 per GPU).
 Rank 0 prints ONE JSON line (plus "roofline" for the dominant kernel, timed live with HIP
 events on torch's current stream, and "cpu_baseline": the oracle restatement on host cores).
 """
@@ -44,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba", "avse4", "dpmamba", "avse2"])
+    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba", "avse4", "dpmamba", "avse2", "avmamba"])
     p.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the BASELINE config's)")
     p.add_argument("--size", default="L", choices=["XS", "S", "M", "L"], help="Mamba-TasNet / DPMamba size")
     p.add_argument("--lip-hw", type=int, default=96)
@@ -265,6 +267,69 @@ class DPMambaStep(MambaStep):
         return {"value": round(1.0 / dt, 6), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
                 "sample": f"oracle/dpmamba_ref forward with 1 of {n_dp} dual-path layers on one 4 s utterance, "
                           f"scaled x{n_dp} (forward only)"}
+
+
+class AVMambaStep:
+    """C5 (BASELINE configs[4]): Mamba-TasNet-L conditioned on an avse4 lip encoder, bf16 autocast, 3 s @ 16 kHz
+    (L = 5999 encoder frames), 75 gray lip frames 112x112, SI-SNR loss, 32 utterances per GPU."""
+    unit_desc = "3s@16kHz utterance + 75 lip frames 112x112"
+    graph_ok = True
+    dtype = "bf16"
+
+    def __init__(self, B, dev, rank, world, size):
+        from avse_challenge_amd import avmamba, data
+        self.B, self.size = B, size
+        self.model = avmamba.AVMambaTasNet(**avmamba.AV_MAMBA_SIZES[size]).to(dev).train()
+        self.lr, self.clip = 1.5e-4, 5.0
+        g = torch.Generator(device=dev).manual_seed(999 + rank)
+        noisy, clean, _ = data.avse1_batch(B, dev, 999 + rank, lip_hw=8)
+        self.batch = {"noisy_audio": noisy, "clean": clean,
+                      "vis_feat": torch.rand((B, 1, 75, 112, 112), device=dev, generator=g)}
+
+    def loss(self):
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            return self.model.cal_loss(self.batch)
+
+    def config(self, world):
+        return {"workload": f"AV Mamba-TasNet-{self.size} train step (BASELINE configs[4]): avse4 lip encoder (fp32) + "
+                            "Mamba-TasNet separator under bf16 autocast (bf16 scan / conv activations, fp32 state)",
+                "global_batch": self.B * world, "per_gpu_batch": self.B, "seq_len": 48000, "frames": 5999,
+                "lip_frames": 75, "lip_hw": 112, "parallelism": f"dp{world}"}
+
+    def roofline(self, dev):
+        """Selective scan fwd at the step's shape, bf16 u/delta/z/B/C/out_z: (B, 1024, 5999)."""
+        from avse_challenge_amd import kernels as K
+        d = 2 * self.model.masknet.mamba_net.layers[0].mixer.d_model
+        b, l, bf = self.B, 5999, torch.bfloat16
+        u, z = torch.randn(b, d, l, device=dev, dtype=bf), torch.randn(b, d, l, device=dev, dtype=bf)
+        dl = (0.1 * torch.randn(b, d, l, device=dev)).to(bf)
+        A = -torch.rand(d, 16, device=dev) - 0.5
+        Bm, Cm = torch.randn(b, 16, l, device=dev, dtype=bf), torch.randn(b, 16, l, device=dev, dtype=bf)
+        D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
+        return _time_hbm(lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False),
+                         2.0 * b * l * (4 * d + 2 * 16), f"avse_scan_fwd (bf16, {b} x {d} x {l}, training fwd)")
+
+    def cpu_baseline(self):
+        """oracle/avmamba_ref forward (fp32) of one 3 s utterance: the whole model with 0 and with 1 BiMamba layer
+        timed, the per-layer time scaled to all n layers."""
+        from oracle import avmamba_ref
+        torch.set_num_threads(max(1, min(len(os.sched_getaffinity(0)), 64)))
+        kw = avmamba_ref.AV_MAMBA_SIZES[self.size]
+        m = avmamba_ref.AVMambaTasNet(**kw).eval()
+        layers = m.masknet.mamba_net.layers
+        g = torch.Generator().manual_seed(0)
+        mix, lips = 0.1 * torch.randn(1, 48000, generator=g), torch.rand(1, 1, 75, 112, 112, generator=g)
+        ts = []
+        with torch.no_grad():
+            for n in (0, 1):
+                m.masknet.mamba_net.layers = layers[:n]
+                t0 = time.perf_counter()
+                m(mix, lips)
+                ts.append(time.perf_counter() - t0)
+        dt = ts[0] + kw["n_mamba"] * max(ts[1] - ts[0], 0.0)
+        return {"value": round(1.0 / dt, 6), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
+                "sample": f"oracle/avmamba_ref fp32 forward of one 3 s utterance: front/back end {ts[0]:.2f} s + "
+                          f"{kw['n_mamba']} x one BiMamba layer ({ts[1] - ts[0]:.2f} s); forward only"}
 
 
 class Avse2Step:
@@ -489,6 +554,9 @@ def main():
     elif args.workload == "avse2":
         B = args.batch or 16
         step = Avse2Step(B, dev, rank, world)
+    elif args.workload == "avmamba":
+        B = args.batch or 32
+        step = AVMambaStep(B, dev, rank, world, args.size)
     elif args.workload == "dpmamba":
         B = args.batch or 32
         step = DPMambaStep(B, dev, rank, world, args.size)
@@ -548,10 +616,11 @@ def main():
         rec = {"metric": {"avse1": METRIC, "mamba": "utterances/sec (4s@8kHz WSJ0-2mix, Mamba-TasNet)",
                           "avse4": "utterances/sec (5s@16kHz binaural + 125 lip frames, avse4)",
                           "dpmamba": "utterances/sec (4s@8kHz WSJ0-2mix, DPMamba)",
-                          "avse2": "utterances/sec (3s@16kHz + 75 lip frames 224x224, avse2)"}[args.workload],
+                          "avse2": "utterances/sec (3s@16kHz + 75 lip frames 224x224, avse2)",
+                          "avmamba": "utterances/sec (3s@16kHz + 75 lip frames, AV Mamba-TasNet-L bf16)"}[args.workload],
                "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "scaling": "weak", "vs_baseline": None, "dtype": getattr(work, "dtype", "fp32"),
                "data": "synthetic (speech-like noise with 4 Hz envelope at SNR {0,3,6,9} dB, uint8 lips; "
                        "random-init weights)",
                "config": {**work.config(world), "hip_graph": graph, "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)},

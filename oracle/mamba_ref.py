@@ -54,12 +54,12 @@ def selective_scan(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_sof
     Bx, Cx = expand(B), expand(C)                      # (b, d|1, n, l)
     dA = torch.exp(dt[:, :, None, :] * A[None, :, :, None])     # (b, d, n, l)
     dBu = (dt * u)[:, :, None, :] * Bx                            # (b, d, n, l)
-    h = torch.zeros(b, d, n, dtype=acc_dtype)
+    h = torch.zeros(b, d, n, dtype=acc_dtype, device=u.device)
     ys = []
     for t in range(l):
         h = dA[..., t] * h + dBu[..., t]
         ys.append((h * Cx[..., t]).sum(-1))
-    y = torch.stack(ys, dim=-1) if l > 0 else torch.zeros(b, d, 0, dtype=acc_dtype)
+    y = torch.stack(ys, dim=-1) if l > 0 else torch.zeros(b, d, 0, dtype=acc_dtype, device=u.device)
     out = y if D is None else y + u * D.to(acc_dtype)[:, None]
     if z is not None:
         out = out * F.silu(z.to(acc_dtype))

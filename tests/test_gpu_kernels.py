@@ -72,6 +72,39 @@ def test_scan_fwd_golden_bf16():
     assert rel.max() <= 2 * 2 ** -8 + 1e-6, rel.max()   # within 2 bf16 ulp of the fp32-accumulated reference
 
 
+@pytest.mark.parametrize("reverse", [False, True])
+def test_scan_bwd_bf16_vs_oracle(reverse):
+    """bf16 u/delta/z/B/C/dout (C5): every gradient vs fp64 autograd through the oracle on the same bf16 values.
+    fp32 outputs (dA, dB, dC, dD, ddelta_bias) as tight as the fp32 test; bf16 outputs (du, ddelta, dz)
+    within one bf16 rounding (2^-8 relative) of the fp64 value plus 5e-5 of the tensor's scale."""
+    from oracle import mamba_ref
+    g = load_golden("scan_bf16")
+    bf = lambda k: g2t(g[k], torch.bfloat16)
+    ins = {k: bf(k) for k in ("u", "delta", "B", "C", "z")}
+    A, D, bias = g2t(g["A"]), g2t(g["D"]), g2t(g["delta_bias"])
+    dout = det_input(tuple(ins["u"].shape), 991).to(DEV).to(torch.bfloat16)
+    _, x, _ = K().selective_scan_fwd(ins["u"], ins["delta"], A, ins["B"], ins["C"], D, ins["z"], bias, True,
+                                     reverse=reverse, return_out=False)
+    du, ddelta, dA, dB, dC, dD, dbias, dz, _ = K().selective_scan_bwd(
+        ins["u"], ins["delta"], A, ins["B"], ins["C"], D, ins["z"], bias, dout, x, None, None, True, False,
+        reverse=reverse)
+    assert du.dtype == ddelta.dtype == dz.dtype == torch.bfloat16
+    fl = (lambda t: t.flip(-1)) if reverse else (lambda t: t)
+    r = {k: fl(v.double().cpu()).requires_grad_(True) for k, v in ins.items()}
+    rA, rD, rb = (t.double().cpu().requires_grad_(True) for t in (A, D, bias))
+    out_z = mamba_ref.selective_scan(r["u"], r["delta"], rA, r["B"], r["C"], rD, r["z"], rb, True,
+                                     acc_dtype=torch.float64)
+    out_z.backward(fl(dout.double().cpu()))
+    for name, v, ref, tol in (("du", du, fl(r["u"].grad), 2 ** -8), ("ddelta", ddelta, fl(r["delta"].grad), 2 ** -8),
+                              ("dz", dz, fl(r["z"].grad), 2 ** -8), ("dA", dA, rA.grad, 1e-4),
+                              ("dB", dB.reshape(r["B"].shape), fl(r["B"].grad), 1e-4),
+                              ("dC", dC.reshape(r["C"].shape), fl(r["C"].grad), 1e-4),
+                              ("dD", dD, rD.grad, 1e-4), ("ddelta_bias", dbias, rb.grad, 1e-4)):
+        ref = ref.detach().numpy()
+        scale = max(1.0, float(np.abs(ref).max()))
+        close(v.float(), ref, 5e-5 * scale, tol, name)
+
+
 # ------------------------------------------------------------------ selective scan: edge shapes vs oracle
 
 @pytest.mark.parametrize("b,d,l", [(1, 64, 1), (2, 64, 63), (1, 96, 65), (3, 130, 129), (1, 64, 200)])

@@ -36,3 +36,28 @@ def test_dpmamba_state_dict_keys_match_oracle():
         a = {k: tuple(v.shape) for k, v in DPMambaTasNet(**kw).state_dict().items()}
         b = {k: tuple(v.shape) for k, v in Ref(**kw).state_dict().items()}
         assert a == b
+
+
+@pytest.mark.parametrize("tv,L", [(5, 499), (75, 5999), (7, 7), (3, 10)])
+def test_avmamba_visual_upsampling_matrix_equals_interpolate(tv, L):
+    """C5 visual upsampling: the fixed (T_v, L) GEMM matrix == F.interpolate(linear) by ceil(L/T_v) + crop/pad,
+    the form the oracle assembly uses (oracle/avmamba_ref.py)."""
+    import math
+    import torch.nn.functional as F
+    from avse_challenge_amd import avse4
+    up = max(1, math.ceil(L / tv))
+    v = torch.randn(2, 3, tv, dtype=torch.float64)
+    ref = F.pad(F.interpolate(v, scale_factor=up, mode="linear", align_corners=False), (0, L - up * tv))
+    m = avse4._upsample_matrix(tv, up, L, "cpu").double()
+    torch.testing.assert_close(v @ m, ref, atol=1e-6, rtol=0)
+
+
+def test_avmamba_oracle_assembly_shapes_and_keys():
+    from oracle import avmamba_ref
+    m = avmamba_ref.AVMambaTasNet(N=32, n_mamba=1)
+    with torch.no_grad():
+        y = m(0.1 * torch.randn(1, 800), torch.rand(1, 1, 2, 112, 112))
+    assert y.shape == (1, 800)
+    from avse_challenge_amd import avmamba
+    assert list(dict(avmamba.AVMambaTasNet(N=32, n_mamba=1).named_parameters())) == \
+        list(dict(m.named_parameters()))
