@@ -62,9 +62,27 @@ constexpr int BPT = NSTATE * TC / THREADS;     // 4 B (and C) rows per thread
 
 __device__ inline int tpos(int t, int L, bool rev) { return rev ? L - 1 - t : t; }
 
+// Loaded values stay in the load's destination register until first use: for bf16 the raw 16-bit
+// pattern (zero-extended by buffer_load_u16) is widened to fp32 only where it is consumed, so the
+// prefetch of chunk k + 1 is not waited for right after it is issued (decoding at load time forced
+// s_waitcnt vmcnt(0) there: the bf16 forward ran 1.7x slower than fp32, profiles/r01_scan_study.txt).
+template <typename Tin> struct rawv;
+template <> struct rawv<float> {
+    using R = float;
+    __device__ static inline R ld(__amdgpu_buffer_rsrc_t r, int v, int s) { return bufld<float>::ld(r, v, s); }
+    __device__ static inline float f(R x) { return x; }
+};
+template <> struct rawv<bf16_t> {
+    using R = uint32_t;
+    __device__ static inline R ld(__amdgpu_buffer_rsrc_t r, int v, int s) {
+        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, v * 2, s * 2, 0);
+    }
+    __device__ static inline float f(R x) { return __uint_as_float(x << 16); }
+};
+
 template <typename Tin>
 struct RowRegs {
-    float v[RPT];
+    typename rawv<Tin>::R v[RPT];
     __device__ inline void load(const Tin* p, int64_t bs, int64_t ds, int b, int d0, int D, int t0, int tn, int L,
                                 bool rev) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -72,19 +90,20 @@ struct RowRegs {
         const auto rs = make_rsrc(p + b * bs + (int64_t)d0 * ds, (int64_t)(nrow - 1) * ds + L);
         const int voff = wave * (int)ds + tpos(t0 + lane, L, rev);
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) v[i] = bufld<Tin>::ld(rs, voff, 4 * i * (int)ds);   // raw: masked at use
+        for (int i = 0; i < RPT; ++i) v[i] = rawv<Tin>::ld(rs, voff, 4 * i * (int)ds);   // raw: masked at use
     }
+    __device__ inline float at(int i) const { return rawv<Tin>::f(v[i]); }
     // element i is real data iff the lane's step is inside the chunk and the row exists; the
     // select happens when the registers are consumed, so no wait is forced at load time
     __device__ inline float get(int i, int tn, int nrow) const {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        return (lane < tn && wave + 4 * i < nrow) ? v[i] : 0.f;
+        return (lane < tn && wave + 4 * i < nrow) ? at(i) : 0.f;
     }
 };
 
 template <typename Tin>
 struct BCRegs {
-    float bv[BPT], cv[BPT];
+    typename rawv<Tin>::R bv[BPT], cv[BPT];
     __device__ inline void load(const Tin* B, int64_t B_bs, int64_t B_ns, const Tin* C, int64_t C_bs, int64_t C_ns,
                                 int b, int t0, int tn, int L, bool rev) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -94,8 +113,8 @@ struct BCRegs {
         const int vb = wave * (int)B_ns + pos, vc = wave * (int)C_ns + pos;
 #pragma unroll
         for (int i = 0; i < BPT; ++i) {
-            bv[i] = bufld<Tin>::ld(rb, vb, 4 * i * (int)B_ns);
-            cv[i] = bufld<Tin>::ld(rc, vc, 4 * i * (int)C_ns);
+            bv[i] = rawv<Tin>::ld(rb, vb, 4 * i * (int)B_ns);
+            cv[i] = rawv<Tin>::ld(rc, vc, 4 * i * (int)C_ns);
         }
     }
     __device__ inline void store(float* s_bc, int tn) const {
@@ -103,8 +122,8 @@ struct BCRegs {
         const bool tv = lane < tn;
 #pragma unroll
         for (int i = 0; i < BPT; ++i) {
-            s_bc[lane * BC_STRIDE + wave + 4 * i] = tv ? bv[i] : 0.f;
-            s_bc[lane * BC_STRIDE + NSTATE + wave + 4 * i] = tv ? cv[i] : 0.f;
+            s_bc[lane * BC_STRIDE + wave + 4 * i] = tv ? rawv<Tin>::f(bv[i]) : 0.f;
+            s_bc[lane * BC_STRIDE + NSTATE + wave + 4 * i] = tv ? rawv<Tin>::f(cv[i]) : 0.f;
         }
     }
 };
@@ -118,11 +137,11 @@ __device__ inline void store_ud(float* s_ud, const RowRegs<Tin>& ru, const RowRe
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
         const bool ok = lane < tn && wave + 4 * i < nrow;
-        float dt = rd.v[i];
+        float dt = rd.at(i);
         if (HAS_BIAS) dt += bias_r[i];
         if (SOFTPLUS) dt = softplus(dt);
         *reinterpret_cast<float2*>(&s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]) =
-            make_float2(ok ? ru.v[i] : 0.f, ok ? dt : 0.f);
+            make_float2(ok ? ru.at(i) : 0.f, ok ? dt : 0.f);
     }
 }
 
@@ -258,7 +277,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                     for (int i = 0; i < RPT; ++i)
                         if (wave + 4 * i < nrow)
                             bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds,
-                                           s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane] * siluf_(rz.v[i]));
+                                           s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane] * siluf_(rz.at(i)));
                 }
             }
         }
