@@ -73,8 +73,12 @@ SIGNATURES = {
     "avse_cconv_bwd_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "avse_cconv_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                                c_i32, c_i32, c_vp]),
+    "avse_cconv_fwd_bf16": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                    c_i32, c_i32, c_vp]),
     "avse_cconv_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                                c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+    "avse_cconv_bwd_bf16": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                    c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "avse_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
     "avse_rmsnorm_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

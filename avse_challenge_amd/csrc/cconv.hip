@@ -5,7 +5,8 @@
 // /root/reference/Mamba-TasNet/modules/mamba/selective_scan_interface.py:182,244,286.
 // Semantics pinned by the in-tree fallback bimamba.py:278-279:
 //   out[b,d,t] = act(bias[d] + sum_k w[d,k] * x[b,d,t-(W-1)+k]),  x[<0] = 0.
-// One workgroup per (b, d) row; the row is streamed in TILE-sized pieces through LDS with a
+// x / out / dout / dx are fp32 or bf16 (T; fp32 arithmetic, weights fp32), as causal-conv1d's
+// kernels take the activation dtype under bf16 autocast.  One workgroup per (b, d) row; the row is streamed in TILE-sized pieces through LDS with a
 // (W-1)-sample halo so every HBM byte is read once with lane-contiguous accesses (HBM-bound:
 // fwd 2*4 B/elem, bwd 3*4 B/elem).  The backward reduces dweight/dbias per row in LDS and a
 // second kernel sums the per-row partials over the batch (deterministic).
@@ -21,16 +22,16 @@ constexpr int PER = 8;                     // elements per thread per tile
 constexpr int TILE = THREADS * PER;        // 2048
 constexpr int MAXW = 4;
 
-template <int W, bool SILU, bool HAS_BIAS>
-__global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const float* __restrict__ x, int64_t x_bs,
+template <typename T, int W, bool SILU, bool HAS_BIAS>
+__global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const T* __restrict__ x, int64_t x_bs,
                                                       int64_t x_ds, const float* __restrict__ w,
-                                                      const float* __restrict__ bias, float* __restrict__ out,
+                                                      const float* __restrict__ bias, T* __restrict__ out,
                                                       int64_t o_bs, int64_t o_ds, int rev) {
     __shared__ float s[TILE + MAXW];
     const int row = blockIdx.x;
     const int b = row / D, d = row % D;
-    const float* xr = x + b * x_bs + (int64_t)d * x_ds;
-    float* orow = out + b * o_bs + (int64_t)d * o_ds;
+    const T* xr = x + b * x_bs + (int64_t)d * x_ds;
+    T* orow = out + b * o_bs + (int64_t)d * o_ds;
     float wk[W];
 #pragma unroll
     for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const float*
         // s[i] holds x[t0 - (W-1) + i]
         for (int i = threadIdx.x; i < TILE + W - 1; i += THREADS) {
             const int t = t0 - (W - 1) + i;
-            s[i] = (t >= 0 && t < L) ? xr[rev ? L - 1 - t : t] : 0.f;
+            s[i] = (t >= 0 && t < L) ? io<T>::ld(&xr[rev ? L - 1 - t : t]) : 0.f;
         }
         __syncthreads();
 #pragma unroll
@@ -50,26 +51,26 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const float*
                 float acc = bv;
 #pragma unroll
                 for (int k = 0; k < W; ++k) acc += wk[k] * s[i + k];
-                orow[rev ? L - 1 - t : t] = SILU ? siluf_(acc) : acc;
+                io<T>::st(&orow[rev ? L - 1 - t : t], SILU ? siluf_(acc) : acc);
             }
         }
     }
 }
 
-template <int W, bool SILU, bool HAS_BIAS>
-__global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const float* __restrict__ x, int64_t x_bs,
+template <typename T, int W, bool SILU, bool HAS_BIAS>
+__global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __restrict__ x, int64_t x_bs,
                                                       int64_t x_ds, const float* __restrict__ w,
-                                                      const float* __restrict__ bias, const float* __restrict__ dout,
-                                                      int64_t g_bs, int64_t g_ds, float* __restrict__ dx,
+                                                      const float* __restrict__ bias, const T* __restrict__ dout,
+                                                      int64_t g_bs, int64_t g_ds, T* __restrict__ dx,
                                                       int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws, int rev) {
     __shared__ float sx[TILE + 2 * MAXW];
     __shared__ float sg[TILE + MAXW];
     __shared__ float sred[THREADS / 64][MAXW + 1];
     const int row = blockIdx.x;
     const int b = row / D, d = row % D;
-    const float* xr = x + b * x_bs + (int64_t)d * x_ds;
-    const float* gr = dout + b * g_bs + (int64_t)d * g_ds;
-    float* dxr = dx + b * dx_bs + (int64_t)d * dx_ds;
+    const T* xr = x + b * x_bs + (int64_t)d * x_ds;
+    const T* gr = dout + b * g_bs + (int64_t)d * g_ds;
+    T* dxr = dx + b * dx_bs + (int64_t)d * dx_ds;
     float wk[W];
 #pragma unroll
     for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
@@ -83,14 +84,14 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const float*
         // sx[i] = x[t0 - (W-1) + i], i in [0, TILE + 2(W-1)) ; sg[i] = dpre[t0 + i], i in [0, TILE + W - 1)
         for (int i = threadIdx.x; i < TILE + 2 * (W - 1); i += THREADS) {
             const int t = t0 - (W - 1) + i;
-            sx[i] = (t >= 0 && t < L) ? xr[rev ? L - 1 - t : t] : 0.f;
+            sx[i] = (t >= 0 && t < L) ? io<T>::ld(&xr[rev ? L - 1 - t : t]) : 0.f;
         }
         __syncthreads();
         for (int i = threadIdx.x; i < TILE + W - 1; i += THREADS) {
             const int t = t0 + i;
             float g = 0.f;
             if (t < L) {
-                g = gr[rev ? L - 1 - t : t];
+                g = io<T>::ld(&gr[rev ? L - 1 - t : t]);
                 if (SILU) {
                     float pre = bv;
 #pragma unroll
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const float*
                 float acc = 0.f;
 #pragma unroll
                 for (int k = 0; k < W; ++k) acc += wk[k] * sg[i + (W - 1) - k];
-                dxr[rev ? L - 1 - t : t] = acc;
+                io<T>::st(&dxr[rev ? L - 1 - t : t], acc);
                 const float g = sg[i];
                 db += g;
 #pragma unroll
@@ -141,22 +142,22 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const float*
 constexpr int SHORT_L = 256;
 constexpr int SPAD = SHORT_L + 2 * MAXW;
 
-template <int W, bool SILU, bool HAS_BIAS>
-__global__ __launch_bounds__(THREADS) void fwd_short_kernel(int rows, int D, int L, const float* __restrict__ x,
+template <typename T, int W, bool SILU, bool HAS_BIAS>
+__global__ __launch_bounds__(THREADS) void fwd_short_kernel(int rows, int D, int L, const T* __restrict__ x,
                                                             int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
-                                                            const float* __restrict__ bias, float* __restrict__ out,
+                                                            const float* __restrict__ bias, T* __restrict__ out,
                                                             int64_t o_bs, int64_t o_ds, int rev) {
     __shared__ float s[4][SPAD];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     if (row >= rows) return;                       // no workgroup barrier below: rows are wave-private
     const int b = row / D, d = row % D;
-    const float* xr = x + b * x_bs + (int64_t)d * x_ds;
-    float* orow = out + b * o_bs + (int64_t)d * o_ds;
+    const T* xr = x + b * x_bs + (int64_t)d * x_ds;
+    T* orow = out + b * o_bs + (int64_t)d * o_ds;
     float* sw = s[wave];
     for (int i = lane; i < L + W - 1; i += 64) {   // sw[i] = x[i - (W-1)]
         const int t = i - (W - 1);
-        sw[i] = t >= 0 ? xr[rev ? L - 1 - t : t] : 0.f;
+        sw[i] = t >= 0 ? io<T>::ld(&xr[rev ? L - 1 - t : t]) : 0.f;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -169,16 +170,16 @@ __global__ __launch_bounds__(THREADS) void fwd_short_kernel(int rows, int D, int
         float acc = bv;
 #pragma unroll
         for (int k = 0; k < W; ++k) acc += wk[k] * sw[t + k];
-        orow[rev ? L - 1 - t : t] = SILU ? siluf_(acc) : acc;
+        io<T>::st(&orow[rev ? L - 1 - t : t], SILU ? siluf_(acc) : acc);
     }
 }
 
-template <int W, bool SILU, bool HAS_BIAS>
-__global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int L, const float* __restrict__ x,
+template <typename T, int W, bool SILU, bool HAS_BIAS>
+__global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int L, const T* __restrict__ x,
                                                             int64_t x_bs, int64_t x_ds, const float* __restrict__ w,
                                                             const float* __restrict__ bias,
-                                                            const float* __restrict__ dout, int64_t g_bs, int64_t g_ds,
-                                                            float* __restrict__ dx, int64_t dx_bs, int64_t dx_ds,
+                                                            const T* __restrict__ dout, int64_t g_bs, int64_t g_ds,
+                                                            T* __restrict__ dx, int64_t dx_bs, int64_t dx_ds,
                                                             float* __restrict__ ws, int rev) {
     __shared__ float sx[4][SPAD];
     __shared__ float sg[4][SPAD];
@@ -186,9 +187,9 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
     const int row = blockIdx.x * 4 + wave;
     if (row >= rows) return;
     const int b = row / D, d = row % D;
-    const float* xr = x + b * x_bs + (int64_t)d * x_ds;
-    const float* gr = dout + b * g_bs + (int64_t)d * g_ds;
-    float* dxr = dx + b * dx_bs + (int64_t)d * dx_ds;
+    const T* xr = x + b * x_bs + (int64_t)d * x_ds;
+    const T* gr = dout + b * g_bs + (int64_t)d * g_ds;
+    T* dxr = dx + b * dx_bs + (int64_t)d * dx_ds;
     float wk[W];
 #pragma unroll
     for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
     float* pg = sg[wave];
     for (int i = lane; i < L + 2 * (W - 1); i += 64) {     // px[i] = x[i - (W-1)]
         const int t = i - (W - 1);
-        px[i] = (t >= 0 && t < L) ? xr[rev ? L - 1 - t : t] : 0.f;
+        px[i] = (t >= 0 && t < L) ? io<T>::ld(&xr[rev ? L - 1 - t : t]) : 0.f;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
     for (int i = lane; i < L + W - 1; i += 64) {           // pg[i] = dpre[i]
         float g = 0.f;
         if (i < L) {
-            g = gr[rev ? L - 1 - i : i];
+            g = io<T>::ld(&gr[rev ? L - 1 - i : i]);
             if (SILU) {
                 float pre = bv;
 #pragma unroll
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
         float acc = 0.f;
 #pragma unroll
         for (int k = 0; k < W; ++k) acc += wk[k] * pg[t + (W - 1) - k];
-        dxr[rev ? L - 1 - t : t] = acc;
+        io<T>::st(&dxr[rev ? L - 1 - t : t], acc);
         const float g = pg[t];
         db += g;
 #pragma unroll
@@ -274,6 +275,100 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(const float* ws, int ba
 }  // namespace avse
 
 using namespace avse::cconv;
+using avse::bf16_t;
+
+namespace {
+
+template <typename T, int W, bool S, bool HB>
+void launch_fwd(int64_t batch, int64_t dim, int64_t seqlen, const T* x, int64_t x_bs, int64_t x_ds, const float* w,
+                const float* bias, T* out, int64_t o_bs, int64_t o_ds, int rev, hipStream_t st) {
+    const int rows = (int)(batch * dim);
+    if (seqlen <= SHORT_L)
+        hipLaunchKernelGGL((fwd_short_kernel<T, W, S, HB>), dim3((unsigned)((rows + 3) / 4)), dim3(THREADS), 0, st,
+                           rows, (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, out, o_bs, o_ds, rev);
+    else
+        hipLaunchKernelGGL((fwd_kernel<T, W, S, HB>), dim3((unsigned)rows), dim3(THREADS), 0, st, (int)dim,
+                           (int)seqlen, x, x_bs, x_ds, w, bias, out, o_bs, o_ds, rev);
+}
+
+template <typename T, int W, bool S, bool HB>
+void launch_bwd(int64_t batch, int64_t dim, int64_t seqlen, const T* x, int64_t x_bs, int64_t x_ds, const float* w,
+                const float* bias, const T* dout, int64_t g_bs, int64_t g_ds, T* dx, int64_t dx_bs, int64_t dx_ds,
+                float* ws, int rev, hipStream_t st) {
+    const int rows = (int)(batch * dim);
+    if (seqlen <= SHORT_L)
+        hipLaunchKernelGGL((bwd_short_kernel<T, W, S, HB>), dim3((unsigned)((rows + 3) / 4)), dim3(THREADS), 0, st,
+                           rows, (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws,
+                           rev);
+    else
+        hipLaunchKernelGGL((bwd_kernel<T, W, S, HB>), dim3((unsigned)rows), dim3(THREADS), 0, st, (int)dim,
+                           (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws, rev);
+}
+
+// width / silu / bias -> template instance
+template <template <typename, int, bool, bool> class F, typename T, typename... Args>
+int dispatch(int64_t width, bool silu, bool has_bias, Args... args) {
+#define AVSE_CC(WW)                                                                          \
+    case WW:                                                                                 \
+        if (silu) {                                                                          \
+            if (has_bias) F<T, WW, true, true>::run(args...);                                \
+            else F<T, WW, true, false>::run(args...);                                        \
+        } else {                                                                             \
+            if (has_bias) F<T, WW, false, true>::run(args...);                               \
+            else F<T, WW, false, false>::run(args...);                                       \
+        }                                                                                    \
+        return AVSE_OK;
+    switch ((int)width) {
+        AVSE_CC(1) AVSE_CC(2) AVSE_CC(3) AVSE_CC(4)
+        default: return AVSE_ESHAPE;
+    }
+#undef AVSE_CC
+}
+
+template <typename T, int W, bool S, bool HB>
+struct Fwd {
+    template <typename... A> static void run(A... a) { launch_fwd<T, W, S, HB>(a...); }
+};
+template <typename T, int W, bool S, bool HB>
+struct Bwd {
+    template <typename... A> static void run(A... a) { launch_bwd<T, W, S, HB>(a...); }
+};
+
+template <typename T>
+int cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const T* x, int64_t x_bs, int64_t x_ds,
+              const float* weight, const float* bias, T* out, int64_t out_bs, int64_t out_ds, int32_t silu,
+              int32_t reverse, avse_stream_t stream) {
+    if (!x || !weight || !out) return AVSE_EINVAL;
+    if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
+    if (batch * dim > (1LL << 31) - 1) return AVSE_ESHAPE;
+    const int rc = dispatch<Fwd, T>(width, silu != 0, bias != nullptr, batch, dim, seqlen, x, x_bs, x_ds, weight, bias,
+                                    out, out_bs, out_ds, (int)reverse, (hipStream_t)stream);
+    if (rc != AVSE_OK) return rc;
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+template <typename T>
+int cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const T* x, int64_t x_bs, int64_t x_ds,
+              const float* weight, const float* bias, const T* dout, int64_t dout_bs, int64_t dout_ds, T* dx,
+              int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias, int32_t silu, int32_t reverse,
+              float* workspace, avse_stream_t stream) {
+    if (!x || !weight || !dout || !dx || !dweight || !workspace) return AVSE_EINVAL;
+    if (bias && !dbias) return AVSE_EINVAL;
+    if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
+    if (batch * dim > (1LL << 31) - 1) return AVSE_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    const int rc = dispatch<Bwd, T>(width, silu != 0, bias != nullptr, batch, dim, seqlen, x, x_bs, x_ds, weight, bias,
+                                    dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse, st);
+    if (rc != AVSE_OK) return rc;
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)dim), dim3(THREADS), 0, st, workspace, (int)batch, (int)dim,
+                       (int)width, dweight, dbias);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -285,100 +380,32 @@ int64_t avse_cconv_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t width
 int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const float* x, int64_t x_bs,
                    int64_t x_ds, const float* weight, const float* bias, float* out, int64_t out_bs, int64_t out_ds,
                    int32_t silu, int32_t reverse, avse_stream_t stream) {
-    if (!x || !weight || !out) return AVSE_EINVAL;
-    if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
-    if (batch * dim > (1LL << 31) - 1) return AVSE_ESHAPE;
-    hipStream_t st = (hipStream_t)stream;
-    dim3 grid((unsigned)(batch * dim)), block(THREADS);
-    if (seqlen <= SHORT_L) {
-        const int rows = (int)(batch * dim);
-        dim3 g4((unsigned)((rows + 3) / 4));
-        switch ((int)width) {
-#define SCASE(WW)                                                                                              \
-    case WW:                                                                                                   \
-        if (silu) {                                                                                            \
-            if (bias) hipLaunchKernelGGL((fwd_short_kernel<WW, true, true>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
-            else hipLaunchKernelGGL((fwd_short_kernel<WW, true, false>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
-        } else {                                                                                               \
-            if (bias) hipLaunchKernelGGL((fwd_short_kernel<WW, false, true>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
-            else hipLaunchKernelGGL((fwd_short_kernel<WW, false, false>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
-        }                                                                                                      \
-        break;
-            SCASE(1) SCASE(2) SCASE(3) SCASE(4)
-#undef SCASE
-            default: return AVSE_ESHAPE;
-        }
-        AVSE_CHECK_LAUNCH();
-        return AVSE_OK;
-    }
-    switch ((int)width) {
-#define CASE(WW)                                                                                               \
-    case WW:                                                                                                   \
-        if (silu) {                                                                                            \
-            if (bias) hipLaunchKernelGGL((fwd_kernel<WW, true, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
-            else hipLaunchKernelGGL((fwd_kernel<WW, true, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
-        } else {                                                                                               \
-            if (bias) hipLaunchKernelGGL((fwd_kernel<WW, false, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
-            else hipLaunchKernelGGL((fwd_kernel<WW, false, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, (int)reverse); \
-        }                                                                                                      \
-        break;
-        CASE(1) CASE(2) CASE(3) CASE(4)
-#undef CASE
-        default: return AVSE_ESHAPE;
-    }
-    AVSE_CHECK_LAUNCH();
-    return AVSE_OK;
+    return cconv_fwd<float>(batch, dim, seqlen, width, x, x_bs, x_ds, weight, bias, out, out_bs, out_ds, silu,
+                            reverse, stream);
 }
 
 int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const float* x, int64_t x_bs,
                    int64_t x_ds, const float* weight, const float* bias, const float* dout, int64_t dout_bs,
                    int64_t dout_ds, float* dx, int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias,
                    int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream) {
-    if (!x || !weight || !dout || !dx || !dweight || !workspace) return AVSE_EINVAL;
-    if (bias && !dbias) return AVSE_EINVAL;
-    if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
-    hipStream_t st = (hipStream_t)stream;
-    dim3 grid((unsigned)(batch * dim)), block(THREADS);
-    if (seqlen <= SHORT_L) {
-        const int rows = (int)(batch * dim);
-        dim3 g4((unsigned)((rows + 3) / 4));
-        switch ((int)width) {
-#define SCASE(WW)                                                                                              \
-    case WW:                                                                                                   \
-        if (silu) {                                                                                            \
-            if (bias) hipLaunchKernelGGL((bwd_short_kernel<WW, true, true>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
-            else hipLaunchKernelGGL((bwd_short_kernel<WW, true, false>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
-        } else {                                                                                               \
-            if (bias) hipLaunchKernelGGL((bwd_short_kernel<WW, false, true>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
-            else hipLaunchKernelGGL((bwd_short_kernel<WW, false, false>), g4, block, 0, st, rows, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
-        }                                                                                                      \
-        break;
-            SCASE(1) SCASE(2) SCASE(3) SCASE(4)
-#undef SCASE
-            default: return AVSE_ESHAPE;
-        }
-    } else {
-    switch ((int)width) {
-#define CASE(WW)                                                                                               \
-    case WW:                                                                                                   \
-        if (silu) {                                                                                            \
-            if (bias) hipLaunchKernelGGL((bwd_kernel<WW, true, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
-            else hipLaunchKernelGGL((bwd_kernel<WW, true, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
-        } else {                                                                                               \
-            if (bias) hipLaunchKernelGGL((bwd_kernel<WW, false, true>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
-            else hipLaunchKernelGGL((bwd_kernel<WW, false, false>), grid, block, 0, st, (int)dim, (int)seqlen, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse); \
-        }                                                                                                      \
-        break;
-        CASE(1) CASE(2) CASE(3) CASE(4)
-#undef CASE
-        default: return AVSE_ESHAPE;
-    }
-    }
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)dim), dim3(THREADS), 0, st, workspace, (int)batch, (int)dim,
-                       (int)width, dweight, dbias);
-    AVSE_CHECK_LAUNCH();
-    return AVSE_OK;
+    return cconv_bwd<float>(batch, dim, seqlen, width, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs,
+                            dx_ds, dweight, dbias, silu, reverse, workspace, stream);
+}
+
+int avse_cconv_fwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const uint16_t* x, int64_t x_bs,
+                        int64_t x_ds, const float* weight, const float* bias, uint16_t* out, int64_t out_bs,
+                        int64_t out_ds, int32_t silu, int32_t reverse, avse_stream_t stream) {
+    return cconv_fwd<bf16_t>(batch, dim, seqlen, width, (const bf16_t*)x, x_bs, x_ds, weight, bias, (bf16_t*)out,
+                             out_bs, out_ds, silu, reverse, stream);
+}
+
+int avse_cconv_bwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const uint16_t* x, int64_t x_bs,
+                        int64_t x_ds, const float* weight, const float* bias, const uint16_t* dout, int64_t dout_bs,
+                        int64_t dout_ds, uint16_t* dx, int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias,
+                        int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream) {
+    return cconv_bwd<bf16_t>(batch, dim, seqlen, width, (const bf16_t*)x, x_bs, x_ds, weight, bias,
+                             (const bf16_t*)dout, dout_bs, dout_ds, (bf16_t*)dx, dx_bs, dx_ds, dweight, dbias, silu,
+                             reverse, workspace, stream);
 }
 
 }  // extern "C"

@@ -164,42 +164,48 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
 # ------------------------------------------------------------------------ causal conv1d
 
 def causal_conv1d_fwd(x, weight, bias=None, silu=False, reverse=False):
+    """out = act(depthwise causal conv(x)) in x's dtype (fp32 or bf16; fp32 weights and arithmetic)."""
     _need_gpu(x, weight, bias)
-    in_dtype = x.dtype
-    x = _last_contig(x.float())
+    dt = x.dtype
+    _dtype_code(dt)
+    x = _last_contig(x)
     if weight.dim() == 3:
         weight = weight.reshape(weight.shape[0], -1)
     weight = weight.float().contiguous()
     bias = None if bias is None else bias.float().contiguous()
     b, d, l = x.shape
     w = weight.shape[1]
-    out = torch.empty((b, d, l), device=x.device, dtype=torch.float32)
-    check(_lib.lib().avse_cconv_fwd(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(out),
-                                    out.stride(0), out.stride(1), int(bool(silu)), int(bool(reverse)),
-                                    stream_ptr(x.device)), "avse_cconv_fwd")
-    return out if in_dtype == torch.float32 else out.to(in_dtype)
+    out = torch.empty((b, d, l), device=x.device, dtype=dt)
+    fn = _lib.lib().avse_cconv_fwd if dt == torch.float32 else _lib.lib().avse_cconv_fwd_bf16
+    check(fn(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(out), out.stride(0),
+             out.stride(1), int(bool(silu)), int(bool(reverse)), stream_ptr(x.device)), "avse_cconv_fwd")
+    return out
 
 
 def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False):
+    """[dx, dweight, dbias]: dx in x's dtype (fp32 or bf16; a passed ``dx`` view of that dtype with unit last
+    stride is written in place), dweight / dbias fp32."""
     _need_gpu(x, weight, bias, dout)
-    x = _last_contig(x.float())
+    dt = x.dtype
+    _dtype_code(dt)
+    x = _last_contig(x)
     wshape = weight.shape
     weight = weight.reshape(wshape[0], -1).float().contiguous()
     bias = None if bias is None else bias.float().contiguous()
-    dout = _last_contig(dout.float())
+    dout = _last_contig(dout.to(dt))
     b, d, l = x.shape
     w = weight.shape[1]
     dx_ret = dx
-    if dx is None or dx.dtype != torch.float32 or dx.stride(-1) != 1:
-        dx = torch.empty((b, d, l), device=x.device, dtype=torch.float32)
+    if dx is None or dx.dtype != dt or dx.stride(-1) != 1:
+        dx = torch.empty((b, d, l), device=x.device, dtype=dt)
     dweight = torch.empty((d, w), device=x.device, dtype=torch.float32)
     dbias = torch.empty((d,), device=x.device, dtype=torch.float32) if bias is not None else None
     ws = torch.empty((_lib.lib().avse_cconv_bwd_workspace_bytes(b, d, w) + 3) // 4, device=x.device,
                      dtype=torch.float32)
-    check(_lib.lib().avse_cconv_bwd(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(dout),
-                                    dout.stride(0), dout.stride(1), ptr(dx), dx.stride(0), dx.stride(1), ptr(dweight),
-                                    ptr(dbias), int(bool(silu)), int(bool(reverse)), ptr(ws), stream_ptr(x.device)),
-          "avse_cconv_bwd")
+    fn = _lib.lib().avse_cconv_bwd if dt == torch.float32 else _lib.lib().avse_cconv_bwd_bf16
+    check(fn(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(dout), dout.stride(0),
+             dout.stride(1), ptr(dx), dx.stride(0), dx.stride(1), ptr(dweight), ptr(dbias), int(bool(silu)),
+             int(bool(reverse)), ptr(ws), stream_ptr(x.device)), "avse_cconv_bwd")
     if dx_ret is not None and dx_ret is not dx:
         dx_ret.copy_(dx)
         dx = dx_ret

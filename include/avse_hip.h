@@ -114,6 +114,20 @@ int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
                    float* dx, int64_t dx_bs, int64_t dx_ds,
                    float* dweight /* (d, w) */, float* dbias /* (d) or NULL */,
                    int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream);
+/* bf16 activations (x, out, dout, dx as raw bf16 bit patterns; weights, bias and their gradients fp32;
+ * fp32 arithmetic): the dtype causal_conv1d_cuda sees under bf16 autocast (selective_scan_interface.py:182). */
+int avse_cconv_fwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
+                        const uint16_t* x, int64_t x_bs, int64_t x_ds,
+                        const float* weight, const float* bias,
+                        uint16_t* out, int64_t out_bs, int64_t out_ds, int32_t silu, int32_t reverse,
+                        avse_stream_t stream);
+int avse_cconv_bwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
+                        const uint16_t* x, int64_t x_bs, int64_t x_ds,
+                        const float* weight, const float* bias,
+                        const uint16_t* dout, int64_t dout_bs, int64_t dout_ds,
+                        uint16_t* dx, int64_t dx_bs, int64_t dx_ds,
+                        float* dweight, float* dbias,
+                        int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- add + RMSNorm -------
  * Replaces the Block pre-norm of Mamba-TasNet/modules/mamba/bimamba.py:447-451

@@ -212,6 +212,31 @@ def test_cconv_vs_oracle(b, d, l, w, silu):
     close(db, bias.grad, 1e-3, 1e-5, "dbias")
 
 
+@pytest.mark.parametrize("reverse", [False, True])
+@pytest.mark.parametrize("b,d,l", [(2, 33, 250), (2, 40, 3000)])
+def test_cconv_bf16_vs_oracle(b, d, l, reverse):
+    """bf16 activations (C5): fp64 oracle on the same bf16 values; out / dx within one bf16 rounding (2^-8 relative)
+    plus 1e-5, dweight / dbias (fp32 outputs) as tight as the fp32 test."""
+    bf = lambda t: t.to(torch.bfloat16).double()
+    fl = (lambda t: t.flip(-1)) if reverse else (lambda t: t)
+    x0, gy0 = bf(det_input((b, d, l), 310 + l)), bf(det_input((b, d, l), 311))
+    x = fl(x0).requires_grad_(True)
+    wt = det_input((d, 4), 312).double().requires_grad_(True)
+    bias = det_input((d,), 313).double().requires_grad_(True)
+    ref = mamba_ref.causal_conv1d(x, wt, bias, True)
+    ref.backward(fl(gy0))
+    xg = x0.to(DEV, torch.bfloat16)
+    out = K().causal_conv1d_fwd(xg, wt.detach().float().to(DEV), bias.detach().float().to(DEV), True, reverse=reverse)
+    assert out.dtype == torch.bfloat16
+    close(out.float(), fl(ref.detach()), 1e-5, 2 ** -8, "fwd")
+    dx, dw, db = K().causal_conv1d_bwd(xg, wt.detach().float().to(DEV), bias.detach().float().to(DEV),
+                                       gy0.to(DEV, torch.bfloat16), silu=True, reverse=reverse)
+    assert dx.dtype == torch.bfloat16 and dw.dtype == torch.float32
+    close(dx.float(), fl(x.grad), 1e-5, 2 ** -8, "dx")
+    close(dw, wt.grad, 1e-3, 1e-5, "dweight")
+    close(db, bias.grad, 1e-3, 1e-5, "dbias")
+
+
 # ------------------------------------------------------------------ add + RMSNorm
 
 @pytest.mark.parametrize("n", [32, 128, 512, 1024])
