@@ -12,6 +12,7 @@ The scan, the causal conv and the add+RMSNorm run in libavse_hip.so; the dense p
 are GEMMs (torch.matmul -> hipBLASLt MFMA).  No CPU fallback: CPU tensors raise.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -168,6 +169,20 @@ class RMSNorm(nn.Module):
         return AddRMSNorm.apply(x, residual, self.weight, self.eps)[0]
 
 
+_STREAMS = {}
+
+
+def _direction_stream(device):
+    """Second HIP stream for the v2 backward direction, one per device (default; AVSE_BIMAMBA_STREAMS=0 launches
+    the two directions serially on the current stream). Measured: Mamba-TasNet-L B=64 1443 -> 1402 ms/step,
+    C5 B=32 762 -> 727 ms/step."""
+    if device.type != "cuda" or os.environ.get("AVSE_BIMAMBA_STREAMS", "1") != "1":
+        return None
+    if device not in _STREAMS:
+        _STREAMS[device] = torch.cuda.Stream(device)
+    return _STREAMS[device]
+
+
 class BiMambaV2(nn.Module):
     """bimamba.Mamba(bimamba_type='v2', if_devide_out=True): same parameters and init."""
 
@@ -203,10 +218,28 @@ class BiMambaV2(nn.Module):
         xz = _InProj.apply(h, self.in_proj.weight)                               # (b, 2di, l), no copy
         A = -torch.exp(self.A_log.float())
         A_b = -torch.exp(self.A_b_log.float())
+        side = _direction_stream(xz.device)
+        if side is not None:
+            # the two directions are independent: the backward one runs on a second HIP stream, so its conv /
+            # projection / scan kernels fill the CUs the forward one leaves idle (the scan grid at B=32 is
+            # 512 workgroups for 768 slots). Autograd runs each direction's backward on the same stream.
+            main = torch.cuda.current_stream(xz.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                bk = MambaInnerNoOutProj.apply(xz, self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
+                                               self.dt_proj_b.weight, A_b, self.D_b.float(),
+                                               self.dt_proj_b.bias.float(), True)
+            xz.record_stream(side)
+            A_b.record_stream(side)
         f = MambaInnerNoOutProj.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
                                       self.dt_proj.weight, A, self.D.float(), self.dt_proj.bias.float())
-        bk = MambaInnerNoOutProj.apply(xz, self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
-                                       self.dt_proj_b.weight, A_b, self.D_b.float(), self.dt_proj_b.bias.float(), True)
+        if side is None:
+            bk = MambaInnerNoOutProj.apply(xz, self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
+                                           self.dt_proj_b.weight, A_b, self.D_b.float(), self.dt_proj_b.bias.float(),
+                                           True)
+        else:
+            main.wait_stream(side)
+            bk.record_stream(main)
         # == out_proj(0.5*out + 0.5*out_b.flip(-1)) of bimamba.py:253, flip-free, one batched GEMM
         return _BiOutProj.apply(f, bk, self.out_proj.weight)
 

@@ -300,3 +300,39 @@ def test_bench_trainer_graph_replay_equals_eager():
     np.testing.assert_allclose(l1, l0, rtol=1e-5, atol=1e-6)
     for a, b in zip(p0, p1):
         close(b, a, 1e-5, 1e-5)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_bimamba_direction_streams_equal_serial(monkeypatch, graph):
+    """AVSE_BIMAMBA_STREAMS=1 (backward direction on a second HIP stream, forward and backward; also inside the
+    captured HIP graphs of bench.Trainer) gives the same losses and weights as the serial launch order."""
+    import bench
+    from avse_challenge_amd import losses as PL
+    from avse_challenge_amd import mamba_tasnet as M
+
+    class Step:
+        def __init__(self):
+            self.model = det_init_(M.MambaTasNet(N=64, n_mamba=2), 91).to(DEV).train()
+            self.lr, self.clip = 1e-3, 5.0
+            self.mix = (0.1 * det_input((2, 4000), 911)).to(DEV)
+            self.tgt = (0.1 * det_input((2, 4000, 2), 912)).to(DEV)
+
+        def loss(self):
+            return PL.si_snr_pit(self.tgt, self.model(self.mix)).mean()
+
+    runs = []
+    for streams in ("0", "1"):
+        monkeypatch.setenv("AVSE_BIMAMBA_STREAMS", streams)
+        st = Step()
+        tr = bench.Trainer(st, 1, torch.device(DEV), use_graph=graph)
+        losses = [float(tr())]
+        if graph:
+            tr.capture()
+        for _ in range(3):
+            losses.append(float(tr()))
+        torch.cuda.synchronize()
+        runs.append((losses, [p.detach().clone() for p in st.model.parameters()]))
+    (l0, p0), (l1, p1) = runs
+    np.testing.assert_allclose(l1, l0, rtol=1e-6, atol=1e-7)
+    for a, b in zip(p0, p1):
+        torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-7)
