@@ -213,6 +213,13 @@ class AVNet(nn.Module):
     def configure_optimizers(self):
         return torch.optim.Adam(self.parameters(), lr=self.lr)
 
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, map_location="cpu", strict=True, **kwargs):
+        """test.py:47 `AVNet.load_from_checkpoint(ckpt_path, nets=..., ...)` (Lightning .ckpt, ckpt_io); the
+        reference's `nets=` argument is not a constructor argument here (the sub-nets are built in place)."""
+        from .ckpt_io import load_lightning_checkpoint
+        return load_lightning_checkpoint(cls, checkpoint_path, map_location, strict, **kwargs)
+
     # ---- HIP front-end / back-end (what the reference does on CPU with librosa)
     @staticmethod
     def features_from_waves(noisy, clean=None):

@@ -278,6 +278,12 @@ class AVSE4BaselineModule(nn.Module):
     def configure_optimizers(self):
         return torch.optim.Adam(self.parameters(), lr=self.lr)
 
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, map_location="cpu", strict=True, **kwargs):
+        """test.py:32 `AVSE4BaselineModule.load_from_checkpoint(cfg.ckpt_path)` (Lightning .ckpt, ckpt_io)."""
+        from .ckpt_io import load_lightning_checkpoint
+        return load_lightning_checkpoint(cls, checkpoint_path, map_location, strict, **kwargs)
+
     @torch.no_grad()
     def enhance(self, data):
         """model.py:335-352: forward one utterance and peak-normalise (returns numpy arrays)."""
