@@ -1,0 +1,48 @@
+"""GPU: the checkpoint / wav layer around the HIP path (avse_challenge_amd/ckpt_io.py).
+
+A model restored from either checkpoint format holds bit-identical weights and runs the HIP path to the same
+output (<= 1e-6) as the model that was saved, and an avse4 `enhance` output written as the reference's
+test.py writes it (`sf.write(path, est.T, 16000)`, `baseline/avse4/test.py:47`) reads back as the evaluation reads it (`objective_evaluation.py:23-35`).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.det_init import det_init_, det_input
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def test_speechbrain_checkpoint_restores_hip_forward(tmp_path):
+    from avse_challenge_amd import ckpt_io
+    from avse_challenge_amd.mamba_tasnet import MambaTasNet
+    m = det_init_(MambaTasNet(N=64, n_mamba=2), 31).to(DEV).eval()
+    d = ckpt_io.save_speechbrain_checkpoint(str(tmp_path), ckpt_io.speechbrain_modules(m), {"-si-snr": -9.0})
+    m2 = MambaTasNet(N=64, n_mamba=2)
+    ckpt_io.load_speechbrain_checkpoint(ckpt_io.find_speechbrain_checkpoint(str(tmp_path), min_key="-si-snr"),
+                                        ckpt_io.speechbrain_modules(m2))
+    m2 = m2.to(DEV).eval()
+    mix = (0.1 * det_input((2, 8000), 32)).to(DEV)
+    with torch.no_grad():
+        a, b = m(mix), m2(mix)
+    assert all(torch.equal(v, m2.state_dict()[k]) for k, v in m.state_dict().items())
+    assert a.shape == (2, 8000, 2) and torch.isfinite(a).all() and (a - b).abs().max().item() <= 1e-6
+
+
+def test_avse4_lightning_checkpoint_enhance_to_wav(tmp_path):
+    from avse_challenge_amd import avse4, ckpt_io, data
+    m = det_init_(avse4.AVSE4BaselineModule(num_channels=2), 33).to(DEV).eval()
+    p = ckpt_io.save_lightning_checkpoint(m, str(tmp_path / "best.ckpt"), {"lr": 1e-4, "num_channels": 2})
+    m2 = avse4.AVSE4BaselineModule.load_from_checkpoint(p).to(DEV).eval()
+    b = data.avse4_batch(1, "cpu", 12)
+    utt = {"noisy_audio": b["noisy_audio"][0], "vis_feat": b["vis_feat"][0], "clean": b["clean"][0]}
+    _, _, est = m.enhance(utt)
+    _, _, est2 = m2.enhance(utt)
+    assert all(torch.equal(v, m2.state_dict()[k]) for k, v in m.state_dict().items())
+    assert est.shape == (2, 80000) and np.abs(est - est2).max() <= 1e-6 and np.abs(est).max() == pytest.approx(1.0)
+    wav = ckpt_io.write_wav(os.path.join(tmp_path, "S00001.wav"), est.T, 16000)
+    back, sr = ckpt_io.read_wav(wav)
+    assert sr == 16000 and back.shape == (80000, 2) and np.abs(back - est.T).max() <= 1.5 / 32768
