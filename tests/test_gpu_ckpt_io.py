@@ -2,7 +2,8 @@
 
 A model restored from either checkpoint format holds bit-identical weights and runs the HIP path to the same
 output (<= 1e-6) as the model that was saved, and an avse4 `enhance` output written as the reference's
-test.py writes it (`sf.write(path, est.T, 16000)`, `baseline/avse4/test.py:47`) reads back as the evaluation reads it (`objective_evaluation.py:23-35`).
+test.py writes it (`sf.write(path, est.T, 16000)`, `baseline/avse4/test.py:47`) reads back as the
+evaluation reads it (`objective_evaluation.py:23-35`).
 """
 import os
 
