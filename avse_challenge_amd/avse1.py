@@ -230,10 +230,14 @@ class AVNet(nn.Module):
         return out
 
     @torch.no_grad()
-    def enhance(self, noisy_wave, lip_images, length=None):
-        """test.py:79-89: predicted magnitude x noisy phase -> iSTFT (all on the GPU)."""
+    def enhance(self, noisy_wave, lip_images=None, length=None):
+        """test.py:79-89: predicted magnitude x noisy phase -> iSTFT (all on the GPU); lip_images is
+        unused (None) for the audio-only net (test.py:81)."""
         mag, spec = K.stft(noisy_wave, return_complex=True)
-        pred = self({"noisy_audio_spec": mag.unsqueeze(1), "lip_images": lip_images})[:, 0]
+        inp = {"noisy_audio_spec": mag.unsqueeze(1)}
+        if not self.a_only:
+            inp["lip_images"] = lip_images
+        pred = self(inp)[:, 0]
         return K.istft(pred, spec, noisy_wave.shape[-1] if length is None else length)
 
 

@@ -1,0 +1,225 @@
+"""Batch-sharded data-parallel training step: one process per GPU, RCCL over xGMI.
+
+What Lightning DDP does for the reference (baseline/avse4/train.py:28-42 with conf/train.yaml:16-18 strategy
+ddp; Mamba-TasNet/train_wsj0mix.py:160,718 via SpeechBrain's DDP wrapper), rebuilt around one flat gradient
+buffer instead of DDP's reducer:
+  * every parameter's ``.grad`` is a view into ONE flat fp32 buffer; the buffer is cut into contiguous
+    buckets of ~``bucket_mb`` in reverse registration order (the order backward produces gradients);
+  * a post-accumulate-grad hook per parameter counts arrivals; the moment a bucket is complete its
+    all-reduce is launched asynchronously (RCCL runs it on its own stream after an event wait on the
+    stream that produced the gradients), so the exchange overlaps the rest of the backward;
+  * after backward the remaining buckets (parameters without a gradient this step) are launched, the
+    current stream waits for every collective, and the sum is scaled by 1/world (mean, as DDP);
+  * DDP's ``broadcast_buffers=True``: rank 0's buffers (BatchNorm running stats, num_batches_tracked) are
+    broadcast to every rank before each forward, as two flat tensors (floating / integer) that the modules'
+    buffers are views of; per-rank batch statistics otherwise (no SyncBN, as the reference);
+  * identical initial weights: rank 0's parameters are broadcast once at construction.
+With ``use_graph`` (single GPU) the forward/backward and the optimizer step are each replayed as a captured
+HIP graph; with world > 1 the forward/backward stays eager (the collectives are launched from autograd hooks)
+and only the optimizer step is captured.
+"""
+import functools
+
+import torch
+import torch.distributed as dist
+
+
+class Trainer:
+    """One training step = [buffer broadcast] + forward + loss + backward (+ overlapped bucketed gradient
+    all-reduce when world > 1) + optional grad-norm clip + Adam.  ``step`` provides ``model``, ``loss()``,
+    ``lr`` and ``clip``."""
+
+    def __init__(self, step, world, dev, use_graph, bucket_mb=25.0, broadcast_buffers=True):
+        self.step, self.world, self.dev = step, world, dev
+        self.use_graph = bool(use_graph) and dev.type == "cuda"
+        self.params = [p for p in step.model.parameters() if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(n, device=dev)
+        ranges, off = [], 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            ranges.append((off, off + p.numel()))
+            off += p.numel()
+        self.buf_f = self.buf_i = None
+        self.broadcast_buffers = broadcast_buffers and world > 1
+        if world > 1:
+            for p in step.model.parameters():          # identical initial weights (DDP semantics)
+                dist.broadcast(p.data, 0)
+            self.buf_f, self.buf_i = _flatten_buffers(step.model, dev)
+            self.sync_buffers()
+            self._make_buckets(ranges, bucket_mb)
+            for i, p in enumerate(self.params):
+                p.register_post_accumulate_grad_hook(functools.partial(self._grad_ready, i))
+        self._armed = False
+        self.opt = torch.optim.Adam(self.params, lr=step.lr, capturable=self.use_graph, foreach=True)
+        self.g_fb = self.g_opt = None
+        self.loss = None
+
+    # ------------------------------------------------------------------ buckets
+    def _make_buckets(self, ranges, bucket_mb):
+        cap = max(1, int(bucket_mb * 2 ** 20 / 4))
+        self.bucket_of = [0] * len(ranges)
+        self.bucket_range, self.bucket_params = [], []
+        cur, lo, hi = [], None, None
+        for i in reversed(range(len(ranges))):
+            a, b = ranges[i]
+            cur.append(i)
+            lo, hi = a, (b if hi is None else hi)
+            if hi - lo >= cap:
+                self._close_bucket(cur, lo, hi)
+                cur, lo, hi = [], None, None
+        if cur:
+            self._close_bucket(cur, lo, hi)
+        self.expected = [len(ps) for ps in self.bucket_params]
+        self.seen = [False] * len(ranges)
+        self.first_step = True
+
+    def _close_bucket(self, idx, lo, hi):
+        for i in idx:
+            self.bucket_of[i] = len(self.bucket_range)
+        self.bucket_range.append((lo, hi))
+        self.bucket_params.append(list(idx))
+
+    def _arm(self):
+        self.ready = [0] * len(self.bucket_range)
+        self.launched = [False] * len(self.bucket_range)
+        self.works = []
+        self._armed = True
+
+    def _grad_ready(self, i, _param):
+        if not self._armed:
+            return
+        self.seen[i] = True
+        b = self.bucket_of[i]
+        self.ready[b] += 1
+        if not self.first_step and self.ready[b] == self.expected[b]:
+            self._launch(b)
+
+    def _launch(self, b):
+        lo, hi = self.bucket_range[b]
+        self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
+        self.launched[b] = True
+
+    def _finish_allreduce(self):
+        """Launch what the hooks did not (unused parameters; everything on the first step, which also learns
+        which parameters receive gradients), then make the current stream wait for every collective."""
+        self._armed = False
+        for b in range(len(self.bucket_range)):
+            if not self.launched[b]:
+                self._launch(b)
+        for w in self.works:
+            w.wait()
+        self.works = []
+        if self.first_step:
+            self.expected = [sum(self.seen[i] for i in ps) for ps in self.bucket_params]
+            self.first_step = False
+
+    @property
+    def n_buckets(self):
+        return len(self.bucket_range) if self.world > 1 else 0
+
+    # ------------------------------------------------------------------ buffers
+    def sync_buffers(self):
+        """DDP broadcast_buffers: rank 0's BatchNorm running stats (and counters) to every rank."""
+        if self.buf_f is not None:
+            dist.broadcast(self.buf_f, 0)
+        if self.buf_i is not None:
+            dist.broadcast(self.buf_i, 0)
+
+    # ------------------------------------------------------------------ step
+    def _fwd_bwd(self):
+        self.flat.zero_()
+        if self.world > 1:
+            self._arm()
+        loss = self.step.loss()
+        loss.backward()
+        return loss.detach()
+
+    def _opt(self):
+        if self.world > 1:
+            self.flat.mul_(1.0 / self.world)
+        if self.step.clip is not None:
+            torch.nn.utils.clip_grad_norm_(self.params, self.step.clip, foreach=True)
+        self.opt.step()
+
+    def eager(self):
+        if self.broadcast_buffers:
+            self.sync_buffers()
+        self.loss = self._fwd_bwd()
+        if self.world > 1:
+            self._finish_allreduce()
+        self._opt()
+        return self.loss
+
+    def capture(self):
+        """Capture after eager warm-up (lazy MIOpen / hipBLASLt / Adam-state init done). world > 1: the
+        optimizer step only (the forward/backward launches its collectives from autograd hooks)."""
+        if not self.use_graph:
+            return
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            if self.world == 1:
+                self.g_fb = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g_fb, stream=s):
+                    self.loss = self._fwd_bwd()
+            self.g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_opt, stream=s):
+                self._opt()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+
+    def drop_graphs(self):
+        self.g_fb = self.g_opt = None
+
+    def __call__(self):
+        if self.g_fb is None and self.g_opt is None:
+            return self.eager()
+        if self.broadcast_buffers:
+            self.sync_buffers()
+        if self.g_fb is not None:
+            self.g_fb.replay()
+        else:
+            self.loss = self._fwd_bwd()
+            self._finish_allreduce()
+        self.g_opt.replay()
+        return self.loss
+
+
+def _flatten_buffers(model, dev):
+    """Rebind every floating / integer buffer of ``model`` to a view of one flat tensor per kind (shared
+    buffers stay shared); returns (flat_float | None, flat_int | None)."""
+    groups = {"f": [], "i": []}
+    seen = {}
+    for mod in model.modules():
+        for name, buf in mod._buffers.items():
+            if buf is None:
+                continue
+            key = id(buf)
+            if key not in seen:
+                kind = "f" if buf.is_floating_point() else "i"
+                seen[key] = (kind, len(groups[kind]), buf)
+                groups[kind].append(buf)
+    flats = {}
+    for kind, bufs in groups.items():
+        if not bufs:
+            flats[kind] = None
+            continue
+        if kind == "f" and any(b.dtype != torch.float32 for b in bufs) or \
+                kind == "i" and any(b.dtype != torch.int64 for b in bufs):
+            raise RuntimeError("buffer broadcast expects fp32 floating and int64 integer buffers")
+        flat = torch.empty(sum(b.numel() for b in bufs), device=dev, dtype=bufs[0].dtype)
+        views, off = [], 0
+        for b in bufs:
+            v = flat[off:off + b.numel()].view(b.shape)
+            v.copy_(b)
+            views.append(v)
+            off += b.numel()
+        flats[kind] = (flat, views)
+    for mod in model.modules():
+        for name, buf in list(mod._buffers.items()):
+            if buf is not None:
+                kind, j, _ = seen[id(buf)]
+                mod._buffers[name] = flats[kind][1][j]
+    return tuple(None if flats[k] is None else flats[k][0] for k in ("f", "i"))

@@ -1,8 +1,13 @@
 """Throughput bench: utterances/s of the avse1 AV training step on MI355X (BASELINE configs[1]).
 
-python bench.py [--gpus N --steps K --warmup W --workload avse1|mamba]
-For N > 1 launch under torch.distributed.run (one rank per GPU, RCCL); every rank trains on
-its own synthetic batch (weak scaling, DDP gradient all-reduce overlapped with backward).
+python bench.py [--gpus N --steps K --warmup W --workload avse1|mamba|avse4|avmamba|dpmamba|avse2]
+One rank per GPU over RCCL: under torch.distributed.run (RANK / WORLD_SIZE in the env), or, with
+--gpus N > 1 and no WORLD_SIZE, bench.py starts N ranks itself (a torch.distributed.run child
+process launched before anything touches the GPU) and exits with its status. Every rank trains on
+its own synthetic batch (weak scaling); gradients are all-reduced in buckets launched from autograd
+hooks as they become ready, overlapping the backward, and rank 0's BatchNorm buffers are broadcast
+before every forward (avse_challenge_amd/ddp.py). --device cpu (gloo) with --workload plumbing is
+the CPU test hook of that distributed path.
 
 A step = one pass of the hot path over one batch, inputs already resident in HBM:
   avse1 (default, C2): HIP STFT of the noisy + clean waveforms (B x 48000 @ 16 kHz)
@@ -18,6 +23,9 @@ events on torch's current stream, and "cpu_baseline": the oracle restatement on 
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -46,7 +54,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba", "avse4", "dpmamba", "avse2", "avmamba"])
+    p.add_argument("--workload", default="avse1",
+                   choices=["avse1", "mamba", "avse4", "dpmamba", "avse2", "avmamba", "plumbing"])
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu: gloo test hook of the distributed plumbing (--workload plumbing only)")
+    p.add_argument("--bucket-mb", type=float, default=25.0, help="gradient all-reduce bucket size (world > 1)")
+    p.add_argument("--no-roofline-hip", action="store_true", help="skip the north-star kernel roofline list")
     p.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the BASELINE config's)")
     p.add_argument("--size", default="L", choices=["XS", "S", "M", "L"], help="Mamba-TasNet / DPMamba size")
     p.add_argument("--lip-hw", type=int, default=96)
@@ -56,14 +69,41 @@ def parse():
     return p.parse_args()
 
 
-def setup_dist():
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args):
+    """--gpus N > 1 without a launcher: start N ranks via torch.distributed.run as a CHILD process (this process
+    has not touched the GPU) and return its exit status; rank 0 of the child prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")       # dmabuf IPC for RCCL on this driver
+    return subprocess.call(cmd, env=env)
+
+
+def setup_dist(device):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if device == "cpu":
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+        return world, rank, dev
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank, torch.device("cuda", local)
+        dist.init_process_group("nccl", device_id=dev)
+    return world, rank, dev
+
+
+def sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
 
 
 def barrier(world):
@@ -127,34 +167,22 @@ class Avse1Step:
                               "algorithmic_flops_per_launch": flops}, "conv3" if self.B == 32 else "-")
 
     def cpu_baseline(self):
+        """the oracle's full train step (numpy librosa-0.8.1 STFT + AVNet fwd + bwd + Adam) on the
+        same synthetic inputs, batch min(32, 4) = 4, 1 warm-up + median of 5."""
+        from avse_challenge_amd import data
         from oracle import avse1_ref, stft_ref
-        nthreads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-        torch.set_num_threads(max(1, min(nthreads, 64)))
-        B = 2
+        _cpu_threads()
+        B = 4
         m = avse1_ref.AVNet().train()
-        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
-        g = torch.Generator().manual_seed(0)
-        noisy = 0.1 * torch.randn(B, 48000, generator=g)
-        clean = 0.1 * torch.randn(B, 48000, generator=g)
-        lips = torch.randint(0, 256, (B, 3, 75, self.lip_hw, self.lip_hw), generator=g, dtype=torch.uint8)
+        opt = torch.optim.Adam(m.parameters(), lr=self.lr)
+        noisy, clean, lips = data.avse1_batch(B, "cpu", 1234, self.lip_hw)
 
         def step():
             batch = {"noisy_audio_spec": torch.from_numpy(stft_ref.stft_mag_T(noisy.numpy()))[:, None],
                      "mask": torch.from_numpy(stft_ref.stft_mag_T(clean.numpy()))[:, None], "lip_images": lips}
-            loss = m.cal_loss(batch)
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
-        step()
-        t0 = time.perf_counter()
-        iters = 0
-        while iters < 2 or (time.perf_counter() - t0 < 10.0 and iters < 6):
-            step()
-            iters += 1
-        dt = time.perf_counter() - t0
-        return {"value": round(B * iters / dt, 4), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
-                "sample": f"oracle/avse1_ref AVNet train step (numpy librosa-0.8.1 STFT + fwd + bwd + Adam), "
-                          f"batch {B}, {iters} steps after 1 warm-up, lips {self.lip_hw}x{self.lip_hw}"}
+            _cpu_train_step(m, opt, m.cal_loss(batch))
+        return _cpu_record(step, B, 1.0, f"oracle/avse1_ref AVNet train step (numpy librosa-0.8.1 STFT + fwd + bwd + "
+                                         f"Adam), batch {B}, lips {self.lip_hw}x{self.lip_hw}")
 
 
 class MambaStep:
@@ -205,21 +233,23 @@ class MambaStep:
         return _with_traffic(roof, "scan") if b == 64 else roof
 
     def cpu_baseline(self):
+        """The oracle's full train step (every BiMamba layer, PIT SI-SNR, bwd, Adam), batch 4, 1 warm-up + median
+        of 5 — on a 1/16-length segment of each utterance (2000 samples, L = 249 frames): the oracle's scan is a
+        Python loop over frames (~50 s per 4 s utterance forward alone), so the step time is
+        linear in L and is scaled x16 to the 4 s utterance."""
+        from avse_challenge_amd import data
         from oracle import losses_ref, mamba_ref
-        torch.set_num_threads(max(1, min(len(os.sched_getaffinity(0)), 64)))
-        m = mamba_ref.MambaTasNet(**mamba_ref.MAMBA_TASNET_SIZES[self.size], n_spk=2)
-        m.masknet.mamba_net.layers = m.masknet.mamba_net.layers[:1]      # 1 of n layers, scaled below
-        n_layers = mamba_ref.MAMBA_TASNET_SIZES[self.size]["n_mamba"]
-        g = torch.Generator().manual_seed(0)
-        mix = 0.1 * torch.randn(1, 32000, generator=g)
-        tgt = 0.1 * torch.randn(1, 32000, 2, generator=g)
-        t0 = time.perf_counter()
-        with torch.no_grad():
-            m(mix)
-        dt = (time.perf_counter() - t0) * n_layers      # forward only, 1 layer timed, scaled to all layers
-        return {"value": round(1.0 / dt, 6), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
-                "sample": f"oracle/mamba_ref forward of 1 of {n_layers} BiMamba layers on one 4 s utterance, "
-                          f"scaled x{n_layers} (forward only; the training step is >=3x slower)"}
+        _cpu_threads()
+        B, cut = 4, 16
+        m = mamba_ref.MambaTasNet(**mamba_ref.MAMBA_TASNET_SIZES[self.size], n_spk=2).train()
+        opt = torch.optim.Adam(m.parameters(), lr=self.lr)
+        mix, tgt = data.wsj0mix_batch(B, "cpu", 4321, T=32000 // cut)
+
+        def step():
+            _cpu_train_step(m, opt, losses_ref.si_snr_pit(tgt, m(mix)).mean(), self.clip)
+        return _cpu_record(step, B, cut, f"oracle/mamba_ref Mamba-TasNet-{self.size} train step (all layers, PIT "
+                                         f"SI-SNR, bwd, Adam), batch {B} x {32000 // cut} samples (1/{cut} of 4 s), "
+                                         f"time scaled x{cut}")
 
 
 class DPMambaStep(MambaStep):
@@ -253,20 +283,30 @@ class DPMambaStep(MambaStep):
                          4.0 * b * l * (4 * d + 2 * 16), f"avse_scan_fwd (DPMamba intra, {b} x {d} x {l}, training fwd)")
 
     def cpu_baseline(self):
-        from oracle import dpmamba_ref
-        torch.set_num_threads(max(1, min(len(os.sched_getaffinity(0)), 64)))
+        """The oracle's full train step, batch 4, 1 warm-up + median of 5, on the full 4 s utterance with 2 of the
+        n dual-path layers, the per-layer time (2-layer step minus 1-layer step) scaled to all n layers."""
+        from avse_challenge_amd import data
+        from oracle import dpmamba_ref, losses_ref
+        _cpu_threads()
+        B = 4
         kw = dict(dpmamba_ref.DPMAMBA_SIZES[self.size])
         n_dp = kw.pop("n_dp")
-        m = dpmamba_ref.DPMambaTasNet(n_dp=1, **kw)
-        g = torch.Generator().manual_seed(0)
-        mix = 0.1 * torch.randn(1, 32000, generator=g)
-        t0 = time.perf_counter()
-        with torch.no_grad():
-            m(mix)
-        dt = (time.perf_counter() - t0) * n_dp
-        return {"value": round(1.0 / dt, 6), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
-                "sample": f"oracle/dpmamba_ref forward with 1 of {n_dp} dual-path layers on one 4 s utterance, "
-                          f"scaled x{n_dp} (forward only)"}
+        mix, tgt = data.wsj0mix_batch(B, "cpu", 4321)
+        recs = []
+        for n in (1, 2):
+            m = dpmamba_ref.DPMambaTasNet(n_dp=n, **kw).train()
+            opt = torch.optim.Adam(m.parameters(), lr=self.lr)
+
+            def step():
+                _cpu_train_step(m, opt, losses_ref.si_snr_pit(tgt, m(mix)).mean(), self.clip)
+            recs.append(_cpu_record(step, B, 1.0, "", runs=3))
+        t1, t2 = (B / r["value"] for r in recs)
+        dt = t1 + (n_dp - 1) * max(t2 - t1, 0.0)
+        rec = recs[1]
+        rec.update(value=round(B / dt, 6), sample=f"oracle/dpmamba_ref DPMamba-{self.size} train step (PIT SI-SNR, "
+                   f"bwd, Adam), batch {B} x 4 s: 1-layer {t1:.2f} s, 2-layer {t2:.2f} s (median of 3 each), "
+                   f"extrapolated to {n_dp} dual-path layers")
+        return rec
 
 
 class AVMambaStep:
@@ -310,26 +350,25 @@ class AVMambaStep:
                          2.0 * b * l * (4 * d + 2 * 16), f"avse_scan_fwd (bf16, {b} x {d} x {l}, training fwd)")
 
     def cpu_baseline(self):
-        """oracle/avmamba_ref forward (fp32) of one 3 s utterance: the whole model with 0 and with 1 BiMamba layer
-        timed, the per-layer time scaled to all n layers."""
+        """The oracle's full fp32 train step (lip encoder + all BiMamba layers, SI-SNR, bwd, Adam), batch 4, 1 warm-up
+        + median of 5, on a 1/16 segment of each utterance and its lip track (3000 samples, L = 374 frames, 5 lip
+        frames), the step time scaled x16 to the 3 s utterance (linear in length: the oracle's scan is a Python
+        loop over frames, the lip encoder is per frame)."""
+        from avse_challenge_amd import data
         from oracle import avmamba_ref
-        torch.set_num_threads(max(1, min(len(os.sched_getaffinity(0)), 64)))
-        kw = avmamba_ref.AV_MAMBA_SIZES[self.size]
-        m = avmamba_ref.AVMambaTasNet(**kw).eval()
-        layers = m.masknet.mamba_net.layers
-        g = torch.Generator().manual_seed(0)
-        mix, lips = 0.1 * torch.randn(1, 48000, generator=g), torch.rand(1, 1, 75, 112, 112, generator=g)
-        ts = []
-        with torch.no_grad():
-            for n in (0, 1):
-                m.masknet.mamba_net.layers = layers[:n]
-                t0 = time.perf_counter()
-                m(mix, lips)
-                ts.append(time.perf_counter() - t0)
-        dt = ts[0] + kw["n_mamba"] * max(ts[1] - ts[0], 0.0)
-        return {"value": round(1.0 / dt, 6), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
-                "sample": f"oracle/avmamba_ref fp32 forward of one 3 s utterance: front/back end {ts[0]:.2f} s + "
-                          f"{kw['n_mamba']} x one BiMamba layer ({ts[1] - ts[0]:.2f} s); forward only"}
+        from oracle.losses_ref import avse4_loss
+        _cpu_threads()
+        B, cut = 4, 16
+        m = avmamba_ref.AVMambaTasNet(**avmamba_ref.AV_MAMBA_SIZES[self.size]).train()
+        opt = torch.optim.Adam(m.parameters(), lr=self.lr)
+        noisy, clean, _ = data.avse1_batch(B, "cpu", 999, lip_hw=8, T=48000 // cut)
+        lips = torch.rand((B, 1, 75 // cut + 1, 112, 112), generator=torch.Generator().manual_seed(999))
+
+        def step():
+            _cpu_train_step(m, opt, avse4_loss(clean[:, None], m(noisy, lips)[:, None]), self.clip)
+        return _cpu_record(step, B, cut, f"oracle/avmamba_ref AV Mamba-TasNet-{self.size} fp32 train step, batch {B} x "
+                                         f"{48000 // cut} samples + {75 // cut + 1} lip frames (1/{cut} of 3 s), time "
+                                         f"scaled x{cut}")
 
 
 class Avse2Step:
@@ -394,100 +433,96 @@ class Avse4Step:
         return _with_traffic(roof, "dwconv") if self.B == 16 else roof
 
     def cpu_baseline(self):
+        """the oracle's train step (fwd + SI-SNR + bwd + Adam) on the same synthetic inputs,
+        batch min(16, 4) = 4 binaural 5 s utterances + 125 lip frames, 1 warm-up + median of 5."""
+        from avse_challenge_amd import data
         from oracle import avse4_ref
-        torch.set_num_threads(max(1, min(len(os.sched_getaffinity(0)), 64)))
+        _cpu_threads()
+        B = 4
         m = avse4_ref.AVSE4BaselineModule(num_channels=2).train()
-        opt = torch.optim.Adam(m.parameters(), lr=1e-4)
-        g = torch.Generator().manual_seed(0)
-        batch = {"noisy_audio": 0.1 * torch.randn(1, 2, 80000, generator=g),
-                 "clean": 0.1 * torch.randn(1, 2, 80000, generator=g),
-                 "vis_feat": torch.rand(1, 1, 125, 112, 112, generator=g)}
+        opt = torch.optim.Adam(m.parameters(), lr=self.lr)
+        batch = data.avse4_batch(B, "cpu", 777)
 
         def step():
-            loss = m.cal_loss(batch)
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
-        step()
+            _cpu_train_step(m, opt, m.cal_loss(batch))
+        return _cpu_record(step, B, 1.0, f"oracle/avse4_ref train step (fwd + bwd + Adam), batch {B} x 2 ch x 5 s "
+                                         f"+ 125 lip frames 112x112")
+
+
+from avse_challenge_amd.ddp import Trainer  # noqa: E402  (the data-parallel step; re-exported for tests)
+
+
+class PlumbingStep:
+    """--device cpu test hook of the distributed path (launch, bucketed all-reduce, BatchNorm-buffer broadcast,
+    max-over-ranks timing) under gloo: avse1's AudioFeatNet (dilated Conv2d + BatchNorm2d; PyTorch/MIOpen in the
+    product as well) on a reduced spectrogram (B x 1 x 40 x 257) + a 1028 -> 257 sigmoid mask head, L1 loss.
+    Not a throughput workload."""
+    unit_desc = "reduced spectrogram (plumbing test)"
+    graph_ok = False
+
+    def __init__(self, B, dev, rank, world):
+        from avse_challenge_amd import avse1
+        torch.manual_seed(5 + rank)                   # different init per rank: the Trainer broadcasts rank 0's
+        self.B = B
+        self.model = torch.nn.ModuleDict({"net": avse1.AudioFeatNet(), "head": torch.nn.Linear(1028, 257)}).to(dev)
+        self.lr, self.clip = 1e-3, 1.0
+        g = torch.Generator().manual_seed(300 + rank)
+        self.spec = torch.rand((B, 1, 40, 257), generator=g).to(dev)
+        self.target = torch.rand((B, 1, 40, 257), generator=g).to(dev)
+
+    def loss(self):
+        mask = torch.sigmoid(self.model["head"](self.model["net"](self.spec)))
+        return torch.nn.functional.l1_loss(self.spec * mask[:, None], self.target)
+
+    def config(self, world):
+        return {"workload": "plumbing (CPU test hook of the data-parallel path)", "global_batch": self.B * world,
+                "per_gpu_batch": self.B, "parallelism": f"dp{world}"}
+
+    def roofline(self, dev):
+        return None
+
+    def cpu_baseline(self):
+        return None
+
+
+# ------------------------------------------------------------------------------ CPU baseline helpers
+
+def _cpu_threads():
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    torch.set_num_threads(max(1, n))
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_train_step(m, opt, loss, clip=None):
+    opt.zero_grad(set_to_none=True)
+    loss.backward()
+    if clip is not None:
+        torch.nn.utils.clip_grad_norm_(m.parameters(), clip)
+    opt.step()
+
+
+def _cpu_record(step, batch, scale, sample, runs=5):
+    """1 warm-up + median of ``runs`` timed steps; utt/s = batch / (median * scale)."""
+    step()
+    ts = []
+    for _ in range(runs):
         t0 = time.perf_counter()
-        iters = 0
-        while iters < 1 or (time.perf_counter() - t0 < 10.0 and iters < 4):
-            step()
-            iters += 1
-        dt = time.perf_counter() - t0
-        return {"value": round(iters / dt, 4), "unit": "utt/s", "cores": torch.get_num_threads(), "kind": "port",
-                "sample": f"oracle/avse4_ref train step (fwd + bwd + Adam), batch 1, {iters} steps after 1 warm-up"}
-
-
-class Trainer:
-    """One training step = forward + loss + backward (+ gradient all-reduce over RCCL when N > 1)
-    + optional grad-norm clip + Adam.  Gradients live in ONE flat fp32 buffer (param.grad are views):
-    the data-parallel exchange is a single large all-reduce of it (ring over xGMI), and with
-    --graph (default) the launch-bound forward/backward and the optimizer are each replayed as a
-    captured HIP graph; the collective stays outside the graphs."""
-
-    def __init__(self, step, world, dev, use_graph):
-        self.step, self.world, self.use_graph = step, world, use_graph
-        self.params = [p for p in step.model.parameters() if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(n, device=dev)
-        off = 0
-        for p in self.params:
-            p.grad = self.flat[off:off + p.numel()].view_as(p)
-            off += p.numel()
-        if world > 1:                      # identical initial weights on every rank (DDP semantics)
-            for p in step.model.parameters():
-                dist.broadcast(p.data, 0)
-            for b in step.model.buffers():
-                dist.broadcast(b, 0)
-        self.opt = torch.optim.Adam(self.params, lr=step.lr, capturable=use_graph, foreach=True)
-        self.g_fb = self.g_opt = None
-        self.loss = None
-
-    def _fwd_bwd(self):
-        self.flat.zero_()
-        loss = self.step.loss()
-        loss.backward()
-        return loss.detach()
-
-    def _opt(self):
-        if self.world > 1:
-            self.flat.mul_(1.0 / self.world)
-        if self.step.clip is not None:
-            torch.nn.utils.clip_grad_norm_(self.params, self.step.clip, foreach=True)
-        self.opt.step()
-
-    def _allreduce(self):
-        if self.world > 1:
-            dist.all_reduce(self.flat)
-
-    def eager(self):
-        self.loss = self._fwd_bwd()
-        self._allreduce()
-        self._opt()
-        return self.loss
-
-    def capture(self):
-        """Capture after eager warm-up (lazy MIOpen / hipBLASLt / Adam-state init done)."""
-        torch.cuda.synchronize()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            self.g_fb, self.g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_fb, stream=s):
-                self.loss = self._fwd_bwd()
-            with torch.cuda.graph(self.g_opt, stream=s):
-                self._opt()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-
-    def __call__(self):
-        if self.g_fb is None:
-            return self.eager()
-        self.g_fb.replay()
-        self._allreduce()
-        self.g_opt.replay()
-        return self.loss
+        step()
+        ts.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    return {"value": round(batch / (med * scale), 6), "unit": "utt/s", "cores": torch.get_num_threads(),
+            "cpu_model": _cpu_model(), "kind": "port", "sample": sample,
+            "step_s": [round(t, 3) for t in ts], "median_step_s": round(med, 3), "time_scale": scale}
 
 
 def pmc_traffic(phase):
@@ -536,41 +571,139 @@ def heartbeat(rank, period=60.0):
     threading.Thread(target=run, daemon=True).start()
 
 
+def _event_ms(fn, n=10, warm=3):
+    """Average duration of fn's launches, HIP events on torch's current stream (where the kernels run)."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+BF16_PEAK_TFS = 2500.0         # dense bf16 MFMA peak, MI355X_MICROARCH.md (no sparsity)
+
+
+def roofline_hip(dev):
+    """The north-star kernels at their BASELINE shapes, timed live (HIP events) in the same run as the bench line:
+    hand-written HBM-bound kernels against 8 TB/s (algorithmic bytes of each launch AS THE MODELS MAKE IT, DESIGN.md
+    §3) and the Mamba projections' MFMA rate against the dense peak of their dtype. Returns (hbm_list, projections)."""
+    from avse_challenge_amd import kernels as K
+    from avse_challenge_amd import mamba_tasnet as M
+    hbm, proj = [], []
+    g = torch.Generator(device=dev).manual_seed(7)
+
+    def rnd(*shape, dtype=torch.float32, scale=1.0):
+        return (scale * torch.randn(shape, device=dev, generator=g)).to(dtype)
+
+    def add_hbm(name, shape, dtype, byts, fn):
+        ms = _event_ms(fn)
+        ach = byts / (ms * 1e-3) / 1e9
+        hbm.append({"kernel": name, "shape": shape, "dtype": dtype, "bound": "hbm", "algorithmic_bytes_per_launch": byts,
+                    "avg_ms": round(ms, 4), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4)})
+
+    n = 16
+    for tag, b, l, dt in (("C3", 64, 3999, torch.float32), ("C5", 32, 5999, torch.bfloat16)):
+        d, s = 1024, (2 if dt == torch.bfloat16 else 4)
+        name = "fp32" if s == 4 else "bf16"
+        u, z, dout = rnd(b, d, l, dtype=dt), rnd(b, d, l, dtype=dt), rnd(b, d, l, dtype=dt)
+        delta = rnd(b, d, l, dtype=dt, scale=0.1)
+        A = -torch.rand(d, n, device=dev, generator=g) - 0.5
+        Bm, Cm = rnd(b, n, l, dtype=dt), rnd(b, n, l, dtype=dt)
+        D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
+        _, x, _ = K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, return_out=False)
+        # training fwd: reads u, delta, z, B, C; writes out_z (SURVEY §8d)
+        add_hbm(f"avse_scan_fwd ({tag}, training fwd, out_z only)", [b, d, l], name, s * b * l * (4 * d + 2 * n),
+                lambda: K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, return_out=False))
+        # bwd as the model calls it (out=None, no out_z recompute): reads u, delta, z, dout, B, C; writes du,
+        # ddelta, dz (input dtype) and fp32 dB, dC
+        add_hbm(f"avse_scan_bwd ({tag}, as MambaInnerNoOutProj calls it)", [b, d, l], name,
+                b * l * (7 * s * d + 2 * s * n + 2 * 4 * n),
+                lambda: K.selective_scan_bwd(u, delta, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False))
+        if tag == "C3":
+            w, cb = rnd(d, 4, scale=0.5), rnd(d)
+            add_hbm("avse_cconv_fwd (C3, k4 + SiLU)", [b, d, l], name, 2 * s * b * d * l,
+                    lambda: K.causal_conv1d_fwd(u, w, cb, True))
+            add_hbm("avse_cconv_bwd (C3, k4 + SiLU)", [b, d, l], name, 3 * s * b * d * l,
+                    lambda: K.causal_conv1d_bwd(u, w, cb, dout, silu=True))
+        del u, z, dout, delta, Bm, Cm, x
+        torch.cuda.empty_cache()
+    xd = rnd(16, 512, 3999)
+    wd, gy = rnd(512, 1, 3), rnd(16, 512, 3999)
+    add_hbm("avse_dwconv_fwd (C4 TCN, H=512, K=3999, dil 128)", [16, 512, 3999], "fp32", 8 * xd.numel(),
+            lambda: K.dwconv_fwd(xd, wd, 128))
+    add_hbm("avse_dwconv_bwd (C4 TCN, H=512, K=3999, dil 128)", [16, 512, 3999], "fp32", 12 * xd.numel(),
+            lambda: K.dwconv_bwd(xd, wd, gy, 128))
+    del xd, gy
+    # projections (MFMA): BiMambaV2's in_proj (_InProj) and out_proj (_BiOutProj) at C3 (fp32) and C5 (bf16)
+    for tag, b, l, dt, peak in (("C3", 64, 3999, torch.float32, FP32_PEAK_TFS),
+                                ("C5", 32, 5999, torch.bfloat16, BF16_PEAK_TFS)):
+        dm, di = 512, 1024
+        h, f, bk = rnd(b, l, dm, dtype=dt), rnd(b, di, l, dtype=dt), rnd(b, di, l, dtype=dt)
+        w_in, w_out = rnd(2 * di, dm, scale=0.05), rnd(dm, di, scale=0.05)
+        on = dt == torch.bfloat16
+        for pname, flops, fn in (("in_proj", 2.0 * b * l * dm * 2 * di, lambda: M._InProj.apply(h, w_in)),
+                                 ("out_proj", 2.0 * b * l * di * dm, lambda: M._BiOutProj.apply(f, bk, w_out))):
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=on, cache_enabled=False):
+                ms = _event_ms(fn)
+            ach = flops / (ms * 1e-3) / 1e12
+            proj.append({"gemm": f"BiMambaV2 {pname} ({tag})", "shape": [b, l, dm, di], "dtype": str(dt)[6:],
+                         "bound": "mfma", "flops_per_launch": flops, "avg_ms": round(ms, 4),
+                         "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4)})
+        del h, f, bk
+        torch.cuda.empty_cache()
+    return hbm, proj
+
+
 def main():
     args = parse()
-    world, rank, dev = setup_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
+    if args.device == "cpu" and args.workload != "plumbing":
+        raise SystemExit("--device cpu runs --workload plumbing only (the HIP kernels are GPU-only)")
+    world, rank, dev = setup_dist(args.device)
+    if world != args.gpus and rank == 0:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE {world}: timing {world} rank(s)", file=sys.stderr, flush=True)
     heartbeat(rank)
-    torch.backends.cuda.matmul.allow_tf32 = False
-    torch.backends.cudnn.allow_tf32 = False
-    # MIOpen immediate mode: find mode (benchmark=True, as avse1 train.py:11 sets for cuDNN) JIT-compiles
-    # every candidate solver on a fresh box (minutes); immediate mode compiles only the chosen one.
-    torch.backends.cudnn.benchmark = bool(int(os.environ.get("AVSE_MIOPEN_FIND", "0")))
+    if dev.type == "cuda":
+        torch.backends.cuda.matmul.allow_tf32 = False
+        torch.backends.cudnn.allow_tf32 = False
+        # MIOpen immediate mode: find mode (benchmark=True, as avse1 train.py:11 sets for cuDNN) JIT-compiles
+        # every candidate solver on a fresh box (minutes); immediate mode compiles only the chosen one.
+        torch.backends.cudnn.benchmark = bool(int(os.environ.get("AVSE_MIOPEN_FIND", "0")))
     if args.workload == "avse1":
         B = args.batch or 32
-        step = Avse1Step(B, dev, rank, world, args.lip_hw)
+        work = Avse1Step(B, dev, rank, world, args.lip_hw)
     elif args.workload == "avse4":
         B = args.batch or 16
-        step = Avse4Step(B, dev, rank, world)
+        work = Avse4Step(B, dev, rank, world)
     elif args.workload == "avse2":
         B = args.batch or 16
-        step = Avse2Step(B, dev, rank, world)
+        work = Avse2Step(B, dev, rank, world)
     elif args.workload == "avmamba":
         B = args.batch or 32
-        step = AVMambaStep(B, dev, rank, world, args.size)
+        work = AVMambaStep(B, dev, rank, world, args.size)
     elif args.workload == "dpmamba":
         B = args.batch or 32
-        step = DPMambaStep(B, dev, rank, world, args.size)
+        work = DPMambaStep(B, dev, rank, world, args.size)
+    elif args.workload == "plumbing":
+        B = args.batch or 2
+        work = PlumbingStep(B, dev, rank, world)
     else:
         B = args.batch or 64
-        step = MambaStep(B, dev, rank, world, args.size)
+        work = MambaStep(B, dev, rank, world, args.size)
 
-    work = step
-    use_graph = work.graph_ok and not args.no_graph
-    step = Trainer(work, world, dev, use_graph=use_graph)
+    use_graph = work.graph_ok and not args.no_graph and dev.type == "cuda"
+    step = Trainer(work, world, dev, use_graph=use_graph, bucket_mb=args.bucket_mb)
     for i in range(max(args.warmup, 1 if use_graph else 0)):
         t = time.perf_counter()
         step()
-        torch.cuda.synchronize()
+        sync(dev)
         if rank == 0:
             print(f"[bench] warmup {i + 1}/{args.warmup}: {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
     graph = False
@@ -578,16 +711,16 @@ def main():
         try:
             step.capture()
             step()
-            torch.cuda.synchronize()
-            graph = True
+            sync(dev)
+            graph = "fwd+bwd+opt" if step.g_fb is not None else "opt"
         except Exception as e:      # noqa: BLE001 - report and fall back to eager launches
             print(f"[bench] HIP graph capture failed ({type(e).__name__}: {e}); eager launches", file=sys.stderr,
                   flush=True)
-            step.g_fb = step.g_opt = None
-            torch.cuda.synchronize()
-    torch.cuda.synchronize()
+            step.drop_graphs()
+            sync(dev)
+    sync(dev)
     barrier(world)
-    torch.cuda.synchronize()
+    sync(dev)
     mark = bool(int(os.environ.get("AVSE_PROFILE_MARK", "0")))   # tools/ktrace_window.py brackets the timed steps
     if mark:
         torch.cuda._sleep(1000)
@@ -596,9 +729,9 @@ def main():
         loss = step()
     if mark:
         torch.cuda._sleep(1000)
-    torch.cuda.synchronize()
+    sync(dev)
     barrier(world)
-    torch.cuda.synchronize()
+    sync(dev)
     dt = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([dt], device=dev)
@@ -607,24 +740,37 @@ def main():
     if not torch.isfinite(loss.detach()).all():
         raise RuntimeError("non-finite loss in the timed region")
 
-    roof = None if args.no_roofline or rank != 0 else work.roofline(dev)
+    cuda = dev.type == "cuda"
+    roof = None if args.no_roofline or rank != 0 or not cuda else work.roofline(dev)
+    hbm_list = proj = None
+    if rank == 0 and world == 1 and cuda and not args.no_roofline_hip:
+        hbm_list, proj = roofline_hip(dev)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = work.cpu_baseline()
     if rank == 0:
         value = world * B * args.steps / dt
+        cfg = {**work.config(world), "hip_graph": graph}
+        if cuda:
+            cfg["max_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
+        if world > 1:
+            cfg["ddp"] = {"backend": dist.get_backend(), "grad_buckets": step.n_buckets, "bucket_mb": args.bucket_mb,
+                          "allreduce": "async per bucket from post-accumulate-grad hooks (overlaps backward)",
+                          "broadcast_buffers": step.broadcast_buffers}
         rec = {"metric": {"avse1": METRIC, "mamba": "utterances/sec (4s@8kHz WSJ0-2mix, Mamba-TasNet)",
                           "avse4": "utterances/sec (5s@16kHz binaural + 125 lip frames, avse4)",
                           "dpmamba": "utterances/sec (4s@8kHz WSJ0-2mix, DPMamba)",
                           "avse2": "utterances/sec (3s@16kHz + 75 lip frames 224x224, avse2)",
-                          "avmamba": "utterances/sec (3s@16kHz + 75 lip frames, AV Mamba-TasNet-L bf16)"}[args.workload],
+                          "avmamba": "utterances/sec (3s@16kHz + 75 lip frames, AV Mamba-TasNet-L bf16)",
+                          "plumbing": "steps/sec (CPU plumbing test hook)"}[args.workload],
                "value": round(value, 3), "unit": "utt/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": getattr(work, "dtype", "fp32"),
                "data": "synthetic (speech-like noise with 4 Hz envelope at SNR {0,3,6,9} dB, uint8 lips; "
                        "random-init weights)",
-               "config": {**work.config(world), "hip_graph": graph, "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)},
-               "roofline": roof, "cpu_baseline": cpu}
+               "config": cfg, "roofline": roof, "roofline_hip": hbm_list, "projections": proj, "cpu_baseline": cpu}
+        if not cuda:
+            rec["device"] = "cpu (gloo ranks; n_gpus counts ranks)"
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -492,6 +492,100 @@ def gen_avse1():
           {"pred": _maxabs(bb, a), "loss": abs(float(la) - float(lb))})
 
 
+def gen_avse1_aonly():
+    """BASELINE configs[0] (C1): audio-only AVNet, as train.py:28-30 builds it — nets = (None, AudioFeatNet,
+    FusionNet(a_only=True)), model.py:117-118 — on one 3 s utterance (376 STFT frames), eval and train BN,
+    plus the train-mode L1 loss gradients of every parameter."""
+    m1 = _import_from("baseline/avse1", "model")
+    net_r = m1.AVNet((None, m1.build_audiofeat_net(a_only=True), m1.FusionNet(a_only=True)), "l1", a_only=True)
+    net_o = avse1_ref.AVNet(a_only=True)
+    _same_keys(net_r, net_o)
+    det_init_(net_r, 55)
+    det_init_(net_o, 55)
+    batch = {"noisy_audio_spec": det_input((1, 1, 376, 257), 508).abs(),
+             "mask": det_input((1, 1, 376, 257), 509).abs()}
+    out, diffs = {}, {}
+    for mode in ("eval", "train"):
+        net_r.train(mode == "train")
+        net_o.train(mode == "train")
+        net_r.zero_grad()
+        net_o.zero_grad()
+        a = net_r(batch)
+        la = net_r.cal_loss(batch)
+        bb = net_o(batch)
+        lb = net_o.cal_loss(batch)
+        out["pred_" + mode], out["loss_" + mode] = a.detach(), la.detach()
+        diffs[mode] = {"pred": _maxabs(bb, a), "loss": abs(float(la) - float(lb))}
+        if mode == "train":
+            la.backward()
+            lb.backward()
+            grads = {"g_" + k.replace(".", "__"): p.grad.clone() for k, p in net_r.named_parameters()}
+            diffs["param_grads"] = max(_maxabs(p.grad, grads["g_" + k.replace(".", "__")])
+                                       for k, p in net_o.named_parameters())
+    _save("avse1_aonly", dict(**out, **grads),
+          "AVNet audio-only (train.py:28-30, model.py:117-118): AudioFeatNet -> FusionNet(a_only, LSTM 1028->257) "
+          "on (1,1,376,257) det_input seeds 508/509 (abs; regenerated in tests), eval + train BN, L1 loss grads "
+          "in train mode; det_init seed 55", diffs)
+
+
+# ============================================================================ DPMamba wrapper (SURVEY 8f row 2)
+
+def gen_dpmamba():
+    """Pins the dual-path forward the reference holds in-tree (modules/dual_path.py:53-150,
+    Dual_Path_Model_Skip.forward, skip_n_block=0) over a stub base class: speechbrain 1.0.0's
+    Dual_Path_Model.__init__ / _Segmentation / _over_add / Dual_Computation_Block are not vendored, so the
+    stub binds them to oracle/dpmamba_ref.py's restatement (those helpers stay "parity unpinned"); the
+    intra / inter models are the reference's own MambaBlocksSequential (fast path with shimmed natives)."""
+    from oracle import dpmamba_ref
+
+    class SBDualPath(dpmamba_ref.Dual_Path_Model):
+        def __init__(self, in_channels, out_channels, intra_model, inter_model, num_layers=1, norm="ln", K=200,
+                     num_spks=2, skip_around_intra=True, linear_layer_after_inter_intra=True,
+                     use_global_pos_enc=False, max_length=20000):
+            assert norm == "ln" and not linear_layer_after_inter_intra and not use_global_pos_enc
+            super().__init__(in_channels, out_channels, intra_model, inter_model, num_layers, K, num_spks,
+                             skip_around_intra)
+            self.use_global_pos_enc = use_global_pos_enc
+    _mod("speechbrain.lobes.models.dual_path", Dual_Path_Model=SBDualPath)
+    # the fast path of the reference's MambaBlocksSequential (as in gen_mamba's masknet case)
+    ssi = _import_from("Mamba-TasNet", "modules.mamba.selective_scan_interface")
+    ref_scan = ssi.selective_scan_ref
+
+    def ss_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus):
+        out, last = ref_scan(u, delta, A, B, C, D, None, delta_bias, delta_softplus, return_last_state=True)
+        x = torch.stack([torch.zeros_like(last), last], -1).reshape(last.shape[0], last.shape[1], 1, -1)
+        return [out, x, out * F.silu(z.float()).to(out.dtype)]
+    sys.modules["selective_scan_cuda"].fwd = ss_fwd
+    dp_mod = _import_from("Mamba-TasNet", "modules.dual_path")
+    mb = sys.modules["modules.mamba_blocks"] if "modules.mamba_blocks" in sys.modules else \
+        _import_from("Mamba-TasNet", "modules.mamba_blocks")
+    N, K = 64, 10
+    out, diffs = {}, {}
+    mix_w = det_input((2, N, 47), 901).abs()         # L=47: chunking pads (gap > 0)
+    for sia in (True, False):
+        mk = lambda: mb.MambaBlocksSequential(1, bidirectional=True, d_model=N, fused_add_norm=False,  # noqa: E731
+                                              rms_norm=True)
+        ref_dp = dp_mod.Dual_Path_Model_Skip(N, N, mk(), mk(), num_layers=2, norm="ln", K=K, num_spks=2,
+                                             skip_around_intra=sia, skip_n_block=0,
+                                             linear_layer_after_inter_intra=False)
+        ours = dpmamba_ref.Dual_Path_Model(N, N, dpmamba_ref.MambaBlocksSequential(1, N),
+                                           dpmamba_ref.MambaBlocksSequential(1, N), 2, K, 2, sia)
+        _same_keys(ref_dp, ours)
+        det_init_(ref_dp, 91)
+        det_init_(ours, 91)
+        with torch.no_grad():
+            a = ref_dp(mix_w)
+            bb = ours(mix_w)
+        tag = "sia" if sia else "nosia"
+        out["est_mask_" + tag] = a
+        diffs[tag] = _maxabs(bb, a)
+    _save("dpmamba_wrapper", dict(mixture_w=mix_w, **out),
+          "modules/dual_path.py:53-150 Dual_Path_Model_Skip.forward (skip_n_block=0) on a stub speechbrain base "
+          "(oracle restatement of __init__/_Segmentation/_over_add/Dual_Computation_Block), intra/inter = reference "
+          "MambaBlocksSequential(1 BiMamba v2, d_model 64), 2 dual-path layers, K=10, L=47, skip_around_intra "
+          "True/False, det_init seed 91", diffs)
+
+
 # ============================================================================ avse2 (SURVEY 8f row 3)
 
 def gen_avse2():
@@ -540,7 +634,7 @@ def main():
     global MANIFEST
     avse2_dnn = _install_stubs()
     gens = {"losses": partial(gen_losses, avse2_dnn), "mamba": gen_mamba, "avse4": gen_avse4, "avse1": gen_avse1,
-            "avse2": gen_avse2}
+            "avse2": gen_avse2, "avse1_aonly": gen_avse1_aonly, "dpmamba": gen_dpmamba}
     only = sys.argv[1:] or list(gens)
     if sys.argv[1:]:
         with open(os.path.join(HERE, "manifest.json")) as f:

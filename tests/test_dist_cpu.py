@@ -1,8 +1,16 @@
-"""Data-parallel training harness (bench.Trainer) on CPU with gloo, world_size 2: one flat-gradient
-all-reduce per step must give every rank the same weights, equal to single-process training on the
-union of the ranks' batches (mean of per-rank gradients, i.e. DDP semantics)."""
+"""Data-parallel training step (avse_challenge_amd.ddp.Trainer, re-exported as bench.Trainer) on CPU with gloo,
+world_size 2 — the DDP semantics of the reference's Lightning / SpeechBrain DDP:
+  * every rank ends each step with identical weights, equal to one process applying the MEAN of the per-rank
+    gradients (per-rank BatchNorm batch statistics, no SyncBN);
+  * broadcast_buffers: before each forward rank 0's BatchNorm running stats overwrite every rank's, so after the
+    step rank 0's buffers are those of its own shard's forward;
+  * the gradient all-reduce runs in buckets launched from post-accumulate-grad hooks during the backward;
+  * ``python bench.py --gpus 2 --device cpu --workload plumbing`` starts its own 2 ranks and reports n_gpus 2.
+"""
+import json
 import os
 import socket
+import subprocess
 import sys
 
 import pytest
@@ -29,15 +37,37 @@ def _data(rank):
     return torch.randn(4, 8, generator=g), torch.randn(4, 2, generator=g)
 
 
-def _worker(rank, world, port, clip, q):
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(target, extra, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + extra) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _init(rank, world, port):
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _toy_worker(rank, world, port, q, clip):
+    _init(rank, world, port)
     import bench
-    if rank == 1:                                   # different init on rank 1: Trainer must broadcast rank 0's
-        torch.manual_seed(123)
     st = _ToyStep(*_data(rank), clip)
-    if rank == 1:
+    if rank == 1:                                   # different init on rank 1: Trainer must broadcast rank 0's
         with torch.no_grad():
             for p in st.model.parameters():
                 p.add_(1.0)
@@ -48,26 +78,11 @@ def _worker(rank, world, port, clip, q):
     dist.destroy_process_group()
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 @pytest.mark.parametrize("clip", [None, 0.05])
 def test_trainer_gloo_world2_matches_single_process(clip):
     sys.path.insert(0, REPO)
     import bench
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, clip, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    res = _spawn(_toy_worker, (clip,))
     res = {r: [torch.from_numpy(a) for a in v] for r, v in res.items()}
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b)
@@ -79,3 +94,111 @@ def test_trainer_gloo_world2_matches_single_process(clip):
         tr()
     for a, b in zip(res[0], st.model.parameters()):
         torch.testing.assert_close(a, b.detach(), atol=1e-6, rtol=1e-5)
+
+
+# ------------------------------------------------------------------ BatchNorm model (avse1 AudioFeatNet)
+
+STEPS = 3
+
+
+def _bn_worker(rank, world, port, q, bucket_mb):
+    _init(rank, world, port)
+    import bench
+    from avse_challenge_amd import ddp
+    work = bench.PlumbingStep(2, torch.device("cpu"), rank, world)      # rank-dependent init and data
+    tr = bench.Trainer(work, world, torch.device("cpu"), use_graph=False, bucket_mb=bucket_mb)
+    launched_in_hooks = []
+    orig = tr._launch
+
+    def spy(b):
+        launched_in_hooks.append(tr._armed)
+        orig(b)
+    tr._launch = spy
+    for _ in range(STEPS):
+        tr()
+    bufs_before_sync = {k: v.clone() for k, v in work.model.state_dict().items() if k in dict(work.model.named_buffers())}
+    tr.sync_buffers()
+    bufs = {k: v.clone() for k, v in work.model.named_buffers()}
+    npd = lambda d: {k: v.detach().numpy().copy() for k, v in d.items()}      # noqa: E731 (no shared memory)
+    q.put((rank, {"params": npd(dict(work.model.named_parameters())),
+                  "bufs_own": npd(bufs_before_sync), "bufs_synced": npd(bufs), "n_buckets": tr.n_buckets,
+                  "hook_launches": sum(launched_in_hooks), "launches": len(launched_in_hooks),
+                  "flat_buffer_views": all(b.untyped_storage().data_ptr() in
+                                           (tr.buf_f.untyped_storage().data_ptr(), tr.buf_i.untyped_storage().data_ptr())
+                                           for b in work.model.buffers()),
+                  "ddp_module": ddp.__name__}))
+    dist.destroy_process_group()
+
+
+def _emulate_ddp(world, B=2):
+    """One process, DDP semantics: each step starts every shard's forward from rank 0's buffers, applies the mean
+    of the per-shard gradients (clip, Adam), and keeps the buffers of shard 0's forward."""
+    sys.path.insert(0, REPO)
+    import bench
+    shards = [bench.PlumbingStep(B, torch.device("cpu"), r, world) for r in range(world)]
+    model = shards[0].model
+    params = [p for p in model.parameters()]
+    opt = torch.optim.Adam(params, lr=shards[0].lr, foreach=True)
+    for _ in range(STEPS):
+        b0 = {k: v.clone() for k, v in model.named_buffers()}
+        grads, after0 = [], None
+        for r, sh in enumerate(shards):
+            with torch.no_grad():
+                for k, v in model.named_buffers():
+                    v.copy_(b0[k])
+            sh.model = model
+            loss = sh.loss()
+            grads.append(torch.autograd.grad(loss, params))
+            if r == 0:
+                after0 = {k: v.clone() for k, v in model.named_buffers()}
+        with torch.no_grad():
+            for k, v in model.named_buffers():
+                v.copy_(after0[k])
+        for i, p in enumerate(params):
+            p.grad = sum(g[i] for g in grads) / world
+        torch.nn.utils.clip_grad_norm_(params, shards[0].clip, foreach=True)
+        opt.step()
+    return model
+
+
+@pytest.mark.parametrize("bucket_mb", [25.0, 0.05])
+def test_ddp_batchnorm_model_world2_matches_ddp_semantics(bucket_mb):
+    res = _spawn(_bn_worker, (bucket_mb,))
+    for r in res.values():
+        for key in ("params", "bufs_own", "bufs_synced"):
+            r[key] = {k: torch.from_numpy(v) for k, v in r[key].items()}
+    r0, r1 = res[0], res[1]
+    assert r0["flat_buffer_views"] and r1["flat_buffer_views"]
+    for k in r0["params"]:
+        assert torch.equal(r0["params"][k], r1["params"][k]), k
+    ref = _emulate_ddp(2)
+    for k, v in ref.named_parameters():
+        torch.testing.assert_close(r0["params"][k], v.detach(), atol=2e-6, rtol=1e-5, msg=k)
+    n_bn = 0
+    for k, v in ref.named_buffers():
+        torch.testing.assert_close(r0["bufs_own"][k], v, atol=1e-6, rtol=1e-5, msg=k)
+        assert torch.equal(r1["bufs_synced"][k], r0["bufs_own"][k]), k
+        n_bn += k.endswith("running_mean")
+    assert n_bn == 7                                  # bn0..bn5 + bn_last of AudioFeatNet
+    # rank 1 trained on its own shard statistics: its own buffers differ before the broadcast
+    assert any(not torch.equal(r1["bufs_own"][k], r0["bufs_own"][k]) for k in r0["bufs_own"] if "running" in k)
+    if bucket_mb < 1:
+        assert r0["n_buckets"] > 3
+        # after the first step every bucket's all-reduce is launched from a hook during the backward
+        assert r0["hook_launches"] == (STEPS - 1) * r0["n_buckets"], (r0["hook_launches"], r0["n_buckets"])
+
+
+def test_bench_self_launches_two_gloo_ranks():
+    """--gpus 2 without WORLD_SIZE: bench.py starts 2 ranks itself (torch.distributed.run child) and rank 0
+    prints the one JSON line with n_gpus 2."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu",
+                          "--workload", "plumbing", "--steps", "2", "--warmup", "1", "--bucket-mb", "0.05"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["ddp"]["grad_buckets"] > 1 and rec["config"]["ddp"]["broadcast_buffers"]
+    assert rec["value"] > 0

@@ -82,3 +82,21 @@ def test_mamba_tasnet_L_fullsize_4_layers():
         est_r = ref(mix.double())
     # speaker order is the model's own (no PIT needed: same weights); compare per speaker
     check_waveforms(est.transpose(1, 2), est_r.transpose(1, 2), tgt.transpose(1, 2), "Mamba-TasNet-L C3 (4 layers)")
+
+
+def test_avse1_audio_only_c1_enhance():
+    """C1 (BASELINE configs[0]): audio-only AVNet (model.py:117-118) end to end from 3 s waveforms:
+    HIP STFT -> AudioFeatNet -> FusionNet LSTM -> HIP iSTFT with the noisy phase (test.py:71-89)."""
+    from avse_challenge_amd import avse1, data
+    noisy, clean, _ = data.avse1_batch(2, "cpu", 14, lip_hw=8)
+    net = det_init_(avse1.AVNet(a_only=True), 74).to(DEV).eval()
+    ref = det_init_(avse1_ref.AVNet(a_only=True), 74).double().eval()
+    est = net.enhance(noisy.to(DEV), None)
+    spec = stft_ref.stft(noisy.numpy())
+    mag_T = np.swapaxes(np.abs(spec), -1, -2).astype(np.float32)
+    with torch.no_grad():
+        pred = ref({"noisy_audio_spec": torch.from_numpy(mag_T).double()[:, None]})[:, 0]
+    phase = np.angle(spec)
+    est_spec = np.swapaxes(pred.numpy(), -1, -2) * (np.cos(phase) + 1j * np.sin(phase))
+    ref_wave = torch.from_numpy(stft_ref.istft(est_spec, length=noisy.shape[-1]))
+    check_waveforms(est, ref_wave, clean, "avse1 C1 audio-only")

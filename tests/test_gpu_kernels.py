@@ -454,3 +454,84 @@ def test_scan_fwd_without_out_matches():
     out2, x2, oz2 = K().selective_scan_fwd(**ins, delta_softplus=True, return_out=False)
     assert out2 is None
     assert torch.equal(oz, oz2) and torch.equal(x, x2)
+
+
+# ------------------------------------------------------------------ C5 production shape (bf16, d_inner 1024, L 5999)
+
+def _c5_scan_inputs(b, d, l, seed):
+    bf = torch.bfloat16
+    ins = {"u": det_input((b, d, l), seed).to(bf), "delta": (0.2 * det_input((b, d, l), seed + 1)).to(bf),
+           "B": det_input((b, 1, 16, l), seed + 2).to(bf), "C": det_input((b, 1, 16, l), seed + 3).to(bf),
+           "z": det_input((b, d, l), seed + 4).to(bf)}
+    A = -torch.exp(0.5 * det_input((d, 16), seed + 5))
+    D, bias = det_input((d,), seed + 6), 0.3 * det_input((d,), seed + 7)
+    dout = det_input((b, d, l), seed + 8).to(bf)
+    return ins, A, D, bias, dout
+
+
+def test_c5_scan_bf16_production_shape_vs_oracle():
+    """C5 shape (b=2, d_inner=1024, L=5999, bf16 u/delta/z/B/C/dout, fp32 A/D/bias/state): the training
+    forward (return_out=False, as the model runs it) and the backward on the full width, checked against
+    fp64 autograd through the oracle on the SAME bf16 values for channels 0..63 (du, ddelta, dz, dA, dD,
+    ddelta_bias); dB / dC (sums over all 1024 channels) are checked by linearity — the full-width kernel's
+    dB / dC equal the sum of the kernel's per-64-channel-slice dB / dC — and slice 0's dB / dC against the
+    oracle. Tolerances as test_scan_bwd_bf16_vs_oracle (bf16 outputs: one bf16 rounding 2^-8 relative)."""
+    b, d, l, sl = 2, 1024, 5999, slice(0, 64)
+    ins, A, D, bias, dout = _c5_scan_inputs(b, d, l, 1200)
+    gi = {k: v.to(DEV) for k, v in ins.items()}
+    gA, gD, gb, gdo = A.to(DEV), D.to(DEV), bias.to(DEV), dout.to(DEV)
+    _, x, out_z = K().selective_scan_fwd(gi["u"], gi["delta"], gA, gi["B"], gi["C"], gD, gi["z"], gb, True,
+                                         return_out=False)
+    du, ddelta, dA, dB, dC, dD, dbias, dz, _ = K().selective_scan_bwd(
+        gi["u"], gi["delta"], gA, gi["B"], gi["C"], gD, gi["z"], gb, gdo, x, None, None, True, False)
+    r = {k: (v[:, sl] if k in ("u", "delta", "z") else v).double().requires_grad_(True) for k, v in ins.items()}
+    rA, rD, rb = (t[sl].double().requires_grad_(True) for t in (A, D, bias))
+    ref = mamba_ref.selective_scan(r["u"], r["delta"], rA, r["B"], r["C"], rD, r["z"], rb, True,
+                                   acc_dtype=torch.float64)
+    rel = (out_z[:, sl].double().cpu() - ref.detach()).abs() / (ref.detach().abs() + 1e-2)
+    assert float(rel.max()) <= 2 * 2 ** -8 + 1e-6, float(rel.max())
+    ref.backward(dout[:, sl].double())
+    for name, v, rg, tol in (("du", du[:, sl], r["u"].grad, 2 ** -8), ("ddelta", ddelta[:, sl], r["delta"].grad, 2 ** -8),
+                             ("dz", dz[:, sl], r["z"].grad, 2 ** -8), ("dA", dA[sl], rA.grad, 1e-4),
+                             ("dD", dD[sl], rD.grad, 1e-4), ("ddelta_bias", dbias[sl], rb.grad, 1e-4)):
+        rg = rg.detach().numpy()
+        close(v.float(), rg, 5e-5 * max(1.0, float(np.abs(rg).max())), tol, name)
+    # dB / dC: linearity over channel slices, slice 0 vs the oracle
+    sdB, sdC = torch.zeros_like(dB), torch.zeros_like(dC)
+    for c0 in range(0, d, 64):
+        s = slice(c0, c0 + 64)
+        _, xs, _ = K().selective_scan_fwd(gi["u"][:, s], gi["delta"][:, s], gA[s], gi["B"], gi["C"], gD[s],
+                                          gi["z"][:, s], gb[s], True, return_out=False)
+        res = K().selective_scan_bwd(gi["u"][:, s], gi["delta"][:, s], gA[s], gi["B"], gi["C"], gD[s], gi["z"][:, s],
+                                     gb[s], gdo[:, s], xs, None, None, True, False)
+        if c0 == 0:
+            for name, v, rg in (("dB slice0", res[3], r["B"].grad), ("dC slice0", res[4], r["C"].grad)):
+                rg = rg.detach().numpy()
+                close(v, rg, 5e-5 * max(1.0, float(np.abs(rg).max())), 1e-4, name)
+        sdB += res[3]
+        sdC += res[4]
+    for name, full, summed in (("dB", dB, sdB), ("dC", dC, sdC)):
+        close(full, summed, 1e-5 * max(1.0, float(summed.abs().max())), 1e-4, name + " linearity")
+    assert all(torch.isfinite(t).all() for t in (du, ddelta, dz, dA, dB, dC, dD, dbias))
+
+
+def test_c5_cconv_bf16_production_shape_vs_oracle():
+    """C5 causal conv at full width: (2, 1024, 5999) bf16 activations, fp32 weights, SiLU; fwd / dx within one
+    bf16 rounding of fp64 on the same bf16 values, dweight / dbias (fp32) to 1e-5 relative."""
+    b, d, l = 2, 1024, 5999
+    x0 = det_input((b, d, l), 1300).to(torch.bfloat16).double()
+    gy0 = det_input((b, d, l), 1301).to(torch.bfloat16).double()
+    x = x0.clone().requires_grad_(True)
+    wt = (0.5 * det_input((d, 4), 1302)).double().requires_grad_(True)
+    bias = det_input((d,), 1303).double().requires_grad_(True)
+    ref = mamba_ref.causal_conv1d(x, wt, bias, True)
+    ref.backward(gy0)
+    xg = x0.to(DEV, torch.bfloat16)
+    out = K().causal_conv1d_fwd(xg, wt.detach().float().to(DEV), bias.detach().float().to(DEV), True)
+    close(out.float(), ref.detach(), 1e-5, 2 ** -8, "fwd")
+    dx, dw, db = K().causal_conv1d_bwd(xg, wt.detach().float().to(DEV), bias.detach().float().to(DEV),
+                                       gy0.to(DEV, torch.bfloat16), silu=True)
+    close(dx.float(), x.grad, 1e-5, 2 ** -8, "dx")
+    sw, sb = float(wt.grad.abs().max()), float(bias.grad.abs().max())
+    close(dw, wt.grad, 1e-5 * sw, 1e-5, "dweight")
+    close(db, bias.grad, 1e-5 * sb, 1e-5, "dbias")

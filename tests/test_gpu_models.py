@@ -336,3 +336,32 @@ def test_bimamba_direction_streams_equal_serial(monkeypatch, graph):
     np.testing.assert_allclose(l1, l0, rtol=1e-6, atol=1e-7)
     for a, b in zip(p0, p1):
         torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-7)
+
+
+def test_avse1_audio_only_c1_golden():
+    """BASELINE configs[0] (C1): audio-only AVNet on the HIP path (AudioFeatNet -> FusionNet LSTM) vs the
+    reference-generated golden (reference train.py:28-30, model.py:117-118): eval and train-BN predictions
+    and loss, and every train-mode parameter gradient (max error relative to the gradient's max <= 2e-3,
+    cosine > 1 - 1e-6)."""
+    from avse_challenge_amd import avse1
+    g = load_golden("avse1_aonly")
+    net = det_init_(avse1.AVNet(a_only=True), 55).to(DEV)
+    batch = {"noisy_audio_spec": det_input((1, 1, 376, 257), 508).abs().to(DEV),
+             "mask": det_input((1, 1, 376, 257), 509).abs().to(DEV)}
+    for mode in ("eval", "train"):
+        net.train(mode == "train")
+        net.zero_grad()
+        pred = net(batch)
+        close(pred, g["pred_" + mode], 1e-4, 1e-4, "pred " + mode)
+        loss = net.training_step(batch)
+        close(loss, g["loss_" + mode], 1e-5, 1e-5, "loss " + mode)
+    loss.backward()
+    for k, p in net.named_parameters():
+        key = "g_" + k.replace(".", "__")
+        ref = np.asarray(g[key] if key in g else g[key + "__sub97"], np.float64)
+        got = (p.grad if key in g else p.grad.reshape(-1)[::97]).double().cpu().numpy()
+        scale = max(1e-12, float(np.abs(ref).max()))
+        err = float(np.abs(got - ref).max()) / scale
+        cos = float((got * ref).sum() / (np.linalg.norm(got) * np.linalg.norm(ref) + 1e-300))
+        assert err <= 2e-3 and cos > 1 - 1e-6, (k, err, cos)
+

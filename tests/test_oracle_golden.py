@@ -212,3 +212,36 @@ def test_avse2_sepblock_and_full():
     with torch.no_grad():
         _close(m(batch), g["out"], 1e-6)
         _close(m.cal_loss(batch), g["loss"], 1e-5)
+
+
+def test_avse1_audio_only_c1():
+    """BASELINE configs[0] (C1): audio-only AVNet (reference train.py:28-30, model.py:117-118), eval and
+    train BN, and the L1 loss gradients of every parameter."""
+    g = load_golden("avse1_aonly")
+    net = det_init_(avse1_ref.AVNet(a_only=True), 55)
+    batch = {"noisy_audio_spec": det_input((1, 1, 376, 257), 508).abs(),
+             "mask": det_input((1, 1, 376, 257), 509).abs()}
+    for mode in ("eval", "train"):
+        net.train(mode == "train")
+        pred = net(batch)
+        _close(pred, g["pred_" + mode], 1e-5)
+        loss = net.cal_loss(batch)
+        _close(loss, g["loss_" + mode], 1e-6)
+    loss.backward()
+    for k, p in net.named_parameters():
+        key = "g_" + k.replace(".", "__")
+        ref = g[key] if key in g else g[key + "__sub97"]
+        got = p.grad if key in g else p.grad.reshape(-1)[::97]
+        _close(got, ref, 1e-5 * max(1.0, float(np.abs(ref).max())), 1e-4)
+
+
+def test_dpmamba_wrapper_pinned():
+    """oracle/dpmamba_ref.Dual_Path_Model vs the reference's in-tree dual-path forward
+    (modules/dual_path.py:53-150) run over the same components, skip_around_intra True and False."""
+    from oracle import dpmamba_ref
+    g = load_golden("dpmamba_wrapper")
+    for sia in (True, False):
+        m = det_init_(dpmamba_ref.Dual_Path_Model(64, 64, dpmamba_ref.MambaBlocksSequential(1, 64),
+                                                  dpmamba_ref.MambaBlocksSequential(1, 64), 2, 10, 2, sia), 91)
+        with torch.no_grad():
+            _close(m(T(g["mixture_w"])), g["est_mask_" + ("sia" if sia else "nosia")], 1e-5)
