@@ -412,6 +412,9 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     #pragma unroll
                     for (int p = 0; p < NP; ++p) hs[s][p] = h[p];
                     if (s == TC / TS - 1) break;
+#ifdef AVSE_EXP_BWD_NOPASS1
+                    continue;
+#endif
     #pragma unroll 4
                     for (int i = 0; i < TS; ++i) {
                         const int t = s * TS + i;
@@ -502,7 +505,11 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     #pragma unroll
                             for (int p = 0; p < NP; ++p) {
                                 const f2_t hp = (i == 0) ? hs[s][p] : hist[i > 0 ? i - 1 : 0][p];
+#ifdef AVSE_EXP_BWD_NOADJEXP
+                                const f2_t dA = dt2 * A2v[p];
+#else
                                 const f2_t dA = exp2_2(dt2 * A2v[p]);
+#endif
                                 lam[p] = lam[p] * dAn[p] + gv2 * cp[p];
                                 const f2_t lhp = lam[p] * dA * hp;
                                 const f2_t lb = lam[p] * bp[p];
@@ -528,6 +535,10 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     #pragma unroll
                             for (int j = 0; j < 8; ++j) part[j] = 0.f;
                         }
+#ifdef AVSE_EXP_BWD_NORED
+                        if (part[0] == 12345.f) a.dB[0] = part[1] + part[2] + part[3] + part[4] + part[5] + part[6] + part[7];
+                        continue;
+#endif
                         float r2[2];
                         rs8_swap(part, r2);
                         if ((id.lane & 12) == 0) {

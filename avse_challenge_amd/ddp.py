@@ -37,7 +37,10 @@ class Trainer:
         self.flat = torch.zeros(n, device=dev)
         ranges, off = [], 0
         for p in self.params:
-            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            # same strides as the parameter (channels_last conv weights too): autograd accumulates in place
+            # without a layout copy (dense, non-overlapping parameters only)
+            seg = self.flat[off:off + p.numel()]
+            p.grad = seg.as_strided(p.size(), p.stride()) if _dense(p) else seg.view_as(p)
             ranges.append((off, off + p.numel()))
             off += p.numel()
         self.buf_f = self.buf_i = None
@@ -185,6 +188,19 @@ class Trainer:
             self._finish_allreduce()
         self.g_opt.replay()
         return self.loss
+
+
+def _dense(t):
+    """t's strides address exactly numel() distinct elements (a permutation of a contiguous block)."""
+    if t.numel() == 0:
+        return False
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.size()) if sz > 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
 
 
 def _flatten_buffers(model, dev):

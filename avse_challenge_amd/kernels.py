@@ -3,6 +3,8 @@
 Each wrapper validates shapes/dtypes/strides, allocates its outputs and workspace with torch
 (caching allocator, stream-ordered) and enqueues the HIP kernels on torch's current stream.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -24,6 +26,20 @@ def _dtype_code(dt):
     if dt == torch.bfloat16:
         return AVSE_BF16
     raise RuntimeError(f"unsupported dtype {dt} (fp32 or bf16)")
+
+
+# (b, d, l) outputs of the scan / conv kernels get a time stride rounded up to this many bytes when set
+# (> 0): every row then starts on a cache-line boundary (tools/scan_bench.py --pad measures the effect)
+TIME_ALIGN_BYTES = int(os.environ.get("AVSE_TIME_ALIGN_BYTES", "0"))
+
+
+def _bdl_empty(b, d, l, dtype, dev):
+    if TIME_ALIGN_BYTES > 0:
+        per = max(1, TIME_ALIGN_BYTES // torch.empty((), dtype=dtype).element_size())
+        lp = -(-l // per) * per
+        if lp != l:
+            return torch.empty((b, d, lp), device=dev, dtype=dtype)[..., :l]
+    return torch.empty((b, d, l), device=dev, dtype=dtype)
 
 
 def _last_contig(t):
@@ -63,9 +79,9 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
     nck = L.avse_scan_n_chunks(l)
     if not return_out and z is None:
         raise RuntimeError("return_out=False needs z (the gated output is then the only result)")
-    out = torch.empty((b, d, l), device=u.device, dtype=dt) if return_out else None
+    out = _bdl_empty(b, d, l, dt, u.device) if return_out else None
     x = torch.empty((b, d, nck, 2 * NSTATE), device=u.device, dtype=torch.float32)
-    out_z = torch.empty((b, d, l), device=u.device, dtype=dt) if z is not None else None
+    out_z = _bdl_empty(b, d, l, dt, u.device) if z is not None else None
     a = ScanFwdArgs()
     a.batch, a.dim, a.seqlen, a.dstate = b, d, l, NSTATE
     a.in_dtype, a.delta_softplus, a.reverse = _dtype_code(dt), int(bool(delta_softplus)), int(bool(reverse))
@@ -108,8 +124,8 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
     if x.shape != (b, d, L.avse_scan_n_chunks(l), 2 * NSTATE):
         raise RuntimeError(f"scan intermediates have shape {tuple(x.shape)}; expected avse layout")
     dev = u.device
-    du = torch.empty((b, d, l), device=dev, dtype=dt)
-    ddelta = torch.empty((b, d, l), device=dev, dtype=dt)
+    du = _bdl_empty(b, d, l, dt, dev)
+    ddelta = _bdl_empty(b, d, l, dt, dev)
     dA = torch.empty((d, NSTATE), device=dev, dtype=torch.float32)
     def _grad_bc(o):
         if o is None:
@@ -123,7 +139,7 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
     dbias = torch.empty((d,), device=dev, dtype=torch.float32) if delta_bias is not None else None
     if z is not None:
         if dz is None:
-            dz = torch.empty((b, d, l), device=dev, dtype=dt)
+            dz = _bdl_empty(b, d, l, dt, dev)
         elif dz.stride(-1) != 1 or dz.dtype != dt or tuple(dz.shape) != (b, d, l):
             raise RuntimeError("dz must be a (b, d, l) view with unit last stride and the input dtype")
     else:
@@ -175,7 +191,7 @@ def causal_conv1d_fwd(x, weight, bias=None, silu=False, reverse=False):
     bias = None if bias is None else bias.float().contiguous()
     b, d, l = x.shape
     w = weight.shape[1]
-    out = torch.empty((b, d, l), device=x.device, dtype=dt)
+    out = _bdl_empty(b, d, l, dt, x.device)
     fn = _lib.lib().avse_cconv_fwd if dt == torch.float32 else _lib.lib().avse_cconv_fwd_bf16
     check(fn(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(out), out.stride(0),
              out.stride(1), int(bool(silu)), int(bool(reverse)), stream_ptr(x.device)), "avse_cconv_fwd")
@@ -197,7 +213,7 @@ def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False)
     w = weight.shape[1]
     dx_ret = dx
     if dx is None or dx.dtype != dt or dx.stride(-1) != 1:
-        dx = torch.empty((b, d, l), device=x.device, dtype=dt)
+        dx = _bdl_empty(b, d, l, dt, x.device)
     dweight = torch.empty((d, w), device=x.device, dtype=torch.float32)
     dbias = torch.empty((d,), device=x.device, dtype=torch.float32) if bias is not None else None
     ws = torch.empty((_lib.lib().avse_cconv_bwd_workspace_bytes(b, d, w) + 3) // 4, device=x.device,

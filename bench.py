@@ -488,7 +488,12 @@ class PlumbingStep:
 # ------------------------------------------------------------------------------ CPU baseline helpers
 
 def _cpu_threads():
+    """The host cores this process may use: OMP_NUM_THREADS when the launcher sets it (the GPU box sets the
+    box's CPU share there; affinity / cpu_count show the whole machine), else the affinity mask."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
     torch.set_num_threads(max(1, n))
 
 

@@ -67,6 +67,56 @@ def selective_scan(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_sof
     return (out, h) if return_last_state else out
 
 
+@torch.no_grad()
+def selective_scan_grads(u, delta, A, B, C, D, z, delta_bias, delta_softplus, dout, acc_dtype=torch.float64):
+    """Explicit adjoint of ``selective_scan`` — the gradients autograd computes through selective_scan_ref
+    (selective_scan_interface.py:91-157), restated as the backward recurrence with O(L) memory (autograd through the
+    per-step Python loop is O(L^2) in time: 400 s at L = 5999). Pinned against the reference's autograd gradients by
+    tests/golden/scan_fp32 (test_oracle_golden.py). B, C: (b, 1, n, l) or (b, n, l) shared over d.
+    Returns dict(du, ddelta, dA, dB, dC, dD, ddelta_bias, dz), dB / dC shaped like B / C."""
+    f = lambda t: None if t is None else t.to(acc_dtype)      # noqa: E731
+    u, delta, A, D, z, bias, dout = f(u), f(delta), f(A), f(D), f(z), f(delta_bias), f(dout)
+    b, d, l = u.shape
+    Bx, Cx = f(B), f(C)
+    b4 = Bx.dim() == 4
+    Bv = Bx[:, 0] if b4 else Bx                               # (b, n, l)
+    Cv = Cx[:, 0] if b4 else Cx
+    xpre = delta + (bias[:, None] if bias is not None else 0.0)
+    dt = F.softplus(xpre) if delta_softplus else xpre         # (b, d, l)
+    dA = torch.exp(dt[:, :, None, :] * A[None, :, :, None])    # (b, d, n, l)
+    dBu = (dt * u)[:, :, None, :] * Bv[:, None]               # (b, d, n, l)
+    H = torch.empty_like(dA)
+    h = torch.zeros(b, d, A.shape[1], dtype=acc_dtype)
+    for t in range(l):
+        h = dA[..., t] * h + dBu[..., t]
+        H[..., t] = h
+    y = (H * Cv[:, None]).sum(2)                              # (b, d, l)
+    out = y + (u * D[:, None] if D is not None else 0.0)
+    if z is not None:
+        sz = torch.sigmoid(z)
+        g = dout * z * sz                                     # d out_z / d out = silu(z)
+        dz = dout * out * sz * (1 + z * (1 - sz))
+    else:
+        g, dz = dout, None
+    lam = torch.empty_like(dA)
+    acc = torch.zeros(b, d, A.shape[1], dtype=acc_dtype)
+    for t in range(l - 1, -1, -1):                            # lambda_t = g_t C_t + dA_{t+1} lambda_{t+1}
+        acc = g[:, :, None, t] * Cv[:, None, :, t] + acc
+        lam[..., t] = acc
+        acc = acc * dA[..., t]
+    Hprev = torch.cat([torch.zeros_like(H[..., :1]), H[..., :-1]], -1)
+    lam_dA_h = lam * dA * Hprev                               # (b, d, n, l)
+    dC = (g[:, :, None, :] * H).sum(1)                        # (b, n, l)
+    dB = (lam * (dt * u)[:, :, None, :]).sum(1)
+    du = (lam * Bv[:, None]).sum(2) * dt + (g * D[:, None] if D is not None else 0.0)
+    ddt = (lam_dA_h * A[None, :, :, None]).sum(2) + (lam * Bv[:, None]).sum(2) * u
+    dAm = (lam_dA_h * dt[:, :, None, :]).sum((0, 3))
+    ddelta = ddt * torch.sigmoid(xpre) if delta_softplus else ddt
+    return {"du": du, "ddelta": ddelta, "dA": dAm, "dB": dB[:, None] if b4 else dB, "dC": dC[:, None] if b4 else dC,
+            "dD": (g * u).sum((0, 2)) if D is not None else None,
+            "ddelta_bias": ddelta.sum((0, 2)) if bias is not None else None, "dz": dz}
+
+
 def causal_conv1d(x, weight, bias=None, silu=False):
     """Depthwise causal conv: x (b, d, l), weight (d, w), bias (d,) -> (b, d, l)."""
     d, w = weight.shape

@@ -472,7 +472,7 @@ def _c5_scan_inputs(b, d, l, seed):
 def test_c5_scan_bf16_production_shape_vs_oracle():
     """C5 shape (b=2, d_inner=1024, L=5999, bf16 u/delta/z/B/C/dout, fp32 A/D/bias/state): the training
     forward (return_out=False, as the model runs it) and the backward on the full width, checked against
-    fp64 autograd through the oracle on the SAME bf16 values for channels 0..63 (du, ddelta, dz, dA, dD,
+    the fp64 oracle (forward recurrence and its explicit adjoint) on the SAME bf16 values for channels 0..63 (du, ddelta, dz, dA, dD,
     ddelta_bias); dB / dC (sums over all 1024 channels) are checked by linearity — the full-width kernel's
     dB / dC equal the sum of the kernel's per-64-channel-slice dB / dC — and slice 0's dB / dC against the
     oracle. Tolerances as test_scan_bwd_bf16_vs_oracle (bf16 outputs: one bf16 rounding 2^-8 relative)."""
@@ -484,18 +484,19 @@ def test_c5_scan_bf16_production_shape_vs_oracle():
                                          return_out=False)
     du, ddelta, dA, dB, dC, dD, dbias, dz, _ = K().selective_scan_bwd(
         gi["u"], gi["delta"], gA, gi["B"], gi["C"], gD, gi["z"], gb, gdo, x, None, None, True, False)
-    r = {k: (v[:, sl] if k in ("u", "delta", "z") else v).double().requires_grad_(True) for k, v in ins.items()}
-    rA, rD, rb = (t[sl].double().requires_grad_(True) for t in (A, D, bias))
-    ref = mamba_ref.selective_scan(r["u"], r["delta"], rA, r["B"], r["C"], rD, r["z"], rb, True,
+    sl_in = {k: (v[:, sl] if k in ("u", "delta", "z") else v).double() for k, v in ins.items()}
+    ref = mamba_ref.selective_scan(**sl_in, A=A[sl], D=D[sl], delta_bias=bias[sl], delta_softplus=True,
                                    acc_dtype=torch.float64)
-    rel = (out_z[:, sl].double().cpu() - ref.detach()).abs() / (ref.detach().abs() + 1e-2)
+    rel = (out_z[:, sl].double().cpu() - ref).abs() / (ref.abs() + 1e-2)
     assert float(rel.max()) <= 2 * 2 ** -8 + 1e-6, float(rel.max())
-    ref.backward(dout[:, sl].double())
-    for name, v, rg, tol in (("du", du[:, sl], r["u"].grad, 2 ** -8), ("ddelta", ddelta[:, sl], r["delta"].grad, 2 ** -8),
-                             ("dz", dz[:, sl], r["z"].grad, 2 ** -8), ("dA", dA[sl], rA.grad, 1e-4),
-                             ("dD", dD[sl], rD.grad, 1e-4), ("ddelta_bias", dbias[sl], rb.grad, 1e-4)):
-        rg = rg.detach().numpy()
-        close(v.float(), rg, 5e-5 * max(1.0, float(np.abs(rg).max())), tol, name)
+    # fp64 truth: the explicit adjoint (pinned against the reference's autograd by test_oracle_golden.py)
+    rg = mamba_ref.selective_scan_grads(**sl_in, A=A[sl], D=D[sl], delta_bias=bias[sl], delta_softplus=True,
+                                        dout=dout[:, sl])
+    for name, v, key, tol in (("du", du[:, sl], "du", 2 ** -8), ("ddelta", ddelta[:, sl], "ddelta", 2 ** -8),
+                              ("dz", dz[:, sl], "dz", 2 ** -8), ("dA", dA[sl], "dA", 1e-4),
+                              ("dD", dD[sl], "dD", 1e-4), ("ddelta_bias", dbias[sl], "ddelta_bias", 1e-4)):
+        ref_g = rg[key].numpy()
+        close(v.float(), ref_g, 5e-5 * max(1.0, float(np.abs(ref_g).max())), tol, name)
     # dB / dC: linearity over channel slices, slice 0 vs the oracle
     sdB, sdC = torch.zeros_like(dB), torch.zeros_like(dC)
     for c0 in range(0, d, 64):
@@ -505,9 +506,9 @@ def test_c5_scan_bf16_production_shape_vs_oracle():
         res = K().selective_scan_bwd(gi["u"][:, s], gi["delta"][:, s], gA[s], gi["B"], gi["C"], gD[s], gi["z"][:, s],
                                      gb[s], gdo[:, s], xs, None, None, True, False)
         if c0 == 0:
-            for name, v, rg in (("dB slice0", res[3], r["B"].grad), ("dC slice0", res[4], r["C"].grad)):
-                rg = rg.detach().numpy()
-                close(v, rg, 5e-5 * max(1.0, float(np.abs(rg).max())), 1e-4, name)
+            for name, v, key in (("dB slice0", res[3], "dB"), ("dC slice0", res[4], "dC")):
+                ref_g = rg[key].numpy()
+                close(v, ref_g, 5e-5 * max(1.0, float(np.abs(ref_g).max())), 1e-4, name)
         sdB += res[3]
         sdC += res[4]
     for name, full, summed in (("dB", dB, sdB), ("dC", dC, sdC)):

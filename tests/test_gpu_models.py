@@ -340,14 +340,17 @@ def test_bimamba_direction_streams_equal_serial(monkeypatch, graph):
 
 def test_avse1_audio_only_c1_golden():
     """BASELINE configs[0] (C1): audio-only AVNet on the HIP path (AudioFeatNet -> FusionNet LSTM) vs the
-    reference-generated golden (reference train.py:28-30, model.py:117-118): eval and train-BN predictions
-    and loss, and every train-mode parameter gradient (max error relative to the gradient's max <= 2e-3,
-    cosine > 1 - 1e-6)."""
+    reference-generated golden (reference train.py:28-30, model.py:117-118): eval and train-BN predictions and
+    loss. Train-mode parameter gradients vs fp64 truth (the oracle in fp64 on the same weights, whose fp32 run is
+    pinned by the same golden): each gradient's max error relative to its max, and its cosine distance, must stay
+    within 3x those of the reference's own fp32 gradients (the golden) vs that truth (floors 1e-4 / 1e-7); the
+    L1 loss's sign(pred - mask) makes the early-layer errors ~2e-3 already in the reference's fp32 run."""
     from avse_challenge_amd import avse1
     g = load_golden("avse1_aonly")
     net = det_init_(avse1.AVNet(a_only=True), 55).to(DEV)
-    batch = {"noisy_audio_spec": det_input((1, 1, 376, 257), 508).abs().to(DEV),
-             "mask": det_input((1, 1, 376, 257), 509).abs().to(DEV)}
+    ref64 = det_init_(avse1_ref.AVNet(a_only=True), 55).double().train()
+    spec, mask = det_input((1, 1, 376, 257), 508).abs(), det_input((1, 1, 376, 257), 509).abs()
+    batch = {"noisy_audio_spec": spec.to(DEV), "mask": mask.to(DEV)}
     for mode in ("eval", "train"):
         net.train(mode == "train")
         net.zero_grad()
@@ -356,12 +359,21 @@ def test_avse1_audio_only_c1_golden():
         loss = net.training_step(batch)
         close(loss, g["loss_" + mode], 1e-5, 1e-5, "loss " + mode)
     loss.backward()
+    ref64.cal_loss({"noisy_audio_spec": spec.double(), "mask": mask.double()}).backward()
+    p64 = dict(ref64.named_parameters())
+    gscale = max(float(q.grad.abs().max()) for q in p64.values())
     for k, p in net.named_parameters():
         key = "g_" + k.replace(".", "__")
-        ref = np.asarray(g[key] if key in g else g[key + "__sub97"], np.float64)
-        got = (p.grad if key in g else p.grad.reshape(-1)[::97]).double().cpu().numpy()
-        scale = max(1e-12, float(np.abs(ref).max()))
-        err = float(np.abs(got - ref).max()) / scale
-        cos = float((got * ref).sum() / (np.linalg.norm(got) * np.linalg.norm(ref) + 1e-300))
-        assert err <= 2e-3 and cos > 1 - 1e-6, (k, err, cos)
-
+        sub = (lambda t: t) if key in g else (lambda t: t.reshape(-1)[::97])
+        gold = np.asarray(g[key] if key in g else g[key + "__sub97"], np.float64)
+        truth = sub(p64[k].grad).numpy()
+        got = sub(p.grad).double().cpu().numpy()
+        scale = float(np.abs(truth).max())
+        if scale < 1e-7 * gscale:       # conv biases feeding a train-mode BatchNorm: gradient exactly 0, noise only
+            assert float(np.abs(got).max()) < 5e-5 * gscale, (k, float(np.abs(got).max()), gscale)
+            continue
+        e_gpu = float(np.abs(got - truth).max()) / scale
+        e_ref = float(np.abs(gold - truth).max()) / scale
+        cosf = lambda a: float((a * truth).sum() / (np.linalg.norm(a) * np.linalg.norm(truth) + 1e-300))  # noqa: E731
+        cos, cos_ref = cosf(got), cosf(gold)
+        assert e_gpu <= max(3 * e_ref, 1e-4) and 1 - cos <= max(3 * (1 - cos_ref), 1e-7), (k, e_gpu, e_ref, cos, cos_ref)

@@ -245,3 +245,14 @@ def test_dpmamba_wrapper_pinned():
                                                   dpmamba_ref.MambaBlocksSequential(1, 64), 2, 10, 2, sia), 91)
         with torch.no_grad():
             _close(m(T(g["mixture_w"])), g["est_mask_" + ("sia" if sia else "nosia")], 1e-5)
+
+
+def test_scan_explicit_adjoint_matches_reference_autograd():
+    """oracle.mamba_ref.selective_scan_grads (the O(L) explicit backward the full-length GPU tests use as truth)
+    against the gradients of autograd through the reference's selective_scan_ref (golden scan_fp32)."""
+    g = load_golden("scan_fp32")
+    ins = {k: T(g[k]) for k in ("u", "delta", "A", "B", "C", "D", "z", "delta_bias")}
+    r = mamba_ref.selective_scan_grads(**ins, delta_softplus=True, dout=T(g["dout"]))
+    for k in ("u", "delta", "A", "B", "C", "D", "z", "delta_bias"):
+        ref = g["d" + k]
+        _close(r["d" + k], ref, 2e-5 * max(1.0, float(np.abs(ref).max())), 1e-5)
