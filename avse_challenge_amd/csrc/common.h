@@ -79,6 +79,7 @@ __device__ inline float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // packed fp32 pair: v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32 do two lanes' worth of f32 math per
 // issue (MI355X: 64 FLOP/clk/SIMD for v_pk_fma_f32 vs 32 for v_fma_f32)
 typedef float f2_t __attribute__((ext_vector_type(2)));
+__device__ inline f2_t pkfma(f2_t a, f2_t b, f2_t c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ inline f2_t exp2_2(f2_t x) { return f2_t{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; }
 __device__ inline float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * AVSE_LOG2E); }
 

@@ -145,6 +145,9 @@ __device__ inline void store_ud(float* s_ud, const RowRegs<Tin>& ru, const RowRe
     }
 }
 
+// the wave index as a wave-uniform value: row biases (and row offsets) then live in SGPRs
+__device__ inline int wave_u() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 template <bool HAS_BIAS>
 __device__ inline void load_bias_rows(float* bias_r, const float* bias, int d0, int D) {
     const int wave = threadIdx.x >> 6;
@@ -178,13 +181,14 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
         A2v[p] = dvalid ? f2_t{a.A[(int64_t)d * NSTATE + j], a.A[(int64_t)d * NSTATE + j + 1]} * AVSE_LOG2E : f2_t{0.f, 0.f};
         h2[p] = f2_t{0.f, 0.f};
     }
-    float dtsum = 0.f;
     const float Dv = (HAS_D && dvalid) ? a.D[d] : 0.f;
 
     const Tin* u = (const Tin*)a.u;
     const Tin* dl = (const Tin*)a.delta;
     const Tin* z = (const Tin*)a.z;
     const int nck = (L + TC - 1) / TC;
+    const int nck32 = (L + 31) / 32;
+    float* xrow = a.x + ((int64_t)b * D + (dvalid ? d : 0)) * nck32 * (2 * NSTATE) + 2 * id.g * NS;
 
     const int nrow = min(CPB, D - d0);
     float bias_r[RPT];
@@ -229,7 +233,6 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                 const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
                 const float dt = ud.y, dtu = ud.y * ud.x;
                 const f2_t dt2 = f2_t{dt, dt}, dtu2 = f2_t{dtu, dtu};
-                dtsum += dt;
                 f2_t y2 = f2_t{0.f, 0.f};
 #pragma unroll
                 for (int p = 0; p < NS / 2; ++p) {
@@ -249,10 +252,24 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                 my_ud[2 * (t + q)] = out;                              // u slot <- out
             }
         };
-        int t = 0;
+        // always the full 64 steps: the staged tail of the last chunk is zero (dt = 0, u = 0, B = C = 0), which
+        // leaves h unchanged, so no step needs a bounds test; the state is checkpointed every 16 steps
+        // (x slot j = state after logical step 16 j + 15, clamped to the last step)
 #ifndef AVSE_EXP_NOCOMPUTE
-        for (; t + U <= tn; t += U) steps(t, std::integral_constant<int, U>());
-        for (; t < tn; ++t) steps(t, std::integral_constant<int, 1>());
+#pragma unroll 1
+        for (int q32 = 0; q32 < TC / 32; ++q32) {
+            steps(q32 * 32, std::integral_constant<int, U>());
+            steps(q32 * 32 + U, std::integral_constant<int, U>());
+            const f2_t ha0 = h2[0], ha1 = h2[1];               // state after step 16 of the 32
+            steps(q32 * 32 + 2 * U, std::integral_constant<int, U>());
+            steps(q32 * 32 + 3 * U, std::integral_constant<int, U>());
+            const int r = k * (TC / 32) + q32;                  // x row: (after step 32r + 15, after 32r + 31)
+            if (dvalid && r < nck32) {
+                float4* xp = reinterpret_cast<float4*>(xrow + (int64_t)r * (2 * NSTATE));
+                xp[0] = make_float4(ha0.x, h2[0].x, ha0.y, h2[0].y);
+                xp[1] = make_float4(ha1.x, h2[1].x, ha1.y, h2[1].y);
+            }
+        }
 #endif
         RowRegs<Tin> rz;       // this chunk's z for the gate, issued before the barrier wait
         if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t0, tn, L, rev);
@@ -280,13 +297,6 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                                            s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane] * siluf_(rz.at(i)));
                 }
             }
-        }
-        if (dvalid) {
-            float* xp = a.x + (((int64_t)b * D + d) * nck + k) * (2 * NSTATE) + 2 * id.g * NS;
-            float4 v0 = make_float4(fast_exp2(dtsum * A2v[0].x), h2[0].x, fast_exp2(dtsum * A2v[0].y), h2[0].y);
-            float4 v1 = make_float4(fast_exp2(dtsum * A2v[1].x), h2[1].x, fast_exp2(dtsum * A2v[1].y), h2[1].y);
-            reinterpret_cast<float4*>(xp)[0] = v0;
-            reinterpret_cast<float4*>(xp)[1] = v1;
         }
         __syncthreads();
     }
@@ -317,12 +327,21 @@ __device__ inline void rs8_swap(const float v[8], float r[2]) {
 
 constexpr int RED = 8;   // adjoint steps buffered per cross-wave dB/dC flush
 
-template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS>
-__global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int nblk_d) {
+// keeps the scheduler from hoisting the LDS reads of all 16 unrolled steps (which needs ~10 VGPRs per step
+// on top of the 64 of the state history and spills); the other wave of the SIMD covers the LDS latency
+#ifndef AVSE_NO_SCHED_FENCE
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SCHED_FENCE() do {} while (0)
+#endif
+
+template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS, bool FOLD>
+__global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, int nblk_d) {
     __shared__ __attribute__((aligned(16))) float s_ud[CPB * UD_STRIDE];   // (u, dt) -> (du, ddelta)
-    __shared__ __attribute__((aligned(16))) float s_zg[CPB * Z_STRIDE];    // (z, dout) -> (dz, g)
+    __shared__ __attribute__((aligned(16))) float s_zg[CPB * Z_STRIDE];    // (F, g) -> (dz, g)  [(z, dout) unfolded]
     __shared__ __attribute__((aligned(16))) float s_bc[TC * BC_STRIDE];
     __shared__ float s_red[4 * RED * 2 * NSTATE];
+    __shared__ float s_bias[CPB];              // delta_bias of the block's rows (LDS, not 16 VGPRs per thread)
 
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int b = bid / nblk_d, cb = bid % nblk_d, d0 = cb * CPB;
@@ -331,21 +350,23 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     const int d = d0 + id.c;
     const bool dvalid = d < D;
     const int nck = (L + TC - 1) / TC;
+    const int nck32 = (L + 31) / 32;
 
     // the lane's 4 states as 2 packed pairs (v_pk_mul / v_pk_fma), as in the forward
     constexpr int NP = NS / 2;
-    f2_t Av[NP], A2v[NP];
+    f2_t A2v[NP];                              // A log2(e); dL/d(dt) sums A2v terms and is scaled by ln 2 once
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         const int j = id.g * NS + 2 * p;
-        Av[p] = dvalid ? f2_t{a.A[(int64_t)d * NSTATE + j], a.A[(int64_t)d * NSTATE + j + 1]} : f2_t{0.f, 0.f};
-        A2v[p] = Av[p] * AVSE_LOG2E;
+        A2v[p] = dvalid ? f2_t{a.A[(int64_t)d * NSTATE + j], a.A[(int64_t)d * NSTATE + j + 1]} * AVSE_LOG2E
+                        : f2_t{0.f, 0.f};
     }
     const float Dv = (HAS_D && dvalid) ? a.D[d] : 0.f;
 
+    // lam = dL/dh carried backwards over the whole row; dAn = dA of the step after the current one
     f2_t lam[NP], dAn[NP], dA_acc[NP];
 #pragma unroll
-    for (int p = 0; p < NP; ++p) { lam[p] = f2_t{0.f, 0.f}; dAn[p] = f2_t{0.f, 0.f}; dA_acc[p] = f2_t{0.f, 0.f}; }
+    for (int p = 0; p < NP; ++p) { lam[p] = f2_t{0.f, 0.f}; dAn[p] = f2_t{1.f, 1.f}; dA_acc[p] = f2_t{0.f, 0.f}; }
     float dD_acc = 0.f, dbias_acc = 0.f;
 
     const Tin* u = (const Tin*)a.u;
@@ -354,18 +375,20 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
     const Tin* dout = (const Tin*)a.dout;
     float* ws_bc = a.workspace;                                    // (b, nblk_d, 32, L)
     const int64_t slab = (int64_t)2 * NSTATE * L;
+    const float* xrow = a.x + ((int64_t)b * D + (dvalid ? d : 0)) * nck32 * (2 * NSTATE) + 2 * id.g * NS;
 
     const bool rev = a.reverse != 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nrow_b = min(CPB, D - d0);
-    float bias_r[RPT];
-    load_bias_rows<HAS_BIAS>(bias_r, a.delta_bias, d0, D);
-    const bool fold_gate = !a.recompute_out_z;
+    if (threadIdx.x < CPB) s_bias[threadIdx.x] = (HAS_BIAS && d0 + (int)threadIdx.x < D) ? a.delta_bias[d0 + threadIdx.x] : 0.f;
+    __syncthreads();
+    constexpr bool fold_gate = FOLD;        // = !recompute_out_z (the drop-in's reference call recomputes out_z)
 
     for (int k = nck - 1; k >= 0; --k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
         {
-            // all global loads of the chunk in flight before any LDS store
+            // all global loads of the chunk in flight before any LDS store; steps past the row's end stage
+            // as zeros (dt = u = B = C = g = 0): the recurrences then pass through them unchanged
             RowRegs<Tin> ru, rd, rz, rg;
             BCRegs<Tin> rbc;
             ru.load(u, a.u_bs, a.u_ds, b, d0, D, t0, tn, L, rev);
@@ -374,7 +397,12 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
             rg.load(dout, a.dout_bs, a.dout_ds, b, d0, D, t0, tn, L, rev);
             rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t0, tn, L, rev);
             __syncthreads();
-            store_ud<Tin, SOFTPLUS, HAS_BIAS>(s_ud, ru, rd, bias_r, tn, nrow_b);
+            {
+                float bias_r[RPT];
+#pragma unroll
+                for (int i = 0; i < RPT; ++i) bias_r[i] = s_bias[wave + 4 * i];
+                store_ud<Tin, SOFTPLUS, HAS_BIAS>(s_ud, ru, rd, bias_r, tn, nrow_b);
+            }
             rbc.store(s_bc, tn);
             // with z (and no out_z recompute) the gate is folded here, once per element instead of once
             // per lane per step: s_zg = (F, g) with g = dout silu(z) and F = dout sg (1 + z (1 - sg)),
@@ -392,181 +420,160 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(avse_scan_bwd_args a, int 
         }
         __syncthreads();
 
-        // chunk body; FULL (tn == TC) would drop the per-step bounds tests
-        auto chunk_body = [&](auto FULLC) {
-            constexpr bool FULL = decltype(FULLC)::value;
-            // pass 1: state at every sub-chunk start
-            f2_t hs[TC / TS][NP];
+        // 16-step sub-chunks in reverse; each restarts from the forward's 16-step checkpoint (no recompute pass
+        // over the chunk), replays its steps into registers, then runs the adjoint
+#pragma unroll 1
+        for (int s = TC / TS - 1; s >= 0; --s) {
+            const int ts = s * TS;
+            if (ts >= tn) continue;                 // wholly past the row's end: lam stays 0, nothing to add
+            f2_t h0[NP];
+            {
+                const int j = (t0 + ts) / TS - 1;   // checkpoint slot = state after step t0 + ts - 1
+                if (j >= 0 && dvalid) {
+                    const float* xp = xrow + (int64_t)(j >> 1) * (2 * NSTATE) + (j & 1);
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) h0[p] = f2_t{xp[4 * p], xp[4 * p + 2]};
+                } else {
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) h0[p] = f2_t{0.f, 0.f};
+                }
+            }
+            f2_t hist[TS][NP];
             {
                 f2_t h[NP];
-                if (k > 0 && dvalid) {
-                    const float* xp = a.x + (((int64_t)b * D + d) * nck + (k - 1)) * (2 * NSTATE) + 2 * id.g * NS;
-    #pragma unroll
-                    for (int p = 0; p < NP; ++p) h[p] = f2_t{xp[4 * p + 1], xp[4 * p + 3]};
-                } else {
-    #pragma unroll
-                    for (int p = 0; p < NP; ++p) h[p] = f2_t{0.f, 0.f};
-                }
-    #pragma unroll
-                for (int s = 0; s < TC / TS; ++s) {
-    #pragma unroll
-                    for (int p = 0; p < NP; ++p) hs[s][p] = h[p];
-                    if (s == TC / TS - 1) break;
-#ifdef AVSE_EXP_BWD_NOPASS1
-                    continue;
-#endif
-    #pragma unroll 4
-                    for (int i = 0; i < TS; ++i) {
-                        const int t = s * TS + i;
-                        if (!FULL && t >= tn) break;
-                        const float2 ud = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * t]);
-                        const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
-                        const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
-                        const f2_t dt2 = f2_t{ud.y, ud.y}, dtu2 = f2_t{ud.y * ud.x, ud.y * ud.x};
-    #pragma unroll
-                        for (int p = 0; p < NP; ++p) h[p] = exp2_2(dt2 * A2v[p]) * h[p] + dtu2 * bp[p];
+#pragma unroll
+                for (int p = 0; p < NP; ++p) h[p] = h0[p];
+                // the LDS operands of step i + 1 are read while step i computes (one step of software
+                // pipelining: with two waves per SIMD the LDS latency is otherwise exposed every step)
+                float2 ud_n = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * ts]);
+                float4 bq_n = *reinterpret_cast<const float4*>(&s_bc[ts * BC_STRIDE + id.g * NS]);
+                float4 cq_n = *reinterpret_cast<const float4*>(&s_bc[ts * BC_STRIDE + NSTATE + id.g * NS]);
+                float2 zg_n = *reinterpret_cast<const float2*>(&s_zg[id.c * Z_STRIDE + 2 * ts]);
+#pragma unroll
+                for (int i = 0; i < TS; ++i) {
+                    const int t = ts + i;
+                    const float2 ud = ud_n, zg = zg_n;
+                    const float4 bq = bq_n, cq = cq_n;
+                    if (i + 1 < TS) {
+                        ud_n = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * (t + 1)]);
+                        bq_n = *reinterpret_cast<const float4*>(&s_bc[(t + 1) * BC_STRIDE + id.g * NS]);
+                        cq_n = *reinterpret_cast<const float4*>(&s_bc[(t + 1) * BC_STRIDE + NSTATE + id.g * NS]);
+                        zg_n = *reinterpret_cast<const float2*>(&s_zg[id.c * Z_STRIDE + 2 * (t + 1)]);
                     }
+                    const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
+                    const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
+                    const f2_t dt2 = f2_t{ud.y, ud.y}, dtu2 = f2_t{ud.y * ud.x, ud.y * ud.x};
+                    f2_t y2 = f2_t{0.f, 0.f};
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        h[p] = pkfma(exp2_2(dt2 * A2v[p]), h[p], dtu2 * bp[p]);
+                        hist[i][p] = h[p];
+                        y2 = pkfma(h[p], cp[p], y2);
+                    }
+                    const float y = group_sum<G>(y2.x + y2.y);
+                    const float out = y + Dv * ud.x;
+                    float* zg_p = &s_zg[id.c * Z_STRIDE + 2 * t];
+                    float gv, dzv = 0.f, oz = out;
+                    if (HAS_Z && fold_gate) {
+                        dzv = out * zg.x;
+                        gv = zg.y;
+                    } else if (HAS_Z) {
+                        const float sg = sigmoidf_(zg.x);
+                        const float sl = zg.x * sg;
+                        gv = zg.y * sl;
+                        dzv = zg.y * out * sg * (1.f + zg.x * (1.f - sg));
+                        oz = out * sl;
+                    } else {
+                        gv = zg.y;
+                    }
+                    *reinterpret_cast<float2*>(zg_p) = make_float2(dzv, gv);   // same value from the quad
+                    if (!FOLD && HAS_Z && a.recompute_out_z && id.g == 0 && t < tn)   // direct (uncoalesced) store
+                        io<Tin>::st((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d * a.out_z_ds + tpos(t0 + t, L, rev),
+                                    oz);
+                    SCHED_FENCE();
                 }
             }
-
-            // pass 2: sub-chunks in reverse
-    #pragma unroll
-            for (int s = TC / TS - 1; s >= 0; --s) {
-                const int ts = s * TS;
-                if (FULL || ts < tn) {
-                    f2_t hist[TS][NP];
-                    // recompute 16 steps; produce g = dout*silu(z), dz, (out_z)
-                    {
-                        f2_t h[NP];
-    #pragma unroll
-                        for (int p = 0; p < NP; ++p) h[p] = hs[s][p];
-    #pragma unroll
-                        for (int i = 0; i < TS; ++i) {
-                            const int t = ts + i;
-                            if (FULL || t < tn) {
-                                float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
-                                const float2 ud = *reinterpret_cast<const float2*>(ud_p);
-                                const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
-                                const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
-                                const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
-                                const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
-                                const f2_t dt2 = f2_t{ud.y, ud.y}, dtu2 = f2_t{ud.y * ud.x, ud.y * ud.x};
-                                f2_t y2 = f2_t{0.f, 0.f};
-    #pragma unroll
-                                for (int p = 0; p < NP; ++p) {
-                                    h[p] = exp2_2(dt2 * A2v[p]) * h[p] + dtu2 * bp[p];
-                                    hist[i][p] = h[p];
-                                    y2 += h[p] * cp[p];
-                                }
-                                float y = group_sum<G>(y2.x + y2.y);
-                                const float out = y + Dv * ud.x;
-                                float* zg_p = &s_zg[id.c * Z_STRIDE + 2 * t];
-                                const float2 zg = *reinterpret_cast<const float2*>(zg_p);
-                                float gv, dzv = 0.f, oz = out;
-                                if (HAS_Z && fold_gate) {
-                                    dzv = out * zg.x;
-                                    gv = zg.y;
-                                } else if (HAS_Z) {
-                                    const float sg = sigmoidf_(zg.x);
-                                    const float sl = zg.x * sg;
-                                    gv = zg.y * sl;
-                                    dzv = zg.y * out * sg * (1.f + zg.x * (1.f - sg));
-                                    oz = out * sl;
-                                } else {
-                                    gv = zg.y;
-                                }
-                                *reinterpret_cast<float2*>(zg_p) = make_float2(dzv, gv);   // same value from the quad
-                                if (a.recompute_out_z && id.g == 0)   // rare path: direct (uncoalesced) store
-                                    io<Tin>::st((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d * a.out_z_ds +
-                                                    tpos(t0 + t, L, rev), oz);
-                            } else {
-    #pragma unroll
-                                for (int p = 0; p < NP; ++p) hist[i][p] = f2_t{0.f, 0.f};
-                            }
-                        }
+            // adjoint sweep (the LDS operands of step i - 1 are read while step i computes)
+            float2 ud_n = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * (ts + TS - 1)]);
+            float gv_n = s_zg[id.c * Z_STRIDE + 2 * (ts + TS - 1) + 1];
+            float4 bq_n = *reinterpret_cast<const float4*>(&s_bc[(ts + TS - 1) * BC_STRIDE + id.g * NS]);
+            float4 cq_n = *reinterpret_cast<const float4*>(&s_bc[(ts + TS - 1) * BC_STRIDE + NSTATE + id.g * NS]);
+#pragma unroll
+            for (int i = TS - 1; i >= 0; --i) {
+                const int t = ts + i;
+                float part[8];
+                {
+                    float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
+                    const float2 ud = ud_n;
+                    const float gv = gv_n;
+                    const float4 bq = bq_n, cq = cq_n;
+                    if (i > 0) {
+                        ud_n = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * (t - 1)]);
+                        gv_n = s_zg[id.c * Z_STRIDE + 2 * (t - 1) + 1];
+                        bq_n = *reinterpret_cast<const float4*>(&s_bc[(t - 1) * BC_STRIDE + id.g * NS]);
+                        cq_n = *reinterpret_cast<const float4*>(&s_bc[(t - 1) * BC_STRIDE + NSTATE + id.g * NS]);
                     }
-                    // adjoint sweep
-    #pragma unroll
-                    for (int i = TS - 1; i >= 0; --i) {
-                        const int t = ts + i;
-                        float part[8];
-                        if (FULL || t < tn) {
-                            float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
-                            const float2 ud = *reinterpret_cast<const float2*>(ud_p);
-                            const float gv = s_zg[id.c * Z_STRIDE + 2 * t + 1];
-                            const float4 bq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + id.g * NS]);
-                            const float4 cq = *reinterpret_cast<const float4*>(&s_bc[t * BC_STRIDE + NSTATE + id.g * NS]);
-                            const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
-                            const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
-                            const float dt = ud.y, uu = ud.x;
-                            const f2_t dt2 = f2_t{dt, dt}, uu2 = f2_t{uu, uu}, gv2 = f2_t{gv, gv};
-                            const f2_t dtu2 = dt2 * uu2;
-                            f2_t ddt2 = f2_t{0.f, 0.f}, dus2 = f2_t{0.f, 0.f};
-    #pragma unroll
-                            for (int p = 0; p < NP; ++p) {
-                                const f2_t hp = (i == 0) ? hs[s][p] : hist[i > 0 ? i - 1 : 0][p];
-#ifdef AVSE_EXP_BWD_NOADJEXP
-                                const f2_t dA = dt2 * A2v[p];
-#else
-                                const f2_t dA = exp2_2(dt2 * A2v[p]);
-#endif
-                                lam[p] = lam[p] * dAn[p] + gv2 * cp[p];
-                                const f2_t lhp = lam[p] * dA * hp;
-                                const f2_t lb = lam[p] * bp[p];
-                                ddt2 += Av[p] * lhp;            // + u * sum(lb) once per lane, below
-                                dus2 += lb;
-                                dA_acc[p] += dt2 * lhp;
-                                const f2_t pb = lam[p] * dtu2, pc = gv2 * hist[i][p];
-                                part[2 * p] = pb.x;
-                                part[2 * p + 1] = pb.y;
-                                part[4 + 2 * p] = pc.x;
-                                part[4 + 2 * p + 1] = pc.y;
-                                dAn[p] = dA;
-                            }
-                            const float dus = group_sum<G>(dus2.x + dus2.y);
-                            const float ddt = group_sum<G>(ddt2.x + ddt2.y) + uu * dus;
-                            const float du = dus * dt + gv * Dv;
-                            const float sig = SOFTPLUS ? (1.f - fast_exp(-dt)) : 1.f;
-                            const float ddr = ddt * sig;
-                            dD_acc += gv * uu;
-                            dbias_acc += ddr;
-                            *reinterpret_cast<float2*>(ud_p) = make_float2(du, ddr);   // same value from the quad
-                        } else {
-    #pragma unroll
-                            for (int j = 0; j < 8; ++j) part[j] = 0.f;
-                        }
+                    const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
+                    const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
+                    const float dt = ud.y, uu = ud.x;
+                    const f2_t dt2 = f2_t{dt, dt}, gv2 = f2_t{gv, gv};
+                    const f2_t dtu2 = f2_t{dt * uu, dt * uu};
+                    f2_t ddt2 = f2_t{0.f, 0.f}, dus2 = f2_t{0.f, 0.f};
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        const f2_t hp = (i == 0) ? h0[p] : hist[i > 0 ? i - 1 : 0][p];
+                        lam[p] = pkfma(lam[p], dAn[p], gv2 * cp[p]);
+                        const f2_t dA = exp2_2(dt2 * A2v[p]);
+                        const f2_t lhp = (lam[p] * dA) * hp;
+                        ddt2 = pkfma(A2v[p], lhp, ddt2);           // x ln 2 and + u * sum(lam B) once per lane, below
+                        dus2 = pkfma(lam[p], bp[p], dus2);
+                        dA_acc[p] = pkfma(dt2, lhp, dA_acc[p]);
+                        const f2_t pb = lam[p] * dtu2, pc = gv2 * hist[i][p];
+                        part[2 * p] = pb.x;
+                        part[2 * p + 1] = pb.y;
+                        part[4 + 2 * p] = pc.x;
+                        part[4 + 2 * p + 1] = pc.y;
+                        dAn[p] = dA;
+                    }
+                    const float dus = group_sum<G>(dus2.x + dus2.y);
+                    const float ddt = group_sum<G>(ddt2.x + ddt2.y) * AVSE_LN2 + uu * dus;
+                    const float du = dus * dt + gv * Dv;
+                    const float sig = SOFTPLUS ? (1.f - fast_exp(-dt)) : 1.f;
+                    const float ddr = ddt * sig;
+                    dD_acc += gv * uu;
+                    dbias_acc += ddr;
+                    *reinterpret_cast<float2*>(ud_p) = make_float2(du, ddr);   // same value from the quad
+                }
+                SCHED_FENCE();
 #ifdef AVSE_EXP_BWD_NORED
-                        if (part[0] == 12345.f) a.dB[0] = part[1] + part[2] + part[3] + part[4] + part[5] + part[6] + part[7];
-                        continue;
+                if (part[0] == 12345.f) a.dB[0] = part[1] + part[2] + part[3] + part[4] + part[5] + part[6] + part[7];
+                continue;
 #endif
-                        float r2[2];
-                        rs8_swap(part, r2);
-                        if ((id.lane & 12) == 0) {
-                            // vi = 4 b5 + 2 b4 + j: slot = (b5 ? C : B) + g * 4 + 2 b4 + j
-                            const int slot = ((id.lane >> 5) & 1) * NSTATE + id.g * NS + ((id.lane >> 4) & 1) * 2;
-                            float* dst = &s_red[(id.wave * RED + (i & (RED - 1))) * 2 * NSTATE + slot];
-                            dst[0] = r2[0];
-                            dst[1] = r2[1];
-                        }
-                        if ((i & (RED - 1)) == 0) {
-                            // cross-wave sum of steps ts+i .. ts+i+RED-1 -> partial slab
-                            __syncthreads();
-                            for (int idx = threadIdx.x; idx < RED * 2 * NSTATE; idx += THREADS) {
-                                const int slot = idx / RED, ii = idx % RED, tt = ts + i + ii;
-                                if (FULL || tt < tn) {
-                                    float v = 0.f;
-    #pragma unroll
-                                    for (int w = 0; w < 4; ++w) v += s_red[(w * RED + ii) * 2 * NSTATE + slot];
-                                    ws_bc[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + tpos(t0 + tt, L, rev)] = v;
-                                }
-                            }
-                            __syncthreads();
+                float r2[2];
+                rs8_swap(part, r2);
+                if ((id.lane & 12) == 0) {
+                    // vi = 4 b5 + 2 b4 + j: slot = (b5 ? C : B) + g * 4 + 2 b4 + j
+                    const int slot = ((id.lane >> 5) & 1) * NSTATE + id.g * NS + ((id.lane >> 4) & 1) * 2;
+                    float* dst = &s_red[(id.wave * RED + (i & (RED - 1))) * 2 * NSTATE + slot];
+                    dst[0] = r2[0];
+                    dst[1] = r2[1];
+                }
+                if ((i & (RED - 1)) == 0) {
+                    // cross-wave sum of steps ts+i .. ts+i+RED-1 -> partial slab
+                    __syncthreads();
+                    for (int idx = threadIdx.x; idx < RED * 2 * NSTATE; idx += THREADS) {
+                        const int slot = idx / RED, ii = idx % RED, tt = ts + i + ii;
+                        if (tt < tn) {
+                            float v = 0.f;
+#pragma unroll
+                            for (int w = 0; w < 4; ++w) v += s_red[(w * RED + ii) * 2 * NSTATE + slot];
+                            ws_bc[((int64_t)b * nblk_d + cb) * slab + (int64_t)slot * L + tpos(t0 + tt, L, rev)] = v;
                         }
                     }
+                    __syncthreads();
                 }
             }
-        };
-        chunk_body(std::false_type());   // a FULL (bounds-free) instantiation interleaved so far that it spilled
+        }
         __syncthreads();
         // write du, ddelta, dz (+ out_z) tiles (lane = time column): buffer stores, row step in soffset
         {
@@ -673,10 +680,15 @@ static void launch_fwd(const avse_scan_fwd_args& a, int nblk_d, int nblocks, hip
 
 template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS>
 static void launch_bwd(const avse_scan_bwd_args& a, int nblk_d, int nblocks, hipStream_t st) {
-    if (a.delta_softplus)
-        hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, true>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
+    const bool fold = !(HAS_Z && a.recompute_out_z);
+    if (a.delta_softplus && fold)
+        hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, true, true>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
+    else if (a.delta_softplus)
+        hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, true, false>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
+    else if (fold)
+        hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, false, true>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
     else
-        hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, false>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
+        hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, false, false>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
 }
 
 }  // namespace scan
@@ -700,7 +712,7 @@ using namespace avse::scan;
 
 extern "C" {
 
-int64_t avse_scan_n_chunks(int64_t seqlen) { return (seqlen + TC - 1) / TC; }
+int64_t avse_scan_n_chunks(int64_t seqlen) { return (seqlen + 31) / 32; }   // rows of two 16-step checkpoints
 
 int64_t avse_scan_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t seqlen, int64_t dstate) {
     (void)dstate;

@@ -38,9 +38,10 @@ int avse_abi_version(void);
  * B/C "variable" with n_groups == 1 (B, C: (b, 1, n, l)).  dstate n must be 16.
  *
  * x (scan intermediates) layout: (b, d, n_chunks, 2*n) fp32 with n_chunks =
- * avse_scan_n_chunks(l); x[..., k, 2i+1] = state i after chunk k (so x[..., -1, 1::2] is
- * the last state, as SelectiveScanFn reads at :45); x[..., k, 2i] = prod of exp(dt*A_i)
- * up to that point.  The backward restarts each chunk from these checkpoints.
+ * avse_scan_n_chunks(l) = ceil(l / 32); row k holds two 16-step checkpoints of the state:
+ * x[..., k, 2i] = state i after step min(32k + 15, l - 1), x[..., k, 2i+1] = state i after step
+ * min(32k + 31, l - 1) (so x[..., -1, 1::2] is the last state, as SelectiveScanFn reads at :45).
+ * The backward restarts every 16-step sub-chunk from these checkpoints.
  */
 typedef struct {
     int64_t batch, dim, seqlen, dstate;

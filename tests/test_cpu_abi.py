@@ -38,7 +38,7 @@ def test_host_side_validation_without_gpu():
     from avse_challenge_amd import _lib
     L = _lib.lib()
     assert L.avse_abi_version() == 1
-    assert L.avse_scan_n_chunks(3999) == 63 and L.avse_scan_n_chunks(64) == 1
+    assert L.avse_scan_n_chunks(3999) == 125 and L.avse_scan_n_chunks(64) == 2 and L.avse_scan_n_chunks(65) == 3
     assert L.avse_stft_frames(48000) == 376           # baseline/avse1/config.py:19
     a = _lib.ScanFwdArgs()
     assert L.avse_scan_fwd(a, None) == -1             # null pointers -> EINVAL before any launch
