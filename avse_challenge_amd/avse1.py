@@ -10,7 +10,9 @@ MI355X specifics:
     (libavse_hip.so: framing + radix-4 FFT-512 per wave) — ``features_from_waves`` / ``enhance``;
   * the lip front-end Conv3d weight gradient runs on the HIP MFMA implicit-GEMM kernel and every
     PReLU on the HIP fwd / fused-bwd kernels (layers.py);
-  * the remaining convolutions / BatchNorm / LSTM / GEMMs are MIOpen / hipBLASLt MFMA kernels (fp32,
+  * the FusionNet LSTM recurrence runs as one HIP launch per direction and pass (layers.HipLSTM, csrc/lstm.hip)
+    instead of a library kernel + GEMM per time step, so the whole step is capturable in a HIP graph;
+  * the remaining convolutions / BatchNorm / GEMMs are MIOpen / hipBLASLt MFMA kernels (fp32,
     exact f32 MFMA on gfx950 — no TF32 shortcut exists), channels-first like the reference.
 """
 import torch
@@ -18,7 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .layers import LipConv3d, PReLU
+from .layers import HipLSTM, LipConv3d, PReLU
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
@@ -163,7 +165,8 @@ class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 conv
 class FusionNet(nn.Module):               # model.py:81-96
     def __init__(self, a_only=False):
         super().__init__()
-        self.lstm_conv = nn.LSTM((0 if a_only else 512) + 4 * STFT_BINS, STFT_BINS, num_layers=1, batch_first=True)
+        # HIP recurrence (csrc/lstm.hip), nn.LSTM parameters / keys
+        self.lstm_conv = HipLSTM((0 if a_only else 512) + 4 * STFT_BINS, STFT_BINS, num_layers=1, batch_first=True)
         self.time_distributed_1 = nn.Linear(STFT_BINS, STFT_BINS)
 
     def forward(self, x):

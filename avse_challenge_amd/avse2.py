@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .dpmamba import DualPathModel, _gln_cl
-from .layers import LipConv3d, PReLU
+from .layers import HipLSTM, LipConv3d, PReLU
 from .losses import cal_si_snr
 from .mamba_tasnet import Decoder, Encoder
 
@@ -83,8 +83,8 @@ class VisualFeatNet(nn.Module):                # model.py:39-85
 class SeparatorBlock(nn.Module):              # model.py:88-123, on the channels-last state (B, S, K, N)
     def __init__(self, out_channels, hidden_channels, bidirectional=True):
         super().__init__()
-        self.intra_rnn = nn.LSTM(out_channels, hidden_channels, 1, batch_first=True, bidirectional=bidirectional)
-        self.inter_rnn = nn.LSTM(out_channels, hidden_channels, 1, batch_first=True, bidirectional=bidirectional)
+        self.intra_rnn = HipLSTM(out_channels, hidden_channels, 1, batch_first=True, bidirectional=bidirectional)
+        self.inter_rnn = HipLSTM(out_channels, hidden_channels, 1, batch_first=True, bidirectional=bidirectional)
         self.intra_norm = nn.GroupNorm(1, out_channels, eps=1e-8)
         self.inter_norm = nn.GroupNorm(1, out_channels, eps=1e-8)
         h = hidden_channels * (2 if bidirectional else 1)

@@ -415,3 +415,43 @@ def dwconv_bwd(x, w, dy, dilation):
     check(L.avse_dwconv_bwd(Bn, C, Kn, P, int(dilation), ptr(x), ptr(w2), ptr(dy), ptr(dx), ptr(dw), ptr(ws),
                             stream_ptr(x.device)), "avse_dwconv_bwd")
     return dx, dw.view_as(w)
+
+
+# ------------------------------------------------------------------------ LSTM recurrence
+
+def lstm_fwd(gx, w_hh, hout=None, reverse=False):
+    """gx (B, T, 4H) = X W_ih^T + b_ih + b_hh; w_hh (4H, H).  Returns (h (B, T, H) [or the passed strided hout
+    view, unit stride over H], c (B, T, H), gates (B, T, 4H) post-activation i, f, g, o)."""
+    _need_gpu(gx, w_hh)
+    gx = gx.float().contiguous()
+    Bn, T, H4 = gx.shape
+    H = H4 // 4
+    if tuple(w_hh.shape) != (H4, H):
+        raise RuntimeError(f"w_hh must be ({H4}, {H}), got {tuple(w_hh.shape)}")
+    whhT = w_hh.float().t().contiguous()
+    if hout is None:
+        hout = torch.empty((Bn, T, H), device=gx.device, dtype=torch.float32)
+    elif hout.dtype != torch.float32 or hout.stride(-1) != 1 or tuple(hout.shape) != (Bn, T, H):
+        raise RuntimeError("hout must be an fp32 (B, T, H) view with unit stride over H")
+    c_all = torch.empty((Bn, T, H), device=gx.device, dtype=torch.float32)
+    gates = torch.empty((Bn, T, H4), device=gx.device, dtype=torch.float32)
+    check(_lib.lib().avse_lstm_fwd(Bn, T, H, int(bool(reverse)), ptr(gx), ptr(whhT), ptr(hout), hout.stride(0),
+                                   hout.stride(1), ptr(c_all), ptr(gates), stream_ptr(gx.device)), "avse_lstm_fwd")
+    return hout, c_all, gates
+
+
+def lstm_bwd(dh, gates, c_all, w_hh, reverse=False):
+    """dh (B, T, H) gradient of the h output (any strides with unit stride over H) -> dgates (B, T, 4H), the
+    gradient of the pre-activation gates."""
+    _need_gpu(dh, gates, c_all, w_hh)
+    dh = dh.float()
+    if dh.stride(-1) != 1:
+        dh = dh.contiguous()
+    Bn, T, H = dh.shape
+    L = _lib.lib()
+    Hp = int(L.avse_lstm_padded_hidden(H))
+    w_pad = torch.nn.functional.pad(w_hh.float(), (0, Hp - H)).contiguous()
+    dg = torch.empty((Bn, T, 4 * H), device=dh.device, dtype=torch.float32)
+    check(L.avse_lstm_bwd(Bn, T, H, int(bool(reverse)), ptr(dh), dh.stride(0), dh.stride(1), ptr(gates.contiguous()),
+                          ptr(c_all.contiguous()), ptr(w_pad), ptr(dg), stream_ptr(dh.device)), "avse_lstm_bwd")
+    return dg

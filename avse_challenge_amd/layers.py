@@ -4,6 +4,8 @@ prelu_gln    fused PReLU -> GlobalLayerNorm (avse4 TCN) autograd op
 dwconv1d     depthwise dilated "same" conv1d autograd op (avse4 TCN / VisualConv1D)
 
 PReLU        nn.PReLU(num_parameters): fwd + fused dx / slope-gradient bwd kernels
+HipLSTM      nn.LSTM(..., num_layers=1, batch_first=True[, bidirectional]) whose recurrence is one HIP launch
+             per direction (avse1 FusionNet, avse2 DPRNN)
 LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip front-ends:
              forward on MIOpen, weight gradient on the MFMA implicit-GEMM kernel (the lips are
              data: no input gradient is needed on the reference path; if one is requested it is
@@ -112,3 +114,63 @@ def dwconv1d(x, w, dilation):
     if not x.is_cuda:
         raise RuntimeError("dwconv1d runs on the GPU kernels only")
     return _DWConvFn.apply(x, w, dilation)
+
+
+class _LSTMDirFn(torch.autograd.Function):
+    """One direction of a single-layer LSTM: input projection as one GEMM, the recurrence in libavse_hip.so
+    (avse_lstm_fwd / _bwd), the weight / input gradients as GEMMs over all steps."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, reverse):
+        Bn, T, I = x.shape
+        H = w_hh.shape[1]
+        x2 = x.reshape(Bn * T, I)
+        gx = torch.addmm(b_ih + b_hh, x2, w_ih.t()).view(Bn, T, 4 * H)
+        h, c, gates = K.lstm_fwd(gx, w_hh, reverse=reverse)
+        ctx.save_for_backward(x, w_ih, w_hh, h, c, gates)
+        ctx.reverse = reverse
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, w_ih, w_hh, h, c, gates = ctx.saved_tensors
+        Bn, T, I = x.shape
+        H = w_hh.shape[1]
+        dg = K.lstm_bwd(dh, gates, c, w_hh, reverse=ctx.reverse).view(Bn * T, 4 * H)
+        dx = (dg @ w_ih).view(Bn, T, I)
+        dw_ih = dg.t() @ x.reshape(Bn * T, I)
+        hprev = torch.zeros_like(h)                     # h_{t-1} in the direction's own time order (h_0 = 0)
+        if ctx.reverse:
+            hprev[:, :-1] = h[:, 1:]
+        else:
+            hprev[:, 1:] = h[:, :-1]
+        dw_hh = dg.t() @ hprev.view(Bn * T, H)
+        db = dg.sum(0)
+        return dx, dw_ih, dw_hh, db, db, None
+
+
+class HipLSTM(nn.LSTM):
+    """nn.LSTM(input, hidden, num_layers=1, batch_first=True[, bidirectional]) with the same parameters and
+    state_dict keys (weight_ih_l0, weight_hh_l0, bias_ih_l0, bias_hh_l0, ..._reverse) whose recurrence runs as ONE
+    HIP launch per direction (csrc/lstm.hip) instead of a library kernel + GEMM per time step; capturable in a
+    HIP graph.  Zero initial state (the reference never passes one)."""
+
+    def __init__(self, input_size, hidden_size, num_layers=1, bias=True, batch_first=True, dropout=0.0,
+                 bidirectional=False):
+        if num_layers != 1 or not bias or not batch_first:
+            raise NotImplementedError("HipLSTM: single layer, with bias, batch_first (the reference's LSTMs)")
+        super().__init__(input_size, hidden_size, num_layers, bias, batch_first, dropout, bidirectional)
+
+    def forward(self, x, hx=None):
+        if hx is not None:
+            raise NotImplementedError("HipLSTM starts from a zero state (as every reference call does)")
+        if not x.is_cuda:
+            raise RuntimeError("HipLSTM runs on the GPU kernels only")
+        x = x.float()
+        outs = [_LSTMDirFn.apply(x, self.weight_ih_l0, self.weight_hh_l0, self.bias_ih_l0, self.bias_hh_l0, False)]
+        if self.bidirectional:
+            outs.append(_LSTMDirFn.apply(x, self.weight_ih_l0_reverse, self.weight_hh_l0_reverse,
+                                         self.bias_ih_l0_reverse, self.bias_hh_l0_reverse, True))
+        out = outs[0] if len(outs) == 1 else torch.cat(outs, dim=-1)
+        h_n = torch.stack([outs[0][:, -1]] + ([outs[1][:, 0]] if len(outs) > 1 else []))
+        return out, (h_n, None)

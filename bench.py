@@ -115,9 +115,8 @@ def barrier(world):
 
 class Avse1Step:
     unit_desc = "3s@16kHz utterance + 75 lip frames"
-    # MIOpen's LSTM (FusionNet) issues hipBLASLt calls that are illegal under stream capture, and the
-    # step is kernel-bound at B=32 anyway: avse1 runs with eager launches.
-    graph_ok = False
+    # the FusionNet LSTM is the HIP recurrence (layers.HipLSTM), so the whole step captures as HIP graphs
+    graph_ok = True
 
     def __init__(self, B, dev, rank, world, lip_hw):
         from avse_challenge_amd import avse1, data
@@ -375,7 +374,7 @@ class Avse2Step:
     """avse2: time-domain AV separator, 3 s @ 16 kHz + 75 gray lip frames 224x224
     (baseline/avse2/config.py), DPRNN separator, SI-SNR loss, batch 16 (train.py:28)."""
     unit_desc = "3s@16kHz utterance + 75 lip frames 224x224"
-    graph_ok = False            # MIOpen LSTM: not capturable (as avse1)
+    graph_ok = True             # DPRNN LSTMs on the HIP recurrence (layers.HipLSTM)
 
     def __init__(self, B, dev, rank, world):
         from avse_challenge_amd import avse2, data

@@ -201,6 +201,21 @@ int avse_dwconv_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, con
 int avse_dwconv_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
                     const float* dy, float* dx, float* dw, float* workspace, avse_stream_t stream);
 
+/* ---------------------------------------------------------------- LSTM recurrence ----------
+ * Replaces the per-step cuDNN/MIOpen LSTM behind nn.LSTM at baseline/avse1/model.py:88 (FusionNet:
+ * LSTM(1540 -> 257), batch_first) and baseline/avse2/model.py:101-102 (DPRNN, bidirectional: one call per
+ * direction, reverse = 1 for the backward one).  PyTorch semantics: gate order i, f, g, o; h0 = c0 = 0.
+ * Forward: gx (B, T, 4H) = X W_ih^T + b_ih + b_hh precomputed by the caller (one GEMM); whhT = W_hh^T (H, 4H)
+ * contiguous; writes h (strided: hout[b*hout_bs + t*hout_ts + j]), c (B, T, H) and the gate activations
+ * (B, T, 4H) the backward needs.  Backward: dh_out strided like hout; whh_pad = W_hh (4H, H) zero-padded to
+ * (4H, avse_lstm_padded_hidden(H)); writes dgates (B, T, 4H) = dL/d(pre-activation gates).  H <= 512.
+ * One workgroup per sequence, the whole recurrence in one launch; no workspace. */
+int64_t avse_lstm_padded_hidden(int64_t H);
+int avse_lstm_fwd(int64_t B, int64_t T, int64_t H, int32_t reverse, const float* gx, const float* whhT, float* hout,
+                  int64_t hout_bs, int64_t hout_ts, float* c_all, float* gates, avse_stream_t stream);
+int avse_lstm_bwd(int64_t B, int64_t T, int64_t H, int32_t reverse, const float* dh_out, int64_t dh_bs, int64_t dh_ts,
+                  const float* gates, const float* c_all, const float* whh_pad, float* dgates, avse_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

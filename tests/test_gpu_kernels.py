@@ -536,3 +536,33 @@ def test_c5_cconv_bf16_production_shape_vs_oracle():
     sw, sb = float(wt.grad.abs().max()), float(bias.grad.abs().max())
     close(dw, wt.grad, 1e-5 * sw, 1e-5, "dweight")
     close(db, bias.grad, 1e-5 * sb, 1e-5, "dbias")
+
+
+# ------------------------------------------------------------------ LSTM recurrence (avse1 FusionNet, avse2 DPRNN)
+
+@pytest.mark.parametrize("B,T,I,H,bidir", [(2, 376, 1540, 257, False), (3, 40, 1028, 257, False), (2, 17, 64, 128, True),
+                                           (5, 9, 30, 61, True), (1, 1, 8, 5, False)])
+def test_lstm_vs_torch_fp64(B, T, I, H, bidir):
+    """layers.HipLSTM (one HIP launch per direction and pass) vs torch.nn.LSTM in fp64 on the CPU with the same
+    weights: output and the gradients of the input and every parameter (max error relative to the tensor's max
+    <= 2e-5 for the output, 5e-5 for gradients: fp32 accumulation over T steps)."""
+    from avse_challenge_amd.layers import HipLSTM
+    torch.manual_seed(T + H)
+    ref = torch.nn.LSTM(I, H, 1, batch_first=True, bidirectional=bidir).double()
+    ours = HipLSTM(I, H, 1, batch_first=True, bidirectional=bidir).to(DEV)
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = det_input((B, T, I), 1600 + H)
+    gy = det_input((B, T, H * (2 if bidir else 1)), 1601 + H)
+    xr = x.double().requires_grad_(True)
+    yr, _ = ref(xr)
+    (yr * gy.double()).sum().backward()
+    xg = x.to(DEV).requires_grad_(True)
+    y, (hn, _) = ours(xg)
+    (y * gy.to(DEV)).sum().backward()
+    sc = lambda t: max(1e-6, float(t.abs().max()))                                                 # noqa: E731
+    close(y, yr, 2e-5 * sc(yr), 0, "h")
+    close(hn[0], yr[:, -1, :H], 2e-5 * sc(yr), 0, "h_n")
+    close(xg.grad, xr.grad, 5e-5 * sc(xr.grad), 0, "dx")
+    rp = dict(ref.named_parameters())
+    for k, p in ours.named_parameters():
+        close(p.grad, rp[k].grad, 5e-5 * sc(rp[k].grad), 0, k)
