@@ -191,6 +191,12 @@ class MambaStep:
     def __init__(self, B, dev, rank, world, size):
         from avse_challenge_amd import data, losses, mamba_tasnet
         self.B, self.size = B, size
+        # the v2 backward direction on a second stream (mamba_tasnet._direction_stream) needs record_stream on the
+        # shared xz, and blocks with pending stream uses are not reusable inside a graph capture: at B >= 48 the
+        # captured Mamba-TasNet-L step then exceeds 288 GB, so large batches run both directions on one stream
+        # (measured at B=64: captured 1 stream 1402 ms/step; eager at ~200 GB allocator churn 6993 ms/step)
+        self.direction_streams = B < 48 and os.environ.get("AVSE_BIMAMBA_STREAMS", "1") == "1"
+        os.environ["AVSE_BIMAMBA_STREAMS"] = "1" if self.direction_streams else "0"
         self.model = mamba_tasnet.MambaTasNet(**mamba_tasnet.MAMBA_TASNET_SIZES[size]).to(dev).train()
         self.lr, self.clip = 1.5e-4, 5.0
         self.mix, self.tgt = data.wsj0mix_batch(B, dev, 4321 + rank)
@@ -201,7 +207,8 @@ class MambaStep:
 
     def config(self, world):
         return {"workload": f"Mamba-TasNet-{self.size} train step (BASELINE configs[2])", "global_batch": self.B * world,
-                "per_gpu_batch": self.B, "seq_len": 32000, "frames": 3999, "parallelism": f"dp{world}"}
+                "per_gpu_batch": self.B, "seq_len": 32000, "frames": 3999, "parallelism": f"dp{world}",
+                "direction_streams": self.direction_streams}
 
     def roofline(self, dev):
         from avse_challenge_amd import kernels as K
@@ -232,14 +239,15 @@ class MambaStep:
         return _with_traffic(roof, "scan") if b == 64 else roof
 
     def cpu_baseline(self):
-        """The oracle's full train step (every BiMamba layer, PIT SI-SNR, bwd, Adam), batch 4, 1 warm-up + median
-        of 5 — on a 1/16-length segment of each utterance (2000 samples, L = 249 frames): the oracle's scan is a
-        Python loop over frames (~50 s per 4 s utterance forward alone), so the step time is
-        linear in L and is scaled x16 to the 4 s utterance."""
+        """The oracle's full train step (every BiMamba layer, PIT SI-SNR, bwd, Adam), 1 warm-up + median of 3 — on
+        ONE utterance cut to 1/32 of its length (1000 samples, L = 124 frames): the oracle's scan is a Python loop
+        over frames (its train step at batch 4 x 2000 samples took 84-100 s on 8 cores), so the step time, linear
+        in L, is scaled x32 to the 4 s utterance. Deviates from BASELINE.md §4's batch 4 / median of 5 to stay a
+        bounded sample (~30 s)."""
         from avse_challenge_amd import data
         from oracle import losses_ref, mamba_ref
         _cpu_threads()
-        B, cut = 4, 16
+        B, cut = 1, 32
         m = mamba_ref.MambaTasNet(**mamba_ref.MAMBA_TASNET_SIZES[self.size], n_spk=2).train()
         opt = torch.optim.Adam(m.parameters(), lr=self.lr)
         mix, tgt = data.wsj0mix_batch(B, "cpu", 4321, T=32000 // cut)
@@ -248,7 +256,7 @@ class MambaStep:
             _cpu_train_step(m, opt, losses_ref.si_snr_pit(tgt, m(mix)).mean(), self.clip)
         return _cpu_record(step, B, cut, f"oracle/mamba_ref Mamba-TasNet-{self.size} train step (all layers, PIT "
                                          f"SI-SNR, bwd, Adam), batch {B} x {32000 // cut} samples (1/{cut} of 4 s), "
-                                         f"time scaled x{cut}")
+                                         f"time scaled x{cut}", runs=3)
 
 
 class DPMambaStep(MambaStep):
@@ -282,12 +290,12 @@ class DPMambaStep(MambaStep):
                          4.0 * b * l * (4 * d + 2 * 16), f"avse_scan_fwd (DPMamba intra, {b} x {d} x {l}, training fwd)")
 
     def cpu_baseline(self):
-        """The oracle's full train step, batch 4, 1 warm-up + median of 5, on the full 4 s utterance with 2 of the
-        n dual-path layers, the per-layer time (2-layer step minus 1-layer step) scaled to all n layers."""
+        """The oracle's full train step on one 4 s utterance with 1 and with 2 of the n dual-path layers (1 warm-up +
+        median of 3 each), the per-layer time (2-layer step minus 1-layer step) scaled to all n layers."""
         from avse_challenge_amd import data
         from oracle import dpmamba_ref, losses_ref
         _cpu_threads()
-        B = 4
+        B = 1
         kw = dict(dpmamba_ref.DPMAMBA_SIZES[self.size])
         n_dp = kw.pop("n_dp")
         mix, tgt = data.wsj0mix_batch(B, "cpu", 4321)
@@ -349,15 +357,15 @@ class AVMambaStep:
                          2.0 * b * l * (4 * d + 2 * 16), f"avse_scan_fwd (bf16, {b} x {d} x {l}, training fwd)")
 
     def cpu_baseline(self):
-        """The oracle's full fp32 train step (lip encoder + all BiMamba layers, SI-SNR, bwd, Adam), batch 4, 1 warm-up
-        + median of 5, on a 1/16 segment of each utterance and its lip track (3000 samples, L = 374 frames, 5 lip
-        frames), the step time scaled x16 to the 3 s utterance (linear in length: the oracle's scan is a Python
-        loop over frames, the lip encoder is per frame)."""
+        """The oracle's full fp32 train step (lip encoder + all BiMamba layers, SI-SNR, bwd, Adam), 1 warm-up + median
+        of 3, on ONE utterance cut to 1/32 with its lip track (1500 samples, L = 186 frames, 3 lip frames), the step
+        time scaled x32 to the 3 s utterance (linear in length: the oracle's scan is a Python loop over frames, the
+        lip encoder is per frame). A bounded sample (~30 s), not BASELINE.md §4's batch 4 / median of 5."""
         from avse_challenge_amd import data
         from oracle import avmamba_ref
         from oracle.losses_ref import avse4_loss
         _cpu_threads()
-        B, cut = 4, 16
+        B, cut = 1, 32
         m = avmamba_ref.AVMambaTasNet(**avmamba_ref.AV_MAMBA_SIZES[self.size]).train()
         opt = torch.optim.Adam(m.parameters(), lr=self.lr)
         noisy, clean, _ = data.avse1_batch(B, "cpu", 999, lip_hw=8, T=48000 // cut)
@@ -367,7 +375,7 @@ class AVMambaStep:
             _cpu_train_step(m, opt, avse4_loss(clean[:, None], m(noisy, lips)[:, None]), self.clip)
         return _cpu_record(step, B, cut, f"oracle/avmamba_ref AV Mamba-TasNet-{self.size} fp32 train step, batch {B} x "
                                          f"{48000 // cut} samples + {75 // cut + 1} lip frames (1/{cut} of 3 s), time "
-                                         f"scaled x{cut}")
+                                         f"scaled x{cut}", runs=3)
 
 
 class Avse2Step:
@@ -721,6 +729,9 @@ def main():
             print(f"[bench] HIP graph capture failed ({type(e).__name__}: {e}); eager launches", file=sys.stderr,
                   flush=True)
             step.drop_graphs()
+            import gc
+            gc.collect()                       # the half-captured graph's private pool goes back to the device
+            torch.cuda.empty_cache()
             sync(dev)
     sync(dev)
     barrier(world)

@@ -26,8 +26,41 @@ import torch.nn.functional as F
 
 # ----------------------------------------------------------------------------- ops
 
+class _ScanFn(torch.autograd.Function):
+    """selective_scan with its backward from the explicit adjoint (selective_scan_grads, pinned against the
+    reference's autograd gradients by tests/golden/scan_fp32): autograd through the per-step Python loop costs
+    O(L^2) (every step's index backward materialises a full-size gradient), which made a CPU train step of a
+    Mamba layer take minutes at L ~ 400."""
+
+    @staticmethod
+    def forward(ctx, u, delta, A, B, C, D, z, delta_bias, delta_softplus, acc_dtype):
+        ctx.save_for_backward(u, delta, A, B, C, D, z, delta_bias)
+        ctx.delta_softplus, ctx.acc_dtype = delta_softplus, acc_dtype
+        with torch.no_grad():
+            return _selective_scan_loop(u, delta, A, B, C, D, z, delta_bias, delta_softplus, False, acc_dtype)
+
+    @staticmethod
+    def backward(ctx, dout):
+        u, delta, A, B, C, D, z, delta_bias = ctx.saved_tensors
+        acc = torch.float64 if ctx.acc_dtype == torch.float64 else torch.float32
+        g = selective_scan_grads(u, delta, A, B, C, D, z, delta_bias, ctx.delta_softplus, dout, acc_dtype=acc)
+        cast = lambda v, ref: None if (v is None or ref is None) else v.to(ref.dtype)   # noqa: E731
+        return (cast(g["du"], u), cast(g["ddelta"], delta), cast(g["dA"], A), cast(g["dB"], B), cast(g["dC"], C),
+                cast(g["dD"], D), cast(g["dz"], z), cast(g["ddelta_bias"], delta_bias), None, None)
+
+
 def selective_scan(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
                    return_last_state=False, acc_dtype=torch.float32):
+    """Sequential recurrence (selective_scan_ref semantics, see _selective_scan_loop); differentiable through the
+    explicit adjoint when gradients are needed."""
+    ts = [t for t in (u, delta, A, B, C, D, z, delta_bias) if t is not None]
+    if not return_last_state and torch.is_grad_enabled() and any(t.requires_grad for t in ts):
+        return _ScanFn.apply(u, delta, A, B, C, D, z, delta_bias, delta_softplus, acc_dtype)
+    return _selective_scan_loop(u, delta, A, B, C, D, z, delta_bias, delta_softplus, return_last_state, acc_dtype)
+
+
+def _selective_scan_loop(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
+                         return_last_state=False, acc_dtype=torch.float32):
     """Sequential recurrence h_t = exp(dt*A) h_{t-1} + dt*B_t*u_t; y_t = <C_t, h_t>.
 
     u, delta, z: (b, d, l); A: (d, n); B, C: (b, n, l) or (b, g, n, l); D, delta_bias: (d,).
