@@ -96,6 +96,9 @@ SIGNATURES = {
     "avse_dwconv_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_dwconv_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_dwconv_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_i64] + [c_vp] * 7),
+    "avse_dwconv_gln_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "avse_dwconv_gln_fwd": (c_i32, [c_i64] * 5 + [c_vp] * 5 + [c_f32] + [c_vp] * 5),
+    "avse_dwconv_gln_bwd": (c_i32, [c_i64] * 5 + [c_vp] * 14),
     "avse_lstm_padded_hidden": (c_i64, [c_i64]),
     "avse_lstm_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "avse_lstm_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import losses
-from .layers import LipConv3d, _PReLUFn, dwconv1d, prelu_gln
+from .layers import LipConv3d, _PReLUFn, dwconv1d, dwconv_prelu_gln, prelu_gln
 
 NORM_MEAN, NORM_STD = 0.4161, 0.1688
 
@@ -94,8 +94,7 @@ class DepthwiseSeparableConv(nn.Module):
 
     def forward(self, x):
         dw, pr, nm, pw = self.net
-        y = dwconv1d(x, dw.weight, self.dilation)
-        y = prelu_gln(y, pr.weight, nm.gamma, nm.beta)
+        y = dwconv_prelu_gln(x, dw.weight, pr.weight, nm.gamma, nm.beta, self.dilation)   # fused passes (gln.hip)
         return _pw(pw, y)
 
 

@@ -196,6 +196,151 @@ __global__ void alpha_finalize(int rows, const float* __restrict__ ws_alpha, flo
     if (threadIdx.x == 0) dalpha[0] = (float)(red[0] + red[1] + red[2] + red[3]);
 }
 
+// ----------------------------------------------------------------------------------------------------------
+// Fused depthwise dilated conv1d <-> PReLU -> gLN (DepthwiseSeparableConv.net[:3], model.py:278-292)
+//   fwd: ONE pass computes y1 = dwconv(x) per row tile (LDS tile + dilation halo, as dwconv.hip) and, from the
+//        registers, the row's shifted PReLU statistics; finalize; the apply pass reads y1 once (apply_kernel).
+//   bwd: the row reduction of (y1, dy) (bwd_reduce_kernel); finalize; ONE pass whose tile loader turns (y1, dy)
+//        into the gLN/PReLU input gradient on the fly (halo included) and runs the dwconv backward on it
+//        (dx, dW row partials) plus the PReLU-slope partial over the tile's own elements.
+constexpr int DW_PER = 8, DW_TILE = THREADS * DW_PER, DW_MAXP = 7, DW_MAXHALO = 512;
+
+template <int P>
+__global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int C, int K, int dil, const float* __restrict__ x,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ alpha, float* __restrict__ y1,
+                                                               float2* __restrict__ ws) {
+    __shared__ float s[DW_TILE + 2 * DW_MAXHALO];
+    __shared__ float red[4];
+    const int row = blockIdx.x, b = row / C, c = row % C;
+    const int halo = (P - 1) / 2 * dil;
+    const float a = alpha[0];
+    const float* xr = x + (int64_t)row * K;
+    float* yr = y1 + (int64_t)row * K;
+    float wk[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) wk[k] = w[c * P + k];
+    // the sample's shift p(y1[b, 0, 0]), recomputed with row (b, 0)'s exact arithmetic (zero taps add +0)
+    float y00 = 0.f;
+    {
+        const float* x0 = x + (int64_t)b * C * K;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const int t = k * dil - halo;
+            y00 += w[k] * ((t >= 0 && t < K) ? x0[t] : 0.f);
+        }
+    }
+    const float shift = prelu(y00, a);
+    float s1 = 0.f, s2 = 0.f;
+    for (int t0 = 0; t0 < K; t0 += DW_TILE) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < DW_TILE + 2 * halo; i += THREADS) {
+            const int t = t0 - halo + i;
+            s[i] = (t >= 0 && t < K) ? xr[t] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < DW_PER; ++p) {
+            const int i = threadIdx.x + p * THREADS, t = t0 + i;
+            if (t < K) {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < P; ++k) acc += wk[k] * s[i + k * dil];
+                yr[t] = acc;
+                const float v = prelu(acc, a) - shift;
+                s1 += v;
+                s2 += v * v;
+            }
+        }
+    }
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+    if (threadIdx.x == 0) ws[row] = make_float2(s1, s2);
+}
+
+template <int P>
+__global__ __launch_bounds__(THREADS) void dwconv_gln_bwd_kernel(int C, int K, int dil, const float* __restrict__ x,
+                                                                 const float* __restrict__ w, const float* __restrict__ y1,
+                                                                 const float* __restrict__ alpha,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float2* __restrict__ stats,
+                                                                 const float2* __restrict__ smeans,
+                                                                 const float* __restrict__ dy, float* __restrict__ dx,
+                                                                 float* __restrict__ ws_dw, float* __restrict__ ws_alpha) {
+    __shared__ float sx[DW_TILE + 2 * DW_MAXHALO];
+    __shared__ float sg[DW_TILE + 2 * DW_MAXHALO];
+    __shared__ float red[THREADS / 64][DW_MAXP + 1];
+    const int row = blockIdx.x, b = row / C, c = row % C;
+    const int halo = (P - 1) / 2 * dil;
+    const float a = alpha[0];
+    const float2 st = stats[b], sm = smeans[b];
+    const float gm = gamma[c];
+    const float* xr = x + (int64_t)row * K;
+    const float* yr = y1 + (int64_t)row * K;
+    const float* gr = dy + (int64_t)row * K;
+    float* dr = dx + (int64_t)row * K;
+    float wk[P], dw[P], da = 0.f;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        wk[k] = w[c * P + k];
+        dw[k] = 0.f;
+    }
+    for (int t0 = 0; t0 < K; t0 += DW_TILE) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < DW_TILE + 2 * halo; i += THREADS) {
+            const int t = t0 - halo + i;
+            const bool ok = t >= 0 && t < K;
+            float g1 = 0.f;
+            if (ok) {   // d(gLN(PReLU(y1)))/dy1 applied to dy: the PReLU -> gLN backward of gln.hip bwd_apply_kernel
+                const float yv = yr[t];
+                const float xh = (prelu(yv, a) - st.x) * st.y;
+                const float dp = st.y * (gr[t] * gm - sm.x - xh * sm.y);
+                g1 = yv > 0.f ? dp : a * dp;
+                if (i >= halo && i < halo + DW_TILE && yv <= 0.f) da += dp * yv;   // own elements only
+            }
+            sx[i] = ok ? xr[t] : 0.f;
+            sg[i] = g1;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < DW_PER; ++p) {
+            const int i = threadIdx.x + p * THREADS, t = t0 + i;
+            if (t < K) {
+                float acc = 0.f;
+                const float g = sg[i + halo];
+#pragma unroll
+                for (int k = 0; k < P; ++k) {
+                    acc += wk[k] * sg[i + 2 * halo - k * dil];
+                    dw[k] += g * sx[i + k * dil];
+                }
+                dr[t] = acc;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k <= P; ++k) {
+        float v = k < P ? dw[k] : da;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x <= P) {
+        const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        if (threadIdx.x < P) ws_dw[(int64_t)row * DW_MAXP + threadIdx.x] = v;
+        else ws_alpha[row] = v;
+    }
+}
+
+__global__ void dw_sum_kernel(const float* __restrict__ ws, int B, int C, int P, float* __restrict__ dw) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C * P) return;
+    const int c = i / P, k = i % P;
+    float v = 0.f;
+    for (int b = 0; b < B; ++b) v += ws[((int64_t)b * C + c) * DW_MAXP + k];
+    dw[i] = v;
+}
+
 }  // namespace gln
 }  // namespace avse
 
@@ -242,6 +387,82 @@ int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     AVSE_CHECK_LAUNCH();
     hipLaunchKernelGGL(bwd_apply_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, x, alpha, gamma,
                        (const float2*)stats, smeans, dy, dx, ws_a);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(alpha_finalize, dim3(1), dim3(256), 0, st, (int)rows, ws_a, dalpha);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+// ------------------------------------------------------------------ fused dwconv <-> PReLU -> gLN
+
+int64_t avse_dwconv_gln_workspace_bytes(int64_t B, int64_t C) {
+    return 8 * B * C + 4 * B * C + 16 * B + 4 * B * C * DW_MAXP;
+}
+
+#define AVSE_DW_P_SWITCH(P, LAUNCH) \
+    switch ((int)(P)) {              \
+        case 1: LAUNCH(1); break;    \
+        case 3: LAUNCH(3); break;    \
+        case 5: LAUNCH(5); break;    \
+        default: LAUNCH(7); break;   \
+    }
+
+static int dw_check(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil) {
+    if (B <= 0 || C <= 0 || K <= 0 || dil <= 0 || (P != 1 && P != 3 && P != 5 && P != 7) ||
+        (P - 1) / 2 * dil > DW_MAXHALO || B * C > (1LL << 31) - 1)
+        return AVSE_ESHAPE;
+    return AVSE_OK;
+}
+
+int avse_dwconv_gln_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
+                        const float* alpha, const float* gamma, const float* beta, float eps, float* y1, float* y,
+                        float* stats, float* workspace, avse_stream_t stream) {
+    if (!x || !w || !alpha || !gamma || !beta || !y1 || !y || !stats || !workspace) return AVSE_EINVAL;
+    if (int rc = dw_check(B, C, K, P, dil)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned rows = (unsigned)(B * C);
+    float2* ws = (float2*)workspace;
+#define L_(PP) hipLaunchKernelGGL(dwconv_stats_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, (int)dil, \
+                                  x, w, alpha, y1, ws)
+    AVSE_DW_P_SWITCH(P, L_)
+#undef L_
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(stats_finalize, dim3((unsigned)B), dim3(256), 0, st, (int)B, (int)C, (int)K, y1, alpha, ws, eps,
+                       (float2*)stats);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(apply_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, y1, alpha, gamma, beta,
+                       (const float2*)stats, y);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
+                        const float* y1, const float* alpha, const float* gamma, const float* stats, const float* dy,
+                        float* dx, float* dw, float* dalpha, float* dgamma, float* dbeta, float* workspace,
+                        avse_stream_t stream) {
+    if (!x || !w || !y1 || !alpha || !gamma || !stats || !dy || !dx || !dw || !dalpha || !dgamma || !dbeta || !workspace)
+        return AVSE_EINVAL;
+    if (int rc = dw_check(B, C, K, P, dil)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned rows = (unsigned)(B * C);
+    float2* ws = (float2*)workspace;
+    float* ws_a = (float*)(ws + B * C);
+    float2* smeans = (float2*)(ws_a + B * C);
+    float* ws_dw = (float*)(smeans + B);
+    hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, y1, alpha,
+                       (const float2*)stats, dy, ws);
+    AVSE_CHECK_LAUNCH();
+    const unsigned cblocks = (unsigned)((C + 255) / 256);
+    hipLaunchKernelGGL(bwd_finalize, dim3((unsigned)B + cblocks), dim3(256), 0, st, (int)B, (int)C, (int)K, ws, gamma,
+                       smeans, dgamma, dbeta);
+    AVSE_CHECK_LAUNCH();
+#define L_(PP) hipLaunchKernelGGL(dwconv_gln_bwd_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, (int)dil, \
+                                  x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)smeans, dy, dx, ws_dw, ws_a)
+    AVSE_DW_P_SWITCH(P, L_)
+#undef L_
+    AVSE_CHECK_LAUNCH();
+    const int n = (int)(C * P);
+    hipLaunchKernelGGL(dw_sum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ws_dw, (int)B, (int)C, (int)P, dw);
     AVSE_CHECK_LAUNCH();
     hipLaunchKernelGGL(alpha_finalize, dim3(1), dim3(256), 0, st, (int)rows, ws_a, dalpha);
     AVSE_CHECK_LAUNCH();

@@ -417,6 +417,44 @@ def dwconv_bwd(x, w, dy, dilation):
     return dx, dw.view_as(w)
 
 
+# ------------------------------------------------------------------------ fused dwconv <-> PReLU -> gLN (avse4)
+
+def dwconv_gln_fwd(x, w, dilation, alpha, gamma, beta, eps=1e-8):
+    """y1 = depthwise dilated conv1d(x) (w (C, 1, P)), y = gLN(PReLU(y1)); returns (y, y1, stats (B, 2))."""
+    _need_gpu(x, w, alpha, gamma, beta)
+    x = x.float().contiguous()
+    Bn, C, Kn = x.shape
+    w2 = w.reshape(C, -1).float().contiguous()
+    y1, y = torch.empty_like(x), torch.empty_like(x)
+    stats = torch.empty((Bn, 2), device=x.device, dtype=torch.float32)
+    L = _lib.lib()
+    ws = torch.empty((L.avse_dwconv_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    check(L.avse_dwconv_gln_fwd(Bn, C, Kn, w2.shape[1], int(dilation), ptr(x), ptr(w2), ptr(alpha.float().contiguous()),
+                                ptr(gamma.float().contiguous()), ptr(beta.float().contiguous()), float(eps), ptr(y1),
+                                ptr(y), ptr(stats), ptr(ws), stream_ptr(x.device)), "avse_dwconv_gln_fwd")
+    return y, y1, stats
+
+
+def dwconv_gln_bwd(x, w, dilation, y1, alpha, gamma, stats, dy):
+    """-> (dx, dw (like w), dalpha (1,), dgamma (C,), dbeta (C,))."""
+    _need_gpu(x, w, y1, alpha, gamma, stats, dy)
+    x, dy = x.float().contiguous(), dy.float().contiguous()
+    Bn, C, Kn = x.shape
+    w2 = w.reshape(C, -1).float().contiguous()
+    dx = torch.empty_like(x)
+    dw = torch.empty((C, w2.shape[1]), device=x.device, dtype=torch.float32)
+    dalpha = torch.empty((1,), device=x.device, dtype=torch.float32)
+    dgamma = torch.empty((C,), device=x.device, dtype=torch.float32)
+    dbeta = torch.empty((C,), device=x.device, dtype=torch.float32)
+    L = _lib.lib()
+    ws = torch.empty((L.avse_dwconv_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    check(L.avse_dwconv_gln_bwd(Bn, C, Kn, w2.shape[1], int(dilation), ptr(x), ptr(w2), ptr(y1.contiguous()),
+                                ptr(alpha.float().contiguous()), ptr(gamma.float().contiguous()), ptr(stats), ptr(dy),
+                                ptr(dx), ptr(dw), ptr(dalpha), ptr(dgamma), ptr(dbeta), ptr(ws), stream_ptr(x.device)),
+          "avse_dwconv_gln_bwd")
+    return dx, dw.view_as(w), dalpha, dgamma, dbeta
+
+
 # ------------------------------------------------------------------------ LSTM recurrence
 
 def lstm_fwd(gx, w_hh, hout=None, reverse=False):

@@ -1,7 +1,8 @@
 """nn.Module drop-ins whose hot halves run in libavse_hip.so (same parameter names as torch's).
 
 prelu_gln    fused PReLU -> GlobalLayerNorm (avse4 TCN) autograd op
-dwconv1d     depthwise dilated "same" conv1d autograd op (avse4 TCN / VisualConv1D)
+dwconv1d     depthwise dilated "same" conv1d autograd op (avse4 VisualConv1D)
+dwconv_prelu_gln  the avse4 TCN's dwconv -> PReLU -> gLN as two fused passes each way
 
 PReLU        nn.PReLU(num_parameters): fwd + fused dx / slope-gradient bwd kernels
 HipLSTM      nn.LSTM(..., num_layers=1, batch_first=True[, bidirectional]) whose recurrence is one HIP launch
@@ -93,6 +94,30 @@ def prelu_gln(x, alpha, gamma, beta, eps=1e-8):
     if not x.is_cuda:
         raise RuntimeError("prelu_gln runs on the GPU kernels only")
     return _PReluGLNFn.apply(x, alpha, gamma, beta, eps)
+
+
+class _DWConvGLNFn(torch.autograd.Function):
+    """gLN(PReLU(dwconv(x))) as the two fused passes of csrc/gln.hip (avse_dwconv_gln_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, w, alpha, gamma, beta, dilation, eps):
+        y, y1, stats = K.dwconv_gln_fwd(x, w, dilation, alpha, gamma.reshape(-1), beta.reshape(-1), eps)
+        ctx.save_for_backward(x, w, y1, alpha, gamma, stats)
+        ctx.dilation = dilation
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y1, alpha, gamma, stats = ctx.saved_tensors
+        dx, dw, da, dg, db = K.dwconv_gln_bwd(x, w, ctx.dilation, y1, alpha, gamma.reshape(-1), stats, dy)
+        return dx, dw, da.view_as(alpha), dg.view_as(gamma), db.view_as(gamma), None, None
+
+
+def dwconv_prelu_gln(x, w, alpha, gamma, beta, dilation, eps=1e-8):
+    """GlobalLayerNorm(PReLU(depthwise dilated 'same' conv1d(x))) for (B, C, K) fp32 GPU tensors (fused passes)."""
+    if not x.is_cuda:
+        raise RuntimeError("dwconv_prelu_gln runs on the GPU kernels only")
+    return _DWConvGLNFn.apply(x, w, alpha, gamma, beta, dilation, eps)
 
 
 class _DWConvFn(torch.autograd.Function):

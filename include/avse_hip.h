@@ -201,6 +201,21 @@ int avse_dwconv_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, con
 int avse_dwconv_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
                     const float* dy, float* dx, float* dw, float* workspace, avse_stream_t stream);
 
+/* ---------------------------------------------------------------- fused dwconv <-> PReLU -> gLN (avse4 TCN) ----
+ * DepthwiseSeparableConv.net[:3] of baseline/avse4/model.py:278-292: y1 = depthwise dilated "same" conv1d(x)
+ * (w (C, P), no bias, as avse_dwconv_fwd), y = gLN(PReLU(y1)) (as avse_prelu_gln_fwd).  The forward computes the
+ * gLN statistics inside the conv pass (x read once, y1 written once, y1 read once by the apply pass); the
+ * backward turns (y1, dy) into the conv's output gradient inside the conv-backward pass.  y1 and stats (B, 2) are
+ * saved by the caller for the backward.  Workspace: avse_dwconv_gln_workspace_bytes(B, C). */
+int64_t avse_dwconv_gln_workspace_bytes(int64_t B, int64_t C);
+int avse_dwconv_gln_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
+                        const float* alpha, const float* gamma, const float* beta, float eps, float* y1, float* y,
+                        float* stats, float* workspace, avse_stream_t stream);
+int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
+                        const float* y1, const float* alpha, const float* gamma, const float* stats, const float* dy,
+                        float* dx, float* dw, float* dalpha, float* dgamma, float* dbeta, float* workspace,
+                        avse_stream_t stream);
+
 /* ---------------------------------------------------------------- LSTM recurrence ----------
  * Replaces the per-step cuDNN/MIOpen LSTM behind nn.LSTM at baseline/avse1/model.py:88 (FusionNet:
  * LSTM(1540 -> 257), batch_first) and baseline/avse2/model.py:101-102 (DPRNN, bidirectional: one call per

@@ -566,3 +566,35 @@ def test_lstm_vs_torch_fp64(B, T, I, H, bidir):
     rp = dict(ref.named_parameters())
     for k, p in ours.named_parameters():
         close(p.grad, rp[k].grad, 5e-5 * sc(rp[k].grad), 0, k)
+
+
+# ------------------------------------------------------------------ fused dwconv <-> PReLU -> gLN (avse4 TCN)
+
+@pytest.mark.parametrize("B,C,Kn,P,dil", [(2, 512, 3999, 3, 128), (3, 64, 300, 3, 4), (2, 40, 2500, 3, 1), (1, 8, 17, 5, 2),
+                                          (2, 16, 5000, 3, 256)])
+def test_dwconv_prelu_gln_fused_vs_fp64(B, C, Kn, P, dil):
+    """layers.dwconv_prelu_gln (two fused passes each way) vs the fp64 composition of the reference ops
+    (model.py:278-292: depthwise conv1d, PReLU, gLN with EPS 1e-8 inside the sqrt): output and the gradients of
+    x, the conv weight, the PReLU slope and gamma / beta (max error relative to the tensor's max: 1e-5, 1e-4)."""
+    from avse_challenge_amd.layers import dwconv_prelu_gln
+    x = det_input((B, C, Kn), 1700 + Kn)
+    w = 0.5 * det_input((C, 1, P), 1701)
+    alpha = torch.tensor([0.2])
+    gamma = 1 + 0.1 * det_input((1, C, 1), 1702)
+    beta = 0.1 * det_input((1, C, 1), 1703)
+    gy = det_input((B, C, Kn), 1704)
+    leaves = [t.double().requires_grad_(True) for t in (x, w, alpha, gamma, beta)]
+    xr, wr, ar, gr, br = leaves
+    y1 = torch.nn.functional.conv1d(xr, wr, padding=(P - 1) // 2 * dil, dilation=dil, groups=C)
+    p = torch.where(y1 > 0, y1, ar * y1)
+    mean = p.mean((1, 2), keepdim=True)
+    var = ((p - mean) ** 2).mean((1, 2), keepdim=True)
+    ref = gr * (p - mean) / (var + 1e-8) ** 0.5 + br
+    (ref * gy.double()).sum().backward()
+    g_leaves = [t.to(DEV).requires_grad_(True) for t in (x, w, alpha, gamma, beta)]
+    y = dwconv_prelu_gln(*g_leaves, dil)
+    (y * gy.to(DEV)).sum().backward()
+    sc = lambda t: max(1e-6, float(t.abs().max()))                                         # noqa: E731
+    close(y, ref, 1e-5 * sc(ref), 0, "y")
+    for name, a_, r_ in zip(("dx", "dw", "dalpha", "dgamma", "dbeta"), g_leaves, leaves):
+        close(a_.grad, r_.grad, 1e-4 * sc(r_.grad), 0, name)
