@@ -21,14 +21,17 @@ this package's outputs unchanged and this package consumes theirs:
 
 Loads default to `torch.load(weights_only=True)`: checkpoints are data, nothing in them is executed.
 """
+import ast
 import datetime
 import inspect
 import os
+import re
 import struct
 import time
 
 import numpy as np
 import torch
+
 import yaml
 
 # ---------------------------------------------------------------------------------------------- Lightning
@@ -180,20 +183,65 @@ def read_hparams(path):
         return yaml.load(f, Loader=_TagTolerantLoader)  # noqa: S506 (SafeLoader subclass)
 
 
+_REF = re.compile(r"<([A-Za-z_][A-Za-z0-9_]*)>")
+
+
+def _resolve(hp, key, seen=()):
+    """A top-level hparams value with hyperpyyaml's `!ref` resolved as data: `<name>` references are substituted
+    (recursively) and simple integer arithmetic (+ - * // / and parentheses, e.g. `<kernel_size> // 2`) is
+    evaluated on a parsed expression tree — nothing is imported or executed."""
+    v = hp[key]
+    if not isinstance(v, str) or "<" not in v:
+        return v
+    if key in seen:
+        raise ValueError(f"cyclic !ref at {key}")
+
+    def sub(m):
+        r = _resolve(hp, m.group(1), seen + (key,))
+        if not isinstance(r, (int, float)) or isinstance(r, bool):
+            raise ValueError(f"!ref <{m.group(1)}> is not a number: {r!r}")
+        return repr(r)
+    return _arith(_REF.sub(sub, v))
+
+
+def _arith(expr):
+    ops = {ast.Add: lambda a, b: a + b, ast.Sub: lambda a, b: a - b, ast.Mult: lambda a, b: a * b,
+           ast.FloorDiv: lambda a, b: a // b, ast.Div: lambda a, b: a / b}
+
+    def ev(n):
+        if isinstance(n, ast.Expression):
+            return ev(n.body)
+        if isinstance(n, ast.Constant) and isinstance(n.value, (int, float)) and not isinstance(n.value, bool):
+            return n.value
+        if isinstance(n, ast.BinOp) and type(n.op) in ops:
+            return ops[type(n.op)](ev(n.left), ev(n.right))
+        if isinstance(n, ast.UnaryOp) and isinstance(n.op, ast.USub):
+            return -ev(n.operand)
+        raise ValueError(f"unsupported !ref expression {expr!r}")
+    return ev(ast.parse(expr.strip(), mode="eval"))
+
+
 def model_kwargs_from_hparams(hp):
-    """Constructor kwargs of this package's MambaTasNet / DPMambaTasNet from the reference's hparams
-    (`mambatasnet_*.yaml` / `dpmamba_*.yaml` top-level keys).  Returns (kind, kwargs), kind in
-    {"mambatasnet", "dpmamba"}."""
+    """Constructor kwargs of this package's MambaTasNet / DPMambaTasNet from the reference's hparams: the
+    training recipes `mambatasnet_*.yaml` / `dpmamba_*.yaml` (hparams/WSJ0Mix/, `!ref` arithmetic such as
+    `kernel_stride: !ref <kernel_size> // 2` resolved) or a saved `hyperparams.yaml`.  Returns (kind, kwargs),
+    kind in {"mambatasnet", "dpmamba"}.  The MaskNet bottleneck / d_model come from `out_channels`, which this
+    package's models tie to the encoder width `N_encoder_out` (as every reference recipe does)."""
     if isinstance(hp, str):
         hp = read_hparams(hp)
-    common = dict(N=int(hp["N_encoder_out"]), kernel_size=int(hp["kernel_size"]), n_spk=int(hp["num_spks"]),
-                  d_state=int(hp["ssm_dim"]), expand=int(hp["mamba_expand"]), d_conv=int(hp["mamba_conv"]))
-    if int(hp.get("kernel_stride", common["kernel_size"] // 2)) != common["kernel_size"] // 2:
+    g = lambda k: _resolve(hp, k)                                                      # noqa: E731
+    common = dict(N=int(g("N_encoder_out")), kernel_size=int(g("kernel_size")), n_spk=int(g("num_spks")),
+                  d_state=int(g("ssm_dim")), expand=int(g("mamba_expand")), d_conv=int(g("mamba_conv")))
+    if "out_channels" in hp and int(g("out_channels")) != common["N"]:
+        raise ValueError(f"out_channels ({g('out_channels')}) != N_encoder_out ({common['N']}): the MaskNet "
+                         "bottleneck width must equal the encoder width in this package's models")
+    stride = int(g("kernel_stride")) if "kernel_stride" in hp else common["kernel_size"] // 2
+    if stride != common["kernel_size"] // 2:
         raise ValueError("encoder stride must be kernel_size // 2 (the reference's Encoder / Decoder)")
     if "n_dp" in hp:
-        return "dpmamba", dict(common, n_dp=int(hp["n_dp"]), chunk_size=int(hp["chunk_size"]),
-                               skip_around_intra=bool(hp["skip_around_intra"]), n_mamba_dp=int(hp["n_mamba_dp"]))
-    return "mambatasnet", dict(common, n_mamba=int(hp["n_mamba"]))
+        return "dpmamba", dict(common, n_dp=int(g("n_dp")), chunk_size=int(g("chunk_size")),
+                               skip_around_intra=bool(g("skip_around_intra")), n_mamba_dp=int(g("n_mamba_dp")))
+    return "mambatasnet", dict(common, n_mamba=int(g("n_mamba")))
 
 
 def model_from_hparams(hp):

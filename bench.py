@@ -651,7 +651,13 @@ def roofline_hip(dev):
             lambda: K.dwconv_fwd(xd, wd, 128))
     add_hbm("avse_dwconv_bwd (C4 TCN, H=512, K=3999, dil 128)", [16, 512, 3999], "fp32", 12 * xd.numel(),
             lambda: K.dwconv_bwd(xd, wd, gy, 128))
-    del xd, gy
+    al, gm, bt = torch.full((1,), 0.25, device=dev), rnd(1, 512, 1, scale=0.1) + 1, rnd(1, 512, 1, scale=0.1)
+    _, y1, st = K.dwconv_gln_fwd(xd, wd, 128, al, gm, bt)
+    add_hbm("avse_dwconv_gln_fwd (C4 TCN fused dwconv -> PReLU -> gLN: x read, y1 + y written)", [16, 512, 3999], "fp32",
+            12 * xd.numel(), lambda: K.dwconv_gln_fwd(xd, wd, 128, al, gm, bt))
+    add_hbm("avse_dwconv_gln_bwd (C4 TCN fused: x, y1, dy read, dx written)", [16, 512, 3999], "fp32",
+            16 * xd.numel(), lambda: K.dwconv_gln_bwd(xd, wd, 128, y1, al, gm, st, gy))
+    del xd, gy, y1
     # projections (MFMA): BiMambaV2's in_proj (_InProj) and out_proj (_BiOutProj) at C3 (fp32) and C5 (bf16)
     for tag, b, l, dt, peak in (("C3", 64, 3999, torch.float32, FP32_PEAK_TFS),
                                 ("C5", 32, 5999, torch.bfloat16, BF16_PEAK_TFS)):

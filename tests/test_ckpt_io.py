@@ -136,3 +136,35 @@ def test_hparams_of_reference_checkpoints(size):
         if size == "XS":                      # build only the small ones on CPU
             m = ckpt_io.model_from_hparams(hp)
             assert m.encoder.conv1d.weight.shape == (kw["N"], 1, kw["kernel_size"])
+
+
+def test_hparams_ref_arithmetic_resolved(tmp_path):
+    """The training recipes (hparams/WSJ0Mix/*.yaml) carry hyperpyyaml `!ref` arithmetic, e.g.
+    `kernel_stride: !ref <kernel_size> // 2` and `n_mamba: !ref <n_mamba_dp> // 2`: resolved as data."""
+    p = tmp_path / "recipe.yaml"
+    p.write_text("N_encoder_out: 64\nout_channels: !ref <N_encoder_out>\nkernel_size: 16\n"
+                 "kernel_stride: !ref <kernel_size> // 2\nnum_spks: 2\nssm_dim: 16\nmamba_expand: 2\nmamba_conv: 4\n"
+                 "n_mamba: !ref (<kernel_size> - 12) * 2\n")
+    kind, kw = ckpt_io.model_kwargs_from_hparams(str(p))
+    assert kind == "mambatasnet" and kw["n_mamba"] == 8 and kw["N"] == 64 and kw["kernel_size"] == 16
+    p.write_text(p.read_text().replace("out_channels: !ref <N_encoder_out>", "out_channels: 32"))
+    with pytest.raises(ValueError, match="out_channels"):
+        ckpt_io.model_kwargs_from_hparams(str(p))
+    p.write_text(p.read_text().replace("out_channels: 32", "out_channels: 64").replace("// 2", "// 4"))
+    with pytest.raises(ValueError, match="stride"):
+        ckpt_io.model_kwargs_from_hparams(str(p))
+
+
+RECIPES = "/root/reference/Mamba-TasNet/hparams/WSJ0Mix"
+
+
+@pytest.mark.skipif(not os.path.isdir(RECIPES), reason="reference recipes not present")
+@pytest.mark.parametrize("name", ["mambatasnet_XS", "mambatasnet_L", "dpmamba_S", "dpmamba_L"])
+def test_reference_training_recipes_parse(name):
+    from avse_challenge_amd.dpmamba import DPMAMBA_SIZES
+    from avse_challenge_amd.mamba_tasnet import MAMBA_TASNET_SIZES
+    kind, kw = ckpt_io.model_kwargs_from_hparams(os.path.join(RECIPES, name + ".yaml"))
+    fam, size = name.split("_")
+    assert kind == fam
+    ref = (DPMAMBA_SIZES if fam == "dpmamba" else MAMBA_TASNET_SIZES)[size]
+    assert {k: kw[k] for k in ref} == ref
