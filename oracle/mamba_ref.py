@@ -119,7 +119,7 @@ def selective_scan_grads(u, delta, A, B, C, D, z, delta_bias, delta_softplus, do
     dA = torch.exp(dt[:, :, None, :] * A[None, :, :, None])    # (b, d, n, l)
     dBu = (dt * u)[:, :, None, :] * Bv[:, None]               # (b, d, n, l)
     H = torch.empty_like(dA)
-    h = torch.zeros(b, d, A.shape[1], dtype=acc_dtype)
+    h = torch.zeros(b, d, A.shape[1], dtype=acc_dtype, device=u.device)
     for t in range(l):
         h = dA[..., t] * h + dBu[..., t]
         H[..., t] = h
@@ -132,7 +132,7 @@ def selective_scan_grads(u, delta, A, B, C, D, z, delta_bias, delta_softplus, do
     else:
         g, dz = dout, None
     lam = torch.empty_like(dA)
-    acc = torch.zeros(b, d, A.shape[1], dtype=acc_dtype)
+    acc = torch.zeros(b, d, A.shape[1], dtype=acc_dtype, device=u.device)
     for t in range(l - 1, -1, -1):                            # lambda_t = g_t C_t + dA_{t+1} lambda_{t+1}
         acc = g[:, :, None, t] * Cv[:, None, :, t] + acc
         lam[..., t] = acc
