@@ -28,9 +28,15 @@ def _dtype_code(dt):
     raise RuntimeError(f"unsupported dtype {dt} (fp32 or bf16)")
 
 
-# (b, d, l) outputs of the scan / conv kernels get a time stride rounded up to this many bytes when set
-# (> 0): every row then starts on a cache-line boundary (tools/scan_bench.py --pad measures the effect)
-TIME_ALIGN_BYTES = int(os.environ.get("AVSE_TIME_ALIGN_BYTES", "0"))
+# (b, d, l) outputs of the scan / conv kernels (and the Mamba projections feeding them) get a time stride rounded
+# up to this many bytes: every row starts on a 128-B cache line, so a 64-step row segment touches 2 lines, not 3
+# (L = 3999 fp32 rows were read 1.42x, profiles/r01_traffic.json).  0 = plain contiguous tensors.
+TIME_ALIGN_BYTES = int(os.environ.get("AVSE_TIME_ALIGN_BYTES", "128"))
+
+
+def bdl_empty(b, d, l, dtype, dev):
+    """An uninitialised (b, d, l) tensor whose time stride is padded to TIME_ALIGN_BYTES (a view when padded)."""
+    return _bdl_empty(b, d, l, dtype, dev)
 
 
 def _bdl_empty(b, d, l, dtype, dev):

@@ -30,8 +30,17 @@ _BWD = torch.amp.custom_bwd(device_type="cuda")
 
 def _wbmm(w, x):
     """(m, k) weight @ (b, k, n) -> (b, m, n) as one strided-batched GEMM (weight batch stride 0).
-    Keeping every projection in the scan's (b, channels, l) layout means no layout copies."""
-    return torch.bmm(w.expand(x.shape[0], *w.shape), x)
+    Keeping every projection in the scan's (b, channels, l) layout means no layout copies.  The output rows get
+    the kernels' cache-line-aligned time stride (kernels.TIME_ALIGN_BYTES; hipBLASLt writes with ldc = the padded
+    stride), so every (b, d, l) operand of the conv / scan kernels starts its rows on a 128-B line."""
+    if torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        w, x = w.to(dt), x.to(dt)
+    else:
+        dt = torch.result_type(w, x)
+    out = K.bdl_empty(x.shape[0], w.shape[0], x.shape[2], dt, x.device)
+    with torch.autocast("cuda", enabled=False):
+        return torch.bmm(w.expand(x.shape[0], *w.shape), x, out=out)
 
 
 def _bsum_mm(a, bt):
@@ -86,9 +95,9 @@ class MambaInnerNoOutProj(torch.autograd.Function):
         conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=rev)
         delta = _wbmm(dt_proj_w, x_dblT[:, :R])
         Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]
-        dxz = torch.empty_like(xz)
+        dxz = K.bdl_empty(xz.shape[0], xz.shape[1], xz.shape[2], xz.dtype, xz.device)
         dx, dz = dxz.chunk(2, dim=1)
-        dx_dblT = torch.empty(x_dblT.shape, device=x_dblT.device, dtype=torch.float32)   # scan writes fp32 dB/dC
+        dx_dblT = K.bdl_empty(*x_dblT.shape, torch.float32, x_dblT.device)         # scan writes fp32 dB/dC
         dconv, ddelta, dA, _, _, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
             conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, None, dz, True, False, reverse=rev,
             dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:])
