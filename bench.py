@@ -44,7 +44,7 @@ os.environ.setdefault("PYTORCH_MIOPEN_SUGGEST_NHWC_BATCHNORM", "1")
 METRIC = "utterances/sec (3s@16kHz + 75 lip frames)"
 # HBM bytes per launch of each roofline kernel, from rocprofv3 PMC passes (tools/pmc_traffic.sh:
 # FETCH_SIZE and WRITE_SIZE in separate passes, corrected as MI355X_MICROARCH.md prescribes)
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_traffic.json")
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFS = 157.3          # FP32 matrix (= vector) peak, spec
 
@@ -610,14 +610,23 @@ def roofline_hip(dev):
     g = torch.Generator(device=dev).manual_seed(7)
 
     def rnd(*shape, dtype=torch.float32, scale=1.0):
-        return (scale * torch.randn(shape, device=dev, generator=g)).to(dtype)
+        """(b, d, l) operands in the product's layout: 128-B aligned time stride (kernels.bdl_empty)."""
+        v = (scale * torch.randn(shape, device=dev, generator=g)).to(dtype)
+        if len(shape) != 3:
+            return v
+        t = K.bdl_empty(*shape, dtype, dev)
+        t.copy_(v)
+        return t
 
-    def add_hbm(name, shape, dtype, byts, fn):
+    def add_hbm(name, shape, dtype, byts, fn, pmc=None):
         ms = _event_ms(fn)
         ach = byts / (ms * 1e-3) / 1e9
-        hbm.append({"kernel": name, "shape": shape, "dtype": dtype, "bound": "hbm", "algorithmic_bytes_per_launch": byts,
-                    "avg_ms": round(ms, 4), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4)})
+        rec = {"kernel": name, "shape": shape, "dtype": dtype, "bound": "hbm", "algorithmic_bytes_per_launch": byts,
+               "avg_ms": round(ms, 4), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(ach / HBM_PEAK_GBS, 4)}
+        if pmc:
+            rec["traffic"], rec["traffic_source"] = pmc_traffic(pmc)
+        hbm.append(rec)
 
     n = 16
     for tag, b, l, dt in (("C3", 64, 3999, torch.float32), ("C5", 32, 5999, torch.bfloat16)):
@@ -631,27 +640,30 @@ def roofline_hip(dev):
         _, x, _ = K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, return_out=False)
         # training fwd: reads u, delta, z, B, C; writes out_z
         add_hbm(f"avse_scan_fwd ({tag}, training fwd, out_z only)", [b, d, l], name, s * b * l * (4 * d + 2 * n),
-                lambda: K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, return_out=False))
+                lambda: K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, return_out=False),
+                "scan" if tag == "C3" else None)
         # bwd as the model calls it (out=None, no out_z recompute): reads u, delta, z, dout, B, C; writes du,
         # ddelta, dz (input dtype) and fp32 dB, dC
         add_hbm(f"avse_scan_bwd ({tag}, as MambaInnerNoOutProj calls it)", [b, d, l], name,
                 b * l * (7 * s * d + 2 * s * n + 2 * 4 * n),
-                lambda: K.selective_scan_bwd(u, delta, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False))
+                lambda: K.selective_scan_bwd(u, delta, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False),
+                "scan_bwd" if tag == "C3" else None)
         if tag == "C3":
             w, cb = rnd(d, 4, scale=0.5), rnd(d)
             add_hbm("avse_cconv_fwd (C3, k4 + SiLU)", [b, d, l], name, 2 * s * b * d * l,
-                    lambda: K.causal_conv1d_fwd(u, w, cb, True))
+                    lambda: K.causal_conv1d_fwd(u, w, cb, True), "cconv")
             add_hbm("avse_cconv_bwd (C3, k4 + SiLU)", [b, d, l], name, 3 * s * b * d * l,
                     lambda: K.causal_conv1d_bwd(u, w, cb, dout, silu=True))
         del u, z, dout, delta, Bm, Cm, x
         torch.cuda.empty_cache()
-    xd = rnd(16, 512, 3999)
-    wd, gy = rnd(512, 1, 3), rnd(16, 512, 3999)
+    xd = torch.randn(16, 512, 3999, device=dev, generator=g)          # the TCN kernels take contiguous (B, C, K)
+    wd, gy = rnd(512, 1, 3), torch.randn(16, 512, 3999, device=dev, generator=g)
     add_hbm("avse_dwconv_fwd (C4 TCN, H=512, K=3999, dil 128)", [16, 512, 3999], "fp32", 8 * xd.numel(),
-            lambda: K.dwconv_fwd(xd, wd, 128))
+            lambda: K.dwconv_fwd(xd, wd, 128), "dwconv")
     add_hbm("avse_dwconv_bwd (C4 TCN, H=512, K=3999, dil 128)", [16, 512, 3999], "fp32", 12 * xd.numel(),
             lambda: K.dwconv_bwd(xd, wd, gy, 128))
-    al, gm, bt = torch.full((1,), 0.25, device=dev), rnd(1, 512, 1, scale=0.1) + 1, rnd(1, 512, 1, scale=0.1)
+    al = torch.full((1,), 0.25, device=dev)
+    gm, bt = 1 + 0.1 * torch.randn(1, 512, 1, device=dev, generator=g), 0.1 * torch.randn(1, 512, 1, device=dev, generator=g)
     _, y1, st = K.dwconv_gln_fwd(xd, wd, 128, al, gm, bt)
     add_hbm("avse_dwconv_gln_fwd (C4 TCN fused dwconv -> PReLU -> gLN: x read, y1 + y written)", [16, 512, 3999], "fp32",
             12 * xd.numel(), lambda: K.dwconv_gln_fwd(xd, wd, 128, al, gm, bt))

@@ -1,7 +1,7 @@
 """Launch the bench's roofline kernels at the bench shapes (for rocprofv3 PMC passes: tools/pmc_traffic.sh).
 
 python tools/roofline_kernels.py PHASE [--n N]
-PHASE: scan (Mamba-L C3 training scan fwd, B=64), dwconv (avse4 C4 TCN dwconv fwd, B=16, dil 128),
+PHASE: scan (Mamba-L C3 training scan fwd, B=64), scan_bwd (its backward as the model calls it), dwconv (avse4 C4 TCN dwconv fwd, B=16, dil 128),
        cconv (causal conv fwd, B=64, D=1024: the dword-access calibration kernel, known bytes),
        conv3 (avse1 C2 AudioFeatNet conv3 fwd, B=32, NHWC, MIOpen).
 Inputs are created before a device sync, then the kernel runs N times; the PMC summary counts only
@@ -16,7 +16,15 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from avse_challenge_amd import kernels as K  # noqa: E402
 
-SHAPES = {"scan": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999), "conv3": (32, 64, 376, 257)}
+SHAPES = {"scan": (64, 1024, 3999), "scan_bwd": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999),
+          "conv3": (32, 64, 376, 257)}
+
+
+def aligned(b, d, l, g, scale=1.0):
+    """(b, d, l) fp32 with the product's 128-B aligned time stride (kernels.bdl_empty), filled N(0, scale^2)."""
+    t = K.bdl_empty(b, d, l, torch.float32, "cuda")
+    t.copy_(scale * torch.randn(b, d, l, device="cuda", generator=g))
+    return t
 
 
 def main():
@@ -26,14 +34,17 @@ def main():
     a = p.parse_args()
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
-    if a.phase == "scan":
+    if a.phase in ("scan", "scan_bwd"):
         b, d, l = SHAPES["scan"]
-        u, dl, z = (torch.randn(b, d, l, device=dev, generator=g) for _ in range(3))
-        dl.mul_(0.1)
+        u, dl, z = aligned(b, d, l, g), aligned(b, d, l, g, 0.1), aligned(b, d, l, g)
         A = -torch.rand(d, 16, device=dev, generator=g) - 0.5
-        Bm, Cm = torch.randn(b, 16, l, device=dev, generator=g), torch.randn(b, 16, l, device=dev, generator=g)
+        Bm, Cm = aligned(b, 16, l, g), aligned(b, 16, l, g)
         D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
         fn = lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False)  # noqa: E731
+        if a.phase == "scan_bwd":
+            _, x, _ = fn()
+            dout = aligned(b, d, l, g)
+            fn = lambda: K.selective_scan_bwd(u, dl, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False)  # noqa: E731
     elif a.phase == "dwconv":
         x = torch.randn(*SHAPES["dwconv"], device=dev, generator=g)
         w = torch.randn(512, 1, 3, device=dev, generator=g)

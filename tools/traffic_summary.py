@@ -16,7 +16,8 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1]
-SHAPES = {"scan": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999), "conv3": (32, 64, 376, 257)}
+SHAPES = {"scan": (64, 1024, 3999), "scan_bwd": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999),
+          "conv3": (32, 64, 376, 257)}
 
 
 def per_launch(phase, counter):
@@ -39,12 +40,13 @@ def per_launch(phase, counter):
 
 
 res = {}
-raw = {ph: {c: per_launch(ph, c) for c in ("FETCH_SIZE", "WRITE_SIZE")} for ph in SHAPES}
+raw = {ph: {c: per_launch(ph, c) for c in ("FETCH_SIZE", "WRITE_SIZE")} for ph in SHAPES
+       if os.path.isdir(os.path.join(root, ph))}
 b, d, l = SHAPES["cconv"]
 known = 4.0 * b * d * l
 cal_r = known / raw["cconv"]["FETCH_SIZE"][0] if raw["cconv"]["FETCH_SIZE"][0] else None
 cal_w = known / raw["cconv"]["WRITE_SIZE"][0] if raw["cconv"]["WRITE_SIZE"][0] else None
-for ph in SHAPES:
+for ph in raw:
     fr, kern = raw[ph]["FETCH_SIZE"]
     wr, _ = raw[ph]["WRITE_SIZE"]
     if fr is None or wr is None:
