@@ -214,11 +214,10 @@ class MambaStep:
         from avse_challenge_amd import kernels as K
         d = 2 * self.model.masknet.mamba_net.layers[0].mixer.d_model
         b, l = self.B, 3999
-        u = torch.randn(b, d, l, device=dev)
-        dl = 0.1 * torch.randn(b, d, l, device=dev)
-        z = torch.randn(b, d, l, device=dev)
+        al = lambda *sh, scale=1.0: K.bdl_empty(*sh, torch.float32, dev).copy_(scale * torch.randn(sh, device=dev))  # noqa: E731
+        u, dl, z = al(b, d, l), al(b, d, l, scale=0.1), al(b, d, l)           # the model's aligned layout
         A = -torch.rand(d, 16, device=dev) - 0.5
-        Bm, Cm = torch.randn(b, 16, l, device=dev), torch.randn(b, 16, l, device=dev)
+        Bm, Cm = al(b, 16, l), al(b, 16, l)
         D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
         for _ in range(2):
             K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False)
@@ -348,10 +347,10 @@ class AVMambaStep:
         from avse_challenge_amd import kernels as K
         d = 2 * self.model.masknet.mamba_net.layers[0].mixer.d_model
         b, l, bf = self.B, 5999, torch.bfloat16
-        u, z = torch.randn(b, d, l, device=dev, dtype=bf), torch.randn(b, d, l, device=dev, dtype=bf)
-        dl = (0.1 * torch.randn(b, d, l, device=dev)).to(bf)
+        al = lambda *sh, scale=1.0: K.bdl_empty(*sh, bf, dev).copy_(scale * torch.randn(sh, device=dev))  # noqa: E731
+        u, z, dl = al(b, d, l), al(b, d, l), al(b, d, l, scale=0.1)           # the model's aligned layout
         A = -torch.rand(d, 16, device=dev) - 0.5
-        Bm, Cm = torch.randn(b, 16, l, device=dev, dtype=bf), torch.randn(b, 16, l, device=dev, dtype=bf)
+        Bm, Cm = al(b, 16, l), al(b, 16, l)
         D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
         return _time_hbm(lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False),
                          2.0 * b * l * (4 * d + 2 * 16), f"avse_scan_fwd (bf16, {b} x {d} x {l}, training fwd)")
