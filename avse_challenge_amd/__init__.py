@@ -21,4 +21,11 @@ import os
 MIOPEN_DB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
 os.environ.setdefault("MIOPEN_USER_DB_PATH", MIOPEN_DB)     # read by MIOpen at handle creation
 
+# HIP graphs: the runtime's graph packet capture (ROCm 7.x CLR; AQL packets and kernel arguments prepared at
+# instantiate time) replays some kernel nodes of the long single-stream avse1 train-step graph with the wrong
+# arguments: reduction results land in each other's buffers (tools/avse1_graph_diag4.py; loss -1.0 instead of
+# 0.34).  With the capture off every replay matches the eager step.  Read at HIP runtime init, i.e. at the
+# first GPU call, which comes after this import in every entry point (bench.py, tests, smoke()).
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 __version__ = "0.1.0"

@@ -15,6 +15,8 @@ MI355X specifics:
   * the remaining convolutions / BatchNorm / GEMMs are MIOpen / hipBLASLt MFMA kernels (fp32,
     exact f32 MFMA on gfx950 — no TF32 shortcut exists), channels-first like the reference.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -173,6 +175,18 @@ class FusionNet(nn.Module):               # model.py:81-96
         return torch.sigmoid(self.time_distributed_1(self.lstm_conv(x)[0]))
 
 
+_STREAMS = {}
+
+
+def _branch_stream(device):
+    """Second HIP stream for the lip branch (default; AVSE_AVSE1_STREAMS=0 runs both branches on the current stream)."""
+    if device.type != "cuda" or os.environ.get("AVSE_AVSE1_STREAMS", "1") != "1":
+        return None
+    if device not in _STREAMS:
+        _STREAMS[device] = torch.cuda.Stream(device)
+    return _STREAMS[device]
+
+
 class AVNet(nn.Module):
     """LightningModule surface of baseline/avse1/model.py:AVNet (forward / training_step / cal_loss)."""
 
@@ -193,11 +207,26 @@ class AVNet(nn.Module):
     def forward(self, inp):
         spec = inp["noisy_audio_spec"]
         T = spec.shape[2]
+        side = None if self.a_only else _branch_stream(spec.device)
+        if side is not None:
+            # the lip and audio branches are independent until the concatenation: the lip ResNet/TCN runs on a
+            # second HIP stream (its backward too, via autograd), so each branch's small kernels (BatchNorm,
+            # PReLU, transposes) fill the CUs the other leaves idle; both forks are captured in the step's graphs
+            main = torch.cuda.current_stream(spec.device)
+            side.wait_stream(main)
+            lips = inp["lip_images"]
+            with torch.cuda.stream(side):
+                vis = self.net_visualfeat(lips.float())                        # (B, 75, 512)
+            lips.record_stream(side)
         audio = self.net_audiofeat(spec)
+        if side is not None:
+            main.wait_stream(side)
+            vis.record_stream(main)
         if self.a_only:
             comb = audio
         else:
-            vis = self.net_visualfeat(inp["lip_images"].float())              # (B, 75, 512)
+            if side is None:
+                vis = self.net_visualfeat(inp["lip_images"].float())          # (B, 75, 512)
             # F.interpolate(nearest, size=(T, 512)) on (B, 1, 75, 512) == gather of rows floor(t*75/T)
             idx = torch.div(torch.arange(T, device=spec.device) * vis.shape[1], T, rounding_mode="floor")
             comb = torch.cat((vis.index_select(1, idx), audio), dim=-1)

@@ -130,13 +130,15 @@ class Trainer:
             dist.broadcast(self.buf_i, 0)
 
     # ------------------------------------------------------------------ step
-    def _fwd_bwd(self):
+    def _fwd_bwd(self, out=None):
         self.flat.zero_()
         if self.world > 1:
             self._arm()
         loss = self.step.loss()
+        if out is not None:
+            out.copy_(loss.detach())
         loss.backward()
-        return loss.detach()
+        return loss.detach() if out is None else out
 
     def _opt(self):
         if self.world > 1:
@@ -167,9 +169,13 @@ class Trainer:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             if self.world == 1:
+                # the step's loss lands in a buffer allocated outside the graph's private pool: the pool's block of
+                # the in-graph loss tensor is not guaranteed to hold it after replay (observed on the avse1 step)
+                loss_buf = torch.zeros((), device=self.dev, dtype=torch.float32)
                 self.g_fb = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.g_fb, stream=s):
-                    self.loss = self._fwd_bwd()
+                    self._fwd_bwd(loss_buf)
+                self.loss = loss_buf
             self.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_opt, stream=s):
                 self._opt()

@@ -338,6 +338,92 @@ def test_bimamba_direction_streams_equal_serial(monkeypatch, graph):
         torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-7)
 
 
+def _avse1_fb_values(graph):
+    """One avse1 C2-shaped fwd+bwd (B=2, 96x96 lips, dropout off) from fixed weights: (loss, grads), run eagerly
+    or as a captured HIP graph replayed twice (the second replay read back)."""
+    import bench
+    torch.manual_seed(5)
+    st = bench.Avse1Step(2, torch.device(DEV), 0, 1, 96)
+    for m in st.model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    params = [p for p in st.model.parameters()]
+    loss_buf = torch.zeros((), device=DEV)
+
+    def fb():
+        for p in params:                          # in place: the captured backward accumulates into these
+            if p.grad is not None:
+                p.grad.zero_()
+        loss = st.loss()
+        loss_buf.copy_(loss.detach())
+        loss.backward()
+
+    fb()                                          # eager (lazy library init; allocates the .grad tensors)
+    if graph:
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                fb()
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        g.replay()
+    torch.cuda.synchronize()
+    return float(loss_buf), [None if p.grad is None else p.grad.detach().clone() for p in params]
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_avse1_branch_streams_equal_serial(monkeypatch, graph):
+    """AVSE_AVSE1_STREAMS=1 (lip branch on a second HIP stream, forward and backward; eager and as a captured HIP
+    graph) gives the loss and every gradient of the single-stream eager step."""
+    monkeypatch.setenv("AVSE_AVSE1_STREAMS", "0")
+    l0, g0 = _avse1_fb_values(False)
+    monkeypatch.setenv("AVSE_AVSE1_STREAMS", "1")
+    l1, g1 = _avse1_fb_values(graph)
+    assert abs(l1 - l0) <= 1e-6 * abs(l0)
+    assert [a is None for a in g0] == [b is None for b in g1]      # tcn_output is unused on the feature path
+    f0 = torch.cat([a.reshape(-1) for a in g0 if a is not None])
+    f1 = torch.cat([b.reshape(-1) for b in g1 if b is not None])
+    assert float((f1 - f0).norm() / f0.norm()) <= 1e-4
+    gmax = float(f0.abs().max())
+    for i, (a, b) in enumerate(zip(g0, g1)):
+        if a is None:
+            continue
+        # parameters whose true gradient is ~0 (conv biases ahead of train-mode BatchNorm, unused slopes) carry
+        # rounding noise only: their bar is floored at 1e-2 of the largest gradient entry
+        scale = max(float(a.abs().max()), 1e-2 * gmax)
+        assert float((b - a).abs().max()) <= 1e-3 * scale, (i, tuple(a.shape))
+
+
+def test_avse1_single_stream_trainer_graph_losses_equal_eager(monkeypatch):
+    """The captured avse1 train step on ONE stream (the long linear graph that the HIP runtime's graph packet
+    capture replayed with wrong kernel arguments: loss -1.0) reports the eager losses; the package turns that
+    capture off (avse_challenge_amd/__init__.py)."""
+    import bench
+    monkeypatch.setenv("AVSE_AVSE1_STREAMS", "0")
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(5)
+        st = bench.Avse1Step(2, torch.device(DEV), 0, 1, 96)
+        for m in st.model.modules():
+            if isinstance(m, torch.nn.Dropout):
+                m.p = 0.0
+        tr = bench.Trainer(st, 1, torch.device(DEV), use_graph=graph)
+        losses = [float(tr())]
+        if graph:
+            tr.capture()
+        for _ in range(3):
+            losses.append(float(tr()))
+        torch.cuda.synchronize()
+        runs.append(losses)
+        del tr, st
+    # L1 + Adam amplify rounding differences step by step (MIOpen solver choice); a wrong replay is O(1) off
+    np.testing.assert_allclose(runs[1][:2], runs[0][:2], rtol=1e-5)
+    np.testing.assert_allclose(runs[1], runs[0], rtol=1e-3)
+
+
 def test_avse1_audio_only_c1_golden():
     """BASELINE configs[0] (C1): audio-only AVNet on the HIP path (AudioFeatNet -> FusionNet LSTM) vs the
     reference-generated golden (reference train.py:28-30, model.py:117-118): eval and train-BN predictions and
