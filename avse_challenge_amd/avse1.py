@@ -122,12 +122,23 @@ class VisualFeatNet(nn.Module):           # model.py:17-58
             LipConv3d(3, 64, (5, 7, 7), (1, 2, 2), (2, 3, 3)), nn.BatchNorm3d(64), _prelu(64),
             nn.MaxPool3d((1, 3, 3), (1, 2, 2), (0, 1, 1)))
         self.tcn = _TCN()
+        self.channels_last = False
+
+    def use_channels_last(self, on=True):
+        """NHWC ResNet trunk: MIOpen's NHWC implicit-GEMM convolutions without the batched transposes
+        around each NCHW call, NHWC BatchNorm, and the channels-last PReLU kernels (avse_prelu_nhwc_*)."""
+        self.channels_last = on
+        self.trunk.to(memory_format=torch.channels_last if on else torch.contiguous_format)
+        return self
 
     def forward(self, lips):              # (B, 3, T, H, W) raw 0..255 float -> (B, T, 512)
         Bn = lips.shape[0]
         x = self.frontend3D(lips)
-        Tn = x.shape[2]
-        x = x.transpose(1, 2).reshape(Bn * Tn, x.shape[1], x.shape[3], x.shape[4])
+        Tn, C, H, W = x.shape[2], x.shape[1], x.shape[3], x.shape[4]
+        if self.channels_last:            # (B, C, T, H, W) -> (B*T, H, W, C) in memory, viewed as NCHW
+            x = x.permute(0, 2, 3, 4, 1).reshape(Bn * Tn, H, W, C).permute(0, 3, 1, 2)
+        else:
+            x = x.transpose(1, 2).reshape(Bn * Tn, C, H, W)
         x = self.trunk(x).view(Bn, Tn, -1)
         return self.tcn(x).transpose(1, 2)
 

@@ -8,6 +8,8 @@
 // (n, c) row of the (N, C, S) view, float4 streaming, the slope gradient reduced in registers /
 // LDS per row and summed over n by a second tiny kernel (deterministic).  HBM-bound:
 // fwd 8 B/elem, bwd 12 B/elem.
+#include <algorithm>
+
 #include "common.h"
 
 namespace avse {
@@ -94,6 +96,90 @@ __global__ void reduce_kernel(const float* __restrict__ ws, int64_t N, int C, in
     if (threadIdx.x == 0) da[c] = red[0] + red[1] + red[2] + red[3];
 }
 
+// ---- channels-last (NHWC) layout: an (R, C) row-major view, C % 4 == 0, slope index = column.
+// The avse1 lip ResNet runs channels-last (MIOpen's NHWC convolutions); the NCS kernels above would
+// launch one 256-thread workgroup per 9-element (n, c) row at layer4 (3x3 maps).
+
+__global__ __launch_bounds__(THREADS) void nhwc_fwd_kernel(int64_t n4, int C4, int per_channel,
+                                                           const float4* __restrict__ x, const float* __restrict__ a,
+                                                           float4* __restrict__ y) {
+    const float a0 = a[0];
+    for (int64_t f = (int64_t)blockIdx.x * THREADS + threadIdx.x; f < n4; f += (int64_t)gridDim.x * THREADS) {
+        const float4 av = per_channel ? reinterpret_cast<const float4*>(a)[f % C4] : make_float4(a0, a0, a0, a0);
+        float4 v = x[f];
+        v.x = v.x > 0.f ? v.x : av.x * v.x;
+        v.y = v.y > 0.f ? v.y : av.y * v.y;
+        v.z = v.z > 0.f ? v.z : av.z * v.z;
+        v.w = v.w > 0.f ? v.w : av.w * v.w;
+        y[f] = v;
+    }
+}
+
+// thread = (row offset, 4-channel group): RPI = 256 / C4 rows per workgroup pass, the group fixed for the
+// whole grid-stride loop, so the slope-gradient partial stays in registers; the workgroup's RPI partials per
+// group are summed in LDS and written as one C-wide row of ws (summed over workgroups by nhwc_reduce_kernel)
+__global__ __launch_bounds__(THREADS) void nhwc_bwd_kernel(int64_t R, int C4, int per_channel,
+                                                           const float4* __restrict__ x, const float* __restrict__ a,
+                                                           const float4* __restrict__ dy, float4* __restrict__ dx,
+                                                           float* __restrict__ ws) {
+    __shared__ float4 part[THREADS];
+    const int RPI = THREADS / C4;
+    const int cg = threadIdx.x % C4, roff = threadIdx.x / C4;
+    const float a0 = a[0];
+    const float4 av = per_channel ? reinterpret_cast<const float4*>(a)[cg] : make_float4(a0, a0, a0, a0);
+    float4 da = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (roff < RPI) {
+        for (int64_t r = (int64_t)blockIdx.x * RPI + roff; r < R; r += (int64_t)gridDim.x * RPI) {
+            const int64_t f = r * C4 + cg;
+            const float4 v = x[f], g = dy[f];
+            float4 o;
+            o.x = v.x > 0.f ? g.x : av.x * g.x; da.x += v.x > 0.f ? 0.f : g.x * v.x;
+            o.y = v.y > 0.f ? g.y : av.y * g.y; da.y += v.y > 0.f ? 0.f : g.y * v.y;
+            o.z = v.z > 0.f ? g.z : av.z * g.z; da.z += v.z > 0.f ? 0.f : g.z * v.z;
+            o.w = v.w > 0.f ? g.w : av.w * g.w; da.w += v.w > 0.f ? 0.f : g.w * v.w;
+            dx[f] = o;
+        }
+    }
+    part[threadIdx.x] = da;
+    __syncthreads();
+    if (roff == 0) {
+        float4 s = da;
+        for (int k = 1; k < RPI; ++k) {
+            const float4 q = part[k * C4 + cg];
+            s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
+        }
+        reinterpret_cast<float4*>(ws + (int64_t)blockIdx.x * 4 * C4)[cg] = s;
+    }
+}
+
+// da[c] = sum_w ws[w * C + c] (per channel) or the sum of everything (single slope); one workgroup
+__global__ void nhwc_reduce_kernel(const float* __restrict__ ws, int nblk, int C, int per_channel, float* __restrict__ da) {
+    __shared__ float red[256 / 64];
+    if (per_channel) {
+        for (int c = threadIdx.x; c < C; c += blockDim.x) {
+            float v = 0.f;
+            for (int w = 0; w < nblk; ++w) v += ws[(int64_t)w * C + c];
+            da[c] = v;
+        }
+        return;
+    }
+    float v = 0.f;
+    for (int64_t i = threadIdx.x; i < (int64_t)nblk * C; i += blockDim.x) v += ws[i];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) da[0] = red[0] + red[1] + red[2] + red[3];
+}
+
+inline bool nhwc_ok(int64_t R, int64_t C) {
+    return R > 0 && C > 0 && C % 4 == 0 && C / 4 <= THREADS && THREADS % (C / 4) == 0 && R * C < (1LL << 40);
+}
+inline int nhwc_bwd_blocks(int64_t R, int64_t C) {
+    const int64_t rpi = THREADS / (C / 4);
+    return (int)std::min<int64_t>(1024, (R + rpi - 1) / rpi);
+}
+
 }  // namespace prelu
 }  // namespace avse
 
@@ -124,6 +210,40 @@ int avse_prelu_bwd(int64_t N, int64_t C, int64_t S, int32_t num_params, const fl
     hipLaunchKernelGGL(bwd_kernel, dim3((unsigned)(N * C)), dim3(THREADS), 0, st, (int)C, S, pc, x, a, dy, dx, workspace);
     AVSE_CHECK_LAUNCH();
     hipLaunchKernelGGL(reduce_kernel, dim3(pc ? (unsigned)C : 1u), dim3(256), 0, st, workspace, N, (int)C, pc, da);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_prelu_nhwc_fwd(int64_t R, int64_t C, int32_t num_params, const float* x, const float* a, float* y,
+                        avse_stream_t stream) {
+    if (!x || !a || !y) return AVSE_EINVAL;
+    if (!nhwc_ok(R, C) || (num_params != 1 && num_params != C)) return AVSE_ESHAPE;
+    if (((uintptr_t)x | (uintptr_t)y | (num_params > 1 ? (uintptr_t)a : 0)) & 15) return AVSE_EALIGN;
+    const int64_t n4 = R * C / 4;
+    const int blocks = (int)std::min<int64_t>(8192, (n4 + THREADS - 1) / THREADS);
+    hipLaunchKernelGGL(nhwc_fwd_kernel, dim3(blocks), dim3(THREADS), 0, (hipStream_t)stream, n4, (int)(C / 4),
+                       (int)(num_params > 1), reinterpret_cast<const float4*>(x), a, reinterpret_cast<float4*>(y));
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int64_t avse_prelu_nhwc_bwd_workspace_bytes(int64_t R, int64_t C) {
+    return nhwc_ok(R, C) ? 4 * (int64_t)nhwc_bwd_blocks(R, C) * C : 0;
+}
+
+int avse_prelu_nhwc_bwd(int64_t R, int64_t C, int32_t num_params, const float* x, const float* a, const float* dy,
+                        float* dx, float* da, float* workspace, avse_stream_t stream) {
+    if (!x || !a || !dy || !dx || !da || !workspace) return AVSE_EINVAL;
+    if (!nhwc_ok(R, C) || (num_params != 1 && num_params != C)) return AVSE_ESHAPE;
+    if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)workspace | (num_params > 1 ? (uintptr_t)a : 0)) & 15)
+        return AVSE_EALIGN;
+    hipStream_t st = (hipStream_t)stream;
+    const int nblk = nhwc_bwd_blocks(R, C), pc = num_params > 1;
+    hipLaunchKernelGGL(nhwc_bwd_kernel, dim3(nblk), dim3(THREADS), 0, st, R, (int)(C / 4), pc,
+                       reinterpret_cast<const float4*>(x), a, reinterpret_cast<const float4*>(dy),
+                       reinterpret_cast<float4*>(dx), workspace);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(nhwc_reduce_kernel, dim3(1), dim3(256), 0, st, workspace, nblk, (int)C, pc, da);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

@@ -338,8 +338,24 @@ def _ncs(x):
     return N, C, S
 
 
+def _nhwc(x):
+    """(R, C) of a channels-last 4-D activation the NHWC PReLU kernels take, else None."""
+    if x.dim() != 4 or x.is_contiguous() or not x.is_contiguous(memory_format=torch.channels_last):
+        return None
+    C = x.shape[1]
+    if C % 4 or 256 % (C // 4):
+        return None
+    return x.numel() // C, C
+
+
 def prelu_fwd(x, a):
     _need_gpu(x, a)
+    if x.dtype == torch.float32 and _nhwc(x) is not None:
+        R, C = _nhwc(x)
+        y = torch.empty_like(x)                      # preserves channels-last strides
+        check(_lib.lib().avse_prelu_nhwc_fwd(R, C, a.numel(), ptr(x), ptr(a.contiguous()), ptr(y),
+                                             stream_ptr(x.device)), "avse_prelu_nhwc_fwd")
+        return y
     x = x.contiguous()
     if x.dtype != torch.float32:
         raise RuntimeError("prelu kernels are fp32")
@@ -352,6 +368,17 @@ def prelu_fwd(x, a):
 
 def prelu_bwd(x, a, dy):
     _need_gpu(x, a, dy)
+    if x.dtype == torch.float32 and _nhwc(x) is not None:
+        R, C = _nhwc(x)
+        dy = dy.float().contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x)
+        da = torch.empty((a.numel(),), device=x.device, dtype=torch.float32)
+        L = _lib.lib()
+        ws = torch.empty((max(4, L.avse_prelu_nhwc_bwd_workspace_bytes(R, C)) + 3) // 4, device=x.device,
+                         dtype=torch.float32)
+        check(L.avse_prelu_nhwc_bwd(R, C, a.numel(), ptr(x), ptr(a.contiguous()), ptr(dy), ptr(dx), ptr(da), ptr(ws),
+                                    stream_ptr(x.device)), "avse_prelu_nhwc_bwd")
+        return dx, da.view_as(a)
     x, dy = x.contiguous(), dy.contiguous().float()
     N, C, S = _ncs(x)
     dx = torch.empty_like(x)

@@ -178,6 +178,14 @@ int avse_prelu_fwd(int64_t N, int64_t C, int64_t S, int32_t num_params, const fl
 int64_t avse_prelu_bwd_workspace_bytes(int64_t N, int64_t C);
 int avse_prelu_bwd(int64_t N, int64_t C, int64_t S, int32_t num_params, const float* x, const float* a,
                    const float* dy, float* dx, float* da, float* workspace, avse_stream_t stream);
+/* The same on a channels-last (R, C) row-major view (NHWC activations: R = N*H*W; the avse1 lip ResNet,
+ * utils/resnet.py:45-46, in the layout MIOpen's NHWC convolutions use).  C % 4 == 0 and (C / 4) divides 256;
+ * x, y, dy, dx, workspace (and a when num_params == C) 16-byte aligned. */
+int avse_prelu_nhwc_fwd(int64_t R, int64_t C, int32_t num_params, const float* x, const float* a, float* y,
+                        avse_stream_t stream);
+int64_t avse_prelu_nhwc_bwd_workspace_bytes(int64_t R, int64_t C);
+int avse_prelu_nhwc_bwd(int64_t R, int64_t C, int32_t num_params, const float* x, const float* a, const float* dy,
+                        float* dx, float* da, float* workspace, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- PReLU -> gLN (avse4) ----
  * y = gLN(PReLU(x)) of baseline/avse4/model.py:259-266,284-292 (PReLU with one slope; gLN

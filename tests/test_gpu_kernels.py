@@ -341,6 +341,28 @@ def test_prelu_vs_torch(shape, npar):
     close(m.weight.grad, a.grad, 1e-4, 1e-5, "da")
 
 
+@pytest.mark.parametrize("shape,npar", [((6, 64, 24, 24), 64), ((10, 512, 3, 3), 512), ((7, 128, 5, 5), 1),
+                                        ((3, 256, 6, 6), 256), ((2, 16, 4, 3), 16)])
+def test_prelu_channels_last_vs_torch(shape, npar):
+    """Channels-last (NHWC) activations take avse_prelu_nhwc_*; output keeps the channels-last strides."""
+    from avse_challenge_amd.layers import PReLU
+    x = det_input(shape, 730).double().requires_grad_(True)
+    a = (0.1 + torch.rand(npar, generator=torch.Generator().manual_seed(2))).double().requires_grad_(True)
+    y = torch.nn.functional.prelu(x, a)
+    gy = det_input(shape, 731).double()
+    y.backward(gy)
+    m = PReLU(npar).to(DEV)
+    with torch.no_grad():
+        m.weight.copy_(a.detach().float())
+    xg = x.detach().float().to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    yg = m(xg)
+    assert yg.is_contiguous(memory_format=torch.channels_last) and not yg.is_contiguous()
+    close(yg, y, 1e-6, 1e-6, "y")
+    yg.backward(gy.float().to(DEV).contiguous(memory_format=torch.channels_last))
+    close(xg.grad, x.grad, 1e-6, 1e-6, "dx")
+    close(m.weight.grad, a.grad, 1e-4, 1e-5, "da")
+
+
 # ------------------------------------------------------------------ flip-by-index (BiMamba v2 backward direction)
 
 @pytest.mark.parametrize("l", [1, 64, 150, 257])

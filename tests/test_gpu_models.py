@@ -75,10 +75,14 @@ def test_mamba_tasnet_xs_train_step_vs_oracle():
         close(p.grad, r, 2e-3 * scale, 2e-3, k)
 
 
-def test_avse1_full_golden_eval():
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_avse1_full_golden_eval(channels_last):
     from avse_challenge_amd import avse1
     g = load_golden("avse1_full")
     net = det_init_(avse1.AVNet(), 54).to(DEV).eval()
+    if channels_last:                 # the bench layout: NHWC audio convs and lip ResNet trunk
+        net.net_audiofeat.use_channels_last()
+        net.net_visualfeat.use_channels_last()
     batch = {"noisy_audio_spec": det_input((1, 1, 376, 257), 505).abs().to(DEV),
              "lip_images": det_input((1, 3, 75, 96, 96), 506, "uint8").to(DEV),
              "mask": det_input((1, 1, 376, 257), 507).abs().to(DEV)}
@@ -88,7 +92,8 @@ def test_avse1_full_golden_eval():
         close(net.cal_loss(batch), g["loss"], 1e-5, 1e-5, "loss")
 
 
-def test_avse1_wave_frontend_and_train_step_vs_oracle():
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_avse1_wave_frontend_and_train_step_vs_oracle(channels_last):
     """HIP STFT front-end + train step (train-mode BN, dropout off) vs the oracle.
 
     The fp64 oracle is the truth.  The error band of fp32 on this GPU is set by the library
@@ -101,6 +106,9 @@ def test_avse1_wave_frontend_and_train_step_vs_oracle():
     from avse_challenge_amd import avse1
     from oracle import stft_ref
     ours = det_init_(avse1.AVNet(), 55).to(DEV).train()
+    if channels_last:
+        ours.net_audiofeat.use_channels_last()
+        ours.net_visualfeat.use_channels_last()
     ref32 = det_init_(avse1_ref.AVNet(), 55).train()
     ref64 = det_init_(avse1_ref.AVNet(), 55).double().train()
     tg = det_init_(avse1_ref.AVNet(), 55).to(DEV).train()
