@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .layers import HipLSTM, LipConv3d, PReLU
+from .layers import HipLSTM, LipConv3d, PReLU, bn_act
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
@@ -42,8 +42,14 @@ class _BasicBlock(nn.Module):            # utils/resnet.py:26-67 (relu_type='pre
         self.downsample = downsample
 
     def forward(self, x):
-        y = self.bn2(self.conv2(self.relu1(self.bn1(self.conv1(x)))))
-        return self.relu2(y + (x if self.downsample is None else self.downsample(x)))
+        # BN -> PReLU and BN -> (+ shortcut) -> PReLU as fused passes (csrc/bnact.hip)
+        y = self.conv2(bn_act(self.conv1(x), self.bn1, self.relu1))
+        if self.downsample is None:
+            sc = x
+        else:
+            ds_conv, ds_bn = self.downsample
+            sc = bn_act(ds_conv(x), ds_bn)
+        return bn_act(y, self.bn2, self.relu2, res=sc)
 
 
 class _ResNet18(nn.Module):              # utils/resnet.py:70-124
@@ -133,7 +139,8 @@ class VisualFeatNet(nn.Module):           # model.py:17-58
 
     def forward(self, lips):              # (B, 3, T, H, W) raw 0..255 float -> (B, T, 512)
         Bn = lips.shape[0]
-        x = self.frontend3D(lips)
+        conv, bn, act, pool = self.frontend3D
+        x = pool(bn_act(conv(lips), bn, act))
         Tn, C, H, W = x.shape[2], x.shape[1], x.shape[3], x.shape[4]
         if self.channels_last:            # (B, C, T, H, W) -> (B*T, H, W, C) in memory, viewed as NCHW
             x = x.permute(0, 2, 3, 4, 1).reshape(Bn * Tn, H, W, C).permute(0, 3, 1, 2)
@@ -166,12 +173,12 @@ class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 conv
 
     def forward(self, spec):              # (B, 1, T, F) -> (B, T, 4F)
         T, Fb = spec.shape[2], spec.shape[3]
-        x = self.bn0(spec)
+        x = bn_act(spec, self.bn0)
         if self.channels_last:
             x = x.contiguous(memory_format=torch.channels_last)
         for i in range(1, self.num_conv + 1):
-            x = F.relu(getattr(self, f"bn{i}")(getattr(self, f"conv{i}")(x)))
-        x = F.relu(self.bn_last(self.convf(x)))
+            x = bn_act(getattr(self, f"conv{i}")(x), getattr(self, f"bn{i}"), "relu")
+        x = bn_act(self.convf(x), self.bn_last, "relu")
         return x.permute(0, 2, 1, 3).reshape(-1, T, Fb * self.last_filter)
 
 

@@ -1,0 +1,438 @@
+// Fused BatchNorm -> [+ residual] -> activation (none / ReLU / PReLU) for gfx950: forward (training: batch
+// statistics and the running-stat update; eval: running statistics) and backward.
+//
+// Replaces the MIOpen BatchNorm + separate PReLU / ReLU / residual-add passes of the avse1 lip stream
+// (/root/reference/baseline/avse1/model.py:29-34 frontend3D BatchNorm3d -> PReLU; utils/resnet.py:40-67
+// BasicBlock bn1 -> PReLU, bn2 + shortcut -> PReLU, downsample BatchNorm2d) and of the avse1 audio net
+// (model.py:181-267 BatchNorm2d -> ReLU, channels-last).  In the round-2 avse1 step profile MIOpen's
+// BatchNorm kernels and the PReLU passes took ~77 ms of kernel time per step (profiles/r02_avse1_*).
+//
+// One layout covers both memory formats: the activation is an (N, C, S) row-major view -- NCHW / NCDHW
+// (S = H*W or T*H*W) and channels-last NHWC (N = batch*H*W, S = 1).  Every kernel maps a thread to a
+// fixed column j of the (N, C*S) matrix (channel j / S) and walks rows, so all loads are coalesced
+// row segments whatever S is (3x3 ResNet maps or 1-wide NHWC rows), and per-channel sums are per-column
+// register partials, summed over the workgroup's row offsets in LDS, written as one (C*S)-wide row per
+// row block and reduced per channel by a one-workgroup-per-channel kernel in fp64 (deterministic, no
+// atomics).  The forward statistics are shifted by each channel's first element (x[0, c, 0]) so that
+// E[x^2] - E[x]^2 does not cancel for large-mean inputs (raw 0..255 lip pixels through Conv3d).
+//
+// HBM traffic per element: forward 4 B (statistics) + 8 B (apply, +4 with a residual); backward 8 B
+// (partials) + 12 B (apply); with a residual 12 + 4 (dres written) and 12.
+#include <algorithm>
+
+#include "common.h"
+
+namespace avse {
+namespace bnact {
+
+constexpr int THREADS = 256;
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_PRELU = 2 };
+
+struct Geo {
+    int64_t N, CS, S;
+    int C, TW, RPI, tiles, nrb;
+};
+
+template <int V> struct vld;
+template <> struct vld<1> {
+    __device__ static inline void ld(const float* p, float* v) { v[0] = *p; }
+    __device__ static inline void st(float* p, const float* v) { *p = v[0]; }
+};
+template <> struct vld<4> {
+    __device__ static inline void ld(const float* p, float* v) {
+        const float4 q = *reinterpret_cast<const float4*>(p);
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    }
+    __device__ static inline void st(float* p, const float* v) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+};
+
+// per-column constants of the thread's V columns: z = (x - mean) a + b (+ res) -- centred first, as torch does,
+// so large-mean inputs do not lose the low bits of z to a cancelling a x + (beta - mean a) -- act slope, rstd
+// The mean is carried as a float pair (hi + lo): x - hi is exact for x near the mean (Sterbenz), so the
+// centred value keeps its low bits even when |mean| >> std (a ReLU/PReLU mask computed from z would
+// otherwise flip for |z| below a * ulp(mean); torch's CPU kernels centre in double).
+template <int V, int ACT>
+struct ColConst {
+    float a[V], b[V], al[V], mean[V], mlo[V], rstd[V], gam[V];
+    __device__ inline float centred(float v, int k) const { return (v - mean[k]) - mlo[k]; }
+    __device__ inline void load(const Geo& g, int64_t j0, const float* stats, const float* gamma, const float* beta,
+                                const float* alpha, int alpha_n) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const int c = (int)((j0 + k) / g.S);
+            mean[k] = stats[4 * c];
+            mlo[k] = stats[4 * c + 1];
+            rstd[k] = stats[4 * c + 2];
+            gam[k] = gamma ? gamma[c] : 1.f;
+            a[k] = gam[k] * rstd[k];
+            b[k] = beta ? beta[c] : 0.f;
+            al[k] = ACT == ACT_PRELU ? alpha[alpha_n > 1 ? c : 0] : 0.f;
+        }
+    }
+};
+
+template <int ACT>
+__device__ inline float act_fwd(float z, float al) {
+    if constexpr (ACT == ACT_RELU) return z > 0.f ? z : 0.f;
+    else if constexpr (ACT == ACT_PRELU) return z > 0.f ? z : al * z;
+    else return z;
+}
+template <int ACT>
+__device__ inline float act_bwd(float z, float g, float al) {
+    if constexpr (ACT == ACT_RELU) return z > 0.f ? g : 0.f;
+    else if constexpr (ACT == ACT_PRELU) return z > 0.f ? g : al * g;
+    else return g;
+}
+
+// Sum NQ per-thread column partials over the workgroup's RPI row offsets; row offset 0 writes
+// ws[(blockIdx.y * NQ + q) * CS + j].
+template <int V, int NQ>
+__device__ inline void block_partials(const Geo& g, float (&p)[NQ][V], bool valid, int64_t j0, float* ws) {
+    __shared__ float part[NQ][THREADS * V];
+    const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int k = 0; k < V; ++k) part[q][threadIdx.x * V + k] = p[q][k];
+    __syncthreads();
+    if (ty == 0 && valid) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            float s[V];
+#pragma unroll
+            for (int k = 0; k < V; ++k) s[k] = p[q][k];
+            for (int t = 1; t < g.RPI; ++t)
+#pragma unroll
+                for (int k = 0; k < V; ++k) s[k] += part[q][(t * g.TW + tx) * V + k];
+            vld<V>::st(ws + ((int64_t)blockIdx.y * NQ + q) * g.CS + j0, s);
+        }
+    }
+}
+
+// ---- forward: statistics partials (shifted sums), finalize, apply
+template <int V>
+__global__ __launch_bounds__(THREADS) void stats_kernel(Geo g, const float* __restrict__ x, float* __restrict__ ws) {
+    const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
+    const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
+    const bool valid = j0 < g.CS;
+    float p[2][V], K[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        p[0][k] = p[1][k] = 0.f;
+        K[k] = valid ? x[((j0 + k) / g.S) * g.S] : 0.f;
+    }
+    if (valid) {
+        for (int64_t r = (int64_t)blockIdx.y * g.RPI + ty; r < g.N; r += (int64_t)gridDim.y * g.RPI) {
+            float v[V];
+            vld<V>::ld(x + r * g.CS + j0, v);
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                const float d = v[k] - K[k];
+                p[0][k] += d;
+                p[1][k] = fmaf(d, d, p[1][k]);
+            }
+        }
+    }
+    block_partials<V, 2>(g, p, valid, j0, ws);
+}
+
+__device__ inline double block_sum_d(double v, double* red) {
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+    return s;
+}
+
+__global__ __launch_bounds__(THREADS) void stats_finalize(Geo g, const float* __restrict__ x, const float* __restrict__ ws,
+                                                          float eps, float momentum, float* __restrict__ running_mean,
+                                                          float* __restrict__ running_var, float* __restrict__ stats) {
+    __shared__ double red[THREADS / 64];
+    const int c = blockIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+    const int S = (int)g.S, cnt = g.nrb * S;              // < 2^23: nrb * S <= 4096 * 1024 (make_geo)
+    for (int i = threadIdx.x; i < cnt; i += THREADS) {
+        const int y = i / S, s = i - y * S;
+        s1 += ws[((int64_t)y * 2) * g.CS + (int64_t)c * g.S + s];
+        s2 += ws[((int64_t)y * 2 + 1) * g.CS + (int64_t)c * g.S + s];
+    }
+    s1 = block_sum_d(s1, red);
+    s2 = block_sum_d(s2, red);
+    if (threadIdx.x == 0) {
+        const double n = (double)g.N * (double)g.S;
+        const double m1 = s1 / n;
+        double var = s2 / n - m1 * m1;
+        if (var < 0.0) var = 0.0;
+        const double mean = (double)x[(int64_t)c * g.S] + m1;
+        const float hi = (float)mean;
+        stats[4 * c] = hi;
+        stats[4 * c + 1] = (float)(mean - (double)hi);
+        stats[4 * c + 2] = (float)(1.0 / sqrt(var + (double)eps));
+        stats[4 * c + 3] = 0.f;
+        if (running_mean) running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+        if (running_var) running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * var * n / (n - 1.0));
+    }
+}
+
+__global__ void eval_stats_kernel(int C, const float* __restrict__ rm, const float* __restrict__ rv, float eps,
+                                  float* __restrict__ stats) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < C) {
+        stats[4 * c] = rm[c];
+        stats[4 * c + 1] = 0.f;
+        stats[4 * c + 2] = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
+        stats[4 * c + 3] = 0.f;
+    }
+}
+
+template <int V, int ACT, bool RES>
+__global__ __launch_bounds__(THREADS) void apply_kernel(Geo g, const float* __restrict__ x, const float* __restrict__ res,
+                                                        const float* __restrict__ stats, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, const float* __restrict__ alpha,
+                                                        int alpha_n, float* __restrict__ y) {
+    const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
+    const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
+    if (j0 >= g.CS) return;
+    ColConst<V, ACT> cc;
+    cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
+    for (int64_t r = (int64_t)blockIdx.y * g.RPI + ty; r < g.N; r += (int64_t)gridDim.y * g.RPI) {
+        const int64_t o = r * g.CS + j0;
+        float v[V], rv[V];
+        vld<V>::ld(x + o, v);
+        if (RES) vld<V>::ld(res + o, rv);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            float z = fmaf(cc.centred(v[k], k), cc.a[k], cc.b[k]);
+            if (RES) z += rv[k];
+            v[k] = act_fwd<ACT>(z, cc.al[k]);
+        }
+        vld<V>::st(y + o, v);
+    }
+}
+
+// ---- backward: partials of sum dz, sum dz*xhat, PReLU slope; finalize; apply
+template <int V, int ACT, bool RES>
+__global__ __launch_bounds__(THREADS) void bwd_partial_kernel(Geo g, const float* __restrict__ x,
+                                                              const float* __restrict__ res, const float* __restrict__ dy,
+                                                              const float* __restrict__ stats,
+                                                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                              const float* __restrict__ alpha, int alpha_n,
+                                                              float* __restrict__ ws, float* __restrict__ dres) {
+    const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
+    const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
+    const bool valid = j0 < g.CS;
+    float p[3][V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) p[0][k] = p[1][k] = p[2][k] = 0.f;
+    if (valid) {
+        ColConst<V, ACT> cc;
+        cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
+        for (int64_t r = (int64_t)blockIdx.y * g.RPI + ty; r < g.N; r += (int64_t)gridDim.y * g.RPI) {
+            const int64_t o = r * g.CS + j0;
+            float v[V], gv[V], rv[V], dz[V];
+            vld<V>::ld(x + o, v);
+            vld<V>::ld(dy + o, gv);
+            if (RES) vld<V>::ld(res + o, rv);
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                float z = fmaf(cc.centred(v[k], k), cc.a[k], cc.b[k]);
+                if (RES) z += rv[k];
+                dz[k] = act_bwd<ACT>(z, gv[k], cc.al[k]);
+                const float xh = cc.centred(v[k], k) * cc.rstd[k];
+                p[0][k] += dz[k];
+                p[1][k] = fmaf(dz[k], xh, p[1][k]);
+                if (ACT == ACT_PRELU && !(z > 0.f)) p[2][k] = fmaf(gv[k], z, p[2][k]);
+            }
+            if (RES) vld<V>::st(dres + o, dz);
+        }
+    }
+    block_partials<V, 3>(g, p, valid, j0, ws);
+}
+
+__global__ __launch_bounds__(THREADS) void bwd_finalize(Geo g, const float* __restrict__ ws, int training,
+                                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                        float* __restrict__ dalpha_c, float* __restrict__ kbuf) {
+    __shared__ double red[THREADS / 64];
+    const int c = blockIdx.x;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    const int S = (int)g.S, cnt = g.nrb * S;
+    for (int i = threadIdx.x; i < cnt; i += THREADS) {
+        const int y = i / S, s = i - y * S;
+        const int64_t col = (int64_t)c * g.S + s;
+        s0 += ws[((int64_t)y * 3) * g.CS + col];
+        s1 += ws[((int64_t)y * 3 + 1) * g.CS + col];
+        s2 += ws[((int64_t)y * 3 + 2) * g.CS + col];
+    }
+    s0 = block_sum_d(s0, red);
+    s1 = block_sum_d(s1, red);
+    s2 = block_sum_d(s2, red);
+    if (threadIdx.x == 0) {
+        const double n = (double)g.N * (double)g.S;
+        if (dbeta) dbeta[c] = (float)s0;
+        if (dgamma) dgamma[c] = (float)s1;
+        if (dalpha_c) dalpha_c[c] = (float)s2;
+        kbuf[2 * c] = training ? (float)(s0 / n) : 0.f;
+        kbuf[2 * c + 1] = training ? (float)(s1 / n) : 0.f;
+    }
+}
+
+template <int V, int ACT, bool RES>
+__global__ __launch_bounds__(THREADS) void bwd_apply_kernel(Geo g, const float* __restrict__ x,
+                                                            const float* __restrict__ dy, const float* __restrict__ dres,
+                                                            const float* __restrict__ stats,
+                                                            const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                            const float* __restrict__ alpha, int alpha_n,
+                                                            const float* __restrict__ kbuf, float* __restrict__ dx) {
+    const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
+    const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
+    if (j0 >= g.CS) return;
+    ColConst<V, ACT> cc;
+    cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
+    float k1[V], k2[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const int c = (int)((j0 + k) / g.S);
+        k1[k] = kbuf[2 * c];
+        k2[k] = kbuf[2 * c + 1];
+    }
+    for (int64_t r = (int64_t)blockIdx.y * g.RPI + ty; r < g.N; r += (int64_t)gridDim.y * g.RPI) {
+        const int64_t o = r * g.CS + j0;
+        float v[V], dz[V];
+        vld<V>::ld(x + o, v);
+        if (RES) {
+            vld<V>::ld(dres + o, dz);                  // dz of the pre-activation, written by the partial pass
+        } else {
+            float gv[V];
+            vld<V>::ld(dy + o, gv);
+#pragma unroll
+            for (int k = 0; k < V; ++k) dz[k] = act_bwd<ACT>(fmaf(cc.centred(v[k], k), cc.a[k], cc.b[k]), gv[k], cc.al[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const float xh = cc.centred(v[k], k) * cc.rstd[k];
+            v[k] = cc.a[k] * (dz[k] - k1[k] - xh * k2[k]);
+        }
+        vld<V>::st(dx + o, v);
+    }
+}
+
+// ---- host side
+inline int pow2ceil(int64_t v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+inline Geo make_geo(int64_t N, int64_t C, int64_t S, int V) {
+    Geo g;
+    g.N = N; g.S = S; g.C = (int)C; g.CS = C * S;
+    const int64_t cw = (g.CS + V - 1) / V;
+    g.TW = cw >= THREADS ? THREADS : pow2ceil(cw);
+    g.RPI = THREADS / g.TW;
+    g.tiles = (int)((cw + g.TW - 1) / g.TW);
+    const int64_t want = (N + (int64_t)g.RPI * 8 - 1) / ((int64_t)g.RPI * 8);      // >= 8 rows per thread
+    const int64_t cap = std::max<int64_t>(1, 4096 / g.tiles);
+    g.nrb = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(want, cap), 65535));
+    return g;
+}
+
+inline bool shape_ok(int64_t N, int64_t C, int64_t S) {
+    return N > 0 && C > 0 && S > 0 && N * C * S < (1LL << 40) && C * S < (1LL << 31) && C < (1 << 20) &&
+           (C * S + 3) / 4 <= (int64_t)THREADS * 0x7FFFFFFF;
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <template <int, int, bool> class K>
+struct dispatch {
+    template <typename... A>
+    static void run(int V, int act, bool res, dim3 grid, hipStream_t st, A... a) {
+#define AVSE_BNACT_CASE(VV, AA, RR) \
+    if (V == VV && act == AA && res == RR) { hipLaunchKernelGGL((K<VV, AA, RR>::fn), grid, dim3(THREADS), 0, st, a...); return; }
+        AVSE_BNACT_CASE(4, ACT_NONE, false) AVSE_BNACT_CASE(4, ACT_RELU, false) AVSE_BNACT_CASE(4, ACT_PRELU, false)
+        AVSE_BNACT_CASE(4, ACT_NONE, true) AVSE_BNACT_CASE(4, ACT_RELU, true) AVSE_BNACT_CASE(4, ACT_PRELU, true)
+        AVSE_BNACT_CASE(1, ACT_NONE, false) AVSE_BNACT_CASE(1, ACT_RELU, false) AVSE_BNACT_CASE(1, ACT_PRELU, false)
+        AVSE_BNACT_CASE(1, ACT_NONE, true) AVSE_BNACT_CASE(1, ACT_RELU, true) AVSE_BNACT_CASE(1, ACT_PRELU, true)
+#undef AVSE_BNACT_CASE
+    }
+};
+template <int V, int A, bool R> struct ApplyK { static constexpr auto fn = apply_kernel<V, A, R>; };
+template <int V, int A, bool R> struct BwdPartK { static constexpr auto fn = bwd_partial_kernel<V, A, R>; };
+template <int V, int A, bool R> struct BwdApplyK { static constexpr auto fn = bwd_apply_kernel<V, A, R>; };
+
+}  // namespace bnact
+}  // namespace avse
+
+using namespace avse::bnact;
+
+extern "C" {
+
+int64_t avse_bnact_workspace_bytes(int64_t N, int64_t C, int64_t S) {
+    if (!shape_ok(N, C, S)) return 0;
+    const Geo g = make_geo(N, C, S, 1);                 // V = 1 has the most row blocks
+    const Geo g4 = make_geo(N, C, S, 4);
+    const int64_t nrb = std::max(g.nrb, g4.nrb);
+    return 4 * (3 * nrb * C * S + 2 * C) + 16;
+}
+
+int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* gamma,
+                   const float* beta, int32_t act, const float* alpha, int32_t alpha_n, int32_t training, float eps,
+                   float momentum, float* running_mean, float* running_var, float* stats, float* y, float* workspace,
+                   avse_stream_t stream) {
+    if (!x || !y || !stats || !workspace || (act == ACT_PRELU && !alpha)) return AVSE_EINVAL;
+    if (!training && (!running_mean || !running_var)) return AVSE_EINVAL;
+    if (!shape_ok(N, C, S) || act < ACT_NONE || act > ACT_PRELU) return AVSE_ESHAPE;
+    if (act == ACT_PRELU && alpha_n != 1 && alpha_n != C) return AVSE_ESHAPE;
+    if (training && N * S < 2) return AVSE_ESHAPE;       // as torch: more than one value per channel
+    const int V = ((C * S) % 4 == 0 && al16(x) && al16(y) && (!res || al16(res)) && al16(workspace)) ? 4 : 1;
+    const Geo g = make_geo(N, C, S, V);
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(g.tiles, g.nrb);
+    if (training) {
+        if (V == 4) hipLaunchKernelGGL(stats_kernel<4>, grid, dim3(THREADS), 0, st, g, x, workspace);
+        else hipLaunchKernelGGL(stats_kernel<1>, grid, dim3(THREADS), 0, st, g, x, workspace);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(stats_finalize, dim3((unsigned)C), dim3(THREADS), 0, st, g, x, workspace, eps, momentum,
+                           running_mean, running_var, stats);
+    } else {
+        hipLaunchKernelGGL(eval_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, (int)C, running_mean,
+                           running_var, eps, stats);
+    }
+    AVSE_CHECK_LAUNCH();
+    dispatch<ApplyK>::run(V, act, res != nullptr, grid, st, g, x, res, (const float*)stats, gamma, beta, alpha,
+                          (int)alpha_n, y);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* dy, const float* stats,
+                   const float* gamma, const float* beta, int32_t act, const float* alpha, int32_t alpha_n,
+                   int32_t training, float* dx, float* dres, float* dgamma, float* dbeta, float* dalpha_c,
+                   float* workspace, avse_stream_t stream) {
+    if (!x || !dy || !stats || !dx || !workspace || (act == ACT_PRELU && (!alpha || !dalpha_c)) || (res && !dres))
+        return AVSE_EINVAL;
+    if (!shape_ok(N, C, S) || act < ACT_NONE || act > ACT_PRELU) return AVSE_ESHAPE;
+    if (act == ACT_PRELU && alpha_n != 1 && alpha_n != C) return AVSE_ESHAPE;
+    const int V = ((C * S) % 4 == 0 && al16(x) && al16(dy) && al16(dx) && (!res || (al16(res) && al16(dres))) &&
+                   al16(workspace)) ? 4 : 1;
+    const Geo g = make_geo(N, C, S, V);
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(g.tiles, g.nrb);
+    float* kbuf = workspace + 3 * (int64_t)g.nrb * g.CS;
+    dispatch<BwdPartK>::run(V, act, res != nullptr, grid, st, g, x, res, dy, stats, gamma, beta, alpha, (int)alpha_n,
+                            workspace, dres);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bwd_finalize, dim3((unsigned)C), dim3(THREADS), 0, st, g, (const float*)workspace, (int)training,
+                       dgamma, dbeta, dalpha_c, kbuf);
+    AVSE_CHECK_LAUNCH();
+    dispatch<BwdApplyK>::run(V, act, res != nullptr, grid, st, g, x, dy, (const float*)dres, stats, gamma, beta, alpha,
+                             (int)alpha_n, (const float*)kbuf, dx);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+}  // extern "C"

@@ -389,6 +389,81 @@ def prelu_bwd(x, a, dy):
     return dx, da.view_as(a)
 
 
+# ------------------------------------------------------------------------ BatchNorm -> [+ res] -> act
+
+ACT_NONE, ACT_RELU, ACT_PRELU = 0, 1, 2
+
+
+def _bn_view(x):
+    """(N, C, S) of x as the bnact kernels read it: contiguous (N, C, *spatial) or channels-last (S = 1)."""
+    if x.is_contiguous():
+        N, C = x.shape[0], x.shape[1]
+        return N, C, x.numel() // max(1, N * C)
+    if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
+        return x.numel() // x.shape[1], x.shape[1], 1
+    if x.dim() == 5 and x.is_contiguous(memory_format=torch.channels_last_3d):
+        return x.numel() // x.shape[1], x.shape[1], 1
+    return None
+
+
+def _same_layout(t, like):
+    if t.stride() == like.stride():
+        return t
+    fmt = (torch.channels_last if like.dim() == 4 else torch.channels_last_3d) if not like.is_contiguous() \
+        else torch.contiguous_format
+    return t.contiguous(memory_format=fmt)
+
+
+def _opt(t):
+    return ptr(t) if t is not None else None
+
+
+def bnact_fwd(x, gamma, beta, running_mean, running_var, training, momentum, eps, act=ACT_NONE, alpha=None, res=None):
+    """act(BatchNorm(x) [+ res]); returns (y, stats (C, 4) = mean hi, mean lo, rstd, 0).  y keeps x's format."""
+    _need_gpu(x)
+    if x.dtype != torch.float32:
+        raise RuntimeError("bnact kernels are fp32")
+    if _bn_view(x) is None:
+        x = x.contiguous()
+    N, C, S = _bn_view(x)
+    if res is not None:
+        res = _same_layout(res.float(), x)
+    y = torch.empty_like(x)
+    stats = torch.empty((C, 4), device=x.device, dtype=torch.float32)
+    L = _lib.lib()
+    ws = torch.empty((L.avse_bnact_workspace_bytes(N, C, S) + 3) // 4, device=x.device, dtype=torch.float32)
+    a = alpha.float().contiguous() if alpha is not None else None
+    check(L.avse_bnact_fwd(N, C, S, ptr(x), _opt(res), _opt(gamma), _opt(beta), int(act), _opt(a),
+                           a.numel() if a is not None else 0, int(bool(training)), float(eps), float(momentum),
+                           _opt(running_mean), _opt(running_var), ptr(stats), ptr(y), ptr(ws), stream_ptr(x.device)),
+          "avse_bnact_fwd")
+    return y, stats
+
+
+def bnact_bwd(x, res, dy, stats, gamma, beta, act, alpha, training):
+    """-> (dx, dres or None, dgamma, dbeta, dalpha (alpha's shape) or None)."""
+    _need_gpu(x, dy, stats)
+    N, C, S = _bn_view(x)
+    dy = _same_layout(dy.float(), x)
+    if res is not None:
+        res = _same_layout(res.float(), x)
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if res is not None else None
+    dgamma = torch.empty((C,), device=x.device, dtype=torch.float32)
+    dbeta = torch.empty((C,), device=x.device, dtype=torch.float32)
+    a = alpha.float().contiguous() if alpha is not None else None
+    dalpha_c = torch.empty((C,), device=x.device, dtype=torch.float32) if a is not None else None
+    L = _lib.lib()
+    ws = torch.empty((L.avse_bnact_workspace_bytes(N, C, S) + 3) // 4, device=x.device, dtype=torch.float32)
+    check(L.avse_bnact_bwd(N, C, S, ptr(x), _opt(res), ptr(dy), ptr(stats), _opt(gamma), _opt(beta), int(act), _opt(a),
+                           a.numel() if a is not None else 0, int(bool(training)), ptr(dx), _opt(dres), ptr(dgamma),
+                           ptr(dbeta), _opt(dalpha_c), ptr(ws), stream_ptr(x.device)), "avse_bnact_bwd")
+    dalpha = None
+    if a is not None:
+        dalpha = (dalpha_c if a.numel() == C else dalpha_c.sum().reshape(1)).view_as(alpha)
+    return dx, dres, dgamma, dbeta, dalpha
+
+
 # ------------------------------------------------------------------------ PReLU -> gLN (avse4)
 
 def prelu_gln_fwd(x, alpha, gamma, beta, eps=1e-8):

@@ -4,7 +4,8 @@ prelu_gln    fused PReLU -> GlobalLayerNorm (avse4 TCN) autograd op
 dwconv1d     depthwise dilated "same" conv1d autograd op (avse4 VisualConv1D)
 dwconv_prelu_gln  the avse4 TCN's dwconv -> PReLU -> gLN as two fused passes each way
 
-PReLU        nn.PReLU(num_parameters): fwd + fused dx / slope-gradient bwd kernels
+PReLU        nn.PReLU(num_parameters): fwd + fused dx / slope-gradient bwd kernels (NCS and channels-last)
+bn_act       act(nn.BatchNorm{1,2,3}d(x) [+ res]) with act None / ReLU / PReLU, two passes each way
 HipLSTM      nn.LSTM(..., num_layers=1, batch_first=True[, bidirectional]) whose recurrence is one HIP launch
              per direction (avse1 FusionNet, avse2 DPRNN)
 LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip front-ends:
@@ -12,6 +13,8 @@ LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip f
              data: no input gradient is needed on the reference path; if one is requested it is
              computed with the library transposed conv).
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -42,6 +45,52 @@ class PReLU(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("PReLU runs on the GPU kernels only")
         return _PReLUFn.apply(x, self.weight)
+
+
+class _BNActFn(torch.autograd.Function):
+    """act(BatchNorm(x) [+ res]) in two HBM passes forward and two backward (csrc/bnact.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, alpha, res, running_mean, running_var, training, momentum, eps, act):
+        if K._bn_view(x) is None:                  # neither contiguous nor channels-last: the layout the kernels read
+            x = x.contiguous()
+        y, stats = K.bnact_fwd(x, gamma, beta, running_mean, running_var, training, momentum, eps, act, alpha, res)
+        ctx.save_for_backward(x, res, stats, gamma, beta, alpha)
+        ctx.act, ctx.training = act, training
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, stats, gamma, beta, alpha = ctx.saved_tensors
+        dx, dres, dgamma, dbeta, dalpha = K.bnact_bwd(x, res, dy, stats, gamma, beta, ctx.act, alpha, ctx.training)
+        return (dx, dgamma if ctx.needs_input_grad[1] else None, dbeta if ctx.needs_input_grad[2] else None,
+                dalpha if ctx.needs_input_grad[3] else None, dres, None, None, None, None, None, None)
+
+
+def bn_act(x, bn, act=None, res=None):
+    """act(bn(x) [+ res]) for an nn.BatchNorm{1,2,3}d `bn` (its parameters, buffers, momentum and eps; running
+    statistics and num_batches_tracked updated in train mode as torch does).  act: None, "relu" or a PReLU module.
+    x: fp32 contiguous or channels-last; the output keeps x's memory format."""
+    if not x.is_cuda:
+        raise RuntimeError("bn_act runs on the GPU kernels only")
+    if os.environ.get("AVSE_BNACT", "1") != "1":            # A/B switch: the library BatchNorm + separate act
+        y = bn(x) if res is None else bn(x) + res
+        return y if act is None else (F.relu(y) if act == "relu" else act(y))
+    training = bn.training or not bn.track_running_stats
+    if bn.training and bn.track_running_stats:
+        if bn.momentum is None:
+            raise NotImplementedError("bn_act: cumulative-average BatchNorm (momentum=None)")
+        bn.num_batches_tracked.add_(1)
+    if act is None:
+        code, alpha = K.ACT_NONE, None
+    elif act == "relu":
+        code, alpha = K.ACT_RELU, None
+    else:
+        code, alpha = K.ACT_PRELU, act.weight
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    return _BNActFn.apply(x.float(), bn.weight, bn.bias, alpha, res, rm, rv, training,
+                          bn.momentum if bn.momentum is not None else 0.0, bn.eps, code)
 
 
 class _LipConv3dFn(torch.autograd.Function):

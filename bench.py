@@ -460,19 +460,41 @@ class Avse4Step:
 from avse_challenge_amd.ddp import Trainer  # noqa: E402  (the data-parallel step; re-exported for tests)
 
 
+class _PlumbingNet(torch.nn.Module):
+    """avse1 AudioFeatNet's module tree (bn0, 5 dilated 5x5 Conv2d + BatchNorm2d + ReLU, 1x1 -> 4) in stock
+    PyTorch ops: the product's version runs its BatchNorms on the HIP kernels, which the CPU test cannot."""
+
+    def __init__(self, filters=64, k=5):
+        super().__init__()
+        self.bn0 = torch.nn.BatchNorm2d(1)
+        for i in range(5):
+            dil = 2 ** i
+            setattr(self, f"conv{i + 1}", torch.nn.Conv2d(1 if i == 0 else filters, filters, k,
+                                                          padding=(k - 1) * dil // 2, dilation=dil))
+            setattr(self, f"bn{i + 1}", torch.nn.BatchNorm2d(filters))
+        self.convf = torch.nn.Conv2d(filters, 4, 1)
+        self.bn_last = torch.nn.BatchNorm2d(4)
+
+    def forward(self, spec):
+        T, Fb = spec.shape[2], spec.shape[3]
+        x = self.bn0(spec)
+        for i in range(1, 6):
+            x = torch.relu(getattr(self, f"bn{i}")(getattr(self, f"conv{i}")(x)))
+        x = torch.relu(self.bn_last(self.convf(x)))
+        return x.permute(0, 2, 1, 3).reshape(-1, T, Fb * 4)
+
+
 class PlumbingStep:
     """--device cpu test hook of the distributed path (launch, bucketed all-reduce, BatchNorm-buffer broadcast,
-    max-over-ranks timing) under gloo: avse1's AudioFeatNet (dilated Conv2d + BatchNorm2d; PyTorch/MIOpen in the
-    product as well) on a reduced spectrogram (B x 1 x 40 x 257) + a 1028 -> 257 sigmoid mask head, L1 loss.
-    Not a throughput workload."""
+    max-over-ranks timing) under gloo: an AudioFeatNet-shaped net (dilated Conv2d + BatchNorm2d) on a reduced
+    spectrogram (B x 1 x 40 x 257) + a 1028 -> 257 sigmoid mask head, L1 loss.  Not a throughput workload."""
     unit_desc = "reduced spectrogram (plumbing test)"
     graph_ok = False
 
     def __init__(self, B, dev, rank, world):
-        from avse_challenge_amd import avse1
         torch.manual_seed(5 + rank)                   # different init per rank: the Trainer broadcasts rank 0's
         self.B = B
-        self.model = torch.nn.ModuleDict({"net": avse1.AudioFeatNet(), "head": torch.nn.Linear(1028, 257)}).to(dev)
+        self.model = torch.nn.ModuleDict({"net": _PlumbingNet(), "head": torch.nn.Linear(1028, 257)}).to(dev)
         self.lr, self.clip = 1e-3, 1.0
         g = torch.Generator().manual_seed(300 + rank)
         self.spec = torch.rand((B, 1, 40, 257), generator=g).to(dev)

@@ -187,6 +187,28 @@ int64_t avse_prelu_nhwc_bwd_workspace_bytes(int64_t R, int64_t C);
 int avse_prelu_nhwc_bwd(int64_t R, int64_t C, int32_t num_params, const float* x, const float* a, const float* dy,
                         float* dx, float* da, float* workspace, avse_stream_t stream);
 
+/* ---------------------------------------------------------------- BatchNorm -> [+ res] -> act ---
+ * y = act(BN(x) [+ res]) with BN over the (N, S) axes of an (N, C, S) row-major view: NCHW / NCDHW
+ * (S = H*W, T*H*W) or channels-last NHWC (N = batch*H*W, S = 1).  act: 0 none, 1 ReLU, 2 PReLU (alpha_n 1 or C).
+ * training != 0: batch statistics (biased variance for the normalisation), running_mean / running_var (may be
+ * null) updated with momentum and the unbiased variance, as nn.BatchNorm{1,2,3}d in train mode; training == 0:
+ * the running statistics.  stats (C, 4) = (mean as a float pair hi + lo, rstd, 0) written by fwd, read by bwd.  gamma / beta may be null
+ * (affine=False).  bwd writes dx, dgamma, dbeta (C, may be null), the per-channel PReLU slope gradient
+ * dalpha_c (C; sum it for a single slope) and, with res, dres (= the gradient of the pre-activation).
+ * Replaces nn.BatchNorm3d/2d + nn.PReLU / F.relu (+ the residual add) of the avse1 lip front-end and ResNet
+ * BasicBlock (/root/reference/baseline/avse1/model.py:29-34, utils/resnet.py:40-67) and of the avse1 audio net
+ * (model.py:181-267).  workspace: avse_bnact_workspace_bytes.
+ */
+int64_t avse_bnact_workspace_bytes(int64_t N, int64_t C, int64_t S);
+int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* gamma,
+                   const float* beta, int32_t act, const float* alpha, int32_t alpha_n, int32_t training, float eps,
+                   float momentum, float* running_mean, float* running_var, float* stats, float* y, float* workspace,
+                   avse_stream_t stream);
+int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* dy, const float* stats,
+                   const float* gamma, const float* beta, int32_t act, const float* alpha, int32_t alpha_n,
+                   int32_t training, float* dx, float* dres, float* dgamma, float* dbeta, float* dalpha_c,
+                   float* workspace, avse_stream_t stream);
+
 /* ---------------------------------------------------------------- PReLU -> gLN (avse4) ----
  * y = gLN(PReLU(x)) of baseline/avse4/model.py:259-266,284-292 (PReLU with one slope; gLN
  * :225-252, EPS inside the sqrt).  x, y: (B, C, K) contiguous; gamma, beta: (C); stats: (B, 2)

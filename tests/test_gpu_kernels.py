@@ -363,6 +363,78 @@ def test_prelu_channels_last_vs_torch(shape, npar):
     close(m.weight.grad, a.grad, 1e-4, 1e-5, "da")
 
 
+# ------------------------------------------------------------------ BatchNorm -> [+ res] -> act (bnact.hip)
+
+BNACT_CASES = [
+    ((4, 64, 10, 12), False, "prelu_c", True, True),     # ResNet bn2 + shortcut -> PReLU (NCHW)
+    ((6, 64, 3, 3), False, "prelu_c", False, True),      # layer4-like 3x3 maps
+    ((2, 16, 5, 7, 7), False, "prelu_c", False, True),   # frontend BatchNorm3d -> PReLU (NCDHW)
+    ((4, 64, 10, 12), True, "relu", False, True),        # audio net BatchNorm2d -> ReLU, channels-last
+    ((3, 4, 9, 11), True, "relu", True, True),           # 4 channels (one 4-wide column per row), + res
+    ((2, 1, 37, 29), False, None, False, True),          # bn0: one channel, no act
+    ((3, 3, 5, 7), False, "prelu_1", True, True),        # odd C*S: scalar path, single slope
+    ((5, 32, 6, 6), False, "prelu_c", True, False),      # eval mode (running statistics)
+    ((4, 8, 50), False, None, False, True),              # BatchNorm1d-shaped
+]
+
+
+@pytest.mark.parametrize("mean,scale", [(30.0, 2.0), (100.0, 0.01)])
+@pytest.mark.parametrize("shape,cl,act,res,training", BNACT_CASES)
+def test_bnact_vs_fp64(shape, cl, act, res, training, mean, scale):
+    """act(BatchNorm(x) [+ res]) through layers.bn_act vs torch fp64 modules: output, every gradient and the
+    running-statistic update (momentum 0.1, unbiased variance).  mean / std up to 1e4 (the mean is carried as
+    a float pair, so the activation mask does not flip on the rounding of the mean)."""
+    from avse_challenge_amd.layers import PReLU, bn_act
+    C = shape[1]
+    bn_cls = {3: torch.nn.BatchNorm1d, 4: torch.nn.BatchNorm2d, 5: torch.nn.BatchNorm3d}[len(shape)]
+    gen = torch.Generator().manual_seed(11)
+    # large-mean input (as raw-pixel Conv3d outputs): the shifted statistics must not cancel
+    # fp32-representable inputs: the reference sees exactly the values the kernels read
+    x = (scale * det_input(shape, 740) + mean).float().double().requires_grad_(True)
+    r = det_input(shape, 741).double().requires_grad_(True) if res else None
+    gy = det_input(shape, 742).double()
+    ref = bn_cls(C).double()
+    with torch.no_grad():
+        ref.weight.copy_(0.5 + torch.rand(C, generator=gen))
+        ref.bias.copy_(0.1 * torch.randn(C, generator=gen))
+        ref.running_mean.copy_(mean + scale * torch.randn(C, generator=gen))
+        ref.running_var.copy_(scale * scale * (1.0 + torch.rand(C, generator=gen)))
+    npar = {"prelu_c": C, "prelu_1": 1}.get(act, 0)
+    a = (0.1 + 0.3 * torch.rand(max(npar, 1), generator=gen)).double().requires_grad_(True)
+    bn = bn_cls(C).to(DEV)
+    bn.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    ref.train(training)
+    bn.train(training)
+    z = ref(x) + (r if res else 0.0)
+    y = torch.relu(z) if act == "relu" else (torch.nn.functional.prelu(z, a) if npar else z)
+    y.backward(gy)
+    m_act = None
+    if npar:
+        m_act = PReLU(npar).to(DEV)
+        with torch.no_grad():
+            m_act.weight.copy_(a.detach().float())
+    elif act == "relu":
+        m_act = "relu"
+    fmt = torch.channels_last if cl else torch.contiguous_format
+    xg = x.detach().float().to(DEV).contiguous(memory_format=fmt).requires_grad_(True)
+    rg = r.detach().float().to(DEV).contiguous(memory_format=fmt).requires_grad_(True) if res else None
+    yg = bn_act(xg, bn, m_act, res=rg)
+    assert yg.stride() == xg.stride()
+    close(yg, y, 2e-5, 1e-5, "y")
+    yg.backward(gy.float().to(DEV).contiguous(memory_format=fmt))
+    gs = float(x.grad.abs().max())
+    close(xg.grad, x.grad, 2e-5 * gs, 1e-4, "dx")
+    if res:
+        close(rg.grad, r.grad, 1e-6, 1e-6, "dres")
+    close(bn.weight.grad, ref.weight.grad, 1e-4 * float(ref.weight.grad.abs().max()), 1e-4, "dgamma")
+    close(bn.bias.grad, ref.bias.grad, 1e-4 * float(ref.bias.grad.abs().max()), 1e-4, "dbeta")
+    if npar:
+        close(m_act.weight.grad, a.grad, 1e-4 * float(a.grad.abs().max()) + 1e-7, 1e-4, "dalpha")
+    close(bn.running_mean, ref.running_mean, 1e-5, 1e-6, "running_mean")
+    close(bn.running_var, ref.running_var, 1e-5, 1e-5, "running_var")
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked)
+
+
 # ------------------------------------------------------------------ flip-by-index (BiMamba v2 backward direction)
 
 @pytest.mark.parametrize("l", [1, 64, 150, 257])
