@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import losses
-from .layers import LipConv3d, _PReLUFn, dwconv1d, dwconv_prelu_gln, prelu_gln
+from .layers import LipConv3d, _PReLUFn, bn_act, dwconv1d, dwconv_prelu_gln, prelu_gln
 
 NORM_MEAN, NORM_STD = 0.4161, 0.1688
 
@@ -216,12 +216,13 @@ class ResNetLayer(nn.Module):
         self.outbnb = nn.BatchNorm2d(cout, **bn)
 
     def forward(self, x):
-        y = self.conv2a(F.relu(self.bn1a(self.conv1a(x))))
+        # BN -> ReLU pairs as fused passes (csrc/bnact.hip); the residual adds precede their BatchNorm here
+        y = self.conv2a(bn_act(self.conv1a(x), self.bn1a, "relu"))
         y = y + (x if self.stride == 1 else self.downsample(x))
         mid = y
-        y = F.relu(self.outbna(y))
-        y = self.conv2b(F.relu(self.bn1b(self.conv1b(y)))) + mid
-        return F.relu(self.outbnb(y))
+        y = bn_act(y, self.outbna, "relu")
+        y = self.conv2b(bn_act(self.conv1b(y), self.bn1b, "relu")) + mid
+        return bn_act(y, self.outbnb, "relu")
 
 
 class ResNet(nn.Module):
@@ -247,7 +248,8 @@ class VisualFrontend(nn.Module):
 
     def forward(self, x):                                   # (B, 1, T, 112, 112) -> (B, T, 512)
         bsz = x.shape[0]
-        y = self.frontend3D((x - NORM_MEAN) / NORM_STD).transpose(1, 2)
+        conv, bn, _, pool = self.frontend3D
+        y = pool(bn_act(conv((x - NORM_MEAN) / NORM_STD), bn, "relu")).transpose(1, 2)
         y = y.reshape(y.shape[0] * y.shape[1], y.shape[2], y.shape[3], y.shape[4])
         return self.resnet(y).reshape(bsz, -1, 512)
 
