@@ -90,6 +90,9 @@ SIGNATURES = {
     "avse_prelu_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "avse_prelu_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_prelu_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_maxpool2d_out_size": (c_i64, [c_i64] * 4),
+    "avse_maxpool2d_fwd": (c_i32, [c_i64] * 9 + [c_vp, c_vp, c_vp, c_vp]),
+    "avse_maxpool2d_bwd": (c_i32, [c_i64] * 9 + [c_vp, c_vp, c_vp, c_vp]),
     "avse_bnact_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "avse_bnact_fwd": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_f32, c_f32,
                                c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

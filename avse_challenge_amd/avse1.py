@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .layers import HipLSTM, LipConv3d, PReLU, bn_act
+from .layers import HipLSTM, LipConv3d, PReLU, bn_act, maxpool3d
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
@@ -140,7 +140,7 @@ class VisualFeatNet(nn.Module):           # model.py:17-58
     def forward(self, lips):              # (B, 3, T, H, W) raw 0..255 float -> (B, T, 512)
         Bn = lips.shape[0]
         conv, bn, act, pool = self.frontend3D
-        x = pool(bn_act(conv(lips), bn, act))
+        x = maxpool3d(bn_act(conv(lips), bn, act), pool)
         Tn, C, H, W = x.shape[2], x.shape[1], x.shape[3], x.shape[4]
         if self.channels_last:            # (B, C, T, H, W) -> (B*T, H, W, C) in memory, viewed as NCHW
             x = x.permute(0, 2, 3, 4, 1).reshape(Bn * Tn, H, W, C).permute(0, 3, 1, 2)

@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import losses
-from .layers import LipConv3d, _PReLUFn, bn_act, dwconv1d, dwconv_prelu_gln, prelu_gln
+from .layers import LipConv3d, _PReLUFn, bn_act, dwconv1d, dwconv_prelu_gln, maxpool3d, prelu_gln
 
 NORM_MEAN, NORM_STD = 0.4161, 0.1688
 
@@ -249,7 +249,7 @@ class VisualFrontend(nn.Module):
     def forward(self, x):                                   # (B, 1, T, 112, 112) -> (B, T, 512)
         bsz = x.shape[0]
         conv, bn, _, pool = self.frontend3D
-        y = pool(bn_act(conv((x - NORM_MEAN) / NORM_STD), bn, "relu")).transpose(1, 2)
+        y = maxpool3d(bn_act(conv((x - NORM_MEAN) / NORM_STD), bn, "relu"), pool).transpose(1, 2)
         y = y.reshape(y.shape[0] * y.shape[1], y.shape[2], y.shape[3], y.shape[4])
         return self.resnet(y).reshape(bsz, -1, 512)
 

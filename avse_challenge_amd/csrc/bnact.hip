@@ -148,34 +148,61 @@ __device__ inline double block_sum_d(double v, double* red) {
     return s;
 }
 
-__global__ __launch_bounds__(THREADS) void stats_finalize(Geo g, const float* __restrict__ x, const float* __restrict__ ws,
-                                                          float eps, float momentum, float* __restrict__ running_mean,
-                                                          float* __restrict__ running_var, float* __restrict__ stats) {
+// Per-channel reduction of the column partials in two launches: chan_partial_kernel splits channel c's
+// nrb * S partial entries over G workgroups (grid (C, G), fp64 sums, one value per workgroup and quantity),
+// then a one-thread-per-channel combine.  (One workgroup per channel left most CUs idle: 64-512 workgroups
+// looping over up to 172800 entries each took ~150 us per call at the avse1 shapes.)
+constexpr int MAXG = 64;
+inline int chan_groups(const Geo& g) {
+    const int64_t cnt = (int64_t)g.nrb * g.S;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(MAXG, (cnt + 2047) / 2048));
+}
+
+template <int NQ>
+__global__ __launch_bounds__(THREADS) void chan_partial_kernel(Geo g, const float* __restrict__ ws,
+                                                               double* __restrict__ fin) {
     __shared__ double red[THREADS / 64];
-    const int c = blockIdx.x;
-    double s1 = 0.0, s2 = 0.0;
+    const int c = blockIdx.x, G = gridDim.y, gi = blockIdx.y;
     const int S = (int)g.S, cnt = g.nrb * S;              // < 2^23: nrb * S <= 4096 * 1024 (make_geo)
-    for (int i = threadIdx.x; i < cnt; i += THREADS) {
-        const int y = i / S, s = i - y * S;
-        s1 += ws[((int64_t)y * 2) * g.CS + (int64_t)c * g.S + s];
-        s2 += ws[((int64_t)y * 2 + 1) * g.CS + (int64_t)c * g.S + s];
+    const int per = (cnt + G - 1) / G, i0 = gi * per, i1 = min(cnt, i0 + per);
+    double acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+    for (int i = i0 + threadIdx.x; i < i1; i += THREADS) {
+        const int y = i / S, sidx = i - y * S;
+        const int64_t col = (int64_t)c * g.S + sidx;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] += ws[((int64_t)y * NQ + q) * g.CS + col];
     }
-    s1 = block_sum_d(s1, red);
-    s2 = block_sum_d(s2, red);
-    if (threadIdx.x == 0) {
-        const double n = (double)g.N * (double)g.S;
-        const double m1 = s1 / n;
-        double var = s2 / n - m1 * m1;
-        if (var < 0.0) var = 0.0;
-        const double mean = (double)x[(int64_t)c * g.S] + m1;
-        const float hi = (float)mean;
-        stats[4 * c] = hi;
-        stats[4 * c + 1] = (float)(mean - (double)hi);
-        stats[4 * c + 2] = (float)(1.0 / sqrt(var + (double)eps));
-        stats[4 * c + 3] = 0.f;
-        if (running_mean) running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
-        if (running_var) running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * var * n / (n - 1.0));
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const double v = block_sum_d(acc[q], red);
+        if (threadIdx.x == 0) fin[((int64_t)c * G + gi) * NQ + q] = v;
     }
+}
+
+__global__ void stats_combine(Geo g, const float* __restrict__ x, const double* __restrict__ fin, int G, float eps,
+                              float momentum, float* __restrict__ running_mean, float* __restrict__ running_var,
+                              float* __restrict__ stats) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= g.C) return;
+    double s1 = 0.0, s2 = 0.0;
+    for (int gi = 0; gi < G; ++gi) {
+        s1 += fin[((int64_t)c * G + gi) * 2];
+        s2 += fin[((int64_t)c * G + gi) * 2 + 1];
+    }
+    const double n = (double)g.N * (double)g.S;
+    const double m1 = s1 / n;
+    double var = s2 / n - m1 * m1;
+    if (var < 0.0) var = 0.0;
+    const double mean = (double)x[(int64_t)c * g.S] + m1;
+    const float hi = (float)mean;
+    stats[4 * c] = hi;
+    stats[4 * c + 1] = (float)(mean - (double)hi);
+    stats[4 * c + 2] = (float)(1.0 / sqrt(var + (double)eps));
+    stats[4 * c + 3] = 0.f;
+    if (running_mean) running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+    if (running_var) running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * var * n / (n - 1.0));
 }
 
 __global__ void eval_stats_kernel(int C, const float* __restrict__ rm, const float* __restrict__ rv, float eps,
@@ -253,31 +280,22 @@ __global__ __launch_bounds__(THREADS) void bwd_partial_kernel(Geo g, const float
     block_partials<V, 3>(g, p, valid, j0, ws);
 }
 
-__global__ __launch_bounds__(THREADS) void bwd_finalize(Geo g, const float* __restrict__ ws, int training,
-                                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                        float* __restrict__ dalpha_c, float* __restrict__ kbuf) {
-    __shared__ double red[THREADS / 64];
-    const int c = blockIdx.x;
+__global__ void bwd_combine(Geo g, const double* __restrict__ fin, int G, int training, float* __restrict__ dgamma,
+                            float* __restrict__ dbeta, float* __restrict__ dalpha_c, float* __restrict__ kbuf) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= g.C) return;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    const int S = (int)g.S, cnt = g.nrb * S;
-    for (int i = threadIdx.x; i < cnt; i += THREADS) {
-        const int y = i / S, s = i - y * S;
-        const int64_t col = (int64_t)c * g.S + s;
-        s0 += ws[((int64_t)y * 3) * g.CS + col];
-        s1 += ws[((int64_t)y * 3 + 1) * g.CS + col];
-        s2 += ws[((int64_t)y * 3 + 2) * g.CS + col];
+    for (int gi = 0; gi < G; ++gi) {
+        s0 += fin[((int64_t)c * G + gi) * 3];
+        s1 += fin[((int64_t)c * G + gi) * 3 + 1];
+        s2 += fin[((int64_t)c * G + gi) * 3 + 2];
     }
-    s0 = block_sum_d(s0, red);
-    s1 = block_sum_d(s1, red);
-    s2 = block_sum_d(s2, red);
-    if (threadIdx.x == 0) {
-        const double n = (double)g.N * (double)g.S;
-        if (dbeta) dbeta[c] = (float)s0;
-        if (dgamma) dgamma[c] = (float)s1;
-        if (dalpha_c) dalpha_c[c] = (float)s2;
-        kbuf[2 * c] = training ? (float)(s0 / n) : 0.f;
-        kbuf[2 * c + 1] = training ? (float)(s1 / n) : 0.f;
-    }
+    const double n = (double)g.N * (double)g.S;
+    if (dbeta) dbeta[c] = (float)s0;
+    if (dgamma) dgamma[c] = (float)s1;
+    if (dalpha_c) dalpha_c[c] = (float)s2;
+    kbuf[2 * c] = training ? (float)(s0 / n) : 0.f;
+    kbuf[2 * c + 1] = training ? (float)(s1 / n) : 0.f;
 }
 
 template <int V, int ACT, bool RES>
@@ -347,6 +365,14 @@ inline bool shape_ok(int64_t N, int64_t C, int64_t S) {
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// fp64 per-channel partials after the column partials and kbuf (the largest nrb of either vector width)
+inline double* fin_ptr(float* workspace, const Geo& g) {
+    const Geo g1 = make_geo(g.N, g.C, g.S, 1), g4 = make_geo(g.N, g.C, g.S, 4);
+    const int64_t nrb = std::max(g1.nrb, g4.nrb);
+    const uintptr_t p = (uintptr_t)(workspace + 3 * nrb * g.CS + 2 * (int64_t)g.C);
+    return reinterpret_cast<double*>((p + 15) & ~(uintptr_t)15);
+}
+
 template <template <int, int, bool> class K>
 struct dispatch {
     template <typename... A>
@@ -376,7 +402,8 @@ int64_t avse_bnact_workspace_bytes(int64_t N, int64_t C, int64_t S) {
     const Geo g = make_geo(N, C, S, 1);                 // V = 1 has the most row blocks
     const Geo g4 = make_geo(N, C, S, 4);
     const int64_t nrb = std::max(g.nrb, g4.nrb);
-    return 4 * (3 * nrb * C * S + 2 * C) + 16;
+    // column partials (3 rows of C*S per row block), kbuf (2 C floats), then 8-aligned fp64 per-channel partials
+    return 4 * (3 * nrb * C * S + 2 * C) + 16 + 8 * (int64_t)C * MAXG * 3;
 }
 
 int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* gamma,
@@ -396,8 +423,13 @@ int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float*
         if (V == 4) hipLaunchKernelGGL(stats_kernel<4>, grid, dim3(THREADS), 0, st, g, x, workspace);
         else hipLaunchKernelGGL(stats_kernel<1>, grid, dim3(THREADS), 0, st, g, x, workspace);
         AVSE_CHECK_LAUNCH();
-        hipLaunchKernelGGL(stats_finalize, dim3((unsigned)C), dim3(THREADS), 0, st, g, x, workspace, eps, momentum,
-                           running_mean, running_var, stats);
+        const int G = chan_groups(g);
+        double* fin = fin_ptr(workspace, g);
+        hipLaunchKernelGGL(chan_partial_kernel<2>, dim3((unsigned)C, G), dim3(THREADS), 0, st, g, (const float*)workspace,
+                           fin);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(stats_combine, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, g, x, (const double*)fin,
+                           G, eps, momentum, running_mean, running_var, stats);
     } else {
         hipLaunchKernelGGL(eval_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, (int)C, running_mean,
                            running_var, eps, stats);
@@ -426,8 +458,13 @@ int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float*
     dispatch<BwdPartK>::run(V, act, res != nullptr, grid, st, g, x, res, dy, stats, gamma, beta, alpha, (int)alpha_n,
                             workspace, dres);
     AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(bwd_finalize, dim3((unsigned)C), dim3(THREADS), 0, st, g, (const float*)workspace, (int)training,
-                       dgamma, dbeta, dalpha_c, kbuf);
+    const int G = chan_groups(g);
+    double* fin = fin_ptr(workspace, g);
+    hipLaunchKernelGGL(chan_partial_kernel<3>, dim3((unsigned)C, G), dim3(THREADS), 0, st, g, (const float*)workspace,
+                       fin);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bwd_combine, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, g, (const double*)fin, G,
+                       (int)training, dgamma, dbeta, dalpha_c, kbuf);
     AVSE_CHECK_LAUNCH();
     dispatch<BwdApplyK>::run(V, act, res != nullptr, grid, st, g, x, dy, (const float*)dres, stats, gamma, beta, alpha,
                              (int)alpha_n, (const float*)kbuf, dx);

@@ -389,6 +389,34 @@ def prelu_bwd(x, a, dy):
     return dx, da.view_as(a)
 
 
+# ------------------------------------------------------------------------ max pooling over (H, W) planes
+
+def maxpool_planes_fwd(x, k, s, p):
+    """x (..., H, W) contiguous fp32, window k = (KH, KW), stride s, padding p -> (y (..., Ho, Wo), idx uint8)."""
+    _need_gpu(x)
+    x = x.float().contiguous()
+    H, W = x.shape[-2], x.shape[-1]
+    planes = x.numel() // (H * W)
+    L = _lib.lib()
+    Ho, Wo = L.avse_maxpool2d_out_size(H, k[0], s[0], p[0]), L.avse_maxpool2d_out_size(W, k[1], s[1], p[1])
+    y = torch.empty(x.shape[:-2] + (Ho, Wo), device=x.device, dtype=torch.float32)
+    idx = torch.empty(y.shape, device=x.device, dtype=torch.uint8)
+    check(L.avse_maxpool2d_fwd(planes, H, W, k[0], k[1], s[0], s[1], p[0], p[1], ptr(x), ptr(y), ptr(idx),
+                               stream_ptr(x.device)), "avse_maxpool2d_fwd")
+    return y, idx
+
+
+def maxpool_planes_bwd(dy, idx, in_shape, k, s, p):
+    _need_gpu(dy, idx)
+    dy = dy.float().contiguous()
+    H, W = in_shape[-2], in_shape[-1]
+    planes = dy.numel() // (dy.shape[-2] * dy.shape[-1])
+    dx = torch.empty(in_shape, device=dy.device, dtype=torch.float32)
+    check(_lib.lib().avse_maxpool2d_bwd(planes, H, W, k[0], k[1], s[0], s[1], p[0], p[1], ptr(dy), ptr(idx), ptr(dx),
+                                        stream_ptr(dy.device)), "avse_maxpool2d_bwd")
+    return dx
+
+
 # ------------------------------------------------------------------------ BatchNorm -> [+ res] -> act
 
 ACT_NONE, ACT_RELU, ACT_PRELU = 0, 1, 2

@@ -6,6 +6,7 @@ dwconv_prelu_gln  the avse4 TCN's dwconv -> PReLU -> gLN as two fused passes eac
 
 PReLU        nn.PReLU(num_parameters): fwd + fused dx / slope-gradient bwd kernels (NCS and channels-last)
 bn_act       act(nn.BatchNorm{1,2,3}d(x) [+ res]) with act None / ReLU / PReLU, two passes each way
+maxpool3d    nn.MaxPool3d((1, k, k), (1, s, s), (0, p, p)) of the lip front-ends (byte argmax, gather backward)
 HipLSTM      nn.LSTM(..., num_layers=1, batch_first=True[, bidirectional]) whose recurrence is one HIP launch
              per direction (avse1 FusionNet, avse2 DPRNN)
 LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip front-ends:
@@ -91,6 +92,34 @@ def bn_act(x, bn, act=None, res=None):
     rv = bn.running_var if bn.track_running_stats else None
     return _BNActFn.apply(x.float(), bn.weight, bn.bias, alpha, res, rm, rv, training,
                           bn.momentum if bn.momentum is not None else 0.0, bn.eps, code)
+
+
+class _MaxPoolPlanesFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, idx = K.maxpool_planes_fwd(x, k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.cfg, ctx.in_shape = (k, s, p), x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        k, s, p = ctx.cfg
+        return K.maxpool_planes_bwd(dy, idx, ctx.in_shape, k, s, p), None, None, None
+
+
+def maxpool3d(x, pool):
+    """nn.MaxPool3d `pool` with a (1, KH, KW) window, stride (1, SH, SW), padding (0, PH, PW) (the lip front-ends)
+    on the HIP plane kernels (csrc/maxpool.hip); any other configuration raises."""
+    k, s, p = (tuple(v) if isinstance(v, (tuple, list)) else (v,) * 3 for v in (pool.kernel_size, pool.stride,
+                                                                                 pool.padding))
+    d = pool.dilation if isinstance(pool.dilation, (tuple, list)) else (pool.dilation,) * 3
+    if k[0] != 1 or s[0] != 1 or p[0] != 0 or tuple(d) != (1, 1, 1) or pool.ceil_mode or pool.return_indices:
+        raise NotImplementedError(f"maxpool3d: only (1, KH, KW) windows, got {pool}")
+    if not x.is_cuda:
+        raise RuntimeError("maxpool3d runs on the GPU kernels only")
+    return _MaxPoolPlanesFn.apply(x, k[1:], s[1:], p[1:])
 
 
 class _LipConv3dFn(torch.autograd.Function):

@@ -209,6 +209,18 @@ int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float*
                    int32_t training, float* dx, float* dres, float* dgamma, float* dbeta, float* dalpha_c,
                    float* workspace, avse_stream_t stream);
 
+/* ---------------------------------------------------------------- max pooling over planes -------
+ * nn.MaxPool3d((1, KH, KW), (1, SH, SW), (0, PH, PW)) of the lip front-ends (avse1 model.py:29-34, avse4
+ * VisualFrontend) on `planes` = B*C*T contiguous H x W planes; y: planes x Ho x Wo, idx: the argmax's position
+ * in its window (kh * KW + kw, one byte), read by bwd.  torch semantics: first maximum, NaN taken; bwd gathers
+ * (deterministic).  KH * KW <= 255, pad <= kernel / 2.
+ */
+int64_t avse_maxpool2d_out_size(int64_t H, int64_t K, int64_t S, int64_t P);
+int avse_maxpool2d_fwd(int64_t planes, int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t SH, int64_t SW, int64_t PH,
+                       int64_t PW, const float* x, float* y, uint8_t* idx, avse_stream_t stream);
+int avse_maxpool2d_bwd(int64_t planes, int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t SH, int64_t SW, int64_t PH,
+                       int64_t PW, const float* dy, const uint8_t* idx, float* dx, avse_stream_t stream);
+
 /* ---------------------------------------------------------------- PReLU -> gLN (avse4) ----
  * y = gLN(PReLU(x)) of baseline/avse4/model.py:259-266,284-292 (PReLU with one slope; gLN
  * :225-252, EPS inside the sqrt).  x, y: (B, C, K) contiguous; gamma, beta: (C); stats: (B, 2)

@@ -435,6 +435,24 @@ def test_bnact_vs_fp64(shape, cl, act, res, training, mean, scale):
     assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked)
 
 
+@pytest.mark.parametrize("shape,k,s,p", [((2, 3, 4, 48, 48), 3, 2, 1), ((1, 2, 3, 7, 9), 3, 2, 1),
+                                         ((2, 2, 2, 10, 11), 2, 2, 0), ((1, 1, 2, 5, 6), 3, 1, 1)])
+def test_maxpool3d_planes_vs_torch(shape, k, s, p):
+    """nn.MaxPool3d((1,k,k), (1,s,s), (0,p,p)) through layers.maxpool3d vs torch fp64 (values with exact ties and a
+    NaN-free plateau: the first maximum wins, as torch); dx vs torch's backward."""
+    from avse_challenge_amd.layers import maxpool3d
+    pool = torch.nn.MaxPool3d((1, k, k), (1, s, s), (0, p, p))
+    x = torch.round(4 * det_input(shape, 750)).double().requires_grad_(True)      # many ties
+    y = pool(x)
+    gy = det_input(y.shape, 751).double()
+    y.backward(gy)
+    xg = x.detach().float().to(DEV).requires_grad_(True)
+    yg = maxpool3d(xg, pool)
+    close(yg, y, 0, 0, "y")
+    yg.backward(gy.float().to(DEV))
+    close(xg.grad, x.grad, 1e-6, 1e-6, "dx")
+
+
 # ------------------------------------------------------------------ flip-by-index (BiMamba v2 backward direction)
 
 @pytest.mark.parametrize("l", [1, 64, 150, 257])

@@ -388,13 +388,15 @@ def test_avse1_branch_streams_equal_serial(monkeypatch, graph):
     graph) gives the loss and every gradient of the single-stream eager step."""
     monkeypatch.setenv("AVSE_AVSE1_STREAMS", "0")
     l0, g0 = _avse1_fb_values(False)
-    monkeypatch.setenv("AVSE_AVSE1_STREAMS", "1")
+    _, g0b = _avse1_fb_values(False)               # run-to-run noise of the same launch order (library split-K
+    monkeypatch.setenv("AVSE_AVSE1_STREAMS", "1")  # weight-gradient convolutions accumulate atomically)
     l1, g1 = _avse1_fb_values(graph)
     assert abs(l1 - l0) <= 1e-6 * abs(l0)
     assert [a is None for a in g0] == [b is None for b in g1]      # tcn_output is unused on the feature path
-    f0 = torch.cat([a.reshape(-1) for a in g0 if a is not None])
-    f1 = torch.cat([b.reshape(-1) for b in g1 if b is not None])
-    assert float((f1 - f0).norm() / f0.norm()) <= 1e-4
+    flat = lambda gs: torch.cat([a.reshape(-1) for a in gs if a is not None])      # noqa: E731
+    f0, f0b, f1 = flat(g0), flat(g0b), flat(g1)
+    noise = float((f0b - f0).norm() / f0.norm())
+    assert float((f1 - f0).norm() / f0.norm()) <= max(1e-4, 3 * noise), noise
     gmax = float(f0.abs().max())
     for i, (a, b) in enumerate(zip(g0, g1)):
         if a is None:
