@@ -4,7 +4,7 @@
 // + 2.3 ms backward per avse1 C2 step (profiles/r02_avse1_*) for ~2.5 GB of traffic.
 //
 // Forward: one thread per output element, the window's first maximum (strict '>'; a NaN is taken, as torch),
-// its position in the window stored as one byte.  Backward: one thread per input element gathers dy from the
+// its position in the window stored as one byte (kh << 4 | kw).  Backward: one thread per input element gathers dy from the
 // (at most ceil(K/S)^2) windows that contain it and chose it -- deterministic, no atomics, every dx written.
 #include "common.h"
 
@@ -13,9 +13,24 @@ namespace maxpool {
 
 constexpr int THREADS = 256;
 
+// n / d for a runtime-invariant d by multiply-high (Granlund-Montgomery round-up): exact for every 32-bit n.
+// The plane / row / column decompositions are the only per-element integer work: hardware-less 32-bit division
+// by a runtime value costs ~25 VALU instructions, which made the gather backward VALU-bound (2.4 ms, 0.10 HBM).
+struct FastDiv {
+    uint32_t d, m, s;
+    void init(uint32_t dv) {
+        d = dv;
+        s = 0;
+        while ((1ull << s) < dv) ++s;
+        m = (uint32_t)(((1ull << 32) * ((1ull << s) - dv)) / dv + 1);
+    }
+    __device__ inline uint32_t div(uint32_t n) const { return (uint32_t)(((uint64_t)__umulhi(n, m) + n) >> s); }
+};
+
 struct P2 {
     int64_t planes;
     int H, W, Ho, Wo, KH, KW, SH, SW, PH, PW;
+    FastDiv fW, fH, fWo, fHo, fSH, fSW;
 };
 
 // I: uint32_t when the element count fits (the index divisions are then 32-bit), else int64_t
@@ -24,16 +39,25 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(P2 p, const float* __restr
                                                       uint8_t* __restrict__ idx) {
     const I n = (I)(p.planes * p.Ho * p.Wo);
     for (I o = (I)blockIdx.x * THREADS + threadIdx.x; o < n; o += (I)gridDim.x * THREADS) {
-        const int wo = (int)(o % (I)p.Wo);
-        const I t = o / (I)p.Wo;
-        const int ho = (int)(t % (I)p.Ho);
-        const int64_t pl = (int64_t)(t / (I)p.Ho);
+        int wo, ho;
+        int64_t pl;
+        if constexpr (sizeof(I) == 4) {
+            const uint32_t t = p.fWo.div(o), q = p.fHo.div(t);
+            wo = (int)(o - t * p.Wo);
+            ho = (int)(t - q * p.Ho);
+            pl = q;
+        } else {
+            wo = (int)(o % p.Wo);
+            const I t = o / p.Wo;
+            ho = (int)(t % p.Ho);
+            pl = t / p.Ho;
+        }
         const float* xp = x + pl * p.H * p.W;
         const int h0 = ho * p.SH - p.PH, w0 = wo * p.SW - p.PW;
         // torch: maxval = -inf, index = first in-bounds element; take v if v > maxval or v is NaN
         const int kh0 = h0 < 0 ? -h0 : 0, kw0 = w0 < 0 ? -w0 : 0;
         float best = -__builtin_inff();
-        int arg = kh0 * p.KW + kw0;
+        int arg = (kh0 << 4) | kw0;                 // (kh, kw) packed in one byte: KH, KW <= 15
         for (int kh = kh0; kh < p.KH; ++kh) {
             const int h = h0 + kh;
             if (h >= p.H) break;
@@ -43,7 +67,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(P2 p, const float* __restr
                 const float v = xp[h * p.W + w];
                 if (v > best || v != v) {
                     best = v;
-                    arg = kh * p.KW + kw;
+                    arg = (kh << 4) | kw;
                 }
             }
         }
@@ -57,21 +81,30 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(P2 p, const float* __restr
                                                       float* __restrict__ dx) {
     const I n = (I)(p.planes * p.H * p.W);
     for (I i = (I)blockIdx.x * THREADS + threadIdx.x; i < n; i += (I)gridDim.x * THREADS) {
-        const int w = (int)(i % (I)p.W);
-        const I t = i / (I)p.W;
-        const int h = (int)(t % (I)p.H);
-        const int64_t pl = (int64_t)(t / (I)p.H);
+        int w, h;
+        int64_t pl;
+        if constexpr (sizeof(I) == 4) {
+            const uint32_t t = p.fW.div(i), q = p.fH.div(t);
+            w = (int)(i - t * p.W);
+            h = (int)(t - q * p.H);
+            pl = q;
+        } else {
+            w = (int)(i % p.W);
+            const I t = i / p.W;
+            h = (int)(t % p.H);
+            pl = t / p.H;
+        }
         // windows ho with ho*SH - PH <= h <= ho*SH - PH + KH - 1
         const int hh = h + p.PH, ww = w + p.PW;
-        const int ho_lo = hh >= p.KH ? (hh - p.KH) / p.SH + 1 : 0, ho_hi = min(p.Ho - 1, hh / p.SH);
-        const int wo_lo = ww >= p.KW ? (ww - p.KW) / p.SW + 1 : 0, wo_hi = min(p.Wo - 1, ww / p.SW);
+        const int ho_lo = hh >= p.KH ? (int)p.fSH.div(hh - p.KH) + 1 : 0, ho_hi = min(p.Ho - 1, (int)p.fSH.div(hh));
+        const int wo_lo = ww >= p.KW ? (int)p.fSW.div(ww - p.KW) + 1 : 0, wo_hi = min(p.Wo - 1, (int)p.fSW.div(ww));
         float g = 0.f;
         const int64_t ob = pl * p.Ho * p.Wo;
         for (int ho = ho_lo; ho <= ho_hi; ++ho)
             for (int wo = wo_lo; wo <= wo_hi; ++wo) {
                 const int64_t o = ob + (int64_t)ho * p.Wo + wo;
                 const int a = idx[o];
-                if (ho * p.SH - p.PH + a / p.KW == h && wo * p.SW - p.PW + a % p.KW == w) g += dy[o];
+                if (ho * p.SH - p.PH + (a >> 4) == h && wo * p.SW - p.PW + (a & 15) == w) g += dy[o];
             }
         dx[i] = g;
     }
@@ -80,12 +113,15 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(P2 p, const float* __restr
 inline bool make(P2& p, int64_t planes, int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t SH, int64_t SW,
                  int64_t PH, int64_t PW) {
     if (planes <= 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || SH <= 0 || SW <= 0 || PH < 0 || PW < 0) return false;
-    if (KH * KW > 255 || 2 * PH > KH || 2 * PW > KW || H > (1 << 20) || W > (1 << 20)) return false;   // torch: pad <= k/2
+    if (KH > 15 || KW > 15 || 2 * PH > KH || 2 * PW > KW || H > (1 << 20) || W > (1 << 20)) return false;  // pad <= k/2
     p.planes = planes; p.H = (int)H; p.W = (int)W; p.KH = (int)KH; p.KW = (int)KW;
     p.SH = (int)SH; p.SW = (int)SW; p.PH = (int)PH; p.PW = (int)PW;
     p.Ho = (int)((H + 2 * PH - KH) / SH + 1);
     p.Wo = (int)((W + 2 * PW - KW) / SW + 1);
-    return p.Ho > 0 && p.Wo > 0;
+    if (p.Ho <= 0 || p.Wo <= 0) return false;
+    p.fW.init((uint32_t)p.W); p.fH.init((uint32_t)p.H); p.fWo.init((uint32_t)p.Wo); p.fHo.init((uint32_t)p.Ho);
+    p.fSH.init((uint32_t)p.SH); p.fSW.init((uint32_t)p.SW);
+    return true;
 }
 
 inline unsigned blocks_for(int64_t n) {

@@ -693,6 +693,34 @@ def roofline_hip(dev):
     add_hbm("avse_dwconv_gln_bwd (C4 TCN fused: x, y1, dy read, dx written)", [16, 512, 3999], "fp32",
             16 * xd.numel(), lambda: K.dwconv_gln_bwd(xd, wd, 128, y1, al, gm, st, gy))
     del xd, gy, y1
+    # avse1 C2 lip front-end: BatchNorm3d -> PReLU (bnact) and the (1,3,3) max pool on (32, 64, 75, 48, 48), and the
+    # ResNet layer4 bn2 + shortcut -> PReLU site on (2400, 512, 3, 3).  Two passes each way: fwd reads x twice and
+    # writes y (12 B/elem, +4 with the residual); bwd reads x, dy twice, writes dx (20 B/elem; with the residual
+    # x, dy, res -> dres then x, dres -> dx: 28 B/elem).  Max pool: x read, y and the byte argmax written (fwd),
+    # dy and argmax read, dx written (bwd): 4 + 4/4 + 1/4 B per input element each way.
+    for tag, shape, res in (("C2 frontend BatchNorm3d -> PReLU", (32, 64, 75, 48, 48), False),
+                            ("C2 ResNet layer4 bn2 + shortcut -> PReLU", (2400, 512, 3, 3), True)):
+        xb = torch.randn(shape, device=dev, generator=g)
+        rb = torch.randn(shape, device=dev, generator=g) if res else None
+        gb = torch.randn(shape, device=dev, generator=g)
+        C = shape[1]
+        gam, bet, alp = torch.ones(C, device=dev), torch.zeros(C, device=dev), torch.full((C,), 0.25, device=dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        _, stt = K.bnact_fwd(xb, gam, bet, rm, rv, True, 0.1, 1e-5, K.ACT_PRELU, alp, rb)
+        ne = xb.numel()
+        add_hbm(f"avse_bnact_fwd ({tag})", list(shape), "fp32", (16 if res else 12) * ne,
+                lambda: K.bnact_fwd(xb, gam, bet, rm, rv, True, 0.1, 1e-5, K.ACT_PRELU, alp, rb))
+        add_hbm(f"avse_bnact_bwd ({tag})", list(shape), "fp32", (28 if res else 20) * ne,
+                lambda: K.bnact_bwd(xb, rb, gb, stt, gam, bet, K.ACT_PRELU, alp, True))
+        if not res:
+            yp, ip = K.maxpool_planes_fwd(xb, (3, 3), (2, 2), (1, 1))
+            add_hbm("avse_maxpool2d_fwd (C2 frontend (1,3,3)/(1,2,2))", list(shape), "fp32", int(5.25 * ne),
+                    lambda: K.maxpool_planes_fwd(xb, (3, 3), (2, 2), (1, 1)))
+            add_hbm("avse_maxpool2d_bwd (C2 frontend (1,3,3)/(1,2,2))", list(shape), "fp32", int(5.25 * ne),
+                    lambda: K.maxpool_planes_bwd(yp, ip, xb.shape, (3, 3), (2, 2), (1, 1)))
+            del yp, ip
+        del xb, rb, gb
+        torch.cuda.empty_cache()
     # projections (MFMA): BiMambaV2's in_proj (_InProj) and out_proj (_BiOutProj) at C3 (fp32) and C5 (bf16)
     for tag, b, l, dt, peak in (("C3", 64, 3999, torch.float32, FP32_PEAK_TFS),
                                 ("C5", 32, 5999, torch.bfloat16, BF16_PEAK_TFS)):

@@ -212,8 +212,8 @@ int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float*
 /* ---------------------------------------------------------------- max pooling over planes -------
  * nn.MaxPool3d((1, KH, KW), (1, SH, SW), (0, PH, PW)) of the lip front-ends (avse1 model.py:29-34, avse4
  * VisualFrontend) on `planes` = B*C*T contiguous H x W planes; y: planes x Ho x Wo, idx: the argmax's position
- * in its window (kh * KW + kw, one byte), read by bwd.  torch semantics: first maximum, NaN taken; bwd gathers
- * (deterministic).  KH * KW <= 255, pad <= kernel / 2.
+ * in its window (kh << 4 | kw, one byte), read by bwd.  torch semantics: first maximum, NaN taken; bwd gathers
+ * (deterministic).  KH, KW <= 15, pad <= kernel / 2.
  */
 int64_t avse_maxpool2d_out_size(int64_t H, int64_t K, int64_t S, int64_t P);
 int avse_maxpool2d_fwd(int64_t planes, int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t SH, int64_t SW, int64_t PH,
