@@ -3,8 +3,10 @@
 Hand-written gfx950 HIP kernels (libavse_hip.so, C ABI in include/avse_hip.h) behind the
 reference's operator / module surfaces:
   kernels        torch wrappers of the C ABI (selective scan, causal conv1d, add+RMSNorm, STFT/iSTFT,
-                 lip Conv3d weight gradient, PReLU, fused PReLU+gLN, depthwise dilated conv1d)
-  layers         autograd modules over those kernels (PReLU, LipConv3d, prelu_gln, dwconv1d)
+                 lip Conv3d weight gradient, PReLU, fused PReLU+gLN, depthwise dilated conv1d, BatchNorm+act,
+                 max pooling, LSTM recurrence)
+  layers         autograd modules over those kernels (PReLU, LipConv3d, prelu_gln, dwconv1d, dwconv_prelu_gln,
+                 bn_act (BatchNorm -> [+res] -> act), maxpool3d, HipLSTM)
   dropin         importable stand-ins for selective_scan_cuda / causal_conv1d(_cuda) / mamba_ssm
   mamba_tasnet   Mamba-TasNet separator (Encoder, MaskNet of BiMamba v2 blocks, Decoder)
   avse1          avse1 AVNet with the STFT front-end / iSTFT back-end on the GPU
