@@ -1,12 +1,16 @@
 """Per-kernel summary of the timed steps only: reads a rocprofv3 kernel_trace.csv, keeps the kernels
 between the two marker kernels bench.py launches when AVSE_PROFILE_MARK=1 (torch.cuda._sleep -> spin_kernel), and
 prints / writes the same columns as rocprofv3's kernel_stats.csv.
-usage: ktrace_window.py TRACE.csv STEPS OUT_STATS.csv"""
+usage: ktrace_window.py TRACE.csv STEPS OUT_STATS.csv [OUT_POST.csv]
+OUT_POST.csv: the same summary for the kernels after the second marker -- bench.py's isolated roofline /
+roofline_hip measurements, which run after the timed steps (their averages are the live numbers' counterpart;
+the whole-run rocprof average mixes them with the in-step calls, which overlap the avse1 lip stream)."""
 import csv
 import sys
 from collections import defaultdict
 
 trace, steps, out = sys.argv[1], float(sys.argv[2]), sys.argv[3]
+post_out = sys.argv[4] if len(sys.argv) > 4 else None
 rows = []
 with open(trace) as f:
     for r in csv.DictReader(f):
@@ -16,15 +20,24 @@ marks = [i for i, r in enumerate(rows) if "spin_kernel" in r[2]]
 if len(marks) < 2:
     sys.exit(f"expected 2 marker kernels, found {len(marks)}")
 win = rows[marks[-2] + 1:marks[-1]]
-agg = defaultdict(list)
-for s, e, n in win:
-    agg[n].append(e - s)
-tot = sum(sum(v) for v in agg.values())
+
+
+def write_stats(sel, path):
+    agg = defaultdict(list)
+    for s, e, n in sel:
+        agg[n].append(e - s)
+    tot = sum(sum(v) for v in agg.values())
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
+        for n, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+            w.writerow([n, len(v), sum(v), sum(v) / len(v), 100.0 * sum(v) / max(1, tot), min(v), max(v)])
+    return tot
+
+
+tot = write_stats(win, out)
 span = win[-1][1] - win[0][0]
-with open(out, "w", newline="") as f:
-    w = csv.writer(f)
-    w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
-    for n, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
-        w.writerow([n, len(v), sum(v), sum(v) / len(v), 100.0 * sum(v) / tot, min(v), max(v)])
+if post_out:
+    write_stats(rows[marks[-1] + 1:], post_out)
 print(f"timed window: {span / 1e6:.2f} ms wall, {tot / 1e6:.2f} ms kernel busy "
       f"({tot / 1e6 / steps:.2f} ms/step over {steps:g} steps, {len(win)} launches)")
