@@ -72,9 +72,8 @@ def _toy_worker(rank, world, port, q, clip):
             for p in st.model.parameters():
                 p.add_(1.0)
     tr = bench.Trainer(st, world, torch.device("cpu"), use_graph=False)
-    for _ in range(3):
-        tr()
-    q.put((rank, [p.detach().numpy().copy() for p in st.model.parameters()]))
+    losses = [float(tr()) for _ in range(3)]
+    q.put((rank, ([p.detach().numpy().copy() for p in st.model.parameters()], losses)))
     dist.destroy_process_group()
 
 
@@ -82,18 +81,20 @@ def _toy_worker(rank, world, port, q, clip):
 def test_trainer_gloo_world2_matches_single_process(clip):
     sys.path.insert(0, REPO)
     import bench
-    res = _spawn(_toy_worker, (clip,))
-    res = {r: [torch.from_numpy(a) for a in v] for r, v in res.items()}
+    out = _spawn(_toy_worker, (clip,))
+    res = {r: [torch.from_numpy(a) for a in v[0]] for r, v in out.items()}
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b)
     # single process on the union batch: mean-of-means == mean over the concatenation (equal batch sizes)
     xs, ys = zip(*(_data(r) for r in range(2)))
     st = _ToyStep(torch.cat(xs), torch.cat(ys), clip)
     tr = bench.Trainer(st, 1, torch.device("cpu"), use_graph=False)
-    for _ in range(3):
-        tr()
+    losses = [float(tr()) for _ in range(3)]
     for a, b in zip(res[0], st.model.parameters()):
         torch.testing.assert_close(a, b.detach(), atol=1e-6, rtol=1e-5)
+    # the returned loss is the mean over ranks on every rank (sync_dist=True, baseline/avse4/model.py:325)
+    assert out[0][1] == out[1][1]
+    torch.testing.assert_close(torch.tensor(out[0][1]), torch.tensor(losses), atol=1e-6, rtol=1e-5)
 
 
 # ------------------------------------------------------------------ BatchNorm model (avse1 AudioFeatNet)
