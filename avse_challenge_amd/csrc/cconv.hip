@@ -135,6 +135,183 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __r
     }
 }
 
+// ---------------------------------------------------------------- vectorised rows (the Mamba layout)
+// Rows with a 4-element-aligned stride (the product's 128-B aligned time stride): thread = 4 consecutive
+// outputs, operands in registers.  The forward reads its own 4-vector and the neighbouring one (the (W-1)-sample
+// halo: the neighbour's own vector, so an L1/L2 hit, not HBM); no LDS, no barriers, one vector load/store per
+// 4 elements instead of the scalar LDS staging of fwd_kernel.  REV = the BiMamba backward direction: the conv
+// runs in reversed time, i.e. over memory positions m with taps x[m .. m+W-1].
+template <typename T> struct v4io;
+template <> struct v4io<float> {
+    __device__ static inline void ld(const float* p, float* v) {
+        const float4 q = *reinterpret_cast<const float4*>(p);
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    }
+    __device__ static inline void st(float* p, const float* v) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+};
+template <> struct v4io<bf16_t> {
+    __device__ static inline void ld(const bf16_t* p, float* v) {
+        const uint2 q = *reinterpret_cast<const uint2*>(p);
+        v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+        v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+    }
+    __device__ static inline void st(bf16_t* p, const float* v) {
+        bf16_t h[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) io<bf16_t>::st(&h[i], v[i]);
+        *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)h[0].x | ((uint32_t)h[1].x << 16),
+                                                  (uint32_t)h[2].x | ((uint32_t)h[3].x << 16));
+    }
+};
+
+template <typename T>
+__device__ inline void ld4z(const T* row, int t, int L, float* v) {   // x[t .. t+3], 0 outside [0, L)
+    if (t >= 0 && t < L) {
+        v4io<T>::ld(row + t, v);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (t + i >= L) v[i] = 0.f;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = 0.f;
+    }
+}
+
+template <typename T>
+__device__ inline void st4(T* row, int t, int L, const float* v) {
+    if (t + 3 < L) {
+        v4io<T>::st(row + t, v);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (t + i < L) io<T>::st(&row[t + i], v[i]);
+    }
+}
+
+__device__ inline float silu_grad(float pre) {
+    const float sgm = sigmoidf_(pre);
+    return sgm * (1.f + pre * (1.f - sgm));
+}
+
+template <typename T, int W, bool SILU, bool HAS_BIAS, bool REV>
+__global__ __launch_bounds__(THREADS) void fwd_vec_kernel(int D, int L, const T* __restrict__ x, int64_t x_bs,
+                                                          int64_t x_ds, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, T* __restrict__ out,
+                                                          int64_t o_bs, int64_t o_ds) {
+    const int row = blockIdx.x;
+    const int b = row / D, d = row % D;
+    const T* xr = x + b * x_bs + (int64_t)d * x_ds;
+    T* orow = out + b * o_bs + (int64_t)d * o_ds;
+    float wk[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
+    const float bv = HAS_BIAS ? bias[d] : 0.f;
+    for (int t = threadIdx.x * 4; t < L; t += THREADS * 4) {
+        float e[8], o[4];
+        if (!REV) {                               // e[i] = x[t - 4 + i]
+            ld4z<T>(xr, t - 4, L, e);
+            ld4z<T>(xr, t, L, e + 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float acc = bv;
+#pragma unroll
+                for (int k = 0; k < W; ++k) acc = fmaf(wk[k], e[4 + j - (W - 1) + k], acc);
+                o[j] = SILU ? siluf_(acc) : acc;
+            }
+        } else {                                  // e[i] = x[t + i]
+            ld4z<T>(xr, t, L, e);
+            ld4z<T>(xr, t + 4, L, e + 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float acc = bv;
+#pragma unroll
+                for (int k = 0; k < W; ++k) acc = fmaf(wk[k], e[j + (W - 1) - k], acc);
+                o[j] = SILU ? siluf_(acc) : acc;
+            }
+        }
+        st4<T>(orow, t, L, o);
+    }
+}
+
+template <typename T, int W, bool SILU, bool HAS_BIAS, bool REV>
+__global__ __launch_bounds__(THREADS) void bwd_vec_kernel(int D, int L, const T* __restrict__ x, int64_t x_bs,
+                                                          int64_t x_ds, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, const T* __restrict__ dout,
+                                                          int64_t g_bs, int64_t g_ds, T* __restrict__ dx,
+                                                          int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws) {
+    __shared__ float sred[THREADS / 64][MAXW + 1];
+    const int row = blockIdx.x;
+    const int b = row / D, d = row % D;
+    const T* xr = x + b * x_bs + (int64_t)d * x_ds;
+    const T* gr = dout + b * g_bs + (int64_t)d * g_ds;
+    T* dxr = dx + b * dx_bs + (int64_t)d * dx_ds;
+    float wk[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
+    const float bv = HAS_BIAS ? bias[d] : 0.f;
+    float dw[W], db = 0.f;
+#pragma unroll
+    for (int k = 0; k < W; ++k) dw[k] = 0.f;
+    for (int t = threadIdx.x * 4; t < L; t += THREADS * 4) {
+        float xs[12], g[8], o[4];                 // xs[i] = x[t - 4 + i]
+        ld4z<T>(xr, t - 4, L, xs);
+        ld4z<T>(xr, t, L, xs + 4);
+        ld4z<T>(xr, t + 4, L, xs + 8);
+        // g[q] = dL/dpre at position p(q) (0 outside [0, L)): !REV p = t + q, REV p = t - 4 + q
+        ld4z<T>(gr, REV ? t - 4 : t, L, g);
+        ld4z<T>(gr, REV ? t : t + 4, L, g + 4);
+        if (SILU) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                float pre = bv;
+#pragma unroll
+                for (int k = 0; k < W; ++k)
+                    pre = fmaf(wk[k], REV ? xs[q + (W - 1) - k] : xs[q + 4 - (W - 1) + k], pre);
+                g[q] *= silu_grad(pre);           // g is already 0 outside the row
+            }
+        }
+        if (!REV) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < W; ++k) acc = fmaf(wk[k], g[j + (W - 1) - k], acc);
+                o[j] = acc;
+                db += g[j];
+#pragma unroll
+                for (int k = 0; k < W; ++k) dw[k] = fmaf(g[j], xs[j + 4 - (W - 1) + k], dw[k]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < W; ++k) acc = fmaf(wk[k], g[j + 4 - (W - 1) + k], acc);
+                o[j] = acc;
+                db += g[4 + j];
+#pragma unroll
+                for (int k = 0; k < W; ++k) dw[k] = fmaf(g[4 + j], xs[4 + j + (W - 1) - k], dw[k]);
+            }
+        }
+        st4<T>(dxr, t, L, o);
+    }
+#pragma unroll
+    for (int k = 0; k <= W; ++k) {
+        float v = (k < W) ? dw[k] : db;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+        if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x <= W) {
+        float v = 0.f;
+        for (int i = 0; i < THREADS / 64; ++i) v += sred[i][threadIdx.x];
+        ws[(int64_t)row * (MAXW + 1) + threadIdx.x] = v;
+    }
+}
+
 // ---------------------------------------------------------------- short rows (L <= SHORT_L)
 // DPMamba's chunked sequences (intra L = 250, inter L = 34) would leave a 2048-wide row tile almost
 // empty: here each wave owns one row, held whole in a wave-private LDS line with its (W-1) halo; a
@@ -279,6 +456,14 @@ using avse::bf16_t;
 
 namespace {
 
+// vectorised-row eligibility: 4-element aligned rows and batch steps, and (for tensors read as 4-vectors) a
+// row stride that covers the last vector (x_ds >= round_up(L, 4), e.g. the 128-B padded time stride)
+template <typename T>
+bool vec_rows(const T* p, int64_t bs, int64_t ds, int64_t L, bool read) {
+    return ((uintptr_t)p % (4 * sizeof(T))) == 0 && bs % 4 == 0 && ds % 4 == 0 && ds > 0 &&
+           (!read || ds >= (L + 3) / 4 * 4);
+}
+
 template <typename T, int W, bool S, bool HB>
 void launch_fwd(int64_t batch, int64_t dim, int64_t seqlen, const T* x, int64_t x_bs, int64_t x_ds, const float* w,
                 const float* bias, T* out, int64_t o_bs, int64_t o_ds, int rev, hipStream_t st) {
@@ -286,7 +471,14 @@ void launch_fwd(int64_t batch, int64_t dim, int64_t seqlen, const T* x, int64_t 
     if (seqlen <= SHORT_L)
         hipLaunchKernelGGL((fwd_short_kernel<T, W, S, HB>), dim3((unsigned)((rows + 3) / 4)), dim3(THREADS), 0, st,
                            rows, (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, out, o_bs, o_ds, rev);
-    else
+    else if (vec_rows<T>(x, x_bs, x_ds, seqlen, true) && vec_rows<T>(out, o_bs, o_ds, seqlen, false)) {
+        if (rev)
+            hipLaunchKernelGGL((fwd_vec_kernel<T, W, S, HB, true>), dim3((unsigned)rows), dim3(THREADS), 0, st,
+                               (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, out, o_bs, o_ds);
+        else
+            hipLaunchKernelGGL((fwd_vec_kernel<T, W, S, HB, false>), dim3((unsigned)rows), dim3(THREADS), 0, st,
+                               (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, out, o_bs, o_ds);
+    } else
         hipLaunchKernelGGL((fwd_kernel<T, W, S, HB>), dim3((unsigned)rows), dim3(THREADS), 0, st, (int)dim,
                            (int)seqlen, x, x_bs, x_ds, w, bias, out, o_bs, o_ds, rev);
 }
@@ -300,7 +492,15 @@ void launch_bwd(int64_t batch, int64_t dim, int64_t seqlen, const T* x, int64_t 
         hipLaunchKernelGGL((bwd_short_kernel<T, W, S, HB>), dim3((unsigned)((rows + 3) / 4)), dim3(THREADS), 0, st,
                            rows, (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws,
                            rev);
-    else
+    else if (vec_rows<T>(x, x_bs, x_ds, seqlen, true) && vec_rows<T>(dout, g_bs, g_ds, seqlen, true) &&
+             vec_rows<T>(dx, dx_bs, dx_ds, seqlen, false)) {
+        if (rev)
+            hipLaunchKernelGGL((bwd_vec_kernel<T, W, S, HB, true>), dim3((unsigned)rows), dim3(THREADS), 0, st,
+                               (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws);
+        else
+            hipLaunchKernelGGL((bwd_vec_kernel<T, W, S, HB, false>), dim3((unsigned)rows), dim3(THREADS), 0, st,
+                               (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws);
+    } else
         hipLaunchKernelGGL((bwd_kernel<T, W, S, HB>), dim3((unsigned)rows), dim3(THREADS), 0, st, (int)dim,
                            (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws, rev);
 }
