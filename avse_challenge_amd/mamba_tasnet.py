@@ -43,6 +43,44 @@ def _wbmm(w, x):
         return torch.bmm(w.expand(x.shape[0], *w.shape), x, out=out)
 
 
+def _padded_full(t):
+    """t's (b, c, Lp) padded storage as a contiguous tensor (the 128-B time stride of kernels.bdl_empty), or None."""
+    if t.dim() != 3 or t.stride(2) != 1 or t.stride(1) < t.size(2) or t.stride(0) != t.size(1) * t.stride(1):
+        return None
+    need = (t.storage_offset() + t.size(0) * t.stride(0)) * t.element_size()
+    if t.untyped_storage().nbytes() < need:
+        return None
+    return t.as_strided((t.size(0), t.size(1), t.stride(1)), t.stride())
+
+
+def _padded_add(a, b):
+    """a + b for two (b, c, l) operands with the same padded time stride: one contiguous vectorised add over the
+    padded storage (the pad columns hold don't-care values), returned as the (b, c, l) view.  torch's add on the
+    strided views takes its generic non-vectorised kernel (~0.75 ms instead of ~0.45 ms per C3 Mamba-L tensor)."""
+    if a is None:
+        return b
+    if b is None:
+        return a
+    if a.stride() == b.stride() and a.dtype == b.dtype:
+        fa, fb = _padded_full(a), _padded_full(b)
+        if fa is not None and fb is not None:
+            return torch.add(fa, fb)[..., :a.size(2)]
+    return a + b
+
+
+class _Fork(torch.autograd.Function):
+    """xz consumed by both BiMamba directions: the two incoming gradients are summed by _padded_add (autograd's own
+    accumulation would take the strided generic kernel)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        return _padded_add(g1, g2)
+
+
 def _bsum_mm(a, bt):
     """sum_b a[b] @ bt[b] for a (b, m, l), bt (b, l, n): the weight gradient of a batched projection.
     The result is fp32 (under bf16 autocast the partials are bf16 GEMM outputs summed in fp32).
@@ -137,7 +175,7 @@ class _BiOutProj(torch.autograd.Function):
     @staticmethod
     @_FWD
     def forward(ctx, f, bk, w):
-        y = f + bk
+        y = _padded_add(f, bk)
         ctx.save_for_backward(y, w)
         wt = 0.5 * w.t()
         return torch.bmm(y.transpose(1, 2), wt.expand(y.shape[0], *wt.shape))
@@ -225,6 +263,7 @@ class BiMambaV2(nn.Module):
 
     def forward(self, h):                                        # (b, l, d_model)
         xz = _InProj.apply(h, self.in_proj.weight)                               # (b, 2di, l), no copy
+        xz, xz_b = _Fork.apply(xz)                # one input per direction; their gradients meet in _padded_add
         A = -torch.exp(self.A_log.float())
         A_b = -torch.exp(self.A_b_log.float())
         side = _direction_stream(xz.device)
@@ -235,15 +274,15 @@ class BiMambaV2(nn.Module):
             main = torch.cuda.current_stream(xz.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                bk = MambaInnerNoOutProj.apply(xz, self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
+                bk = MambaInnerNoOutProj.apply(xz_b, self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
                                                self.dt_proj_b.weight, A_b, self.D_b.float(),
                                                self.dt_proj_b.bias.float(), True)
-            xz.record_stream(side)
+            xz_b.record_stream(side)
             A_b.record_stream(side)
         f = MambaInnerNoOutProj.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
                                       self.dt_proj.weight, A, self.D.float(), self.dt_proj.bias.float())
         if side is None:
-            bk = MambaInnerNoOutProj.apply(xz, self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
+            bk = MambaInnerNoOutProj.apply(xz_b, self.conv1d_b.weight, self.conv1d_b.bias, self.x_proj_b.weight,
                                            self.dt_proj_b.weight, A_b, self.D_b.float(), self.dt_proj_b.bias.float(),
                                            True)
         else:
