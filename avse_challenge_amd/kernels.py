@@ -40,9 +40,14 @@ def bdl_empty(b, d, l, dtype, dev):
 
 
 def _bdl_empty(b, d, l, dtype, dev):
+    """Rows padded to TIME_ALIGN_BYTES when that costs at most 1/16 of the row (Mamba-TasNet: 3999 -> 4000 fp32,
+    5999 -> 6016 bf16; DPMamba intra 250 -> 256); otherwise (DPMamba's 34-step inter rows would grow to 64) to
+    4 elements, the vector width of the causal-conv kernels."""
     if TIME_ALIGN_BYTES > 0:
-        per = max(1, TIME_ALIGN_BYTES // torch.empty((), dtype=dtype).element_size())
+        per = max(1, TIME_ALIGN_BYTES // dtype.itemsize)
         lp = -(-l // per) * per
+        if (lp - l) * 16 > l:
+            lp = -(-l // 4) * 4
         if lp != l:
             return torch.empty((b, d, lp), device=dev, dtype=dtype)[..., :l]
     return torch.empty((b, d, l), device=dev, dtype=dtype)
