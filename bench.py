@@ -770,7 +770,9 @@ def main():
         B = args.batch or 32
         work = AVMambaStep(B, dev, rank, world, args.size)
     elif args.workload == "dpmamba":
-        B = args.batch or 32
+        # B=16: the 16-step scan checkpoints (1 fp32 per step; 64 per 34-step inter row) take ~0.8 GB per utterance
+        # more than round 1's 64-step ones, and B=32 no longer fits 288 GB
+        B = args.batch or 16
         work = DPMambaStep(B, dev, rank, world, args.size)
     elif args.workload == "plumbing":
         B = args.batch or 2
