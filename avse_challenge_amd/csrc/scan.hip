@@ -329,6 +329,8 @@ constexpr int RED = 8;   // adjoint steps buffered per cross-wave dB/dC flush
 
 // keeps the scheduler from hoisting the LDS reads of all 16 unrolled steps (which needs ~10 VGPRs per step
 // on top of the 64 of the state history and spills); the other wave of the SIMD covers the LDS latency
+// (session-3 A/B, tools/gpu_round2z2.sh: masks letting VALU / SALU / transcendentals cross the fence moved the
+// C3 and C5 backward by -0.7 .. +1.8 %: the kernel is VALU-throughput bound, not latency bound)
 #ifndef AVSE_NO_SCHED_FENCE
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
@@ -363,10 +365,11 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
     }
     const float Dv = (HAS_D && dvalid) ? a.D[d] : 0.f;
 
-    // lam = dL/dh carried backwards over the whole row; dAn = dA of the step after the current one
+    // lam = dL/dh carried backwards over the whole row; dAn = lam dA of the step after the current one, so
+    // lam(t) = g(t) C(t) + dAn is one packed FMA (the product is shared with that step's lhp)
     f2_t lam[NP], dAn[NP], dA_acc[NP];
 #pragma unroll
-    for (int p = 0; p < NP; ++p) { lam[p] = f2_t{0.f, 0.f}; dAn[p] = f2_t{1.f, 1.f}; dA_acc[p] = f2_t{0.f, 0.f}; }
+    for (int p = 0; p < NP; ++p) { lam[p] = f2_t{0.f, 0.f}; dAn[p] = f2_t{0.f, 0.f}; dA_acc[p] = f2_t{0.f, 0.f}; }
     float dD_acc = 0.f, dbias_acc = 0.f;
 
     const Tin* u = (const Tin*)a.u;
@@ -522,9 +525,11 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
 #pragma unroll
                     for (int p = 0; p < NP; ++p) {
                         const f2_t hp = (i == 0) ? h0[p] : hist[i > 0 ? i - 1 : 0][p];
-                        lam[p] = pkfma(lam[p], dAn[p], gv2 * cp[p]);
+                        // dAn holds lam(t + 1) dA(t + 1): the product the previous step formed for its lhp
+                        lam[p] = pkfma(gv2, cp[p], dAn[p]);
                         const f2_t dA = exp2_2(dt2 * A2v[p]);
-                        const f2_t lhp = (lam[p] * dA) * hp;
+                        const f2_t ldA = lam[p] * dA;
+                        const f2_t lhp = ldA * hp;
                         ddt2 = pkfma(A2v[p], lhp, ddt2);           // x ln 2 and + u * sum(lam B) once per lane, below
                         dus2 = pkfma(lam[p], bp[p], dus2);
                         dA_acc[p] = pkfma(dt2, lhp, dA_acc[p]);
@@ -533,7 +538,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                         part[2 * p + 1] = pb.y;
                         part[4 + 2 * p] = pc.x;
                         part[4 + 2 * p + 1] = pc.y;
-                        dAn[p] = dA;
+                        dAn[p] = ldA;
                     }
                     const float dus = group_sum<G>(dus2.x + dus2.y);
                     const float ddt = group_sum<G>(ddt2.x + ddt2.y) * AVSE_LN2 + uu * dus;

@@ -272,7 +272,18 @@ def test_avse4_full_train_step_vs_oracle():
         # a scalar PReLU slope's gradient is one sum over B*C*K terms of both signs (cancellation), so its
         # relative error swings with the upstream MIOpen error from process to process (measured 3e-3 ..
         # 5e-2, tools/avse4_grad_diag.py); such 1-element parameters get a 1e-1 floor
-        floor = 1e-1 if p.numel() == 1 else 1e-2
+        # a lip front-end ReLU whose input sits within rounding of 0 flips in one fp32 run and not in another
+        # (MIOpen's solver choice and the BN reduction order both move it): the channel's BN bias / weight
+        # gradient then moves by one term, 1e-2 .. 3e-2 of the gradient's max in every fp32 run alike
+        # (profiles/r02c_avse4_grad_diag.txt, tools/avse4_bn_diag.py: layer4.outbna.bias 2.7e-2 in ours, torch
+        # GPU and torch CPU), so whether ours and torch's flips coincide varies from box to box; the
+        # cosine bar stays 1e-4
+        if p.numel() == 1:
+            floor = 1e-1
+        elif k.startswith("visual_frontend.resnet."):
+            floor = 3e-2
+        else:
+            floor = 1e-2
         assert e_gpu <= max(3 * e_torch, floor) and cos > 1 - 1e-4, (k, e_gpu, e_torch, float(cos))
 
 

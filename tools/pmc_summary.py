@@ -27,6 +27,14 @@ for k, cs in sorted(vals.items()):
         parts = {c: avg.get(c, 0) / wc for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
                                                  "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_LDS")}
         print("   of wave-cycles: " + "  ".join(f"{c[3:]} {v:.2f}" for c, v in parts.items()))
+    if avg.get("GRBM_GUI_ACTIVE") and avg.get("SQ_ACTIVE_INST_VALU"):
+        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles; SQ_ACTIVE_INST_* are quad-cycles summed over waves, and
+        # two waves of one SIMD never issue VALU in the same cycle: VALU-busy share of the 1024 SIMDs' cycles
+        simd_cyc = avg["GRBM_GUI_ACTIVE"] / 8 * 1024
+        print(f"   VALU busy {4 * avg['SQ_ACTIVE_INST_VALU'] / simd_cyc:.2f} of SIMD cycles"
+              + (f", LDS-issue busy {4 * avg.get('SQ_ACTIVE_INST_LDS', 0) / simd_cyc:.2f}" if "SQ_ACTIVE_INST_LDS" in avg else "")
+              + (f", {4 * avg['SQ_ACTIVE_INST_VALU'] / avg['SQ_INSTS_VALU']:.2f} cycles per VALU instruction"
+                 if avg.get("SQ_INSTS_VALU") else ""))
     for c in sorted(avg):
         v = avg[c]
         extra = f"   (x2 = {2 * v / 1e6:.1f} MB)" if c == "FETCH_SIZE" else ""
