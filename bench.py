@@ -570,6 +570,22 @@ def pmc_traffic(phase):
         return None, "no PMC summary"
 
 
+def pmc_valu_busy(fname, kernel_prefix):
+    """(VALU-busy share of SIMD cycles, source) of a scan kernel from a committed tools/pmc_scan.sh summary: the
+    scan kernels are VALU-throughput bound, so this is their compute-roofline fraction."""
+    path = os.path.join(REPO, "profiles", fname)
+    try:
+        lines = open(path).read().split("\n")
+    except OSError:
+        return None, "no PMC summary"
+    for i, ln in enumerate(lines):
+        if ln.startswith(kernel_prefix):
+            for nxt in lines[i + 1:i + 4]:
+                if "VALU busy" in nxt:
+                    return float(nxt.split("VALU busy")[1].split()[0]), f"profiles/{fname} ({kernel_prefix[:48]})"
+    return None, "kernel not in PMC summary"
+
+
 def _with_traffic(roof, phase):
     t, src = pmc_traffic(phase)
     roof["traffic"] = t
@@ -641,7 +657,7 @@ def roofline_hip(dev):
         t.copy_(v)
         return t
 
-    def add_hbm(name, shape, dtype, byts, fn, pmc=None):
+    def add_hbm(name, shape, dtype, byts, fn, pmc=None, valu=None):
         ms = _event_ms(fn)
         ach = byts / (ms * 1e-3) / 1e9
         rec = {"kernel": name, "shape": shape, "dtype": dtype, "bound": "hbm", "algorithmic_bytes_per_launch": byts,
@@ -649,12 +665,16 @@ def roofline_hip(dev):
                "frac": round(ach / HBM_PEAK_GBS, 4)}
         if pmc:
             rec["traffic"], rec["traffic_source"] = pmc_traffic(pmc)
+        if valu:
+            rec["valu_busy"], rec["valu_busy_source"] = pmc_valu_busy(*valu)
         hbm.append(rec)
 
     n = 16
     for tag, b, l, dt in (("C3", 64, 3999, torch.float32), ("C5", 32, 5999, torch.bfloat16)):
         d, s = 1024, (2 if dt == torch.bfloat16 else 4)
         name = "fp32" if s == 4 else "bf16"
+        pmcf = "r02c_scan_pmc_c3_fp32.txt" if tag == "C3" else "r02c_scan_pmc_c5_bf16.txt"
+        ktype = "float" if s == 4 else "avse::bf16_t"
         u, z, dout = rnd(b, d, l, dtype=dt), rnd(b, d, l, dtype=dt), rnd(b, d, l, dtype=dt)
         delta = rnd(b, d, l, dtype=dt, scale=0.1)
         A = -torch.rand(d, n, device=dev, generator=g) - 0.5
@@ -664,13 +684,14 @@ def roofline_hip(dev):
         # training fwd: reads u, delta, z, B, C; writes out_z
         add_hbm(f"avse_scan_fwd ({tag}, training fwd, out_z only)", [b, d, l], name, s * b * l * (4 * d + 2 * n),
                 lambda: K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, return_out=False),
-                "scan" if tag == "C3" else None)
+                "scan" if tag == "C3" else None, (pmcf, f"void avse::scan::fwd_kernel<{ktype},"))
         # bwd as the model calls it (out=None, no out_z recompute): reads u, delta, z, dout, B, C; writes du,
         # ddelta, dz (input dtype) and fp32 dB, dC
         add_hbm(f"avse_scan_bwd ({tag}, as MambaInnerNoOutProj calls it)", [b, d, l], name,
                 b * l * (7 * s * d + 2 * s * n + 2 * 4 * n),
                 lambda: K.selective_scan_bwd(u, delta, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False),
-                "scan_bwd" if tag == "C3" else None)
+                "scan_bwd" if tag == "C3" else None,
+                (pmcf, f"void avse::scan::bwd_kernel<{ktype},"))
         if tag == "C3":
             w, cb = rnd(d, 4, scale=0.5), rnd(d)
             add_hbm("avse_cconv_fwd (C3, k4 + SiLU)", [b, d, l], name, 2 * s * b * d * l,
