@@ -110,6 +110,53 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(P2 p, const float* __restr
     }
 }
 
+// Backward of the lip front-ends' pooling, kernel 3, stride 2, pad 1 (both (H, W) dims): input row h is covered by
+// windows ho in {h/2, h/2 + 1} when h is odd and by ho = h/2 alone when it is even, so one thread owns the 2x2 input
+// block (2m .. 2m+1, 2n .. 2n+1) and reads the 4 candidate windows (m | m+1, n | n+1) once each: 4 dy + 4 argmax
+// byte loads per 4 dx (the generic gather loads up to 4 of each per dx element), float2 row stores.  The per-element
+// sums run over the windows in the generic kernel's (ho, wo) order, so dx is bit-identical to it.
+template <bool EVEN_W>
+__global__ __launch_bounds__(THREADS) void bwd_k3s2p1_kernel(P2 p, FastDiv fNb, FastDiv fMb, uint32_t n_blk,
+                                                             const float* __restrict__ dy,
+                                                             const uint8_t* __restrict__ idx, float* __restrict__ dx) {
+    const int Mb = (p.H + 1) >> 1, Nb = (p.W + 1) >> 1;
+    for (uint32_t i = blockIdx.x * THREADS + threadIdx.x; i < n_blk; i += gridDim.x * THREADS) {
+        const uint32_t t = fNb.div(i), q = fMb.div(t);
+        const int n = (int)(i - t * Nb), m = (int)(t - q * Mb);
+        const int64_t ob = (int64_t)q * p.Ho * p.Wo;
+        float g[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+            const int ho = m + dh;
+            if (ho >= p.Ho) break;
+#pragma unroll
+            for (int dw = 0; dw < 2; ++dw) {
+                const int wo = n + dw;
+                if (wo >= p.Wo) break;
+                const int64_t o = ob + (int64_t)ho * p.Wo + wo;
+                const int a = idx[o];
+                const int di = 2 * dh - 1 + (a >> 4), dj = 2 * dw - 1 + (a & 15);   // target - (2m, 2n)
+                const float v = dy[o];
+                if (di == 0 && dj == 0) g[0][0] += v;
+                if (di == 0 && dj == 1) g[0][1] += v;
+                if (di == 1 && dj == 0) g[1][0] += v;
+                if (di == 1 && dj == 1) g[1][1] += v;
+            }
+        }
+        float* xp = dx + (int64_t)q * p.H * p.W + (int64_t)(2 * m) * p.W + 2 * n;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            if (2 * m + r >= p.H) break;
+            if (EVEN_W) {
+                *reinterpret_cast<float2*>(xp + r * p.W) = make_float2(g[r][0], g[r][1]);
+            } else {
+                xp[r * p.W] = g[r][0];
+                if (2 * n + 1 < p.W) xp[r * p.W + 1] = g[r][1];
+            }
+        }
+    }
+}
+
 inline bool make(P2& p, int64_t planes, int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t SH, int64_t SW,
                  int64_t PH, int64_t PW) {
     if (planes <= 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || SH <= 0 || SW <= 0 || PH < 0 || PW < 0) return false;
@@ -159,7 +206,19 @@ int avse_maxpool2d_bwd(int64_t planes, int64_t H, int64_t W, int64_t KH, int64_t
     P2 p;
     if (!make(p, planes, H, W, KH, KW, SH, SW, PH, PW)) return AVSE_ESHAPE;
     const int64_t n = p.planes * p.H * p.W;
-    if (n < (1LL << 31))
+    const bool k3s2p1 = p.KH == 3 && p.KW == 3 && p.SH == 2 && p.SW == 2 && p.PH == 1 && p.PW == 1;
+    const int64_t nb = p.planes * ((p.H + 1) / 2) * ((p.W + 1) / 2);
+    if (k3s2p1 && n < (1LL << 31) && ((uintptr_t)dx & 7) == 0) {
+        FastDiv fNb, fMb;
+        fNb.init((uint32_t)((p.W + 1) / 2));
+        fMb.init((uint32_t)((p.H + 1) / 2));
+        if (p.W % 2 == 0)
+            hipLaunchKernelGGL(bwd_k3s2p1_kernel<true>, dim3(blocks_for(nb)), dim3(THREADS), 0, (hipStream_t)stream, p,
+                               fNb, fMb, (uint32_t)nb, dy, idx, dx);
+        else
+            hipLaunchKernelGGL(bwd_k3s2p1_kernel<false>, dim3(blocks_for(nb)), dim3(THREADS), 0, (hipStream_t)stream, p,
+                               fNb, fMb, (uint32_t)nb, dy, idx, dx);
+    } else if (n < (1LL << 31))
         hipLaunchKernelGGL(bwd_kernel<uint32_t>, dim3(blocks_for(n)), dim3(THREADS), 0, (hipStream_t)stream, p, dy, idx, dx);
     else
         hipLaunchKernelGGL(bwd_kernel<int64_t>, dim3(blocks_for(n)), dim3(THREADS), 0, (hipStream_t)stream, p, dy, idx, dx);
