@@ -110,6 +110,56 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(P2 p, const float* __restr
     }
 }
 
+// Forward of the same pooling when W % 4 == 0: one thread makes two horizontally adjacent outputs (2wp, 2wp + 1),
+// whose windows span input columns 4wp - 1 .. 4wp + 3 of three rows: per row one float4 (4wp .. 4wp + 3) and one
+// scalar (4wp - 1) instead of 6 scalar loads; y as float2, the two argmax bytes as one 16-bit store.  The scan order
+// and the comparison (first maximum, a NaN taken) are the generic kernel's, so y and idx are bit-identical to it.
+__global__ __launch_bounds__(THREADS) void fwd_k3s2p1_w4_kernel(P2 p, FastDiv fPb, FastDiv fHo, uint32_t n_pair,
+                                                                const float* __restrict__ x, float* __restrict__ y,
+                                                                uint8_t* __restrict__ idx) {
+    const int Pb = p.Wo >> 1;
+    for (uint32_t i = blockIdx.x * THREADS + threadIdx.x; i < n_pair; i += gridDim.x * THREADS) {
+        const uint32_t t = fPb.div(i), q = fHo.div(t);
+        const int wp = (int)(i - t * Pb), ho = (int)(t - q * p.Ho);
+        const float* xp = x + (int64_t)q * p.H * p.W + 4 * wp;
+        float v[3][5];
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const int h = 2 * ho - 1 + kh;
+            const bool ok = h >= 0 && h < p.H;
+            const float4 c = ok ? *reinterpret_cast<const float4*>(xp + (int64_t)h * p.W) : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[kh][0] = (ok && wp > 0) ? xp[(int64_t)h * p.W - 1] : 0.f;
+            v[kh][1] = c.x; v[kh][2] = c.y; v[kh][3] = c.z; v[kh][4] = c.w;
+        }
+        const int kh0 = ho == 0 ? 1 : 0;
+        const int hmax = min(3, p.H - (2 * ho - 1));          // rows past the input's end
+        float best[2];
+        int arg[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int kw0 = (wp == 0 && j == 0) ? 1 : 0;
+            best[j] = -__builtin_inff();
+            arg[j] = (kh0 << 4) | kw0;
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) {
+                if (kh < kh0 || kh >= hmax) continue;
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    if (kw < kw0) continue;
+                    const float e = v[kh][2 * j + kw];
+                    if (e > best[j] || e != e) {
+                        best[j] = e;
+                        arg[j] = (kh << 4) | kw;
+                    }
+                }
+            }
+        }
+        const int64_t o = (int64_t)q * p.Ho * p.Wo + (int64_t)ho * p.Wo + 2 * wp;
+        *reinterpret_cast<float2*>(y + o) = make_float2(best[0], best[1]);
+        *reinterpret_cast<uint16_t*>(idx + o) = (uint16_t)(arg[0] | (arg[1] << 8));
+    }
+}
+
 // Backward of the lip front-ends' pooling, kernel 3, stride 2, pad 1 (both (H, W) dims): input row h is covered by
 // windows ho in {h/2, h/2 + 1} when h is odd and by ho = h/2 alone when it is even, so one thread owns the 2x2 input
 // block (2m .. 2m+1, 2n .. 2n+1) and reads the 4 candidate windows (m | m+1, n | n+1) once each: 4 dy + 4 argmax
@@ -191,8 +241,16 @@ int avse_maxpool2d_fwd(int64_t planes, int64_t H, int64_t W, int64_t KH, int64_t
     P2 p;
     if (!make(p, planes, H, W, KH, KW, SH, SW, PH, PW)) return AVSE_ESHAPE;
     const int64_t n = p.planes * p.Ho * p.Wo;
-    // 32-bit index math needs the input count to fit too (the loop's last increment stays below 2^32)
-    if (p.planes * p.H * p.W < (1LL << 31))
+    const bool k3s2p1 = p.KH == 3 && p.KW == 3 && p.SH == 2 && p.SW == 2 && p.PH == 1 && p.PW == 1;
+    if (k3s2p1 && p.W % 4 == 0 && p.planes * p.H * p.W < (1LL << 31) && ((uintptr_t)x & 15) == 0 &&
+        ((uintptr_t)y & 7) == 0 && ((uintptr_t)idx & 1) == 0) {
+        FastDiv fPb, fHo;
+        fPb.init((uint32_t)(p.Wo / 2));
+        fHo.init((uint32_t)p.Ho);
+        const int64_t np = n / 2;
+        hipLaunchKernelGGL(fwd_k3s2p1_w4_kernel, dim3(blocks_for(np)), dim3(THREADS), 0, (hipStream_t)stream, p, fPb,
+                           fHo, (uint32_t)np, x, y, idx);
+    } else if (p.planes * p.H * p.W < (1LL << 31))   // 32-bit index math needs the input count to fit too
         hipLaunchKernelGGL(fwd_kernel<uint32_t>, dim3(blocks_for(n)), dim3(THREADS), 0, (hipStream_t)stream, p, x, y, idx);
     else
         hipLaunchKernelGGL(fwd_kernel<int64_t>, dim3(blocks_for(n)), dim3(THREADS), 0, (hipStream_t)stream, p, x, y, idx);

@@ -437,7 +437,8 @@ def test_bnact_vs_fp64(shape, cl, act, res, training, mean, scale):
 
 @pytest.mark.parametrize("shape,k,s,p", [((2, 3, 4, 48, 48), 3, 2, 1), ((1, 2, 3, 7, 9), 3, 2, 1),
                                          ((2, 2, 2, 10, 11), 2, 2, 0), ((1, 1, 2, 5, 6), 3, 1, 1),
-                                         ((1, 2, 3, 9, 10), 3, 2, 1), ((1, 1, 1, 1, 2), 3, 2, 1)])
+                                         ((1, 2, 3, 9, 10), 3, 2, 1), ((1, 1, 1, 1, 2), 3, 2, 1),
+                                         ((1, 2, 2, 7, 8), 3, 2, 1), ((1, 1, 1, 1, 4), 3, 2, 1)])
 def test_maxpool3d_planes_vs_torch(shape, k, s, p):
     """nn.MaxPool3d((1,k,k), (1,s,s), (0,p,p)) through layers.maxpool3d vs torch fp64 (values with exact ties and a
     NaN-free plateau: the first maximum wins, as torch); dx vs torch's backward."""
