@@ -122,11 +122,32 @@ def maxpool3d(x, pool):
     return _MaxPoolPlanesFn.apply(x, k[1:], s[1:], p[1:])
 
 
+def _conv3d_fwd_folded(x, w, padding):
+    """Conv3d with time stride 1 as one Conv2d over frames: the KT time taps fold into the input channels
+    (x_unf[b*T + t, ci*KT + kt] = x_pad[b, ci, t + kt], plane copies), the weight (Cout, Cin, KT, KH, KW) is then
+    (Cout, Cin*KT, KH, KW) as it lies, and the (B*T, Cout, Ho, Wo) result is permuted back to (B, Cout, T, Ho, Wo).
+    MIOpen runs this 2-D shape (Winograd f3x2, find-db record) in 7.1 ms against 8.6 ms for its 3-D path at the avse1
+    C2 shape, copies included (tools/conv3d_fold_probe.py; AVSE_CONV3D_FOLD=0 restores F.conv3d)."""
+    B, Cin, T, H, W = x.shape
+    Co, _, KT, KH, KW = w.shape
+    PT, PH, PW = padding
+    xp = F.pad(x, (0, 0, 0, 0, PT, PT))
+    Tn = T + 2 * PT - KT + 1
+    xu = xp.unfold(2, KT, 1)                                   # (B, Cin, Tn, H, W, KT)
+    xu = xu.permute(0, 2, 1, 5, 3, 4).reshape(B * Tn, Cin * KT, H, W)
+    y = F.conv2d(xu, w.reshape(Co, Cin * KT, KH, KW), None, (2, 2), (PH, PW))
+    return y.view(B, Tn, Co, y.shape[-2], y.shape[-1]).transpose(1, 2).contiguous()
+
+
 class _LipConv3dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, padding):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.padding = stride, padding
+        # the avse1 front-end (Cin = 3) only: the Cin = 1 front-ends of avse2 / avse4 fold to a 5-channel Conv2d
+        # without a find-db record (a find pass over the avse4 step did not finish in 400 s): they keep conv3d
+        if os.environ.get("AVSE_CONV3D_FOLD", "1") == "1" and tuple(stride) == (1, 2, 2) and x.shape[1] == 3:
+            return _conv3d_fwd_folded(x, w, padding)
         return F.conv3d(x, w, None, stride, padding)
 
     @staticmethod
