@@ -28,6 +28,27 @@ os.environ.setdefault("MIOPEN_USER_DB_PATH", MIOPEN_DB)     # read by MIOpen at 
 # arguments: reduction results land in each other's buffers (tools/avse1_graph_diag4.py; loss -1.0 instead of
 # 0.34).  With the capture off every replay matches the eager step.  Read at HIP runtime init, i.e. at the
 # first GPU call, which comes after this import in every entry point (bench.py, tests, smoke()).
+_PRESET = os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE")
 os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
+
+def _graph_capture_safe():
+    """False when the HIP runtime did (or will) start with graph packet capture on: the variable was set to
+    something other than "0" by the caller, or a host program initialised the GPU before importing this package
+    (then the setdefault above came too late).  ddp.Trainer.capture() then keeps the step eager."""
+    import sys
+    import warnings
+    if _PRESET is not None and _PRESET != "0":
+        warnings.warn("DEBUG_CLR_GRAPH_PACKET_CAPTURE is not 0: HIP-graph replay of the train steps is disabled")
+        return False
+    torch = sys.modules.get("torch")
+    if _PRESET is None and torch is not None and torch.cuda.is_initialized():
+        warnings.warn("the GPU was initialised before importing avse_challenge_amd, so DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 "
+                      "came too late: HIP-graph replay of the train steps is disabled (import the package first)")
+        return False
+    return True
+
+
+GRAPH_CAPTURE_SAFE = _graph_capture_safe()
 
 __version__ = "0.1.0"

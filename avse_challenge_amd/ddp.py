@@ -7,7 +7,12 @@ buffer instead of DDP's reducer:
     buckets of ~``bucket_mb`` in reverse registration order (the order backward produces gradients);
   * a post-accumulate-grad hook per parameter counts arrivals; the moment a bucket is complete its
     all-reduce is launched asynchronously (RCCL runs it on its own stream after an event wait on the
-    stream that produced the gradients), so the exchange overlaps the rest of the backward;
+    current stream), so the exchange overlaps the rest of the backward; each hook records an event on the
+    stream that accumulated its gradient, and the launch first makes the current stream wait for the events
+    of every other stream in the bucket (the avse1 lip branch and the BiMamba reverse direction run their
+    backward on a side stream, so one bucket can hold gradients written by two streams);
+  * a parameter that got no gradient on the first step (its bucket is sized without it) and gets one later
+    raises, as DDP without find_unused_parameters does, instead of going un-averaged;
   * after backward the remaining buckets (parameters without a gradient this step) are launched, the
     current stream waits for every collective, and the sum is scaled by 1/world (mean, as DDP);
   * DDP's ``broadcast_buffers=True``: rank 0's buffers (BatchNorm running stats, num_batches_tracked) are
@@ -78,7 +83,9 @@ class Trainer:
             self._close_bucket(cur, lo, hi)
         self.expected = [len(ps) for ps in self.bucket_params]
         self.seen = [False] * len(ranges)
+        self.used = [True] * len(ranges)
         self.first_step = True
+        self._events = {}
 
     def _close_bucket(self, idx, lo, hi):
         for i in idx:
@@ -90,19 +97,42 @@ class Trainer:
         self.ready = [0] * len(self.bucket_range)
         self.launched = [False] * len(self.bucket_range)
         self.works = []
+        # per bucket: the streams its gradients were accumulated on this step, each with an event recorded after
+        # the latest of them (the avse1 lip branch and the BiMamba reverse direction run their backward on a side
+        # stream, so one bucket can hold gradients of two streams)
+        self.bucket_streams = [{} for _ in self.bucket_range]
         self._armed = True
 
     def _grad_ready(self, i, _param):
         if not self._armed:
             return
+        if not self.first_step and not self.used[i]:
+            # its bucket was sized on the first step without it and may already be reduced: DDP without
+            # find_unused_parameters raises here too, instead of leaving this gradient un-averaged
+            raise RuntimeError(f"parameter {i} received a gradient after getting none on the first step; its "
+                               "bucket's all-reduce may already have been launched")
         self.seen[i] = True
         b = self.bucket_of[i]
+        if self.dev.type == "cuda":
+            s = torch.cuda.current_stream(self.dev)     # autograd runs the hook on the stream that accumulated
+            ev = self._events.get((b, s.stream_id))
+            if ev is None:
+                ev = self._events[(b, s.stream_id)] = torch.cuda.Event()
+            ev.record(s)
+            self.bucket_streams[b][s.stream_id] = ev
         self.ready[b] += 1
         if not self.first_step and self.ready[b] == self.expected[b]:
             self._launch(b)
 
     def _launch(self, b):
         lo, hi = self.bucket_range[b]
+        if self.dev.type == "cuda":
+            # the collective is ordered after the CURRENT stream only: make that stream wait for every other
+            # stream that wrote a gradient of this bucket
+            cur = torch.cuda.current_stream(self.dev)
+            for sid, ev in self.bucket_streams[b].items():
+                if sid != cur.stream_id:
+                    cur.wait_event(ev)
         self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
         self.launched[b] = True
 
@@ -123,6 +153,7 @@ class Trainer:
             self.loss.div_(self.world)
         if self.first_step:
             self.expected = [sum(self.seen[i] for i in ps) for ps in self.bucket_params]
+            self.used = list(self.seen)
             self.first_step = False
 
     @property
@@ -168,6 +199,10 @@ class Trainer:
         """Capture after eager warm-up (lazy MIOpen / hipBLASLt / Adam-state init done). world > 1: the
         optimizer step only (the forward/backward launches its collectives from autograd hooks)."""
         if not self.use_graph:
+            return
+        from . import GRAPH_CAPTURE_SAFE
+        if not GRAPH_CAPTURE_SAFE:          # replays could run kernels with another node's arguments (__init__.py)
+            self.use_graph = False
             return
         torch.cuda.synchronize()
         # hand the eager warm-up's cached blocks back: the graphs allocate from a private pool, which cannot reuse

@@ -253,10 +253,12 @@ class _LSTMDirFn(torch.autograd.Function):
         h, c, gates = K.lstm_fwd(gx, w_hh, reverse=reverse)
         ctx.save_for_backward(x, w_ih, w_hh, h, c, gates)
         ctx.reverse = reverse
-        return h
+        c_n = (c[:, 0] if reverse else c[:, -1]).clone()        # final cell state in the direction's time order
+        ctx.mark_non_differentiable(c_n)
+        return h, c_n
 
     @staticmethod
-    def backward(ctx, dh):
+    def backward(ctx, dh, _dc_n):
         x, w_ih, w_hh, h, c, gates = ctx.saved_tensors
         Bn, T, I = x.shape
         H = w_hh.shape[1]
@@ -291,10 +293,14 @@ class HipLSTM(nn.LSTM):
         if not x.is_cuda:
             raise RuntimeError("HipLSTM runs on the GPU kernels only")
         x = x.float()
-        outs = [_LSTMDirFn.apply(x, self.weight_ih_l0, self.weight_hh_l0, self.bias_ih_l0, self.bias_hh_l0, False)]
+        dirs = [_LSTMDirFn.apply(x, self.weight_ih_l0, self.weight_hh_l0, self.bias_ih_l0, self.bias_hh_l0, False)]
         if self.bidirectional:
-            outs.append(_LSTMDirFn.apply(x, self.weight_ih_l0_reverse, self.weight_hh_l0_reverse,
+            dirs.append(_LSTMDirFn.apply(x, self.weight_ih_l0_reverse, self.weight_hh_l0_reverse,
                                          self.bias_ih_l0_reverse, self.bias_hh_l0_reverse, True))
+        outs = [h for h, _ in dirs]
         out = outs[0] if len(outs) == 1 else torch.cat(outs, dim=-1)
+        # nn.LSTM's (h_n, c_n): (num_directions, B, H), forward direction's last step, reverse direction's first;
+        # h_n carries gradients, c_n does not (no reference caller reads either: model.py:94, avse2 dnn.py)
         h_n = torch.stack([outs[0][:, -1]] + ([outs[1][:, 0]] if len(outs) > 1 else []))
-        return out, (h_n, None)
+        c_n = torch.stack([c for _, c in dirs])
+        return out, (h_n, c_n)

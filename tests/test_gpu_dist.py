@@ -1,0 +1,136 @@
+"""Two data-parallel ranks on ONE GPU (gloo on CUDA tensors, both ranks on cuda:0): the hook-launched bucket
+all-reduce of avse_challenge_amd.ddp.Trainer must wait for EVERY stream that wrote a bucket's gradients.
+
+The avse1 step runs its lip branch (forward and backward) on a side stream and Mamba-TasNet at B < 48 runs the
+BiMamba reverse direction on one, so single buckets hold gradients of two streams (ddp.py:_launch).
+Gloo's CUDA all-reduce, like RCCL's, orders itself after the current stream only.  Each rank records, on the
+second step (every bucket launched from a hook during the backward), the weights the step started from and the
+summed gradient the collectives produced; it then recomputes both shards' gradients from those weights in one
+process on one stream, eagerly, and the two must agree.  A bucket reduced before its side-stream gradients
+landed would be O(1) off; library run-to-run noise (split-K weight-gradient atomics) is ~1e-6 of the norm.
+Reference semantics: Lightning DDP, baseline/avse4/train.py:28-42, conf/train.yaml:16-18; SpeechBrain DDP,
+Mamba-TasNet/train_wsj0mix.py:160,718."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _make(workload, rank, world):
+    import bench
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(7)                                  # same init on both ranks (rank 0's is broadcast anyway)
+    if workload == "avse1":
+        st = bench.Avse1Step(2, dev, rank, world, 64)
+    else:
+        st = bench.MambaStep(2, dev, rank, world, "XS")
+    for m in st.model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    return st
+
+
+def _worker(rank, world, port, q, workload, bucket_mb):
+    try:
+        sys.path.insert(0, REPO)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        os.environ["AVSE_AVSE1_STREAMS"] = "1"
+        os.environ["AVSE_BIMAMBA_STREAMS"] = "1"
+        import bench  # noqa: F401  (imports the package before the GPU is touched)
+        import torch.distributed as dist
+        from avse_challenge_amd.ddp import _dense
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        st = _make(workload, rank, world)
+        tr = bench.Trainer(st, world, torch.device("cuda", 0), use_graph=False, bucket_mb=bucket_mb)
+        rec = {}
+        orig_opt, orig_launch = tr._opt, tr._launch
+        hook_launches = []
+
+        def spy_launch(b):
+            hook_launches.append(tr._armed)
+            orig_launch(b)
+
+        def spy_opt():
+            torch.cuda.synchronize()
+            rec["grad_sum"] = tr.flat.detach().clone().cpu()
+            rec["weights"] = [p.detach().clone().cpu() for p in tr.params]
+            orig_opt()
+
+        tr._opt, tr._launch = spy_opt, spy_launch
+        tr()                                              # first step: learns which parameters get gradients
+        hook_launches.clear()
+        tr()                                              # second step: every bucket launched from a hook
+        torch.cuda.synchronize()
+        n_buckets = tr.n_buckets
+        in_hooks = sum(hook_launches)
+        dist.destroy_process_group()
+
+        # single-process, single-stream reference on the same weights: sum of both shards' gradients
+        os.environ["AVSE_AVSE1_STREAMS"] = "0"
+        os.environ["AVSE_BIMAMBA_STREAMS"] = "0"
+        ref_sum = None
+        for shard in range(world):
+            ref = _make(workload, shard, world)
+            params = [p for p in ref.model.parameters() if p.requires_grad]
+            with torch.no_grad():
+                for p, w in zip(params, rec["weights"]):
+                    p.copy_(w.to(p.device))
+            grads = torch.autograd.grad(ref.loss(), params, allow_unused=True)
+            flat = torch.cat([(torch.zeros_like(p) if g is None else g).reshape(-1) for p, g in zip(params, grads)])
+            ref_sum = flat if ref_sum is None else ref_sum + flat
+        # the Trainer's flat buffer holds each gradient with its parameter's strides: compare per parameter
+        errs, off = [], 0
+        got = rec["grad_sum"]
+        for p, w in zip(params, rec["weights"]):
+            n = p.numel()
+            seg = got[off:off + n].as_strided(p.shape, p.stride()) if _dense(p) else got[off:off + n].view(p.shape)
+            r = ref_sum[off:off + n].view(p.shape).cpu()
+            errs.append((float((seg - r).norm()), float(r.norm())))
+            off += n
+        tot = (float((torch.tensor([e for e, _ in errs]) ** 2).sum().sqrt()),
+               float((torch.tensor([r for _, r in errs]) ** 2).sum().sqrt()))
+        q.put((rank, {"errs": errs, "total": tot, "n_buckets": n_buckets, "in_hooks": in_hooks}))
+    except Exception as e:                                # surface the failure instead of a queue timeout
+        import traceback
+        q.put((rank, {"error": repr(e) + "\n" + traceback.format_exc()}))
+        raise
+
+
+@pytest.mark.parametrize("workload", ["avse1", "mamba"])
+def test_two_ranks_one_gpu_side_stream_buckets(workload):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, workload, 0.5)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+    for p in procs:
+        assert p.exitcode == 0
+    for r in range(world):
+        rec = res[r]
+        assert rec["n_buckets"] > 2 and rec["in_hooks"] == rec["n_buckets"], (rec["n_buckets"], rec["in_hooks"])
+        e, n = rec["total"]
+        assert e <= 1e-4 * n, (workload, r, e, n)
+        # per parameter: no parameter's summed gradient may be off by more than 1e-3 of its norm (a bucket reduced
+        # before a side stream's gradient landed holds zeros / partial sums there: O(1))
+        for i, (ei, ni) in enumerate(rec["errs"]):
+            assert ei <= 1e-3 * ni + 1e-6 * n, (workload, r, i, ei, ni)

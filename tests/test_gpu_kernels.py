@@ -668,14 +668,17 @@ def test_lstm_vs_torch_fp64(B, T, I, H, bidir):
     x = det_input((B, T, I), 1600 + H)
     gy = det_input((B, T, H * (2 if bidir else 1)), 1601 + H)
     xr = x.double().requires_grad_(True)
-    yr, _ = ref(xr)
+    yr, (hnr, cnr) = ref(xr)
     (yr * gy.double()).sum().backward()
     xg = x.to(DEV).requires_grad_(True)
-    y, (hn, _) = ours(xg)
+    y, (hn, cn) = ours(xg)
     (y * gy.to(DEV)).sum().backward()
     sc = lambda t: max(1e-6, float(t.abs().max()))                                                 # noqa: E731
     close(y, yr, 2e-5 * sc(yr), 0, "h")
     close(hn[0], yr[:, -1, :H], 2e-5 * sc(yr), 0, "h_n")
+    assert hn.shape == hnr.shape and cn.shape == cnr.shape          # nn.LSTM's (h_n, c_n) contract
+    close(hn, hnr, 2e-5 * sc(hnr), 0, "h_n (both directions)")
+    close(cn, cnr, 2e-5 * sc(cnr), 0, "c_n")
     close(xg.grad, xr.grad, 5e-5 * sc(xr.grad), 0, "dx")
     rp = dict(ref.named_parameters())
     for k, p in ours.named_parameters():
