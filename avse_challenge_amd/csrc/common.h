@@ -89,11 +89,14 @@ __device__ inline float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 // hardware log2 with Kahan's correction (u = 1 + t; log1p(t) = log(u) * t / (u - 1)), which keeps
 // ~1 ulp for tiny t (dt biases sit at softplus^-1 of [1e-3, 1e-1]) without the libm call and its
 // branches; exp / rcp are the hardware instructions.
+// Branch-free: both sides are computed and selected (v_cndmask), so a loop of softplus calls has no
+// exec-mask branches (the unselected side may be inf / NaN for x > 88 or t ~ 0; it is discarded).
 __device__ inline float softplus(float x) {
-    if (x > 20.f) return x;
     const float t = fast_exp(x);
     const float u = 1.f + t;
-    return (u == 1.f) ? t : __builtin_amdgcn_logf(u) * AVSE_LN2 * t * fast_rcp(u - 1.f);
+    const float lp = __builtin_amdgcn_logf(u) * AVSE_LN2 * t * fast_rcp(u - 1.f);
+    const float r = (u == 1.f) ? t : lp;
+    return (x > 20.f) ? x : r;
 }
 __device__ inline float sigmoidf_(float x) { return fast_rcp(1.f + fast_exp(-x)); }
 __device__ inline float siluf_(float x) { return x * sigmoidf_(x); }
