@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .layers import HipLSTM, LipConv3d, PReLU, bn_act, maxpool3d
+from .layers import DilatedConv2d, HipLSTM, LipConv3d, PReLU, bn_act, maxpool3d
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
@@ -157,8 +157,8 @@ class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 conv
         self.bn0 = nn.BatchNorm2d(1)
         for i in range(num_conv):
             dil = 2 ** i
-            setattr(self, f"conv{i + 1}", nn.Conv2d(1 if i == 0 else filters, filters, k, padding=(k - 1) * dil // 2,
-                                                    dilation=dil))
+            setattr(self, f"conv{i + 1}", DilatedConv2d(1 if i == 0 else filters, filters, k, padding=(k - 1) * dil // 2,
+                                                        dilation=dil))
             setattr(self, f"bn{i + 1}", nn.BatchNorm2d(filters))
         self.convf = nn.Conv2d(filters, last_filter, 1)
         self.bn_last = nn.BatchNorm2d(last_filter)

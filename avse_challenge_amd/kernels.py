@@ -335,6 +335,30 @@ def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
     return out
 
 
+# ------------------------------------------------------------------------ dilated Conv2d dW (AudioFeatNet)
+
+DCONV_WGRAD_MAX_DIL = 16       # dconv_wgrad.hip MAX_DIL
+
+
+def dconv_wgrad(x, dy, dilation):
+    """dW (64, 64, 5, 5) of Conv2d(64, 64, 5, padding=2*dilation, dilation) from the conv input x and the output
+    gradient dy, both (N, 64, H, W) fp32; channels-last memory is read as it lies, anything else is made so."""
+    _need_gpu(x, dy)
+    if x.shape[1] != 64 or dy.shape != x.shape:
+        raise RuntimeError(f"dconv_wgrad expects (N, 64, H, W) input and gradient, got {tuple(x.shape)}, {tuple(dy.shape)}")
+    cl = torch.channels_last
+    x = x.float().contiguous(memory_format=cl)
+    dy = dy.float().contiguous(memory_format=cl)
+    Bn, _, H, W = x.shape
+    L = _lib.lib()
+    out = torch.empty((64, 64, 5, 5), device=x.device, dtype=torch.float32)
+    ws = torch.empty((L.avse_dconv_wgrad_workspace_bytes(Bn, H, W, dilation) + 3) // 4, device=x.device,
+                     dtype=torch.float32)
+    check(L.avse_dconv_wgrad(Bn, H, W, dilation, ptr(x), ptr(dy), ptr(out), ptr(ws), stream_ptr(x.device)),
+          "avse_dconv_wgrad")
+    return out
+
+
 # ------------------------------------------------------------------------ PReLU
 
 def _ncs(x):

@@ -9,6 +9,8 @@ bn_act       act(nn.BatchNorm{1,2,3}d(x) [+ res]) with act None / ReLU / PReLU, 
 maxpool3d    nn.MaxPool3d((1, k, k), (1, s, s), (0, p, p)) of the lip front-ends (byte argmax, gather backward)
 HipLSTM      nn.LSTM(..., num_layers=1, batch_first=True[, bidirectional]) whose recurrence is one HIP launch
              per direction (avse1 FusionNet, avse2 DPRNN)
+DilatedConv2d  nn.Conv2d(64, 64, 5, padding=2d, dilation=d) of the avse1 AudioFeatNet: weight gradient on the
+             MFMA implicit-GEMM kernel (channels-last activations)
 LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip front-ends:
              forward on MIOpen, weight gradient on the MFMA implicit-GEMM kernel (the lips are
              data: no input gradient is needed on the reference path; if one is requested it is
@@ -172,6 +174,50 @@ class LipConv3d(nn.Conv3d):
 
     def forward(self, x):
         return _LipConv3dFn.apply(x, self.weight, tuple(self.stride), tuple(self.padding))
+
+
+class _DilatedConvFn(torch.autograd.Function):
+    """Conv2d(64, 64, 5, padding=2d, dilation=d) with the weight gradient on the MFMA implicit-GEMM kernel
+    (csrc/dconv_wgrad.hip); forward and input gradient on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, dilation):
+        ctx.save_for_backward(x, w)
+        ctx.dilation = dilation
+        pad = 2 * dilation
+        return F.conv2d(x, w, b, 1, pad, dilation)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        d = ctx.dilation
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.nn.grad.conv2d_input(x.shape, w, dy, 1, 2 * d, d)
+        if ctx.needs_input_grad[1]:
+            dw = K.dconv_wgrad(x, dy, d)
+        if ctx.needs_input_grad[2]:
+            db = dy.sum((0, 2, 3))
+        return dx, dw, db, None
+
+
+class DilatedConv2d(nn.Conv2d):
+    """nn.Conv2d(cin, cout, 5, padding=2*dilation, dilation) — the avse1 AudioFeatNet convs (same parameters and
+    state_dict keys).  The 64 -> 64 ones on GPU tensors in channels-last memory (the benchmarked layout) take their
+    weight gradient from csrc/dconv_wgrad.hip; other inputs (the 1 -> 64 conv1, NCHW activations) run the library
+    convolution unchanged."""
+
+    def __init__(self, cin, cout, kernel_size=5, padding=0, dilation=1):
+        super().__init__(cin, cout, kernel_size, padding=padding, dilation=dilation)
+        assert self.padding == (2 * self.dilation[0],) * 2 and self.kernel_size == (5, 5)
+
+    def forward(self, x):
+        d = self.dilation[0]
+        if (os.environ.get("AVSE_DCONV_WGRAD", "1") == "1" and x.is_cuda and self.in_channels == 64
+                and self.out_channels == 64 and d <= K.DCONV_WGRAD_MAX_DIL and x.dtype == torch.float32
+                and x.is_contiguous(memory_format=torch.channels_last)):
+            return _DilatedConvFn.apply(x, self.weight, self.bias, d)
+        return super().forward(x)
 
 
 class _PReluGLNFn(torch.autograd.Function):

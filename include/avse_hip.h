@@ -168,6 +168,16 @@ int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, i
                       int64_t PT, int64_t PH, int64_t PW, const float* x, const float* dy, float* dw,
                       int32_t accumulate, float* workspace, avse_stream_t stream);
 
+/* ---------------------------------------------------------------- dilated Conv2d dW --------
+ * Weight gradient of nn.Conv2d(64, 64, 5, padding=2*dil, dilation=dil) — conv2..conv5 of the avse1 AudioFeatNet
+ * (baseline/avse1/model.py:199-215, dil 2, 4, 8, 16).  x, dy: (N, H, W, 64) channels-last fp32 (x the conv input, dy
+ * the output gradient); dw: (64, 64, 5, 5) (Cout, Cin, KH, KW) contiguous, overwritten.  Exact-fp32 MFMA implicit GEMM;
+ * dil <= 16, N*H*W*64 < 2^29.  The bias gradient is dy's channel sum (not computed here).
+ */
+int64_t avse_dconv_wgrad_workspace_bytes(int64_t N, int64_t H, int64_t W, int64_t dil);
+int avse_dconv_wgrad(int64_t N, int64_t H, int64_t W, int64_t dil, const float* x, const float* dy, float* dw,
+                     float* workspace, avse_stream_t stream);
+
 /* ---------------------------------------------------------------- PReLU -----------------
  * nn.PReLU(num_parameters in {1, C}) on an (N, C, S) contiguous view — avse1 lip stream
  * (model.py:32, utils/resnet.py:45-46, utils/tcn.py) and avse4 TCN (model.py:260,282).

@@ -54,6 +54,11 @@ def test_host_side_validation_without_gpu():
     assert b"shape" in L.avse_strerror(-2)
     ws = L.avse_scan_bwd_workspace_bytes(2, 128, 100, 16)
     assert ws == 4 * (2 * 2 * 32 * 100 + 2 * 128 * 18)
+    # dilated Conv2d weight gradient: null pointers, dilation range
+    assert L.avse_dconv_wgrad(2, 10, 257, 4, None, dummy, dummy, dummy, None) == -1
+    assert L.avse_dconv_wgrad(2, 10, 257, 0, dummy, dummy, dummy, dummy, None) == -2
+    assert L.avse_dconv_wgrad(2, 10, 257, 17, dummy, dummy, dummy, dummy, None) == -2
+    assert L.avse_dconv_wgrad_workspace_bytes(32, 376, 257, 16) % (4 * 25 * 64 * 64) == 0
 
 
 def test_product_never_imports_oracle():

@@ -715,3 +715,50 @@ def test_dwconv_prelu_gln_fused_vs_fp64(B, C, Kn, P, dil):
     close(y, ref, 1e-5 * sc(ref), 0, "y")
     for name, a_, r_ in zip(("dx", "dw", "dalpha", "dgamma", "dbeta"), g_leaves, leaves):
         close(a_.grad, r_.grad, 1e-4 * sc(r_.grad), 0, name)
+
+
+# ------------------------------------------------------------------ dilated Conv2d weight gradient (avse1 AudioFeatNet)
+
+@pytest.mark.parametrize("N,H,W,dil", [(2, 37, 257, 2), (2, 37, 257, 4), (1, 40, 257, 8), (2, 33, 257, 16),
+                                       (1, 9, 64, 16), (1, 5, 65, 2), (3, 7, 130, 8), (1, 3, 31, 4), (2, 70, 100, 16)])
+def test_dconv_wgrad_vs_fp64(N, H, W, dil):
+    """K.dconv_wgrad (csrc/dconv_wgrad.hip) vs the fp64 weight gradient of Conv2d(64, 64, 5, padding=2d, dilation=d)
+    (baseline/avse1/model.py:199-215) on channels-last inputs: every element within 3e-7 of its sum of |terms| (the
+    exact-f32 MFMA accumulates one rounding per product, ~1e-7 of it, cdna_hip_programming.md 'FP32-input MFMA'),
+    which covers rows shorter than the dilation halo, pieces of 31..66 pixels and images smaller than the kernel."""
+    x = det_input((N, 64, H, W), 1800 + dil + W)
+    dy = det_input((N, 64, H, W), 1801 + dil + H)
+    xd, dyd = x.double(), dy.double()
+    truth = torch.nn.grad.conv2d_weight(xd, (64, 64, 5, 5), dyd, 1, 2 * dil, dil)
+    bound = torch.nn.grad.conv2d_weight(xd.abs(), (64, 64, 5, 5), dyd.abs(), 1, 2 * dil, dil)
+    cl = torch.channels_last
+    got = K().dconv_wgrad(x.to(DEV).contiguous(memory_format=cl), dy.to(DEV).contiguous(memory_format=cl), dil)
+    err = (got.double().cpu() - truth).abs()
+    worst = float((err / (bound + 1e-30)).max())
+    assert worst <= 3e-7, worst
+    # NCHW inputs are converted, same result; deterministic (no atomics): bitwise equal on rerun
+    got2 = K().dconv_wgrad(x.to(DEV), dy.to(DEV), dil)
+    assert torch.equal(got, got2)
+
+
+def test_dilated_conv2d_module_grads_vs_torch():
+    """layers.DilatedConv2d (AudioFeatNet conv2..conv5 module, channels-last): output, input / weight / bias gradients
+    vs nn.Conv2d in fp64 on the same parameters."""
+    from avse_challenge_amd.layers import DilatedConv2d
+    torch.manual_seed(3)
+    ref = torch.nn.Conv2d(64, 64, 5, padding=8, dilation=4).double()
+    ours = DilatedConv2d(64, 64, 5, padding=8, dilation=4).to(DEV)
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    ours.to(memory_format=torch.channels_last)
+    x = det_input((2, 64, 30, 70), 1850)
+    gy = det_input((2, 64, 30, 70), 1851)
+    xr = x.double().requires_grad_(True)
+    (ref(xr) * gy.double()).sum().backward()
+    xg = x.to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = ours(xg)
+    (y * gy.to(DEV)).sum().backward()
+    sc = lambda t: max(1e-6, float(t.abs().max()))                                                 # noqa: E731
+    close(y, ref(xr), 2e-5 * sc(ref(xr)), 0, "y")
+    close(xg.grad, xr.grad, 2e-5 * sc(xr.grad), 0, "dx")
+    close(ours.weight.grad, ref.weight.grad, 2e-5 * sc(ref.weight.grad), 0, "dw")
+    close(ours.bias.grad, ref.bias.grad, 2e-5 * sc(ref.bias.grad), 0, "db")
