@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .layers import DilatedConv2d, HipLSTM, LipConv3d, PReLU, bn_act, maxpool3d
+from .layers import DilatedConv2d, HipLSTM, LipConv3d, PReLU, TrunkConv2d, bn_act, maxpool3d
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
@@ -34,10 +34,10 @@ def _prelu(c):
 class _BasicBlock(nn.Module):            # utils/resnet.py:26-67 (relu_type='prelu')
     def __init__(self, cin, cout, stride=1, downsample=None):
         super().__init__()
-        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.conv1 = TrunkConv2d(cin, cout, stride)      # weight gradient on csrc/rconv_wgrad.hip (NCHW)
         self.bn1 = nn.BatchNorm2d(cout)
         self.relu1, self.relu2 = _prelu(cout), _prelu(cout)
-        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.conv2 = TrunkConv2d(cout, cout, 1)
         self.bn2 = nn.BatchNorm2d(cout)
         self.downsample = downsample
 

@@ -359,6 +359,34 @@ def dconv_wgrad(x, dy, dilation):
     return out
 
 
+# ------------------------------------------------------------------------ ResNet trunk 3x3 Conv2d dW
+
+def rconv_wgrad_supported(x, cout, stride):
+    """True when csrc/rconv_wgrad.hip takes this weight gradient (NCHW fp32 input, channels multiples of 64)."""
+    n, cin, h, w = x.shape
+    return (x.is_cuda and x.dtype == torch.float32 and stride in (1, 2)
+            and _lib.lib().avse_rconv_wgrad_workspace_bytes(n, cin, cout, h, w, stride) > 0)
+
+
+def rconv_wgrad(x, dy, stride):
+    """dW (COUT, CIN, 3, 3) of Conv2d(CIN, COUT, 3, stride, padding=1, bias=False) from the input x (N, CIN, H, W) and
+    the output gradient dy (N, COUT, HO, WO); both are read as contiguous NCHW fp32."""
+    _need_gpu(x, dy)
+    x = x.float().contiguous()
+    dy = dy.float().contiguous()
+    n, cin, h, w = x.shape
+    cout = dy.shape[1]
+    L = _lib.lib()
+    nb = L.avse_rconv_wgrad_workspace_bytes(n, cin, cout, h, w, stride)
+    if nb <= 0:
+        raise RuntimeError(f"rconv_wgrad: unsupported shape x {tuple(x.shape)}, cout {cout}, stride {stride}")
+    out = torch.empty((cout, cin, 3, 3), device=x.device, dtype=torch.float32)
+    ws = torch.empty((nb + 3) // 4, device=x.device, dtype=torch.float32)
+    check(L.avse_rconv_wgrad(n, cin, cout, h, w, stride, ptr(x), ptr(dy), ptr(out), ptr(ws), stream_ptr(x.device)),
+          "avse_rconv_wgrad")
+    return out
+
+
 # ------------------------------------------------------------------------ PReLU
 
 def _ncs(x):

@@ -11,6 +11,8 @@ HipLSTM      nn.LSTM(..., num_layers=1, batch_first=True[, bidirectional]) whose
              per direction (avse1 FusionNet, avse2 DPRNN)
 DilatedConv2d  nn.Conv2d(64, 64, 5, padding=2d, dilation=d) of the avse1 AudioFeatNet: weight gradient on the
              MFMA implicit-GEMM kernel (channels-last activations)
+TrunkConv2d  nn.Conv2d(cin, cout, 3, stride, padding=1, bias=False) of the lip ResNet trunks: weight gradient on
+             the MFMA implicit-GEMM kernel (NCHW activations)
 LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip front-ends:
              forward on MIOpen, weight gradient on the MFMA implicit-GEMM kernel (the lips are
              data: no input gradient is needed on the reference path; if one is requested it is
@@ -217,6 +219,43 @@ class DilatedConv2d(nn.Conv2d):
                 and self.out_channels == 64 and d <= K.DCONV_WGRAD_MAX_DIL and x.dtype == torch.float32
                 and x.is_contiguous(memory_format=torch.channels_last)):
             return _DilatedConvFn.apply(x, self.weight, self.bias, d)
+        return super().forward(x)
+
+
+class _TrunkConvFn(torch.autograd.Function):
+    """Conv2d(cin, cout, 3, stride, padding=1, bias=False) with the weight gradient on the MFMA implicit-GEMM kernel
+    (csrc/rconv_wgrad.hip); forward and input gradient on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride):
+        ctx.save_for_backward(x, w)
+        ctx.stride = stride
+        return F.conv2d(x, w, None, stride, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.nn.grad.conv2d_input(x.shape, w, dy, ctx.stride, 1)
+        if ctx.needs_input_grad[1]:
+            dw = K.rconv_wgrad(x, dy, ctx.stride)
+        return dx, dw, None
+
+
+class TrunkConv2d(nn.Conv2d):
+    """nn.Conv2d(cin, cout, 3, stride, padding=1, bias=False) of the lip-encoder ResNet trunks (same parameters and
+    state_dict keys).  NCHW fp32 GPU activations with channel counts that are multiples of 64 take their weight
+    gradient from csrc/rconv_wgrad.hip; channels-last activations (use_channels_last) run the library convolution."""
+
+    def __init__(self, cin, cout, stride=1):
+        super().__init__(cin, cout, 3, stride=stride, padding=1, bias=False)
+
+    def forward(self, x):
+        s = self.stride[0]
+        if (os.environ.get("AVSE_RCONV_WGRAD", "0") == "1" and x.is_contiguous()
+                and K.rconv_wgrad_supported(x, self.out_channels, s)):
+            return _TrunkConvFn.apply(x, self.weight, s)
         return super().forward(x)
 
 

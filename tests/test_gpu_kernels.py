@@ -762,3 +762,52 @@ def test_dilated_conv2d_module_grads_vs_torch():
     close(xg.grad, xr.grad, 2e-5 * sc(xr.grad), 0, "dx")
     close(ours.weight.grad, ref.weight.grad, 2e-5 * sc(ref.weight.grad), 0, "dw")
     close(ours.bias.grad, ref.bias.grad, 2e-5 * sc(ref.bias.grad), 0, "db")
+
+
+# ------------------------------------------------------------------ ResNet trunk 3x3 Conv2d weight gradient
+
+@pytest.mark.parametrize("N,cin,cout,H,W,stride", [(6, 64, 64, 24, 24, 1), (5, 64, 128, 24, 24, 2),
+                                                   (7, 128, 128, 12, 12, 1), (9, 128, 256, 12, 12, 2),
+                                                   (11, 256, 256, 6, 6, 1), (13, 256, 512, 6, 6, 2),
+                                                   (17, 512, 512, 3, 3, 1), (3, 64, 64, 28, 28, 1), (5, 64, 128, 28, 28, 2),
+                                                   (3, 256, 512, 7, 7, 2), (19, 512, 512, 4, 4, 1), (2, 64, 64, 56, 56, 1)])
+def test_rconv_wgrad_vs_fp64(N, cin, cout, H, W, stride):
+    """K.rconv_wgrad (csrc/rconv_wgrad.hip) vs the fp64 weight gradient of Conv2d(cin, cout, 3, stride, padding=1,
+    bias=False) (baseline/avse1/utils/resnet.py:11-13): the avse1 trunk shapes at 96x96 lips (24..3 pixels, stride 1
+    and 2), the avse4 / C5 ones at 112x112 (28 .. 4: row bands, odd 7x7), the avse2 56x56 layer, frame counts that leave a
+    partial last chunk; every element within 3e-7 of its sum of |terms| (exact-f32 MFMA: one rounding per product),
+    deterministic on rerun.  Shapes outside the lip encoders' table report no workspace (the module keeps the library)."""
+    from avse_challenge_amd import _lib
+    assert _lib.lib().avse_rconv_wgrad_workspace_bytes(2, 64, 128, 7, 9, 2) == 0
+    x = det_input((N, cin, H, W), 1900 + cin + H)
+    HO, WO = (H - 1) // stride + 1, (W - 1) // stride + 1
+    dy = det_input((N, cout, HO, WO), 1901 + cout + W)
+    xd, dyd = x.double(), dy.double()
+    truth = torch.nn.grad.conv2d_weight(xd, (cout, cin, 3, 3), dyd, stride, 1)
+    bound = torch.nn.grad.conv2d_weight(xd.abs(), (cout, cin, 3, 3), dyd.abs(), stride, 1)
+    got = K().rconv_wgrad(x.to(DEV), dy.to(DEV), stride)
+    worst = float(((got.double().cpu() - truth).abs() / (bound + 1e-30)).max())
+    assert worst <= 3e-7, worst
+    assert torch.equal(got, K().rconv_wgrad(x.to(DEV), dy.to(DEV), stride))
+
+
+def test_trunk_conv2d_module_grads_vs_torch(monkeypatch):
+    """layers.TrunkConv2d (stride 2, NCHW): output and input / weight gradients vs nn.Conv2d in fp64."""
+    from avse_challenge_amd.layers import TrunkConv2d
+    monkeypatch.setenv("AVSE_RCONV_WGRAD", "1")
+    torch.manual_seed(4)
+    ref = torch.nn.Conv2d(64, 128, 3, stride=2, padding=1, bias=False).double()
+    ours = TrunkConv2d(64, 128, 2).to(DEV)
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = det_input((3, 64, 24, 24), 1950)
+    gy = det_input((3, 128, 12, 12), 1951)
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr)
+    (yr * gy.double()).sum().backward()
+    xg = x.to(DEV).requires_grad_(True)
+    y = ours(xg)
+    (y * gy.to(DEV)).sum().backward()
+    sc = lambda t: max(1e-6, float(t.abs().max()))                                                 # noqa: E731
+    close(y, yr, 2e-5 * sc(yr), 0, "y")
+    close(xg.grad, xr.grad, 2e-5 * sc(xr.grad), 0, "dx")
+    close(ours.weight.grad, ref.weight.grad, 2e-5 * sc(ref.weight.grad), 0, "dw")
