@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .layers import DilatedConv2d, HipLSTM, LipConv3d, PReLU, TrunkConv2d, bn_act, maxpool3d
+from .layers import DilatedConv2d, HipLSTM, LipConv3d, PointwiseConv2d, PReLU, TrunkConv2d, bn_act, maxpool3d
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
@@ -58,7 +58,7 @@ class _ResNet18(nn.Module):              # utils/resnet.py:70-124
         chans, cin = (64, 128, 256, 512), 64
         for i, c in enumerate(chans):
             s = 1 if i == 0 else 2
-            ds = None if (s == 1 and cin == c) else nn.Sequential(nn.Conv2d(cin, c, 1, s, bias=False), nn.BatchNorm2d(c))
+            ds = None if (s == 1 and cin == c) else nn.Sequential(PointwiseConv2d(cin, c, s), nn.BatchNorm2d(c))
             setattr(self, f"layer{i + 1}", nn.Sequential(_BasicBlock(cin, c, s, ds), _BasicBlock(c, c)))
             cin = c
         self.avgpool = nn.AdaptiveAvgPool2d(1)

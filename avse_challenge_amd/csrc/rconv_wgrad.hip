@@ -11,15 +11,15 @@
 //
 // GEMM view: M = cout, N = cin * 9, K = frames * HO * WO.  The spatial shape (H, W, stride) is a template parameter
 // (the lip encoders have a handful, see the dispatch table at the end), so every index is constant-divided and the
-// staging loops unroll.  Workgroup (co block, ci block, k split) owns a 64 x 64 (co, ci) block for all 9 taps (wave w:
-// the 32 x 32 tile (w / 2, w % 2), 9 accumulators) over a contiguous range of K chunks; a chunk is F whole frames or
-// R output rows of one frame (at most P_MAX pixels).  Per chunk the dY pixels [p][co] and the zero-padded input
-// window [frame][row][col][ci] sit in LDS pixel-major with an odd 65-float pixel stride: the coalesced global loads
-// (consecutive lanes = consecutive pixels of one channel) write conflict-free and the MFMA operand reads (consecutive
-// lanes = consecutive channels of one pixel) read conflict-free.  Staging is direct (global -> LDS at the chunk start;
-// the 144 accumulators leave no registers for a prefetch): the other workgroups on the CU compute meanwhile.  A K-step
-// takes 2 pixels (lanes 0-31 pixel 2j, 32-63 pixel 2j + 1): one A read, 9 B reads, 9 MFMAs.  Per-split partial sums
-// go to a workspace summed by a second kernel (deterministic).
+// staging loops unroll.  Workgroup (co block, ci block, kernel row kh, k split) owns a 64 x 64 (co, ci) block for the
+// 3 taps of row kh (wave w: the 32 x 32 tile (w / 2, w % 2), 3 accumulators) over a contiguous range of K chunks; a
+// chunk is F whole frames or R output rows of one frame (at most P_MAX pixels).  Per chunk the dY pixels [p][co] and
+// the zero-padded input rows S r + kh - 1 [frame][row][col][ci] sit in LDS pixel-major with an odd 65-float pixel
+// stride: the coalesced global loads (consecutive lanes = consecutive pixels of one channel) write conflict-free and
+// the MFMA operand reads (consecutive lanes = consecutive channels of one pixel) read conflict-free.  With 48
+// accumulators the next chunk is loaded into registers (raw buffer loads, 32-bit offsets) while the current one's
+// MFMAs run.  A K-step takes 2 pixels (lanes 0-31 pixel 2j, 32-63 pixel 2j + 1): one A read, 3 B reads, 3 MFMAs.
+// Per-split partial sums go to a workspace summed by a second kernel (deterministic).
 #include <algorithm>
 
 #include "common.h"
@@ -30,33 +30,28 @@ namespace rcw {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int THREADS = 256, CB = 64, PS = CB + 1;   // channel block, LDS pixel stride (floats)
-constexpr int KK = 9;                                // 3x3 taps
+constexpr int KS = 3, KK = 9;                        // 3x3 taps; a workgroup owns one kernel row (3 taps)
 constexpr int P_MAX = 96;                            // output pixels per chunk
-constexpr int LDS_BUDGET = 72 * 1024;                // bytes per workgroup: 2 workgroups per CU
+constexpr int LDS_BUDGET = 72 * 1024;                // bytes per workgroup: 2 workgroups per CU (~235 VGPRs)
 
-constexpr int lds_floats(int P, int F, int RIN, int WIN) { return (((P + 1) & ~1) + 1) * PS + F * RIN * WIN * PS; }
+constexpr int lds_floats(int P, int rows, int WIN) { return (((P + 1) & ~1) + 1) * PS + rows * WIN * PS; }
 
 template <int H, int W, int S>
 struct Geo {
     static constexpr int HO = (H - 1) / S + 1, WO = (W - 1) / S + 1, HWO = HO * WO, HW = H * W;
-    static constexpr int WIN = (WO - 1) * S + 3;
+    static constexpr int WIN = (WO - 1) * S + 3;                     // staged input columns (-1 .. )
     static constexpr bool FRAMES = HWO <= P_MAX;                      // chunk = F whole frames, else R rows
-    static constexpr int fit_f(int f) {
-        return (f <= 1 || lds_floats(f * HWO, f, (HO - 1) * S + 3, WIN) * 4 <= LDS_BUDGET) ? f : fit_f(f - 1);
-    }
-    static constexpr int fit_r(int r) {
-        return (r <= 1 || lds_floats(r * WO, 1, (r - 1) * S + 3, WIN) * 4 <= LDS_BUDGET) ? r : fit_r(r - 1);
-    }
+    static constexpr int fit_f(int f) { return (f <= 1 || lds_floats(f * HWO, f * HO, WIN) * 4 <= LDS_BUDGET) ? f : fit_f(f - 1); }
+    static constexpr int fit_r(int r) { return (r <= 1 || lds_floats(r * WO, r, WIN) * 4 <= LDS_BUDGET) ? r : fit_r(r - 1); }
     static constexpr int F = FRAMES ? fit_f(P_MAX / HWO) : 1;
     static constexpr int R = FRAMES ? HO : fit_r(P_MAX / WO > 0 ? P_MAX / WO : 1);
-    static constexpr int RIN = (R - 1) * S + 3;
     static constexpr int P = F * R * WO;                                // pixels of a full chunk
     static constexpr int P2 = (P + 1) & ~1;
     static constexpr int BANDS = (HO + R - 1) / R;                     // row bands per frame (FRAMES: 1)
-    static constexpr int NXW = F * RIN * WIN;                          // staged input pixels per channel
+    static constexpr int NXW = F * R * WIN;                            // staged input pixels per channel (one kh)
     static constexpr int YV = (P2 * CB + THREADS - 1) / THREADS;       // staging registers per thread
     static constexpr int XV = (NXW * CB + THREADS - 1) / THREADS;
-    static constexpr int LDSB = lds_floats(P, F, RIN, WIN) * 4;
+    static constexpr int LDSB = lds_floats(P, F * R, WIN) * 4;
     static_assert(P <= P_MAX && LDSB <= LDS_BUDGET, "chunk does not fit");
 };
 
@@ -72,86 +67,96 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(Args s, const float* 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nblk = s.nco * s.nci;
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);       // the co/ci blocks of one k split share an XCD
-    const int ks = bid / nblk, blk = bid % nblk;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);       // the 3 kernel rows x co / ci blocks of a split share an XCD
+    const int kh = bid % KS, ks = bid / KS / nblk, blk = (bid / KS) % nblk;
     const int cob = blk / s.nci, cib = blk % s.nci;
     const int c_lo = __builtin_amdgcn_readfirstlane((int)((int64_t)ks * s.chunks / s.ksplit));
     const int c_hi = __builtin_amdgcn_readfirstlane((int)((int64_t)(ks + 1) * s.chunks / s.ksplit));
 
     float* sy = lds;                                        // [P2 + 1][PS]: dY pixels
-    float* sx = sy + (G::P2 + 1) * PS;                      // [NXW][PS]: input window
-    const int xs_n = s.CIN * G::HW, ys_n = s.COUT * G::HWO;     // 32-bit offsets: tensors < 2^31 elements (checked)
-    const float* xb = x + (int64_t)cib * CB * G::HW;
-    const float* yb = dy + (int64_t)cob * CB * G::HWO;
+    float* sx = sy + (G::P2 + 1) * PS;                      // [F * R][WIN][PS]: input rows S * r + kh - 1
+    const int xs_n = s.CIN * G::HW, ys_n = s.COUT * G::HWO;     // 32-bit offsets: tensors < 2^29 elements (checked)
+    // raw buffer loads with 32-bit element offsets (one VGPR per address; an offset past num_records reads 0)
+    const auto rx = make_rsrc(x, (int64_t)s.N * xs_n);
+    const auto ry = make_rsrc(dy, (int64_t)s.N * ys_n);
+    const int OOBX = s.N * xs_n, OOBY = s.N * ys_n;
+    const int xb = cib * CB * G::HW, yb = cob * CB * G::HWO;
 
-    // chunk c -> LDS: dY element e = co * P2 + p, input element e = ci * NXW + q (consecutive threads walk the pixels
-    // of one channel: coalesced loads, conflict-free stores); everything past the chunk / outside the image is 0
-    auto stage = [&](int c) {
+    float yv[G::YV], xv[G::XV];
+    // chunk c -> registers: dY element e = co * P2 + p, input element e = ci * NXW + q (consecutive threads walk the
+    // pixels of one channel: coalesced); everything past the chunk / outside the image is 0
+    auto prefetch = [&](int c) {
         int f0, r0, nf, nr;
         if (G::FRAMES) {
             f0 = c * G::F; r0 = 0; nf = min(G::F, s.N - f0); nr = G::HO;
         } else {
             f0 = c / G::BANDS; r0 = (c % G::BANDS) * G::R; nf = 1; nr = min(G::R, G::HO - r0);
         }
-        const int np = nf * nr * G::WO;
-        const int ybase = f0 * ys_n + r0 * G::WO, xbase = f0 * xs_n;
-#pragma unroll 8
+        const int ybase = yb + f0 * ys_n + r0 * G::WO, xbase = xb + f0 * xs_n;
+#pragma unroll
         for (int i = 0; i < G::YV; ++i) {
             const int e = threadIdx.x + i * THREADS, p = e % G::P2, co = e / G::P2;
             const int f = p / (G::R * G::WO), rem = p % (G::R * G::WO);
-            const bool ok = co < CB && p < np;
-            const float v = ok ? yb[ybase + f * ys_n + co * G::HWO + rem] : 0.f;
-            if (co < CB) sy[p * PS + co] = v;
+            const bool ok = co < CB && f < nf && rem / G::WO < nr;
+            yv[i] = bufld<float>::ld(ry, ok ? ybase + f * ys_n + co * G::HWO + rem : OOBY, 0);
         }
-#pragma unroll 8
+#pragma unroll
         for (int i = 0; i < G::XV; ++i) {
             const int e = threadIdx.x + i * THREADS, q = e % G::NXW, ci = e / G::NXW;
-            const int f = q / (G::RIN * G::WIN), rem = q % (G::RIN * G::WIN);
-            const int hi = S * r0 - 1 + rem / G::WIN, wi = rem % G::WIN - 1;
-            const bool ok = ci < CB && f < nf && hi >= 0 && hi < H && wi >= 0 && wi < W;
-            const float v = ok ? xb[xbase + f * xs_n + ci * G::HW + hi * W + wi] : 0.f;
-            if (ci < CB) sx[q * PS + ci] = v;
+            const int fr = q / G::WIN, col = q % G::WIN;                 // staged row fr = f * R + r
+            const int f = fr / G::R, r = fr % G::R;
+            const int hi = S * (r0 + r) + kh - 1, wi = col - 1;
+            const bool ok = ci < CB && f < nf && r < nr && hi >= 0 && hi < H && wi >= 0 && wi < W;
+            xv[i] = bufld<float>::ld(rx, ok ? xbase + f * xs_n + ci * G::HW + hi * W + wi : OOBX, 0);
         }
-        return np;
+        return nf * nr * G::WO;
     };
 
-    floatx16 acc[KK];
+    floatx16 acc[KS];
 #pragma unroll
-    for (int k = 0; k < KK; ++k)
+    for (int k = 0; k < KS; ++k)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[k][q] = 0.f;
     const int half = lane >> 5;
     const int co_l = (wave >> 1) * 32 + (lane & 31), ci_l = (wave & 1) * 32 + (lane & 31);
 
+    int np = c_lo < c_hi ? prefetch(c_lo) : 0;
     for (int c = c_lo; c < c_hi; ++c) {
+        const int npc = np;
         __syncthreads();                                    // previous chunk's MFMAs are done with LDS
-        const int npc = stage(c);
+#pragma unroll
+        for (int i = 0; i < G::YV; ++i) {
+            const int e = threadIdx.x + i * THREADS, p = e % G::P2, co = e / G::P2;
+            if (co < CB) sy[p * PS + co] = yv[i];
+        }
+#pragma unroll
+        for (int i = 0; i < G::XV; ++i) {
+            const int e = threadIdx.x + i * THREADS, q = e % G::NXW, ci = e / G::NXW;
+            if (ci < CB) sx[q * PS + ci] = xv[i];
+        }
         __syncthreads();
+        if (c + 1 < c_hi) np = prefetch(c + 1);             // in flight while this chunk's MFMAs run
         const int nk = (npc + 1) >> 1;
         for (int j = 0; j < nk; ++j) {
             const int p = 2 * j + half;                     // output pixel of this lane half
-            const int f = p / (G::R * G::WO), rem = p % (G::R * G::WO);
-            const int org = (f * G::RIN + S * (rem / G::WO)) * G::WIN + S * (rem % G::WO);   // window origin
+            const int fr = p / G::WO, w = p % G::WO;        // staged row (f * R + r), column
             const float a = sy[p * PS + co_l];
-            const float* pb = sx + org * PS + ci_l;
-            float b[KK];
-#pragma unroll
-            for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-                for (int kw = 0; kw < 3; ++kw) b[kh * 3 + kw] = pb[(kh * G::WIN + kw) * PS];
-#pragma unroll
-            for (int k = 0; k < KK; ++k) acc[k] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[k], acc[k], 0, 0, 0);
+            const float* pb = sx + (fr * G::WIN + S * w) * PS + ci_l;
+            const float b0 = pb[0], b1 = pb[PS], b2 = pb[2 * PS];
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc[1], 0, 0, 0);
+            acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b2, acc[2], 0, 0, 0);
         }
     }
-    // partial out: part[ks][co][ci][tap]; C map col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
+    // partial out: part[ks][co][ci][kh][kw]; C map col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
     float* pp = part + (int64_t)ks * s.COUT * s.CIN * KK;
     const int ci = cib * CB + ci_l;
 #pragma unroll
-    for (int k = 0; k < KK; ++k)
+    for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int co = cob * CB + (wave >> 1) * 32 + (q & 3) + 8 * (q >> 2) + 4 * half;
-            pp[((int64_t)co * s.CIN + ci) * KK + k] = acc[k][q];
+            pp[((int64_t)co * s.CIN + ci) * KK + kh * KS + kw] = acc[kw][q];
         }
 }
 
@@ -169,8 +174,8 @@ int chunks_of(int N) {
     return G::FRAMES ? (N + G::F - 1) / G::F : N * G::BANDS;
 }
 
-// k splits: about two workgroups per CU over the 256 CUs, at most one chunk per split
-inline int ksplit_for(int chunks, int nblk) { return std::max(1, std::min(chunks, 512 / nblk)); }
+// k splits: about two workgroups per CU over the 256 CUs (3 kernel rows per block), at most one chunk per split
+inline int ksplit_for(int chunks, int nblk) { return std::max(1, std::min(chunks, 512 / (KS * nblk))); }
 
 template <int H, int W, int S>
 int launch(int N, int CIN, int COUT, const float* x, const float* dy, float* dw, float* ws, hipStream_t st) {
@@ -180,7 +185,8 @@ int launch(int N, int CIN, int COUT, const float* x, const float* dy, float* dw,
     a.chunks = chunks_of<H, W, S>(N);
     a.nci = CIN / CB; a.nco = COUT / CB;
     a.ksplit = ksplit_for(a.chunks, a.nci * a.nco);
-    hipLaunchKernelGGL((wgrad_kernel<H, W, S>), dim3(a.ksplit * a.nci * a.nco), dim3(THREADS), G::LDSB, st, a, x, dy, ws);
+    hipLaunchKernelGGL((wgrad_kernel<H, W, S>), dim3(a.ksplit * a.nci * a.nco * KS), dim3(THREADS), G::LDSB, st, a, x, dy,
+                       ws);
     AVSE_CHECK_LAUNCH();
     const int total = COUT * CIN * KK;
     hipLaunchKernelGGL(reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, ws, a.ksplit, total, dw);
@@ -209,7 +215,7 @@ using namespace avse::rcw;
 
 static bool supported(int64_t N, int64_t CIN, int64_t COUT, int64_t H, int64_t W, int64_t stride) {
     if (N <= 0 || CIN <= 0 || COUT <= 0 || CIN % CB || COUT % CB) return false;
-    if (N * CIN * H * W >= (1LL << 31) || N * COUT * H * W >= (1LL << 31)) return false;
+    if (N * CIN * H * W >= (1LL << 29) || N * COUT * H * W >= (1LL << 29)) return false;   // buffer bytes < 2^31
     return chunks_for((int)H, (int)W, (int)stride, 1) > 0;
 }
 

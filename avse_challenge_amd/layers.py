@@ -11,8 +11,9 @@ HipLSTM      nn.LSTM(..., num_layers=1, batch_first=True[, bidirectional]) whose
              per direction (avse1 FusionNet, avse2 DPRNN)
 DilatedConv2d  nn.Conv2d(64, 64, 5, padding=2d, dilation=d) of the avse1 AudioFeatNet: weight gradient on the
              MFMA implicit-GEMM kernel (channels-last activations)
-TrunkConv2d  nn.Conv2d(cin, cout, 3, stride, padding=1, bias=False) of the lip ResNet trunks: weight gradient on
-             the MFMA implicit-GEMM kernel (NCHW activations)
+TrunkConv2d  nn.Conv2d(cin, cout, 3, stride, padding=1, bias=False) of the lip ResNet trunks: frames of <= 36 output
+             pixels as one im2col GEMM (hipBLASLt), the 64 -> 64 layer's weight gradient on the MFMA kernel (NCHW)
+PointwiseConv2d  the 1x1 shortcut convs as one GEMM
 LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip front-ends:
              forward on MIOpen, weight gradient on the MFMA implicit-GEMM kernel (the lips are
              data: no input gradient is needed on the reference path; if one is requested it is
@@ -243,6 +244,74 @@ class _TrunkConvFn(torch.autograd.Function):
         return dx, dw, None
 
 
+class _GemmConvFn(torch.autograd.Function):
+    """Conv2d(cin, cout, k in {1, 3}, stride, padding (k - 1) / 2, bias=False) as ONE hipBLASLt GEMM over all frames'
+    pixels: (N * HO * WO, cin * k * k) im2col rows times the (cout, cin * k * k) weight; backward = two GEMMs + col2im.
+    For the lip trunks' small-spatial layers (<= 36 output pixels per frame) and 1x1 shortcut convs, where MIOpen's
+    NCHW backward ran NHWC kernels behind batched transposes at ~32 TF/s or less (tools/avse1_op_profile.py)."""
+
+    @staticmethod
+    def _rows(x, k, stride):
+        n, cin, h, w = x.shape
+        if k == 1:
+            xs = x[:, :, ::stride, ::stride]
+            return xs.permute(0, 2, 3, 1).reshape(-1, cin), xs.shape[2], xs.shape[3]
+        cols = F.unfold(x, k, padding=(k - 1) // 2, stride=stride)               # (N, cin * k * k, P)
+        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+        return cols.transpose(1, 2).reshape(-1, cin * k * k), ho, wo
+
+    @staticmethod
+    def forward(ctx, x, w, stride):
+        k = w.shape[-1]
+        a, ho, wo = _GemmConvFn._rows(x, k, stride)
+        y = a @ w.reshape(w.shape[0], -1).t()                                     # (N * P, cout)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.hw = stride, (ho, wo)
+        return y.view(x.shape[0], ho, wo, -1).permute(0, 3, 1, 2).contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        s, (ho, wo) = ctx.stride, ctx.hw
+        n, cin, h, ww = x.shape
+        cout, k = w.shape[0], w.shape[-1]
+        dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)                            # (N * P, cout)
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            a, _, _ = _GemmConvFn._rows(x, k, s)
+            dw = (dy2.t() @ a).view_as(w)
+        if ctx.needs_input_grad[0]:
+            da = dy2 @ w.reshape(cout, -1)                                        # (N * P, cin * k * k)
+            if k == 1:
+                dx = x.new_zeros(x.shape)
+                dx[:, :, ::s, ::s] = da.view(n, ho, wo, cin).permute(0, 3, 1, 2)
+            else:
+                dx = F.fold(da.view(n, ho * wo, -1).transpose(1, 2), (h, ww), k, padding=(k - 1) // 2, stride=s)
+        return dx, dw, None
+
+
+def gemm_conv_ok(x, k, stride):
+    """The GEMM form is used for NCHW fp32 GPU inputs whose output frames have <= 36 pixels (lip-trunk layers 3-4 at
+    96 / 112 pixel lips) and for every 1x1 shortcut conv (AVSE_TRUNK_GEMM=0 keeps MIOpen)."""
+    if os.environ.get("AVSE_TRUNK_GEMM", "1") != "1" or not x.is_cuda or x.dtype != torch.float32 or not x.is_contiguous():
+        return False
+    ho, wo = (x.shape[2] - 1) // stride + 1, (x.shape[3] - 1) // stride + 1
+    return k == 1 or ho * wo <= 36
+
+
+class PointwiseConv2d(nn.Conv2d):
+    """nn.Conv2d(cin, cout, 1, stride, bias=False) — the ResNet shortcut (utils/resnet.py:86-95 downsample): one GEMM
+    (same parameters and state_dict keys)."""
+
+    def __init__(self, cin, cout, stride=1):
+        super().__init__(cin, cout, 1, stride=stride, bias=False)
+
+    def forward(self, x):
+        if gemm_conv_ok(x, 1, self.stride[0]):
+            return _GemmConvFn.apply(x, self.weight, self.stride[0])
+        return super().forward(x)
+
+
 class TrunkConv2d(nn.Conv2d):
     """nn.Conv2d(cin, cout, 3, stride, padding=1, bias=False) of the lip-encoder ResNet trunks (same parameters and
     state_dict keys).  NCHW fp32 GPU activations with channel counts that are multiples of 64 take their weight
@@ -253,10 +322,20 @@ class TrunkConv2d(nn.Conv2d):
 
     def forward(self, x):
         s = self.stride[0]
-        if (os.environ.get("AVSE_RCONV_WGRAD", "0") == "1" and x.is_contiguous()
-                and K.rconv_wgrad_supported(x, self.out_channels, s)):
+        if gemm_conv_ok(x, 3, s):                          # small frames: one GEMM over all pixels (_GemmConvFn)
+            return _GemmConvFn.apply(x, self.weight, s)
+        if x.is_contiguous() and self._use_hip(x, s) and K.rconv_wgrad_supported(x, self.out_channels, s):
             return _TrunkConvFn.apply(x, self.weight, s)
         return super().forward(x)
+
+    def _use_hip(self, x, s):
+        # AVSE_RCONV_WGRAD: "all", "0", or the default "layer1": the 64 -> 64 stride-1 convs, where the kernel beats
+        # MIOpen inside the avse1 step (1.1 vs ~1.5 ms per launch); the wider layers run slower than MIOpen's
+        # (profiles/r03_rconv_wgrad_bench.jsonl, r03_avse1_step_rconv_all_window_stats.csv)
+        mode = os.environ.get("AVSE_RCONV_WGRAD", "layer1")
+        if mode == "all":
+            return True
+        return mode == "layer1" and s == 1 and self.in_channels == 64 and self.out_channels == 64
 
 
 class _PReluGLNFn(torch.autograd.Function):
