@@ -252,13 +252,18 @@ class _GemmConvFn(torch.autograd.Function):
 
     @staticmethod
     def _rows(x, k, stride):
+        """(N * HO * WO, cin * k * k) im2col rows as ONE gather copy of a strided view of the zero-padded input
+        (F.unfold launches one kernel per frame on this build: 38400 per step); for a 1x1 conv on channels-last memory
+        at stride 1 the rows ARE the input (a view)."""
         n, cin, h, w = x.shape
+        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
         if k == 1:
             xs = x[:, :, ::stride, ::stride]
-            return xs.permute(0, 2, 3, 1).reshape(-1, cin), xs.shape[2], xs.shape[3]
-        cols = F.unfold(x, k, padding=(k - 1) // 2, stride=stride)               # (N, cin * k * k, P)
-        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
-        return cols.transpose(1, 2).reshape(-1, cin * k * k), ho, wo
+            return xs.permute(0, 2, 3, 1).reshape(-1, cin), ho, wo
+        xp = F.pad(x, (1, 1, 1, 1))
+        hp, wp = h + 2, w + 2
+        v = xp.as_strided((n, ho, wo, cin, 3, 3), (cin * hp * wp, stride * wp, stride, hp * wp, wp, 1))
+        return v.reshape(-1, cin * 9), ho, wo
 
     @staticmethod
     def forward(ctx, x, w, stride):
@@ -267,7 +272,8 @@ class _GemmConvFn(torch.autograd.Function):
         y = a @ w.reshape(w.shape[0], -1).t()                                     # (N * P, cout)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.hw = stride, (ho, wo)
-        return y.view(x.shape[0], ho, wo, -1).permute(0, 3, 1, 2).contiguous()
+        y = y.view(x.shape[0], ho, wo, -1).permute(0, 3, 1, 2)                    # channels-last memory (a view)
+        return y if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous() else y.contiguous()
 
     @staticmethod
     def backward(ctx, dy):
@@ -281,22 +287,33 @@ class _GemmConvFn(torch.autograd.Function):
             a, _, _ = _GemmConvFn._rows(x, k, s)
             dw = (dy2.t() @ a).view_as(w)
         if ctx.needs_input_grad[0]:
-            da = dy2 @ w.reshape(cout, -1)                                        # (N * P, cin * k * k)
+            da = (dy2 @ w.reshape(cout, -1)).view(n, ho, wo, cin, k, k)           # im2col-row gradients
             if k == 1:
-                dx = x.new_zeros(x.shape)
-                dx[:, :, ::s, ::s] = da.view(n, ho, wo, cin).permute(0, 3, 1, 2)
-            else:
-                dx = F.fold(da.view(n, ho * wo, -1).transpose(1, 2), (h, ww), k, padding=(k - 1) // 2, stride=s)
+                dx = torch.zeros_like(x)                                          # x's memory format
+                dx[:, :, ::s, ::s] = da[..., 0, 0].permute(0, 3, 1, 2)
+            else:                                     # col2im: the 9 taps' strided adds into the padded gradient
+                dxp = x.new_zeros((n, cin, h + 2, ww + 2))
+                for kh in range(3):
+                    for kw in range(3):
+                        dxp[:, :, kh:kh + s * (ho - 1) + 1:s, kw:kw + s * (wo - 1) + 1:s] += da[..., kh, kw].permute(0, 3, 1, 2)
+                dx = dxp[:, :, 1:-1, 1:-1].contiguous()
         return dx, dw, None
 
 
 def gemm_conv_ok(x, k, stride):
-    """The GEMM form is used for NCHW fp32 GPU inputs whose output frames have <= 36 pixels (lip-trunk layers 3-4 at
-    96 / 112 pixel lips) and for every 1x1 shortcut conv (AVSE_TRUNK_GEMM=0 keeps MIOpen)."""
-    if os.environ.get("AVSE_TRUNK_GEMM", "1") != "1" or not x.is_cuda or x.dtype != torch.float32 or not x.is_contiguous():
+    """AVSE_TRUNK_GEMM: "1x1" (default) runs the 1x1 shortcut convs as one GEMM; "all" also the 3x3 convs whose output
+    frames have <= 36 pixels (lip-trunk layers 3-4), which measured slower in the avse1 step (179.6 vs 199 utt/s: the
+    im2col gathers, the col2im adds and hipBLASLt's fp32 tiles for these shapes, profiles/r03_trunk_gemm_op_profile.txt);
+    "0" keeps MIOpen for all.  fp32 GPU inputs; the 3x3 form NCHW only."""
+    mode = os.environ.get("AVSE_TRUNK_GEMM", "1x1")
+    if mode == "0" or not x.is_cuda or x.dtype != torch.float32:
+        return False
+    if k == 1:                                     # NCHW or channels-last
+        return x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last)
+    if not x.is_contiguous():
         return False
     ho, wo = (x.shape[2] - 1) // stride + 1, (x.shape[3] - 1) // stride + 1
-    return k == 1 or ho * wo <= 36
+    return mode == "all" and ho * wo <= 36
 
 
 class PointwiseConv2d(nn.Conv2d):

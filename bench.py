@@ -124,8 +124,8 @@ class Avse1Step:
         self.model = avse1.AVNet().to(dev).train()
         if int(os.environ.get("AVSE_CHANNELS_LAST", "1")):      # NHWC audio convs (+4.5% step rate)
             self.model.net_audiofeat.use_channels_last()
-        if int(os.environ.get("AVSE_LIP_CHANNELS_LAST", "0")):  # NHWC lip trunk: 148 vs 170 utt/s without find-db records for its shapes
-            self.model.net_visualfeat.use_channels_last()
+        if int(os.environ.get("AVSE_LIP_CHANNELS_LAST", "1")):  # NHWC lip trunk: no NCHW<->NHWC transposes around MIOpen's
+            self.model.net_visualfeat.use_channels_last()       # NHWC kernels (201.4 vs 195.7 utt/s, round 3)
         self.lr, self.clip = self.model.lr, None
         self.noisy, self.clean, self.lips = data.avse1_batch(B, dev, 1234 + rank, lip_hw)
         self.avse1 = avse1

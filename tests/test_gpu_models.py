@@ -176,7 +176,7 @@ def test_avse1_wave_frontend_and_train_step_vs_oracle(channels_last):
 
 def test_avse1_bench_step_graph_vs_masked_oracle():
     """The benchmarked avse1 step exactly as bench.py runs it (BASELINE configs[1] layout at B=2, 96x96 lips): HIP STFT
-    inside the step, AudioFeatNet channels-last, lip trunk NCHW, lip branch on its side stream, forward + backward
+    inside the step, AudioFeatNet and lip trunk channels-last, lip branch on its side stream, forward + backward
     replayed from the captured HIP graph.  Loss and every parameter gradient of the second replay vs the fp64 oracle
     (reference baseline/avse1/model.py:114-133) on the step's own STFT features, with the masks of the eager warm-up
     step imposed (same weights and inputs)."""
@@ -187,7 +187,7 @@ def test_avse1_bench_step_graph_vs_masked_oracle():
     st = bench.Avse1Step(2, torch.device(DEV), 0, 1, 96)
     det_init_(st.model, 55)
     _nodrop(st.model)
-    assert st.model.net_audiofeat.channels_last and not st.model.net_visualfeat.channels_last
+    assert st.model.net_audiofeat.channels_last and st.model.net_visualfeat.channels_last
     assert avse1._branch_stream(torch.device(DEV)) is not None          # the lip branch runs on the side stream
     params = list(st.model.named_parameters())
     loss_buf = torch.zeros((), device=DEV)

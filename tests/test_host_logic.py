@@ -63,19 +63,24 @@ def test_avmamba_oracle_assembly_shapes_and_keys():
         list(dict(m.named_parameters()))
 
 
-@pytest.mark.parametrize("k,stride,hw", [(3, 1, 3), (3, 2, 6), (3, 1, 6), (3, 2, 12), (1, 2, 12), (1, 2, 7), (3, 2, 7)])
-def test_gemm_conv_matches_conv2d_fp64(k, stride, hw):
+@pytest.mark.parametrize("k,stride,hw,cl", [(3, 1, 3, False), (3, 2, 6, False), (3, 1, 6, False), (3, 2, 12, False),
+                                           (1, 2, 12, False), (1, 2, 7, False), (3, 2, 7, False), (1, 2, 12, True),
+                                           (1, 1, 6, True)])
+def test_gemm_conv_matches_conv2d_fp64(k, stride, hw, cl):
     """layers._GemmConvFn (the lip-trunk small-frame convs and 1x1 shortcuts as one im2col GEMM, col2im backward) equals
     F.conv2d(padding (k-1)/2, stride, bias=False) in fp64: output and input / weight gradients (pure torch ops, so the
     host runs the same arithmetic the GPU path launches as hipBLASLt GEMMs)."""
     import torch.nn.functional as F
     from avse_challenge_amd.layers import _GemmConvFn
     g = torch.Generator().manual_seed(k * 100 + stride * 10 + hw)
-    x = torch.randn(5, 8, hw, hw, generator=g, dtype=torch.float64, requires_grad=True)
+    x = torch.randn(5, 8, hw, hw, generator=g, dtype=torch.float64)
+    if cl:                                            # the channels-last lip trunk (bench layout)
+        x = x.contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
     w = torch.randn(6, 8, k, k, generator=g, dtype=torch.float64, requires_grad=True)
     y = _GemmConvFn.apply(x, w, stride)
     yr = F.conv2d(x, w, None, stride, (k - 1) // 2)
-    assert y.shape == yr.shape
+    assert y.shape == yr.shape and (not cl or y.is_contiguous(memory_format=torch.channels_last))
     torch.testing.assert_close(y, yr, rtol=1e-12, atol=1e-12)
     gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
     dx, dw = torch.autograd.grad(y, (x, w), gy)
