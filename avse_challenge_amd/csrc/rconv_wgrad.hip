@@ -1,5 +1,5 @@
 // Weight gradient of the ResNet-18 trunk 3x3 convolutions of the lip encoders for gfx950, as an implicit GEMM on the
-// exact-fp32 MFMA (v_mfma_f32_32x32x2_f32), NCHW activations.
+// exact-fp32 MFMA (v_mfma_f32_32x32x2_f32), NCHW or channels-last (NHWC) activations.
 //
 // Replaces the weight-gradient half of nn.Conv2d(cin, cout, 3, stride s, padding 1, bias=False) in the BasicBlocks of
 // /root/reference/baseline/avse1/utils/resnet.py:26-67 (conv3x3 :11-13; cin, cout in {64, 128, 256, 512}, s in {1, 2})
@@ -160,6 +160,111 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(Args s, const float* 
         }
 }
 
+// Channels-last (NHWC) activations (the avse1 bench's lip trunk): same decomposition; the staged tiles are 64-channel
+// slices of contiguous pixel rows, loaded as float4 (16 B per lane, coalesced) and stored as float4 into a 64-float
+// pixel stride (ds_write_b128; the MFMA b32 reads of 32 consecutive channels stay conflict-free).
+__device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, int voff_elems) {
+    const auto raw = __builtin_amdgcn_raw_buffer_load_b128(r, voff_elems * 4, 0, 0);
+    return make_float4(__uint_as_float(raw[0]), __uint_as_float(raw[1]), __uint_as_float(raw[2]), __uint_as_float(raw[3]));
+}
+
+template <int H, int W, int S>
+__global__ __launch_bounds__(THREADS, 2) void wgrad_nhwc_kernel(Args s, const float* __restrict__ x,
+                                                                const float* __restrict__ dy, float* __restrict__ part) {
+    using G = Geo<H, W, S>;
+    constexpr int PSN = CB;                                 // 64-float pixel stride (16-B aligned rows)
+    constexpr int YV4 = (G::P2 * CB / 4 + THREADS - 1) / THREADS, XV4 = (G::NXW * CB / 4 + THREADS - 1) / THREADS;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nblk = s.nco * s.nci;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int kh = bid % KS, ks = bid / KS / nblk, blk = (bid / KS) % nblk;
+    const int cob = blk / s.nci, cib = blk % s.nci;
+    const int c_lo = __builtin_amdgcn_readfirstlane((int)((int64_t)ks * s.chunks / s.ksplit));
+    const int c_hi = __builtin_amdgcn_readfirstlane((int)((int64_t)(ks + 1) * s.chunks / s.ksplit));
+
+    float* sy = lds;                                        // [P2 + 1][64]: dY pixels
+    float* sx = sy + (G::P2 + 1) * PSN;                     // [F * R][WIN][64]: input rows S * r + kh - 1
+    const auto rx = make_rsrc(x, (int64_t)s.N * G::HW * s.CIN);
+    const auto ry = make_rsrc(dy, (int64_t)s.N * G::HWO * s.COUT);
+    const int OOBX = s.N * G::HW * s.CIN, OOBY = s.N * G::HWO * s.COUT;
+
+    float4 yv[YV4], xv[XV4];
+    auto prefetch = [&](int c) {
+        int f0, r0, nf, nr;
+        if (G::FRAMES) {
+            f0 = c * G::F; r0 = 0; nf = min(G::F, s.N - f0); nr = G::HO;
+        } else {
+            f0 = c / G::BANDS; r0 = (c % G::BANDS) * G::R; nf = 1; nr = min(G::R, G::HO - r0);
+        }
+        const int ypix0 = f0 * G::HWO + r0 * G::WO;
+#pragma unroll
+        for (int i = 0; i < YV4; ++i) {
+            const int e = threadIdx.x + i * THREADS, p = e / (CB / 4), c4 = e % (CB / 4);
+            const int f = p / (G::R * G::WO), rem = p % (G::R * G::WO);
+            const bool ok = p < G::P2 && f < nf && rem / G::WO < nr;
+            yv[i] = ld4(ry, ok ? (ypix0 + f * G::HWO + rem) * s.COUT + cob * CB + 4 * c4 : OOBY);
+        }
+#pragma unroll
+        for (int i = 0; i < XV4; ++i) {
+            const int e = threadIdx.x + i * THREADS, q = e / (CB / 4), c4 = e % (CB / 4);
+            const int fr = q / G::WIN, col = q % G::WIN;
+            const int f = fr / G::R, r = fr % G::R;
+            const int hi = S * (r0 + r) + kh - 1, wi = col - 1;
+            const bool ok = q < G::NXW && f < nf && r < nr && hi >= 0 && hi < H && wi >= 0 && wi < W;
+            xv[i] = ld4(rx, ok ? ((f0 + f) * G::HW + hi * W + wi) * s.CIN + cib * CB + 4 * c4 : OOBX);
+        }
+        return nf * nr * G::WO;
+    };
+
+    floatx16 acc[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[k][q] = 0.f;
+    const int half = lane >> 5;
+    const int co_l = (wave >> 1) * 32 + (lane & 31), ci_l = (wave & 1) * 32 + (lane & 31);
+
+    int np = c_lo < c_hi ? prefetch(c_lo) : 0;
+    for (int c = c_lo; c < c_hi; ++c) {
+        const int npc = np;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < YV4; ++i) {
+            const int e = threadIdx.x + i * THREADS;
+            if (e < G::P2 * CB / 4) *reinterpret_cast<float4*>(&sy[e * 4]) = yv[i];
+        }
+#pragma unroll
+        for (int i = 0; i < XV4; ++i) {
+            const int e = threadIdx.x + i * THREADS;
+            if (e < G::NXW * CB / 4) *reinterpret_cast<float4*>(&sx[e * 4]) = xv[i];
+        }
+        __syncthreads();
+        if (c + 1 < c_hi) np = prefetch(c + 1);
+        const int nk = (npc + 1) >> 1;
+        for (int j = 0; j < nk; ++j) {
+            const int p = 2 * j + half;
+            const int fr = p / G::WO, w = p % G::WO;
+            const float a = sy[p * PSN + co_l];
+            const float* pb = sx + (fr * G::WIN + S * w) * PSN + ci_l;
+            const float b0 = pb[0], b1 = pb[PSN], b2 = pb[2 * PSN];
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc[1], 0, 0, 0);
+            acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b2, acc[2], 0, 0, 0);
+        }
+    }
+    float* pp = part + (int64_t)ks * s.COUT * s.CIN * KK;
+    const int ci = cib * CB + ci_l;
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int co = cob * CB + (wave >> 1) * 32 + (q & 3) + 8 * (q >> 2) + 4 * half;
+            pp[((int64_t)co * s.CIN + ci) * KK + kh * KS + kw] = acc[kw][q];
+        }
+}
+
 __global__ void reduce_kernel(const float* __restrict__ part, int nparts, int total, float* __restrict__ dw) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
@@ -178,15 +283,19 @@ int chunks_of(int N) {
 inline int ksplit_for(int chunks, int nblk) { return std::max(1, std::min(chunks, 512 / (KS * nblk))); }
 
 template <int H, int W, int S>
-int launch(int N, int CIN, int COUT, const float* x, const float* dy, float* dw, float* ws, hipStream_t st) {
+int launch(int N, int CIN, int COUT, bool nhwc, const float* x, const float* dy, float* dw, float* ws, hipStream_t st) {
     using G = Geo<H, W, S>;
     Args a;
     a.N = N; a.CIN = CIN; a.COUT = COUT;
     a.chunks = chunks_of<H, W, S>(N);
     a.nci = CIN / CB; a.nco = COUT / CB;
     a.ksplit = ksplit_for(a.chunks, a.nci * a.nco);
-    hipLaunchKernelGGL((wgrad_kernel<H, W, S>), dim3(a.ksplit * a.nci * a.nco * KS), dim3(THREADS), G::LDSB, st, a, x, dy,
-                       ws);
+    if (nhwc)
+        hipLaunchKernelGGL((wgrad_nhwc_kernel<H, W, S>), dim3(a.ksplit * a.nci * a.nco * KS), dim3(THREADS), G::LDSB, st, a,
+                           x, dy, ws);
+    else
+        hipLaunchKernelGGL((wgrad_kernel<H, W, S>), dim3(a.ksplit * a.nci * a.nco * KS), dim3(THREADS), G::LDSB, st, a, x,
+                           dy, ws);
     AVSE_CHECK_LAUNCH();
     const int total = COUT * CIN * KK;
     hipLaunchKernelGGL(reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, ws, a.ksplit, total, dw);
@@ -227,13 +336,14 @@ int64_t avse_rconv_wgrad_workspace_bytes(int64_t N, int64_t CIN, int64_t COUT, i
     return 4 * (int64_t)ksplit_for(chunks_for((int)H, (int)W, (int)stride, (int)N), nblk) * COUT * CIN * KK;
 }
 
-int avse_rconv_wgrad(int64_t N, int64_t CIN, int64_t COUT, int64_t H, int64_t W, int64_t stride, const float* x,
-                     const float* dy, float* dw, float* workspace, avse_stream_t stream) {
+int avse_rconv_wgrad(int64_t N, int64_t CIN, int64_t COUT, int64_t H, int64_t W, int64_t stride, int32_t nhwc,
+                     const float* x, const float* dy, float* dw, float* workspace, avse_stream_t stream) {
     if (!x || !dy || !dw || !workspace) return AVSE_EINVAL;
     if (!supported(N, CIN, COUT, H, W, stride)) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
 #define X_(h, w, s) \
-    if (H == h && W == w && stride == s) return launch<h, w, s>((int)N, (int)CIN, (int)COUT, x, dy, dw, workspace, st);
+    if (H == h && W == w && stride == s) \
+        return launch<h, w, s>((int)N, (int)CIN, (int)COUT, nhwc != 0, x, dy, dw, workspace, st);
     AVSE_RCW_SHAPES(X_)
 #undef X_
     return AVSE_ESHAPE;

@@ -370,10 +370,13 @@ def rconv_wgrad_supported(x, cout, stride):
 
 def rconv_wgrad(x, dy, stride):
     """dW (COUT, CIN, 3, 3) of Conv2d(CIN, COUT, 3, stride, padding=1, bias=False) from the input x (N, CIN, H, W) and
-    the output gradient dy (N, COUT, HO, WO); both are read as contiguous NCHW fp32."""
+    the output gradient dy (N, COUT, HO, WO), fp32; channels-last x takes the NHWC kernel (dy made channels-last),
+    anything else is read as contiguous NCHW."""
     _need_gpu(x, dy)
-    x = x.float().contiguous()
-    dy = dy.float().contiguous()
+    nhwc = x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
+    fmt = torch.channels_last if nhwc else torch.contiguous_format
+    x = x.float().contiguous(memory_format=fmt)
+    dy = dy.float().contiguous(memory_format=fmt)
     n, cin, h, w = x.shape
     cout = dy.shape[1]
     L = _lib.lib()
@@ -382,8 +385,8 @@ def rconv_wgrad(x, dy, stride):
         raise RuntimeError(f"rconv_wgrad: unsupported shape x {tuple(x.shape)}, cout {cout}, stride {stride}")
     out = torch.empty((cout, cin, 3, 3), device=x.device, dtype=torch.float32)
     ws = torch.empty((nb + 3) // 4, device=x.device, dtype=torch.float32)
-    check(L.avse_rconv_wgrad(n, cin, cout, h, w, stride, ptr(x), ptr(dy), ptr(out), ptr(ws), stream_ptr(x.device)),
-          "avse_rconv_wgrad")
+    check(L.avse_rconv_wgrad(n, cin, cout, h, w, stride, int(nhwc), ptr(x), ptr(dy), ptr(out), ptr(ws),
+                             stream_ptr(x.device)), "avse_rconv_wgrad")
     return out
 
 

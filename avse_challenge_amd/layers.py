@@ -341,15 +341,16 @@ class TrunkConv2d(nn.Conv2d):
         s = self.stride[0]
         if gemm_conv_ok(x, 3, s):                          # small frames: one GEMM over all pixels (_GemmConvFn)
             return _GemmConvFn.apply(x, self.weight, s)
-        if x.is_contiguous() and self._use_hip(x, s) and K.rconv_wgrad_supported(x, self.out_channels, s):
+        if ((x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last)) and self._use_hip(x, s)
+                and K.rconv_wgrad_supported(x, self.out_channels, s)):
             return _TrunkConvFn.apply(x, self.weight, s)
         return super().forward(x)
 
     def _use_hip(self, x, s):
-        # AVSE_RCONV_WGRAD: "all", "0", or the default "layer1": the 64 -> 64 stride-1 convs, where the kernel beats
-        # MIOpen inside the avse1 step (1.1 vs ~1.5 ms per launch); the wider layers run slower than MIOpen's
-        # (profiles/r03_rconv_wgrad_bench.jsonl, r03_avse1_step_rconv_all_window_stats.csv)
-        mode = os.environ.get("AVSE_RCONV_WGRAD", "layer1")
+        # AVSE_RCONV_WGRAD: "all", "layer1" (the 64 -> 64 stride-1 convs) or "0" (default).  On the channels-last trunk
+        # the kernel runs 0.50-0.59 of the fp32 peak against MIOpen NHWC's 0.63-0.80 (profiles/r03_rconv_wgrad_nhwc_bench
+        # .jsonl); in the avse1 step: MIOpen 204.1 / 203.3, layer1 202.8, all 198.8 utt/s (profiles/r03_rconv_modes.txt)
+        mode = os.environ.get("AVSE_RCONV_WGRAD", "0")
         if mode == "all":
             return True
         return mode == "layer1" and s == 1 and self.in_channels == 64 and self.out_channels == 64

@@ -771,7 +771,8 @@ def test_dilated_conv2d_module_grads_vs_torch():
                                                    (11, 256, 256, 6, 6, 1), (13, 256, 512, 6, 6, 2),
                                                    (17, 512, 512, 3, 3, 1), (3, 64, 64, 28, 28, 1), (5, 64, 128, 28, 28, 2),
                                                    (3, 256, 512, 7, 7, 2), (19, 512, 512, 4, 4, 1), (2, 64, 64, 56, 56, 1)])
-def test_rconv_wgrad_vs_fp64(N, cin, cout, H, W, stride):
+@pytest.mark.parametrize("cl", [False, True])
+def test_rconv_wgrad_vs_fp64(N, cin, cout, H, W, stride, cl):
     """K.rconv_wgrad (csrc/rconv_wgrad.hip) vs the fp64 weight gradient of Conv2d(cin, cout, 3, stride, padding=1,
     bias=False) (baseline/avse1/utils/resnet.py:11-13): the avse1 trunk shapes at 96x96 lips (24..3 pixels, stride 1
     and 2), the avse4 / C5 ones at 112x112 (28 .. 4: row bands, odd 7x7), the avse2 56x56 layer, frame counts that leave a
@@ -785,10 +786,12 @@ def test_rconv_wgrad_vs_fp64(N, cin, cout, H, W, stride):
     xd, dyd = x.double(), dy.double()
     truth = torch.nn.grad.conv2d_weight(xd, (cout, cin, 3, 3), dyd, stride, 1)
     bound = torch.nn.grad.conv2d_weight(xd.abs(), (cout, cin, 3, 3), dyd.abs(), stride, 1)
-    got = K().rconv_wgrad(x.to(DEV), dy.to(DEV), stride)
+    fmt = torch.channels_last if cl else torch.contiguous_format          # cl: the NHWC kernel (bench trunk layout)
+    xg, dyg = x.to(DEV).contiguous(memory_format=fmt), dy.to(DEV).contiguous(memory_format=fmt)
+    got = K().rconv_wgrad(xg, dyg, stride)
     worst = float(((got.double().cpu() - truth).abs() / (bound + 1e-30)).max())
     assert worst <= 1e-6, worst
-    assert torch.equal(got, K().rconv_wgrad(x.to(DEV), dy.to(DEV), stride))
+    assert torch.equal(got, K().rconv_wgrad(xg, dyg, stride))
 
 
 def test_trunk_conv2d_module_grads_vs_torch(monkeypatch):

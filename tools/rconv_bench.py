@@ -33,14 +33,16 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--frames", type=int, default=2400)
     p.add_argument("--iters", type=int, default=5)
+    p.add_argument("--nhwc", action="store_true", help="channels-last activations (the NHWC kernel / MIOpen NHWC)")
     a = p.parse_args()
     N = a.frames
     for cin, cout, hw, s in SHAPES:
         ho = (hw - 1) // s + 1
-        x = torch.randn(N, cin, hw, hw, device="cuda")
-        dy = torch.randn(N, cout, ho, ho, device="cuda")
+        fmt = torch.channels_last if a.nhwc else torch.contiguous_format
+        x = torch.randn(N, cin, hw, hw, device="cuda").contiguous(memory_format=fmt)
+        dy = torch.randn(N, cout, ho, ho, device="cuda").contiguous(memory_format=fmt)
         flops = 2.0 * N * cout * cin * 9 * ho * ho
-        rec = {"cin": cin, "cout": cout, "hw": hw, "stride": s, "gflop": round(flops / 1e9, 1)}
+        rec = {"cin": cin, "cout": cout, "hw": hw, "stride": s, "nhwc": a.nhwc, "gflop": round(flops / 1e9, 1)}
         for name, fn in (("hip", lambda: K.rconv_wgrad(x, dy, s)),
                          ("miopen", lambda: torch.nn.grad.conv2d_weight(x, (cout, cin, 3, 3), dy, s, 1))):
             ms = timeit(fn, a.iters)
