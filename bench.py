@@ -44,7 +44,7 @@ os.environ.setdefault("PYTORCH_MIOPEN_SUGGEST_NHWC_BATCHNORM", "1")
 METRIC = "utterances/sec (3s@16kHz + 75 lip frames)"
 # HBM bytes per launch of each roofline kernel, from rocprofv3 PMC passes (tools/pmc_traffic.sh:
 # FETCH_SIZE and WRITE_SIZE in separate passes, corrected as MI355X_MICROARCH.md prescribes)
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFS = 157.3          # FP32 matrix (= vector) peak, spec
 
@@ -142,30 +142,30 @@ class Avse1Step:
                 "stft_frames": 376, "lip_frames": 75, "lip_hw": self.lip_hw, "parallelism": f"dp{world}"}
 
     def roofline(self, dev):
-        """Dominant kernel class of the step: the 64->64 5x5 dilated Conv2d of AudioFeatNet (MFMA-bound).
-        Times conv3 (dilation 4) forward at the step's shape with HIP events; FLOPs = 2*B*64*64*25*376*257."""
-        conv = self.model.net_audiofeat.conv3
-        x = torch.randn(self.B, 64, 376, 257, device=dev)
-        if getattr(self.model.net_audiofeat, "channels_last", False):
-            x = x.to(memory_format=torch.channels_last)        # the layout the step runs the conv in
-        with torch.no_grad():
-            for _ in range(3):
-                conv(x)
-            torch.cuda.synchronize()
-            n = 10
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(n):
-                conv(x)
-            e1.record()
-            torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / n
+        """Dominant kernel class of the step: the weight gradient of AudioFeatNet's 64->64 5x5 dilated Conv2d on the
+        hand-written MFMA kernel (csrc/dconv_wgrad.hip; 4 launches, the largest per-step kernel time in the rocprofv3
+        trace).  Times conv3's (dilation 4) at the step's shape, channels-last, with HIP events on torch's current
+        stream (the kernel's launch stream); FLOPs = 2*B*64*64*25*376*257.  The library forward of the same conv is
+        reported beside it (roofline_library)."""
+        from avse_challenge_amd import kernels as K
+        cl = torch.channels_last
+        x = torch.randn(self.B, 64, 376, 257, device=dev).contiguous(memory_format=cl)
+        dy = torch.randn(self.B, 64, 376, 257, device=dev).contiguous(memory_format=cl)
         flops = 2.0 * self.B * 64 * 64 * 25 * 376 * 257
+        ms = _event_ms(lambda: K.dconv_wgrad(x, dy, 4), n=10, warm=3)
         ach = flops / (ms * 1e-3) / 1e12
-        return _with_traffic({"kernel": "AudioFeatNet.conv3 fwd (Conv2d 64->64 5x5 dil 4, MIOpen)", "bound": "mfma",
-                              "achieved": round(ach, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
-                              "frac": round(ach / FP32_PEAK_TFS, 4), "traffic": None, "avg_ms": round(ms, 4),
-                              "algorithmic_flops_per_launch": flops}, "conv3" if self.B == 32 else "-")
+        roof = _with_traffic({"kernel": "avse_dconv_wgrad (AudioFeatNet.conv3 weight gradient: Conv2d 64->64 5x5 dil 4, "
+                                        "HIP MFMA implicit GEMM)", "bound": "mfma", "achieved": round(ach, 2),
+                              "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFS, 4),
+                              "traffic": None, "avg_ms": round(ms, 4), "algorithmic_flops_per_launch": flops},
+                             "dconv_wgrad" if self.B == 32 else "-")
+        conv = self.model.net_audiofeat.conv3
+        with torch.no_grad():
+            ms_f = _event_ms(lambda: conv(x), n=10, warm=3)
+        ach_f = flops / (ms_f * 1e-3) / 1e12
+        roof["roofline_library"] = {"kernel": "AudioFeatNet.conv3 fwd (MIOpen)", "achieved": round(ach_f, 2),
+                                    "frac": round(ach_f / FP32_PEAK_TFS, 4), "avg_ms": round(ms_f, 4)}
+        return roof
 
     def cpu_baseline(self):
         """the oracle's full train step (numpy librosa-0.8.1 STFT + AVNet fwd + bwd + Adam) on the

@@ -3,7 +3,8 @@
 python tools/roofline_kernels.py PHASE [--n N]
 PHASE: scan (Mamba-L C3 training scan fwd, B=64), scan_bwd (its backward as the model calls it), dwconv (avse4 C4 TCN dwconv fwd, B=16, dil 128),
        cconv (causal conv fwd, B=64, D=1024: the dword-access calibration kernel, known bytes),
-       conv3 (avse1 C2 AudioFeatNet conv3 fwd, B=32, NHWC, MIOpen).
+       conv3 (avse1 C2 AudioFeatNet conv3 fwd, B=32, NHWC, MIOpen),
+       dconv_wgrad (the same conv's weight gradient on csrc/dconv_wgrad.hip: the step's largest kernel class).
 Inputs are created before a device sync, then the kernel runs N times; the PMC summary counts only
 non-PyTorch kernels, so input generation does not enter the per-launch numbers.
 """
@@ -17,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from avse_challenge_amd import kernels as K  # noqa: E402
 
 SHAPES = {"scan": (64, 1024, 3999), "scan_bwd": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999),
-          "conv3": (32, 64, 376, 257)}
+          "conv3": (32, 64, 376, 257), "dconv_wgrad": (32, 64, 376, 257)}
 
 
 def aligned(b, d, l, g, scale=1.0):
@@ -54,6 +55,11 @@ def main():
         x = torch.randn(b, d, l, device=dev, generator=g)
         w, cb = torch.randn(d, 4, device=dev, generator=g), torch.randn(d, device=dev, generator=g)
         fn = lambda: K.causal_conv1d_fwd(x, w, cb, True)  # noqa: E731
+    elif a.phase == "dconv_wgrad":
+        cl = torch.channels_last
+        x = torch.randn(*SHAPES["dconv_wgrad"], device=dev, generator=g).to(memory_format=cl)
+        dy = torch.randn(*SHAPES["dconv_wgrad"], device=dev, generator=g).to(memory_format=cl)
+        fn = lambda: K.dconv_wgrad(x, dy, 4)  # noqa: E731
     else:
         from avse_challenge_amd import avse1
         conv = avse1.AVNet().to(dev).net_audiofeat

@@ -5,8 +5,8 @@ averaged over the dispatches of the phase's timed kernel; PyTorch's own kernels 
 are excluded.  Correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE reports half the bytes of 16-B/lane
 streaming reads; other widths are uncalibrated, so the dword-access correction is calibrated here on
 the causal conv forward, whose bytes are known exactly (reads x once, writes out once: 4 B each per
-element), and applied to the dword-access kernels (scan, dwconv, cconv).  MIOpen's conv kernels use
-wide loads: the documented x2 applies.
+element), and applied to the dword-access kernels (scan, dwconv, cconv).  MIOpen's conv kernels and the dilated-conv
+weight gradient (float4 buffer loads) use wide loads: the documented x2 applies.
 """
 import csv
 import glob
@@ -17,7 +17,7 @@ from collections import defaultdict
 
 root = sys.argv[1]
 SHAPES = {"scan": (64, 1024, 3999), "scan_bwd": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999),
-          "conv3": (32, 64, 376, 257)}
+          "conv3": (32, 64, 376, 257), "dconv_wgrad": (32, 64, 376, 257)}
 
 
 def per_launch(phase, counter):
@@ -51,7 +51,7 @@ for ph in raw:
     wr, _ = raw[ph]["WRITE_SIZE"]
     if fr is None or wr is None:
         continue
-    rf, wf = (2.0, 1.0) if ph == "conv3" else (cal_r, cal_w)
+    rf, wf = (2.0, 1.0) if ph in ("conv3", "dconv_wgrad") else (cal_r, cal_w)     # 16-B/lane loads: the documented x2
     res[ph] = {"kernel": kern, "fetch_bytes": round(fr * rf), "write_bytes": round(wr * wf),
                "traffic_bytes": round(fr * rf + wr * wf), "raw_fetch_size_bytes": round(fr), "raw_write_size_bytes": round(wr),
                "read_correction": round(rf, 4), "write_correction": round(wf, 4)}
