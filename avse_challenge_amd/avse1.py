@@ -137,7 +137,7 @@ class VisualFeatNet(nn.Module):           # model.py:17-58
         self.trunk.to(memory_format=torch.channels_last if on else torch.contiguous_format)
         return self
 
-    def forward(self, lips):              # (B, 3, T, H, W) raw 0..255 float -> (B, T, 512)
+    def forward(self, lips):              # (B, 3, T, H, W) raw 0..255 (uint8 as stored, or float) -> (B, T, 512)
         Bn = lips.shape[0]
         conv, bn, act, pool = self.frontend3D
         x = maxpool3d(bn_act(conv(lips), bn, act), pool)
@@ -177,7 +177,12 @@ class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 conv
         if self.channels_last:
             x = x.contiguous(memory_format=torch.channels_last)
         for i in range(1, self.num_conv + 1):
-            x = bn_act(getattr(self, f"conv{i}")(x), getattr(self, f"bn{i}"), "relu")
+            conv, bn = getattr(self, f"conv{i}"), getattr(self, f"bn{i}")
+            if bn.training and bn.track_running_stats and conv.bias is not None and conv.hip_ok(x):
+                # the conv bias goes into the BatchNorm (no separate bias-add pass): DilatedConv2d docstring
+                x = bn_act(conv(x, bias_to_bn=True), bn, "relu", folded_bias=conv.bias)
+            else:
+                x = bn_act(conv(x), bn, "relu")
         x = bn_act(self.convf(x), self.bn_last, "relu")
         return x.permute(0, 2, 1, 3).reshape(-1, T, Fb * self.last_filter)
 
@@ -234,7 +239,7 @@ class AVNet(nn.Module):
             side.wait_stream(main)
             lips = inp["lip_images"]
             with torch.cuda.stream(side):
-                vis = self.net_visualfeat(lips.float())                        # (B, 75, 512)
+                vis = self.net_visualfeat(lips)          # (B, 75, 512); lips.float() of model.py:122 in the conv
             lips.record_stream(side)
         audio = self.net_audiofeat(spec)
         if side is not None:
@@ -244,7 +249,7 @@ class AVNet(nn.Module):
             comb = audio
         else:
             if side is None:
-                vis = self.net_visualfeat(inp["lip_images"].float())          # (B, 75, 512)
+                vis = self.net_visualfeat(inp["lip_images"])                  # (B, 75, 512)
             # F.interpolate(nearest, size=(T, 512)) on (B, 1, 75, 512) == gather of rows floor(t*75/T)
             idx = torch.div(torch.arange(T, device=spec.device) * vis.shape[1], T, rounding_mode="floor")
             comb = torch.cat((vis.index_select(1, idx), audio), dim=-1)

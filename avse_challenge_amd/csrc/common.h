@@ -54,6 +54,11 @@ template <> struct bufld<bf16_t> {
         return __uint_as_float(((uint32_t)v) << 16);
     }
 };
+template <> struct bufld<uint8_t> {
+    __device__ static inline float ld(__amdgpu_buffer_rsrc_t r, int voff_elems, int soff_elems) {
+        return (float)__builtin_amdgcn_raw_buffer_load_b8(r, voff_elems, soff_elems, 0);
+    }
+};
 template <typename T> struct bufst;
 template <> struct bufst<float> {
     __device__ static inline void st(__amdgpu_buffer_rsrc_t r, int voff_elems, int soff_elems, float v) {

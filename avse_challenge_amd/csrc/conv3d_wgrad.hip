@@ -1,5 +1,6 @@
 // Weight gradient of the lip front-end Conv3d (Cout 64, small Cin, kernel (KT,KH,KW), stride (1,2,2))
-// for gfx950, as an implicit GEMM on the exact-fp32 MFMA (v_mfma_f32_32x32x2_f32).
+// for gfx950, as an implicit GEMM on the exact-fp32 MFMA (v_mfma_f32_32x32x2_f32).  The input is read in its
+// stored dtype: fp32, or the uint8 lip frames themselves (avse_conv3d_wgrad_u8: no fp32 copy of the clip).
 //
 // Replaces the weight-gradient half of nn.Conv3d(3, 64, (5,7,7), stride (1,2,2), pad (2,3,3))
 // in /root/reference/baseline/avse1/model.py:29-34 (frontend3D; avse4 utils.py:100-106 is the
@@ -37,8 +38,8 @@ struct Shape {
 // (blockIdx.y), so a slice stages only the input rows its columns touch.  Software pipelined:
 // the next row's input window and dY row are loaded into registers (raw buffer loads, out-of-range
 // -> 0, no waits at issue) while the MFMAs of the current row run out of LDS.
-template <int NTW, int RPW>
-__global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(Shape s, const float* __restrict__ x,
+template <typename T, int NTW, int RPW>
+__global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(Shape s, const T* __restrict__ x,
                                                            const float* __restrict__ dy, float* __restrict__ part) {
     extern __shared__ float lds[];
     const int WIN = 2 * (s.WO - 1) + s.KW;
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(Shape s, const float*
             for (int q = 0; q < 2; ++q) {
                 const int c = lane + 64 * q, wi = c - s.PW;
                 const bool ok = rowok && c < WIN && wi >= 0 && wi < s.W;
-                xr[i][q] = bufld<float>::ld(rx, ok ? base + c : nx, 0);
+                xr[i][q] = bufld<T>::ld(rx, ok ? base + c : nx, 0);
             }
         }
         const int64_t yb = ((int64_t)b * COUT * s.TO + t) * yplane + (int64_t)ho * s.WO;
@@ -165,15 +166,10 @@ inline int nparts_for(int rows) { return rows < 1024 ? rows : 1024; }
 
 using namespace avse::c3w;
 
-extern "C" {
-
-int64_t avse_conv3d_wgrad_workspace_bytes(int64_t B, int64_t TO, int64_t HO, int64_t N) {
-    return 4 * (int64_t)nparts_for((int)(B * TO * HO)) * COUT * N;
-}
-
-int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,
-                      int64_t PT, int64_t PH, int64_t PW, const float* x, const float* dy, float* dw, int32_t accumulate,
-                      float* workspace, avse_stream_t stream) {
+template <typename XT>
+static int conv3d_wgrad_impl(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH,
+                             int64_t KW, int64_t PT, int64_t PH, int64_t PW, const XT* x, const float* dy, float* dw,
+                             int32_t accumulate, float* workspace, avse_stream_t stream) {
     if (!x || !dy || !dw || !workspace) return AVSE_EINVAL;
     Shape s;
     s.B = (int)B; s.CIN = (int)CIN; s.T = (int)T; s.H = (int)H; s.W = (int)W;
@@ -191,7 +187,8 @@ int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, i
     const int WIN = 2 * (s.WO - 1) + s.KW;
     if (WIN > 128) return AVSE_ESHAPE;
     // 32-bit buffer offsets: both tensors must stay under 2 GiB
-    if ((int64_t)s.B * s.CIN * s.T * s.H * s.W >= (1LL << 29) || (int64_t)s.B * COUT * s.TO * s.HO * s.WO >= (1LL << 29))
+    if ((int64_t)s.B * s.CIN * s.T * s.H * s.W * (int64_t)sizeof(XT) >= (1LL << 31) ||
+        (int64_t)s.B * COUT * s.TO * s.HO * s.WO >= (1LL << 29))
         return AVSE_ESHAPE;
     // staged rows of the widest slice must fit the RPW registers per wave
     int max_nrs = 0;
@@ -205,13 +202,31 @@ int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, i
     if (lds > 64 * 1024) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid(s.nparts, nsplit), block(THREADS);
-    hipLaunchKernelGGL((wgrad_kernel<NTW, RPW>), grid, block, lds, st, s, x, dy, workspace);
+    hipLaunchKernelGGL((wgrad_kernel<XT, NTW, RPW>), grid, block, lds, st, s, x, dy, workspace);
     AVSE_CHECK_LAUNCH();
     const int total = COUT * s.N;
     hipLaunchKernelGGL(reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, workspace, s.nparts, total, dw,
                        (int)accumulate);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
+}
+
+extern "C" {
+
+int64_t avse_conv3d_wgrad_workspace_bytes(int64_t B, int64_t TO, int64_t HO, int64_t N) {
+    return 4 * (int64_t)nparts_for((int)(B * TO * HO)) * COUT * N;
+}
+
+int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,
+                      int64_t PT, int64_t PH, int64_t PW, const float* x, const float* dy, float* dw,
+                      int32_t accumulate, float* workspace, avse_stream_t stream) {
+    return conv3d_wgrad_impl<float>(B, CIN, T, H, W, KT, KH, KW, PT, PH, PW, x, dy, dw, accumulate, workspace, stream);
+}
+
+int avse_conv3d_wgrad_u8(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,
+                         int64_t PT, int64_t PH, int64_t PW, const uint8_t* x, const float* dy, float* dw,
+                         int32_t accumulate, float* workspace, avse_stream_t stream) {
+    return conv3d_wgrad_impl<uint8_t>(B, CIN, T, H, W, KT, KH, KW, PT, PH, PW, x, dy, dw, accumulate, workspace, stream);
 }
 
 }  // extern "C"

@@ -16,6 +16,8 @@
 // per K-step (2 pixels: lanes 0-31 pixel 2j, lanes 32-63 pixel 2j + 1) one A read, 5 B reads (the kw-shifted pixel)
 // and 5 MFMAs.  The next chunk's tiles are loaded into registers (float4 buffer loads, out-of-range -> 0) while the
 // current chunk's MFMAs run.  Per-workgroup partial sums go to a workspace summed by a second kernel (deterministic).
+// The bias gradient db[co] = sum dY[.][co] comes along: the kh = 0 workgroups add up the dY pieces they already hold
+// in registers (a fixed 4-channel group per thread), so the avse1 step needs no separate reduction pass over dY.
 #include <algorithm>
 
 #include "common.h"
@@ -48,7 +50,8 @@ __device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, int voff_elems) {
 }
 
 __global__ __launch_bounds__(THREADS, 3) void wgrad_kernel(Shape s, const float* __restrict__ x,
-                                                           const float* __restrict__ dy, float* __restrict__ part) {
+                                                           const float* __restrict__ dy, float* __restrict__ part,
+                                                           float* __restrict__ dbpart) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -99,6 +102,8 @@ __global__ __launch_bounds__(THREADS, 3) void wgrad_kernel(Shape s, const float*
         for (int q = 0; q < 16; ++q) acc[k][q] = 0.f;
 
     const int co = (wave >> 1) * 32 + (lane & 31), ci = (wave & 1) * 32 + (lane & 31), half = lane >> 5;
+    const bool want_db = dbpart != nullptr && kh == 0;     // workgroup-uniform
+    float4 dsum = {0.f, 0.f, 0.f, 0.f};                    // channels 4 (tid % 16) .. + 3
     if (c_lo_u < c_hi_u) prefetch(c_lo_u, cur_len);
     for (int c = c_lo_u; c < c_hi_u; ++c) {
         const int len = cur_len;
@@ -107,6 +112,12 @@ __global__ __launch_bounds__(THREADS, 3) void wgrad_kernel(Shape s, const float*
         for (int i = 0; i < A_V4; ++i) {
             const int e = (threadIdx.x + i * THREADS) * 4;
             if (e < PX_MAX * C) *reinterpret_cast<float4*>(&sa[e]) = ar[i];
+        }
+        if (want_db) {                                     // pixels past the piece loaded as 0
+#pragma unroll
+            for (int i = 0; i < A_V4; ++i) {
+                dsum.x += ar[i].x; dsum.y += ar[i].y; dsum.z += ar[i].z; dsum.w += ar[i].w;
+            }
         }
 #pragma unroll
         for (int i = 0; i < X_V4; ++i) {
@@ -137,6 +148,17 @@ __global__ __launch_bounds__(THREADS, 3) void wgrad_kernel(Shape s, const float*
             for (int k = 0; k < KS; ++k) b0[k] = b1[k];
         }
     }
+    if (want_db) {                                         // 16 threads per channel group -> dbpart[r][co]
+        __syncthreads();
+        reinterpret_cast<float4*>(lds)[threadIdx.x] = dsum;
+        __syncthreads();
+        if (threadIdx.x < C) {
+            const int g = threadIdx.x >> 2, k = threadIdx.x & 3;
+            float v = 0.f;
+            for (int t = 0; t < THREADS / 16; ++t) v += lds[(t * 16 + g) * 4 + k];
+            dbpart[(int64_t)r * C + threadIdx.x] = v;
+        }
+    }
     // partial tiles out: part[bid][kw][co][ci]; C map col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
     float* p = part + ((int64_t)r * KS + kh) * KS * C * C;
 #pragma unroll
@@ -148,11 +170,19 @@ __global__ __launch_bounds__(THREADS, 3) void wgrad_kernel(Shape s, const float*
         }
 }
 
-// dW[co][ci][kh][kw] = sum over ranges of part[range][kh][kw][co][ci]
-__global__ void reduce_kernel(const float* __restrict__ part, int ranges, float* __restrict__ dw) {
+// dW[co][ci][kh][kw] = sum over ranges of part[range][kh][kw][co][ci]; db[co] = sum over ranges of dbpart[range][co]
+__global__ void reduce_kernel(const float* __restrict__ part, const float* __restrict__ dbpart, int ranges,
+                              float* __restrict__ dw, float* __restrict__ db) {
     constexpr int TOTAL = KS * KS * C * C;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= TOTAL) return;
+    if (i >= TOTAL) {
+        if (db != nullptr && i < TOTAL + C) {
+            float v = 0.f;
+            for (int g = 0; g < ranges; ++g) v += dbpart[(int64_t)g * C + i - TOTAL];
+            db[i - TOTAL] = v;
+        }
+        return;
+    }
     float v = 0.f;
     for (int g = 0; g < ranges; ++g) v += part[(int64_t)g * TOTAL + i];
     const int ci = i % C, co = (i / C) % C, kw = (i / (C * C)) % KS, kh = i / (KS * C * C);
@@ -175,11 +205,11 @@ extern "C" {
 
 int64_t avse_dconv_wgrad_workspace_bytes(int64_t N, int64_t H, int64_t W, int64_t dil) {
     const int64_t npieces = (W + PX_MAX - 1) / PX_MAX;
-    return 4 * (int64_t)ranges_for((int)dil, (int)(N * H * npieces)) * KS * KS * C * C;
+    return 4 * (int64_t)ranges_for((int)dil, (int)(N * H * npieces)) * (KS * KS * C * C + C);
 }
 
 int avse_dconv_wgrad(int64_t N, int64_t H, int64_t W, int64_t dil, const float* x, const float* dy, float* dw,
-                     float* workspace, avse_stream_t stream) {
+                     float* db, float* workspace, avse_stream_t stream) {
     if (!x || !dy || !dw || !workspace) return AVSE_EINVAL;
     if (N <= 0 || H <= 0 || W <= 0 || dil <= 0 || dil > MAX_DIL) return AVSE_ESHAPE;
     const int64_t npieces = (W + PX_MAX - 1) / PX_MAX;
@@ -191,10 +221,13 @@ int avse_dconv_wgrad(int64_t N, int64_t H, int64_t W, int64_t dil, const float* 
     s.chunks = (int)(N * H * npieces);
     s.ranges = ranges_for(s.dil, s.chunks);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(wgrad_kernel, dim3(s.ranges * KS), dim3(THREADS), lds_bytes(s.dil), st, s, x, dy, workspace);
-    AVSE_CHECK_LAUNCH();
     constexpr int TOTAL = KS * KS * C * C;
-    hipLaunchKernelGGL(reduce_kernel, dim3((TOTAL + 255) / 256), dim3(256), 0, st, workspace, s.ranges, dw);
+    float* dbpart = db ? workspace + (int64_t)s.ranges * TOTAL : nullptr;
+    hipLaunchKernelGGL(wgrad_kernel, dim3(s.ranges * KS), dim3(THREADS), lds_bytes(s.dil), st, s, x, dy, workspace,
+                       dbpart);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(reduce_kernel, dim3((TOTAL + C + 255) / 256), dim3(256), 0, st, workspace, dbpart, s.ranges,
+                       dw, db);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

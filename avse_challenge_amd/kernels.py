@@ -314,9 +314,11 @@ CONV3D_WGRAD_MAX_WO = 64      # output width the MFMA kernel stages per LDS row 
 
 
 def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
-    """dW of Conv3d(Cin, 64, kernel_size, stride (1,2,2), padding, bias=False) -> (64, Cin, KT, KH, KW)."""
+    """dW of Conv3d(Cin, 64, kernel_size, stride (1,2,2), padding, bias=False) -> (64, Cin, KT, KH, KW).
+    x: fp32, or the uint8 lip frames as stored (read as their float values, no fp32 copy)."""
     _need_gpu(x, dy)
-    x = x.float().contiguous()
+    u8 = x.dtype == torch.uint8
+    x = x.contiguous() if u8 else x.float().contiguous()
     dy = dy.float().contiguous()
     Bn, Cin, Tn, H, W = x.shape
     KT, KH, KW = kernel_size
@@ -330,9 +332,40 @@ def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
     L = _lib.lib()
     ws = torch.empty((L.avse_conv3d_wgrad_workspace_bytes(Bn, dy.shape[2], dy.shape[3], N) + 3) // 4,
                      device=x.device, dtype=torch.float32)
-    check(L.avse_conv3d_wgrad(Bn, Cin, Tn, H, W, KT, KH, KW, PT, PH, PW, ptr(x), ptr(dy), ptr(out),
-                              int(bool(accumulate)), ptr(ws), stream_ptr(x.device)), "avse_conv3d_wgrad")
+    fn = L.avse_conv3d_wgrad_u8 if u8 else L.avse_conv3d_wgrad
+    check(fn(Bn, Cin, Tn, H, W, KT, KH, KW, PT, PH, PW, ptr(x), ptr(dy), ptr(out),
+             int(bool(accumulate)), ptr(ws), stream_ptr(x.device)), "avse_conv3d_wgrad")
     return out
+
+
+def conv3d_fwd_supported(x, w, stride, padding):
+    """True when the MFMA forward (conv3d_fwd.hip) is compiled for this lip front-end shape."""
+    return (tuple(stride) == (1, 2, 2) and tuple(padding) == (2, 3, 3) and tuple(w.shape[0:1]) == (64,)
+            and tuple(w.shape[2:]) == (5, 7, 7) and x.dim() == 5 and x.shape[1] == w.shape[1]
+            and x.dtype in (torch.uint8, torch.float32)
+            and _lib.lib().avse_conv3d_fwd_workspace_bytes(x.shape[1], x.shape[3], x.shape[4]) > 0)
+
+
+def conv3d_fwd(x, w):
+    """Conv3d(Cin, 64, (5, 7, 7), stride (1, 2, 2), padding (2, 3, 3), bias=False) forward of the lip front-end:
+    x (B, Cin, T, H, W) uint8 frames or fp32, w (64, Cin, 5, 7, 7) fp32 -> (B, 64, T, Ho, Wo) fp32."""
+    _need_gpu(x, w)
+    if x.dtype not in (torch.uint8, torch.float32):
+        raise RuntimeError(f"conv3d_fwd: x must be uint8 or float32, got {x.dtype}")
+    x = x.contiguous()
+    w = w.float().contiguous()
+    Bn, Cin, Tn, H, W = x.shape
+    if tuple(w.shape) != (64, Cin, 5, 7, 7):
+        raise RuntimeError(f"conv3d_fwd: weight {tuple(w.shape)} is not (64, {Cin}, 5, 7, 7)")
+    L = _lib.lib()
+    nb = L.avse_conv3d_fwd_workspace_bytes(Cin, H, W)
+    if nb <= 0:
+        raise RuntimeError(f"conv3d_fwd: shape Cin={Cin} {H}x{W} is not compiled in (conv3d_fwd.hip)")
+    ws = torch.empty((nb + 3) // 4, device=x.device, dtype=torch.float32)
+    y = torch.empty((Bn, 64, Tn, (H - 1) // 2 + 1, (W - 1) // 2 + 1), device=x.device, dtype=torch.float32)
+    check(L.avse_conv3d_fwd(Bn, Cin, Tn, H, W, 2 if x.dtype == torch.uint8 else 0, ptr(x), ptr(w), ptr(y), ptr(ws),
+                            stream_ptr(x.device)), "avse_conv3d_fwd")
+    return y
 
 
 # ------------------------------------------------------------------------ dilated Conv2d dW (AudioFeatNet)
@@ -340,9 +373,10 @@ def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
 DCONV_WGRAD_MAX_DIL = 16       # dconv_wgrad.hip MAX_DIL
 
 
-def dconv_wgrad(x, dy, dilation):
+def dconv_wgrad(x, dy, dilation, bias_grad=False):
     """dW (64, 64, 5, 5) of Conv2d(64, 64, 5, padding=2*dilation, dilation) from the conv input x and the output
-    gradient dy, both (N, 64, H, W) fp32; channels-last memory is read as it lies, anything else is made so."""
+    gradient dy, both (N, 64, H, W) fp32; channels-last memory is read as it lies, anything else is made so.
+    bias_grad: return (dW, db) with db = dy summed over (N, H, W), computed in the same pass."""
     _need_gpu(x, dy)
     if x.shape[1] != 64 or dy.shape != x.shape:
         raise RuntimeError(f"dconv_wgrad expects (N, 64, H, W) input and gradient, got {tuple(x.shape)}, {tuple(dy.shape)}")
@@ -354,9 +388,10 @@ def dconv_wgrad(x, dy, dilation):
     out = torch.empty((64, 64, 5, 5), device=x.device, dtype=torch.float32)
     ws = torch.empty((L.avse_dconv_wgrad_workspace_bytes(Bn, H, W, dilation) + 3) // 4, device=x.device,
                      dtype=torch.float32)
-    check(L.avse_dconv_wgrad(Bn, H, W, dilation, ptr(x), ptr(dy), ptr(out), ptr(ws), stream_ptr(x.device)),
-          "avse_dconv_wgrad")
-    return out
+    db = torch.empty(64, device=x.device, dtype=torch.float32) if bias_grad else None
+    check(L.avse_dconv_wgrad(Bn, H, W, dilation, ptr(x), ptr(dy), ptr(out), ptr(db) if bias_grad else None, ptr(ws),
+                             stream_ptr(x.device)), "avse_dconv_wgrad")
+    return (out, db) if bias_grad else out
 
 
 # ------------------------------------------------------------------------ ResNet trunk 3x3 Conv2d dW

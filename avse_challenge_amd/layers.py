@@ -73,10 +73,21 @@ class _BNActFn(torch.autograd.Function):
                 dalpha if ctx.needs_input_grad[3] else None, dres, None, None, None, None, None, None)
 
 
-def bn_act(x, bn, act=None, res=None):
+def bn_act(x, bn, act=None, res=None, folded_bias=None):
     """act(bn(x) [+ res]) for an nn.BatchNorm{1,2,3}d `bn` (its parameters, buffers, momentum and eps; running
     statistics and num_batches_tracked updated in train mode as torch does).  act: None, "relu" or a PReLU module.
-    x: fp32 contiguous or channels-last; the output keeps x's memory format."""
+    x: fp32 contiguous or channels-last; the output keeps x's memory format.
+    folded_bias (training mode only): x is a convolution output whose per-channel bias was left out; the result is
+    act(bn(x + bias)) — equal to act(bn(x)), the batch statistics shift with the bias — and the running mean takes
+    the bias in (momentum * bias)."""
+    if folded_bias is not None:
+        if not (bn.training and bn.track_running_stats) or res is not None:
+            raise RuntimeError("bn_act: folded_bias needs a training-mode BatchNorm with running stats, no residual")
+        y = bn_act(x, bn, act)
+        # through .data, as the kernel's own running-stat update: no version bump (under DDP the BatchNorm buffers are
+        # views of one flat tensor, and a bump would invalidate every library BatchNorm's saved running stats)
+        bn.running_mean.data.add_(folded_bias.detach(), alpha=bn.momentum)
+        return y
     if not x.is_cuda:
         raise RuntimeError("bn_act runs on the GPU kernels only")
     if os.environ.get("AVSE_BNACT", "1") != "1":            # A/B switch: the library BatchNorm + separate act
@@ -145,12 +156,22 @@ def _conv3d_fwd_folded(x, w, padding):
 
 
 class _LipConv3dFn(torch.autograd.Function):
+    """The lip front-end Conv3d (baseline/avse1/model.py:29-34). x may be the uint8 frames as stored (the
+    reference's `lip_images.float()`, model.py:122, happens inside the kernels: no fp32 copy of the clip)."""
+
     @staticmethod
     def forward(ctx, x, w, stride, padding):
+        hip = (os.environ.get("AVSE_CONV3D_HIP", "1") == "1" and x.is_cuda
+               and K.conv3d_fwd_supported(x, w, stride, padding))
+        if not hip and x.dtype != torch.float32:
+            x = x.float()
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.padding = stride, padding
-        # the avse1 front-end (Cin = 3) only: the Cin = 1 front-ends of avse2 / avse4 fold to a 5-channel Conv2d
-        # without a find-db record (a find pass over the avse4 step did not finish in 400 s): they keep conv3d
+        if hip:                           # MFMA implicit GEMM (csrc/conv3d_fwd.hip)
+            return K.conv3d_fwd(x, w)
+        # other shapes: the avse1 front-end as a Conv2d over frames (Cin = 3); the Cin = 1 front-ends of avse2 /
+        # avse4 fold to a 5-channel Conv2d without a find-db record (a find pass over the avse4 step did not finish
+        # in 400 s): they keep conv3d
         if os.environ.get("AVSE_CONV3D_FOLD", "1") == "1" and tuple(stride) == (1, 2, 2) and x.shape[1] == 3:
             return _conv3d_fwd_folded(x, w, padding)
         return F.conv3d(x, w, None, stride, padding)
@@ -166,7 +187,7 @@ class _LipConv3dFn(torch.autograd.Function):
             if dy.shape[-1] <= K.CONV3D_WGRAD_MAX_WO:
                 dw = K.conv3d_wgrad(x, dy, tuple(w.shape[2:]), ctx.padding)
             else:   # wider frames (avse2's 224x224 lips -> 112 output columns): the library's GPU kernel
-                dw = torch.nn.grad.conv3d_weight(x, w.shape, dy, ctx.stride, ctx.padding)
+                dw = torch.nn.grad.conv3d_weight(x.float(), w.shape, dy, ctx.stride, ctx.padding)
         return dx, dw, None, None
 
 
@@ -179,16 +200,26 @@ class LipConv3d(nn.Conv3d):
         return _LipConv3dFn.apply(x, self.weight, tuple(self.stride), tuple(self.padding))
 
 
+def _conv2d_dgrad(x, w, dy, stride, padding, dilation):
+    """Input gradient of conv2d(x, w) in x's memory format.  torch.nn.grad.conv2d_input builds an NCHW input from
+    the shape alone, so for channels-last activations MIOpen returned NCHW and the consumer copied it back (6 copies
+    of (32, 64, 376, 257) per avse1 step, tools/avse1_op_profile.py --kernels direct_copy)."""
+    pair = lambda v: [v, v] if isinstance(v, int) else list(v)                       # noqa: E731
+    return torch.ops.aten.convolution_backward(dy, x, w, None, pair(stride), pair(padding), pair(dilation), False,
+                                               [0, 0], 1, [True, False, False])[0]
+
+
 class _DilatedConvFn(torch.autograd.Function):
-    """Conv2d(64, 64, 5, padding=2d, dilation=d) with the weight gradient on the MFMA implicit-GEMM kernel
-    (csrc/dconv_wgrad.hip); forward and input gradient on MIOpen."""
+    """Conv2d(64, 64, 5, padding=2d, dilation=d) with the weight (and bias) gradient on the MFMA implicit-GEMM kernel
+    (csrc/dconv_wgrad.hip); forward and input gradient on MIOpen.  add_bias=False leaves the bias out of the output
+    (for a training-mode BatchNorm consumer, which removes it: see DilatedConv2d) but still returns its gradient."""
 
     @staticmethod
-    def forward(ctx, x, w, b, dilation):
+    def forward(ctx, x, w, b, dilation, add_bias):
         ctx.save_for_backward(x, w)
         ctx.dilation = dilation
         pad = 2 * dilation
-        return F.conv2d(x, w, b, 1, pad, dilation)
+        return F.conv2d(x, w, b if add_bias else None, 1, pad, dilation)
 
     @staticmethod
     def backward(ctx, dy):
@@ -196,30 +227,42 @@ class _DilatedConvFn(torch.autograd.Function):
         d = ctx.dilation
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.nn.grad.conv2d_input(x.shape, w, dy, 1, 2 * d, d)
-        if ctx.needs_input_grad[1]:
+            dx = _conv2d_dgrad(x, w, dy, 1, 2 * d, d)
+        if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            dw, db = K.dconv_wgrad(x, dy, d, bias_grad=True)
+        elif ctx.needs_input_grad[1]:
             dw = K.dconv_wgrad(x, dy, d)
-        if ctx.needs_input_grad[2]:
+        elif ctx.needs_input_grad[2]:
             db = dy.sum((0, 2, 3))
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 class DilatedConv2d(nn.Conv2d):
     """nn.Conv2d(cin, cout, 5, padding=2*dilation, dilation) — the avse1 AudioFeatNet convs (same parameters and
     state_dict keys).  The 64 -> 64 ones on GPU tensors in channels-last memory (the benchmarked layout) take their
-    weight gradient from csrc/dconv_wgrad.hip; other inputs (the 1 -> 64 conv1, NCHW activations) run the library
-    convolution unchanged."""
+    weight and bias gradients from csrc/dconv_wgrad.hip; other inputs (the 1 -> 64 conv1, NCHW activations) run the
+    library convolution unchanged.
+
+    forward(x, bias_to_bn=True) on the HIP path returns the convolution WITHOUT the bias: the caller feeds it to a
+    training-mode BatchNorm through bn_act(..., folded_bias=self.bias), which normalises z + b and z alike (batch
+    mean and variance shift with b) and adds momentum * b to the running mean.  That saves the library's separate
+    bias-add pass over the (B, 64, 376, 257) output (5 per avse1 step); the bias gradient is exact either way."""
 
     def __init__(self, cin, cout, kernel_size=5, padding=0, dilation=1):
         super().__init__(cin, cout, kernel_size, padding=padding, dilation=dilation)
         assert self.padding == (2 * self.dilation[0],) * 2 and self.kernel_size == (5, 5)
 
-    def forward(self, x):
-        d = self.dilation[0]
-        if (os.environ.get("AVSE_DCONV_WGRAD", "1") == "1" and x.is_cuda and self.in_channels == 64
-                and self.out_channels == 64 and d <= K.DCONV_WGRAD_MAX_DIL and x.dtype == torch.float32
-                and x.is_contiguous(memory_format=torch.channels_last)):
-            return _DilatedConvFn.apply(x, self.weight, self.bias, d)
+    def hip_ok(self, x):
+        return (os.environ.get("AVSE_DCONV_WGRAD", "1") == "1" and x.is_cuda and self.in_channels == 64
+                and self.out_channels == 64 and self.dilation[0] <= K.DCONV_WGRAD_MAX_DIL
+                and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last))
+
+    def forward(self, x, bias_to_bn=False):
+        if self.hip_ok(x):
+            add_bias = not (bias_to_bn and self.bias is not None)
+            return _DilatedConvFn.apply(x, self.weight, self.bias, self.dilation[0], add_bias)
+        if bias_to_bn:
+            raise RuntimeError("DilatedConv2d: bias_to_bn needs the HIP path (check hip_ok first)")
         return super().forward(x)
 
 
@@ -238,7 +281,7 @@ class _TrunkConvFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.nn.grad.conv2d_input(x.shape, w, dy, ctx.stride, 1)
+            dx = _conv2d_dgrad(x, w, dy, ctx.stride, 1, 1)
         if ctx.needs_input_grad[1]:
             dw = K.rconv_wgrad(x, dy, ctx.stride)
         return dx, dw, None

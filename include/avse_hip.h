@@ -26,7 +26,7 @@ extern "C" {
 typedef void* avse_stream_t; /* a hipStream_t */
 
 enum { AVSE_OK = 0, AVSE_EINVAL = -1, AVSE_ESHAPE = -2, AVSE_EDTYPE = -3, AVSE_ELAUNCH = -4, AVSE_EALIGN = -5 };
-enum { AVSE_F32 = 0, AVSE_BF16 = 1 };
+enum { AVSE_F32 = 0, AVSE_BF16 = 1, AVSE_U8 = 2 };
 
 const char* avse_strerror(int code);
 int avse_abi_version(void);
@@ -157,6 +157,15 @@ int avse_stft_fwd(int64_t batch, int64_t T, const float* wave, float* mag, float
 int avse_istft(int64_t batch, int64_t frames, int64_t length, const float* mag, const float* phase_spec,
                float* frames_buf, float* wave_out, avse_stream_t stream);
 
+/* Forward of the avse1 lip front-end nn.Conv3d(3, 64, (5, 7, 7), stride (1, 2, 2), padding (2, 3, 3), bias=False)
+ * (baseline/avse1/model.py:29-34, frontend3D[0]) as an MFMA implicit GEMM that reads the lips in their stored dtype.
+ * x: (B, CIN, T, H, W) contiguous, x_dtype AVSE_U8 (the raw uint8 frames) or AVSE_F32; w: (64, CIN, 5, 7, 7) fp32;
+ * y: (B, 64, T, HO, WO) fp32 with HO = (H - 1) / 2 + 1.  Compiled shapes: CIN 3, 96 x 96 (workspace_bytes returns 0
+ * for any other; the call then returns AVSE_ESHAPE).  workspace: the weights re-laid per plane pair. */
+int64_t avse_conv3d_fwd_workspace_bytes(int64_t CIN, int64_t H, int64_t W);
+int avse_conv3d_fwd(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int32_t x_dtype, const void* x,
+                    const float* w, float* y, float* workspace, avse_stream_t stream);
+
 /* ---------------------------------------------------------------- lip front-end Conv3d dW
  * Weight gradient of nn.Conv3d(CIN, 64, (KT,KH,KW), stride (1,2,2), pad (PT,PH,PW), bias=False)
  * — baseline/avse1/model.py:29-34 (CIN 3, (5,7,7), pad (2,3,3)); baseline/avse4/utils.py:100-106
@@ -167,16 +176,20 @@ int64_t avse_conv3d_wgrad_workspace_bytes(int64_t B, int64_t TO, int64_t HO, int
 int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,
                       int64_t PT, int64_t PH, int64_t PW, const float* x, const float* dy, float* dw,
                       int32_t accumulate, float* workspace, avse_stream_t stream);
+/* the same with x the uint8 lip frames (values 0..255 read as floats: the cast of baseline/avse1/model.py:122) */
+int avse_conv3d_wgrad_u8(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,
+                         int64_t PT, int64_t PH, int64_t PW, const uint8_t* x, const float* dy, float* dw,
+                         int32_t accumulate, float* workspace, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- dilated Conv2d dW --------
  * Weight gradient of nn.Conv2d(64, 64, 5, padding=2*dil, dilation=dil) — conv2..conv5 of the avse1 AudioFeatNet
  * (baseline/avse1/model.py:199-215, dil 2, 4, 8, 16).  x, dy: (N, H, W, 64) channels-last fp32 (x the conv input, dy
  * the output gradient); dw: (64, 64, 5, 5) (Cout, Cin, KH, KW) contiguous, overwritten.  Exact-fp32 MFMA implicit GEMM;
- * dil <= 16, N*H*W*64 < 2^29.  The bias gradient is dy's channel sum (not computed here).
+ * dil <= 16, N*H*W*64 < 2^29.  db (nullable): the bias gradient, dy's channel sum (64), from the same pass.
  */
 int64_t avse_dconv_wgrad_workspace_bytes(int64_t N, int64_t H, int64_t W, int64_t dil);
 int avse_dconv_wgrad(int64_t N, int64_t H, int64_t W, int64_t dil, const float* x, const float* dy, float* dw,
-                     float* workspace, avse_stream_t stream);
+                     float* db, float* workspace, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- ResNet trunk 3x3 Conv2d dW -----
  * Weight gradient of nn.Conv2d(CIN, COUT, 3, stride, padding=1, bias=False) — the lip-encoder BasicBlock convs

@@ -29,8 +29,8 @@ def capture_masks(model):
     names = {id(m): n for n, m in model.named_modules()}
     orig = avse1.bn_act
 
-    def spy(x, bn, act=None, res=None):
-        y = orig(x, bn, act, res)
+    def spy(x, bn, act=None, res=None, folded_bias=None):
+        y = orig(x, bn, act, res, folded_bias=folded_bias)
         if act is not None:
             key = names[id(bn)] if act == "relu" else names[id(act)]
             if act != "relu":

@@ -55,10 +55,18 @@ def test_host_side_validation_without_gpu():
     ws = L.avse_scan_bwd_workspace_bytes(2, 128, 100, 16)
     assert ws == 4 * (2 * 2 * 32 * 100 + 2 * 128 * 18)
     # dilated Conv2d weight gradient: null pointers, dilation range
-    assert L.avse_dconv_wgrad(2, 10, 257, 4, None, dummy, dummy, dummy, None) == -1
-    assert L.avse_dconv_wgrad(2, 10, 257, 0, dummy, dummy, dummy, dummy, None) == -2
-    assert L.avse_dconv_wgrad(2, 10, 257, 17, dummy, dummy, dummy, dummy, None) == -2
-    assert L.avse_dconv_wgrad_workspace_bytes(32, 376, 257, 16) % (4 * 25 * 64 * 64) == 0
+    assert L.avse_dconv_wgrad(2, 10, 257, 4, None, dummy, dummy, None, dummy, None) == -1
+    assert L.avse_dconv_wgrad(2, 10, 257, 0, dummy, dummy, dummy, None, dummy, None) == -2
+    assert L.avse_dconv_wgrad(2, 10, 257, 17, dummy, dummy, dummy, dummy, dummy, None) == -2
+    assert L.avse_dconv_wgrad_workspace_bytes(32, 376, 257, 16) % (4 * (25 * 64 * 64 + 64)) == 0
+    # lip Conv3d forward: compiled shape table, null pointers, unsupported shape / dtype
+    assert L.avse_conv3d_fwd_workspace_bytes(3, 96, 96) == 4 * 8 * 49 * 2 * 64
+    assert L.avse_conv3d_fwd_workspace_bytes(1, 88, 88) == 0
+    assert L.avse_conv3d_fwd(2, 3, 75, 96, 96, 2, None, dummy, dummy, dummy, None) == -1
+    assert L.avse_conv3d_fwd(2, 1, 75, 88, 88, 2, dummy, dummy, dummy, dummy, None) == -2
+    assert L.avse_conv3d_fwd(0, 3, 75, 96, 96, 2, dummy, dummy, dummy, dummy, None) == -2
+    assert L.avse_conv3d_fwd(2, 3, 75, 96, 96, 1, dummy, dummy, dummy, dummy, None) == -3
+    assert L.avse_conv3d_wgrad_u8(2, 3, 5, 96, 96, 5, 7, 7, 2, 3, 3, None, dummy, dummy, 0, dummy, None) == -1
 
 
 def test_product_never_imports_oracle():

@@ -309,6 +309,66 @@ def test_conv3d_wgrad_vs_fp64(cin, T, H, W):
     close(got2, 2 * ref, 4e-6 * scale * (1 + x.numel() / 1e5) ** 0.5, 0, "dW accumulate")
 
 
+def test_conv3d_wgrad_uint8_equals_fp32():
+    """avse_conv3d_wgrad_u8 reads the uint8 lip frames themselves: bitwise the fp32 kernel's result on their float
+    values (same products, same order)."""
+    g = torch.Generator().manual_seed(704)
+    xu = torch.randint(0, 256, (2, 3, 5, 96, 96), generator=g, dtype=torch.uint8)
+    y = torch.nn.functional.conv3d(xu.double(), det_input((64, 3, 5, 7, 7), 705).double(), None, (1, 2, 2), (2, 3, 3))
+    dy = det_input(tuple(y.shape), 706).to(DEV)
+    a = K().conv3d_wgrad(xu.to(DEV), dy, (5, 7, 7), (2, 3, 3))
+    b = K().conv3d_wgrad(xu.to(DEV).float(), dy, (5, 7, 7), (2, 3, 3))
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype,T", [(torch.uint8, 7), (torch.float32, 6), (torch.uint8, 1)])
+def test_conv3d_fwd_vs_fp64(dtype, T):
+    """K.conv3d_fwd (csrc/conv3d_fwd.hip) vs the fp64 Conv3d(3, 64, (5,7,7), (1,2,2), (2,3,3)) of the avse1 lip
+    front-end (baseline/avse1/model.py:29-34) at its 96 x 96 frames: every output within 1e-6 of its sum of |terms|
+    (one rounding per exact-f32 MFMA product-accumulate); clips of 1 .. 7 frames cover the zero time padding on
+    both sides; uint8 frames are read as stored."""
+    g = torch.Generator().manual_seed(707 + T)
+    if dtype == torch.uint8:
+        x = torch.randint(0, 256, (2, 3, T, 96, 96), generator=g, dtype=torch.uint8)
+    else:
+        x = det_input((2, 3, T, 96, 96), 708, "uniform", 255.0)
+    w = det_input((64, 3, 5, 7, 7), 709) / 50
+    truth = torch.nn.functional.conv3d(x.double(), w.double(), None, (1, 2, 2), (2, 3, 3))
+    bound = torch.nn.functional.conv3d(x.double().abs(), w.double().abs(), None, (1, 2, 2), (2, 3, 3))
+    assert K().conv3d_fwd_supported(x, w, (1, 2, 2), (2, 3, 3))
+    got = K().conv3d_fwd(x.to(DEV), w.to(DEV))
+    assert got.shape == truth.shape and got.dtype == torch.float32
+    worst = float(((got.double().cpu() - truth).abs() / (bound + 1e-30)).max())
+    assert worst <= 1e-6, worst
+    assert torch.equal(got, K().conv3d_fwd(x.to(DEV), w.to(DEV)))          # deterministic
+
+
+def test_conv3d_fwd_unsupported_shapes():
+    x = torch.zeros(1, 1, 5, 88, 88, dtype=torch.uint8)
+    assert not K().conv3d_fwd_supported(x, torch.zeros(64, 1, 5, 7, 7), (1, 2, 2), (2, 3, 3))
+    assert not K().conv3d_fwd_supported(torch.zeros(1, 3, 5, 96, 96, dtype=torch.float64), torch.zeros(64, 3, 5, 7, 7),
+                                        (1, 2, 2), (2, 3, 3))
+    with pytest.raises(RuntimeError):
+        K().conv3d_fwd(x.to(DEV), torch.zeros(64, 1, 5, 7, 7, device=DEV))
+
+
+def test_lip_conv3d_module_uint8_frames():
+    """LipConv3d on the uint8 frames (the HIP forward and the uint8 weight gradient) equals it on their float
+    values, output and weight gradient bitwise."""
+    from avse_challenge_amd.layers import LipConv3d
+    m = LipConv3d(3, 64, (5, 7, 7)).to(DEV)
+    g = torch.Generator().manual_seed(711)
+    xu = torch.randint(0, 256, (2, 3, 4, 96, 96), generator=g, dtype=torch.uint8).to(DEV)
+    y = m(xu)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    w1 = m.weight.grad.clone()
+    m.weight.grad = None
+    y2 = m(xu.float())
+    y2.backward(gy)
+    assert torch.equal(y, y2) and torch.equal(w1, m.weight.grad)
+
+
 def test_lip_conv3d_module_grad():
     from avse_challenge_amd.layers import LipConv3d
     m = LipConv3d(3, 64, (5, 7, 7)).to(DEV)
@@ -739,6 +799,55 @@ def test_dconv_wgrad_vs_fp64(N, H, W, dil):
     # NCHW inputs are converted, same result; deterministic (no atomics): bitwise equal on rerun
     got2 = K().dconv_wgrad(x.to(DEV), dy.to(DEV), dil)
     assert torch.equal(got, got2)
+    # the bias gradient from the same pass: dy's channel sums, within 1e-6 of the sum of |dy|
+    got3, db = K().dconv_wgrad(x.to(DEV).contiguous(memory_format=cl), dy.to(DEV).contiguous(memory_format=cl), dil,
+                               bias_grad=True)
+    assert torch.equal(got3, got)
+    dbt, dbb = dyd.sum((0, 2, 3)), dyd.abs().sum((0, 2, 3))
+    assert float(((db.double().cpu() - dbt).abs() / dbb).max()) <= 1e-6
+
+
+def test_audiofeat_bias_folded_into_batchnorm():
+    """AudioFeatNet (channels-last, training mode) with the conv2..conv5 biases folded into their BatchNorms
+    (DilatedConv2d bias_to_bn + bn_act folded_bias) vs the same net with the biases added by the library convolution
+    (AVSE_DCONV_WGRAD=0): output and BatchNorm running statistics agree to fp32 rounding."""
+    import copy
+    import os
+    from avse_challenge_amd import avse1
+    torch.manual_seed(5)
+    a = avse1.AudioFeatNet().to(DEV).use_channels_last()
+    for m in a.modules():
+        if isinstance(m, torch.nn.Conv2d) and m.bias is not None:
+            torch.nn.init.uniform_(m.bias, -0.5, 0.5)            # a bias large enough to matter
+    b = copy.deepcopy(a)
+    spec = det_input((2, 1, 40, 70), 1860).abs().to(DEV)
+    gy = det_input((2, 40, 280), 1861).to(DEV)
+    assert a.conv2.hip_ok(torch.empty(1, 64, 4, 4, device=DEV).contiguous(memory_format=torch.channels_last))
+    ya = a(spec)
+    (ya * gy).sum().backward()
+    old = os.environ.get("AVSE_DCONV_WGRAD")
+    os.environ["AVSE_DCONV_WGRAD"] = "0"
+    try:
+        yb = b(spec)
+        (yb * gy).sum().backward()
+    finally:
+        if old is None:
+            del os.environ["AVSE_DCONV_WGRAD"]
+        else:
+            os.environ["AVSE_DCONV_WGRAD"] = old
+    sc = lambda t: max(1e-6, float(t.detach().abs().max()))                                        # noqa: E731
+    close(ya, yb, 1e-4 * sc(yb), 0, "y")
+    # gradients: the two fp32 runs round differently, so single ReLU masks flip and the strongly cancelling sums
+    # below them (bn0's 1-element weight gradient: 0.5 % of the whole vector moved) differ by more than any
+    # rounding bar.  The folded model's gradients are checked against the fp64 oracle with the masks imposed
+    # (test_gpu_models.py::test_avse1_wave_frontend_and_train_step_vs_oracle[True]); here: every conv2..conv5 bias
+    # gradient is its output gradient's channel sum, which BatchNorm makes ~0 (<< the weight gradient's scale)
+    pa = dict(a.named_parameters())
+    for i in range(2, 6):
+        assert float(pa[f"conv{i}.bias"].grad.abs().max()) <= 1e-4 * sc(pa[f"conv{i}.weight"].grad), i
+    ba, bb = dict(a.named_buffers()), dict(b.named_buffers())
+    for k in ba:
+        close(ba[k].float(), bb[k].float(), 1e-5 * sc(bb[k].float()), 0, k)
 
 
 def test_dilated_conv2d_module_grads_vs_torch():

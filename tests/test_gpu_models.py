@@ -102,7 +102,7 @@ def _nodrop(m):
 GRAD_FLOOR = 1e-3
 
 
-def _avse1_grads_vs_masked_oracle(loss, grads, masks, rb, seed=55):
+def _avse1_grads_vs_masked_oracle(loss, grads, masks, rb, seed=55, buffers=None):
     """Our avse1 train step (``loss``, ``grads`` {name: tensor}, ``masks`` from avse1_parity.capture_masks) vs the fp64
     oracle on the same weights and the CPU fp32 batch ``rb``, with our activation masks and L1 signs imposed
     (tests/avse1_parity.py): loss within 1e-5; per parameter the max error relative to the fp64 gradient's max within
@@ -119,6 +119,11 @@ def _avse1_grads_vs_masked_oracle(loss, grads, masks, rb, seed=55):
     remove()
     n_flips = check_flips(flips)
     assert abs(float(loss) - float(loss64)) < 1e-5 * max(1.0, abs(float(loss64))), (float(loss), float(loss64))
+    if buffers is not None:           # BatchNorm running statistics after the one step (the folded conv biases)
+        b64 = dict(ref64.named_buffers())
+        for k, v in buffers.items():
+            if "running" in k:
+                close(v, b64[k], 1e-5 * float(b64[k].abs().max()) + 1e-6, 0, k)
     ref64u = _nodrop(det_init_(avse1_ref.AVNet(), seed).double().train())
     ref32 = _nodrop(det_init_(avse1_ref.AVNet(), seed).train())
     tg = _nodrop(det_init_(avse1_ref.AVNet(), seed).to(DEV).train())
@@ -171,7 +176,8 @@ def test_avse1_wave_frontend_and_train_step_vs_oracle(channels_last):
     with capture_masks(ours) as masks:
         loss = ours.training_step({k: v.to(DEV) for k, v in rb.items()})
     loss.backward()
-    _avse1_grads_vs_masked_oracle(loss, {k: p.grad for k, p in ours.named_parameters()}, masks, rb)
+    _avse1_grads_vs_masked_oracle(loss, {k: p.grad for k, p in ours.named_parameters()}, masks, rb,
+                                  buffers=dict(ours.named_buffers()))
 
 
 def test_avse1_bench_step_graph_vs_masked_oracle():

@@ -1,7 +1,7 @@
 """torch.profiler view of one eager avse1 C2 train step (bench.Avse1Step, B=32): device time per aten op and input
 shapes, to attribute the copy / transpose / add kernels of the step to their callers.
 python tools/avse1_op_profile.py [--batch 32] [--top 40] [--kernels PATTERN]
---kernels PAT[,PAT...]: instead of the op table, list every launch of a kernel whose name contains PATTERN with the
+--kernels PAT[/PAT...]: instead of the op table, list every launch of a kernel whose name contains PATTERN with the
 aten op that launched it, its input shapes and the innermost avse_challenge_amd / bench source line on the stack."""
 import argparse
 import collections
@@ -50,7 +50,7 @@ def main():
         return
     # kernel -> launching op: the innermost CPU op whose kernels list holds it (autograd backward ops run on a
     # separate thread; their stack is empty, so the site column names the forward op's node instead)
-    for pat in a.kernels.split(","):
+    for pat in a.kernels.split("/"):
         rows = collections.defaultdict(lambda: [0, 0.0])
         for ev in prof.events():
             for k in ev.kernels:
