@@ -118,6 +118,10 @@ SIGNATURES = {
     "avse_dwconv_gln_fwd": (c_i32, [c_i64] * 5 + [c_vp] * 5 + [c_f32] + [c_vp] * 5),
     "avse_dwconv_gln_bwd": (c_i32, [c_i64] * 5 + [c_vp] * 14),
     "avse_lstm_padded_hidden": (c_i64, [c_i64]),
+    "avse_lstm_group_size": (c_i64, [c_i64, c_i64]),
+    "avse_lstm_group_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "avse_lstm_fwd_group": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "avse_lstm_bwd_group": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_lstm_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "avse_lstm_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }

@@ -697,16 +697,46 @@ def lstm_fwd(gx, w_hh, hout=None, reverse=False):
     H = H4 // 4
     if tuple(w_hh.shape) != (H4, H):
         raise RuntimeError(f"w_hh must be ({H4}, {H}), got {tuple(w_hh.shape)}")
-    whhT = w_hh.float().t().contiguous()
     if hout is None:
         hout = torch.empty((Bn, T, H), device=gx.device, dtype=torch.float32)
     elif hout.dtype != torch.float32 or hout.stride(-1) != 1 or tuple(hout.shape) != (Bn, T, H):
         raise RuntimeError("hout must be an fp32 (B, T, H) view with unit stride over H")
     c_all = torch.empty((Bn, T, H), device=gx.device, dtype=torch.float32)
     gates = torch.empty((Bn, T, H4), device=gx.device, dtype=torch.float32)
-    check(_lib.lib().avse_lstm_fwd(Bn, T, H, int(bool(reverse)), ptr(gx), ptr(whhT), ptr(hout), hout.stride(0),
-                                   hout.stride(1), ptr(c_all), ptr(gates), stream_ptr(gx.device)), "avse_lstm_fwd")
+    L = _lib.lib()
+    ws = _lstm_group_ws(L, Bn, H, gx.device)
+    if ws is not None:      # W_hh resident in LDS, each sequence over G workgroups (csrc/lstm_group.hip)
+        check(L.avse_lstm_fwd_group(Bn, T, H, int(bool(reverse)), ptr(gx), ptr(w_hh.float().contiguous()), ptr(hout),
+                                    hout.stride(0), hout.stride(1), ptr(c_all), ptr(gates), ptr(ws),
+                                    stream_ptr(gx.device)), "avse_lstm_fwd_group")
+        return hout, c_all, gates
+    whhT = w_hh.float().t().contiguous()
+    check(L.avse_lstm_fwd(Bn, T, H, int(bool(reverse)), ptr(gx), ptr(whhT), ptr(hout), hout.stride(0),
+                          hout.stride(1), ptr(c_all), ptr(gates), stream_ptr(gx.device)), "avse_lstm_fwd")
     return hout, c_all, gates
+
+
+_LSTM_GROUP_WS = []     # the workspaces of the grouped launches (status word at offset 0), for lstm_group_status
+
+
+def _lstm_group_ws(L, Bn, H, device):
+    """Workspace of the grouped LSTM kernels, or None when they do not apply (AVSE_LSTM_GROUP=0, or B * G > 256
+    workgroups, or H > 512): those shapes run lstm.hip's one-workgroup-per-sequence kernels."""
+    if os.environ.get("AVSE_LSTM_GROUP", "1") != "1":
+        return None
+    nb = int(L.avse_lstm_group_workspace_bytes(Bn, H))
+    if nb <= 0:
+        return None
+    ws = torch.empty((nb + 15) // 16 * 4, device=device, dtype=torch.int32)
+    _LSTM_GROUP_WS.append(ws)
+    del _LSTM_GROUP_WS[:-8]
+    return ws
+
+
+def lstm_group_status():
+    """0 when every recent grouped LSTM launch completed its hand-offs; else the timeout code one of them wrote
+    (0x71000000 + step): a sequence's workgroups were not co-resident (synchronises the device)."""
+    return max([int(w[0].item()) & 0xFFFFFFFF for w in _LSTM_GROUP_WS] + [0])
 
 
 def lstm_bwd(dh, gates, c_all, w_hh, reverse=False):
@@ -718,9 +748,15 @@ def lstm_bwd(dh, gates, c_all, w_hh, reverse=False):
         dh = dh.contiguous()
     Bn, T, H = dh.shape
     L = _lib.lib()
+    dg = torch.empty((Bn, T, 4 * H), device=dh.device, dtype=torch.float32)
+    ws = _lstm_group_ws(L, Bn, H, dh.device)
+    if ws is not None:
+        check(L.avse_lstm_bwd_group(Bn, T, H, int(bool(reverse)), ptr(dh), dh.stride(0), dh.stride(1),
+                                    ptr(gates.contiguous()), ptr(c_all.contiguous()), ptr(w_hh.float().contiguous()),
+                                    ptr(dg), ptr(ws), stream_ptr(dh.device)), "avse_lstm_bwd_group")
+        return dg
     Hp = int(L.avse_lstm_padded_hidden(H))
     w_pad = torch.nn.functional.pad(w_hh.float(), (0, Hp - H)).contiguous()
-    dg = torch.empty((Bn, T, 4 * H), device=dh.device, dtype=torch.float32)
     check(L.avse_lstm_bwd(Bn, T, H, int(bool(reverse)), ptr(dh), dh.stride(0), dh.stride(1), ptr(gates.contiguous()),
                           ptr(c_all.contiguous()), ptr(w_pad), ptr(dg), stream_ptr(dh.device)), "avse_lstm_bwd")
     return dg

@@ -714,13 +714,16 @@ def test_c5_cconv_bf16_production_shape_vs_oracle():
 
 # ------------------------------------------------------------------ LSTM recurrence (avse1 FusionNet, avse2 DPRNN)
 
+@pytest.mark.parametrize("group", ["1", "0"])
 @pytest.mark.parametrize("B,T,I,H,bidir", [(2, 376, 1540, 257, False), (3, 40, 1028, 257, False), (2, 17, 64, 128, True),
                                            (5, 9, 30, 61, True), (1, 1, 8, 5, False)])
-def test_lstm_vs_torch_fp64(B, T, I, H, bidir):
-    """layers.HipLSTM (one HIP launch per direction and pass) vs torch.nn.LSTM in fp64 on the CPU with the same
-    weights: output and the gradients of the input and every parameter (max error relative to the tensor's max
-    <= 2e-5 for the output, 5e-5 for gradients: fp32 accumulation over T steps)."""
+def test_lstm_vs_torch_fp64(B, T, I, H, bidir, group, monkeypatch):
+    """layers.HipLSTM (one HIP launch per direction and pass; group "1": the grouped kernels of lstm_group.hip, "0":
+    one workgroup per sequence, lstm.hip) vs torch.nn.LSTM in fp64 on the CPU with the same weights: output and the
+    gradients of the input and every parameter (max error relative to the tensor's max <= 2e-5 for the output,
+    5e-5 for gradients: fp32 accumulation over T steps)."""
     from avse_challenge_amd.layers import HipLSTM
+    monkeypatch.setenv("AVSE_LSTM_GROUP", group)
     torch.manual_seed(T + H)
     ref = torch.nn.LSTM(I, H, 1, batch_first=True, bidirectional=bidir).double()
     ours = HipLSTM(I, H, 1, batch_first=True, bidirectional=bidir).to(DEV)
@@ -743,6 +746,34 @@ def test_lstm_vs_torch_fp64(B, T, I, H, bidir):
     rp = dict(ref.named_parameters())
     for k, p in ours.named_parameters():
         close(p.grad, rp[k].grad, 5e-5 * sc(rp[k].grad), 0, k)
+    assert K().lstm_group_status() == 0
+
+
+def test_lstm_group_kernels_at_the_avse1_shape(monkeypatch):
+    """The grouped recurrence at the avse1 C2 FusionNet shape (B = 32 sequences x G = 8 workgroups = 256, the whole
+    chip, T = 376, H = 257) vs lstm.hip's one workgroup per sequence: h, c, gates and the backward gate gradients
+    within 1e-5 of them relative to their max (the dot products are summed in a different order); deterministic;
+    every hand-off completed."""
+    B, T, H = 32, 376, 257
+    assert K()._lib.lib().avse_lstm_group_size(B, H) == 8
+    gx = det_input((B, T, 4 * H), 1620).to(DEV)
+    w = (0.06 * det_input((4 * H, H), 1621)).to(DEV)
+    dh = det_input((B, T, H), 1622).to(DEV)
+    monkeypatch.setenv("AVSE_LSTM_GROUP", "1")
+    h1, c1, g1 = K().lstm_fwd(gx, w)
+    d1 = K().lstm_bwd(dh, g1, c1, w)
+    for rev in (False, True):
+        hr, cr, gr = K().lstm_fwd(gx, w, reverse=rev)
+        dr = K().lstm_bwd(dh, gr, cr, w, reverse=rev)
+        assert K().lstm_group_status() == 0
+        monkeypatch.setenv("AVSE_LSTM_GROUP", "0")
+        h0, c0, g0 = K().lstm_fwd(gx, w, reverse=rev)
+        d0 = K().lstm_bwd(dh, g0, c0, w, reverse=rev)
+        monkeypatch.setenv("AVSE_LSTM_GROUP", "1")
+        for a_, b_, n_ in ((hr, h0, "h"), (cr, c0, "c"), (gr, g0, "gates")):
+            close(a_, b_, 1e-5 * float(b_.abs().max()), 0, f"{n_} reverse={rev}")
+        close(dr, d0, 1e-5 * float(d0.abs().max()), 0, f"dgates reverse={rev}")
+    assert torch.equal(K().lstm_fwd(gx, w)[0], h1) and torch.equal(K().lstm_bwd(dh, g1, c1, w), d1)   # deterministic
 
 
 # ------------------------------------------------------------------ fused dwconv <-> PReLU -> gLN (avse4 TCN)
