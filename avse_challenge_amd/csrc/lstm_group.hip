@@ -13,7 +13,7 @@
 //                  workgroup sweeps all H granules back into LDS (cdna_hip_programming.md §6 Guideline 16, form R2:
 //                  the data is the flag, no fence).
 //   backward step: the own units' pre-activation gate gradients, then the partial dh_{t-1} = W_own^T dg_own over ALL
-//                  H units (thread per unit), published as H granules; each workgroup sums the G partials of its own
+//                  H units (two lanes per unit), published as H granules; each workgroup sums the G partials of its own
 //                  units in a fixed order (deterministic).
 //
 // Granule slots alternate by step parity, so a producer one step ahead never overwrites a slot a slower consumer of
@@ -23,7 +23,6 @@
 // the status word and every later wait of the launch gives up at once (the outputs are then garbage; the host reads
 // the status word, the workspace's first uint32: kernels.lstm_group_status).
 #include <algorithm>
-#include <cstdlib>
 
 #include "common.h"
 
@@ -36,7 +35,9 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 constexpr int MAXG = 16, MAXU = 64, MAXH = 512;
 constexpr unsigned SPIN_MAX = 1u << 22;           // ~ seconds of polling before giving up
 
-__device__ inline float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// hardware exp / rcp (a few ulp; the step's dot products carry more rounding than that)
+__device__ inline float sigm(float x) { return fast_rcp(1.f + fast_exp(-x)); }
+__device__ inline float tanh_(float x) { return fmaf(2.f, sigm(2.f * x), -1.f); }
 
 __device__ inline unsigned long long granule(unsigned tag, float v) {
     return ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v);
@@ -96,7 +97,6 @@ __device__ inline Geo geo(int H, int G, int g) {
 }
 
 // hbuf: [2][B][H] granules.  LDS: W rows [4U][RS] (row rr = gate q * nu + unit), h [RS], gate pre-activations [4U]
-template <int DBG>
 __global__ __launch_bounds__(512) void fwd_kernel(int T, int H, int G, int reverse, const float* __restrict__ gx,
                                                   const float* __restrict__ whh, float* __restrict__ hout,
                                                   int64_t hout_bs, int64_t hout_ts, float* __restrict__ c_all,
@@ -135,14 +135,12 @@ __global__ __launch_bounds__(512) void fwd_kernel(int T, int H, int G, int rever
         return (rowok && hk == 0) ? gx[((int64_t)b * T + t) * H4 + gq * H + jr] : 0.f;
     };
     float gx_next = gx_at(0);
-    long long* probe = (long long*)(hbuf_ + 2 * (int64_t)B * H) + 64;   // DBG 3: per-phase clocks of block 0
     for (int s = 0; s < T; ++s) {
-        if (DBG == 3 && blockIdx.x == 0 && tid == 0 && s >= 100 && s < 116) probe[(s - 100) * 4] = wall_clock64();
         const int t = reverse ? T - 1 - s : s;
         const int64_t bt = (int64_t)b * T + t;
         const float gx_cur = gx_next;
         if (s + 1 < T) gx_next = gx_at(s + 1);
-        if (DBG != 2) {
+        {
             float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 8
             for (int k4 = k4lo; k4 < k4hi; ++k4) {       // padding columns add w = 0 times h = 0
@@ -157,14 +155,13 @@ __global__ __launch_bounds__(512) void fwd_kernel(int T, int H, int G, int rever
             if (rowok && hk == 0) s_gp[rr] = gx_cur + acc;
         }
         lds_barrier();
-        if (DBG == 3 && blockIdx.x == 0 && tid == 0 && s >= 100 && s < 116) probe[(s - 100) * 4 + 1] = wall_clock64();
         gu64* slot = hbuf + ((int64_t)(s & 1) * B + b) * H;
         if (tid < q.nu) {
             const int j = q.u0 + tid;
-            const float ig = sigm(s_gp[tid]), fg = sigm(s_gp[q.nu + tid]), gg = tanhf(s_gp[2 * q.nu + tid]),
+            const float ig = sigm(s_gp[tid]), fg = sigm(s_gp[q.nu + tid]), gg = tanh_(s_gp[2 * q.nu + tid]),
                         og = sigm(s_gp[3 * q.nu + tid]);
             c = fmaf(fg, c, ig * gg);
-            const float h = og * tanhf(c);
+            const float h = og * tanh_(c);
             __hip_atomic_store(slot + j, granule((unsigned)s + 1u, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             hout[(int64_t)b * hout_bs + (int64_t)t * hout_ts + j] = h;
             c_all[bt * H + j] = c;
@@ -174,20 +171,18 @@ __global__ __launch_bounds__(512) void fwd_kernel(int T, int H, int G, int rever
             gt[2 * H + j] = gg;
             gt[3 * H + j] = og;
         }
-        if (DBG == 3 && blockIdx.x == 0 && tid == 0 && s >= 100 && s < 116) probe[(s - 100) * 4 + 2] = wall_clock64();
-        if (tid < 64 && alive && DBG != 1) {              // wave 0 gathers h_t of all units (own ones included)
+        if (tid < 64 && alive) {                          // wave 0 gathers h_t of all units (own ones included)
             alive = sweep<MAXH / 64>(slot, (unsigned)s + 1u, status,
                                      [&](int l, int k) -> int64_t { return l + 64 * k < H ? l + 64 * k : -1; },
                                      [&](int l, int k, float v) { s_h[l + 64 * k] = v; });
         }
         lds_barrier();
-        if (DBG == 3 && blockIdx.x == 0 && tid == 0 && s >= 100 && s < 116) probe[(s - 100) * 4 + 3] = wall_clock64();
     }
 }
 
 // pbuf: [2][B][G][H] granules.  LDS: W^T of the own rows [H][RS4] (column rr = gate q * nu + unit, RS4 = 4U
 // rounded to 4), dg [RS4], dh of the own units from the next step [U]
-__global__ __launch_bounds__(512) void bwd_kernel(int T, int H, int G, int reverse, const float* __restrict__ dh_out,
+__global__ __launch_bounds__(768) void bwd_kernel(int T, int H, int G, int reverse, const float* __restrict__ dh_out,
                                                   int64_t dh_bs, int64_t dh_ts, const float* __restrict__ gates,
                                                   const float* __restrict__ c_all, const float* __restrict__ whh,
                                                   float* __restrict__ dgp, unsigned long long* pbuf_, unsigned* status_) {
@@ -231,6 +226,9 @@ __global__ __launch_bounds__(512) void bwd_kernel(int T, int H, int G, int rever
         }
         return v;
     };
+    const int col = (tid >> 6) * 32 + (tid & 31), hr = (tid & 63) >> 5;   // column, row half
+    const bool colok = col < H;
+    const int NR4 = RS4 / 4, RH4 = (NR4 + 1) / 2, r4lo = hr ? RH4 : 0, r4hi = hr ? NR4 : RH4;
     In nxt = load_in(0);
     __syncthreads();
     for (int s = 0; s < T; ++s) {
@@ -242,7 +240,7 @@ __global__ __launch_bounds__(512) void bwd_kernel(int T, int H, int G, int rever
             const int j = q.u0 + tid;
             const float ig = cur.ig, fg = cur.fg, gg = cur.gg, og = cur.og, c = cur.c, cp = cur.cp;
             const float dh = cur.dho + s_dh[tid];
-            const float tc = tanhf(c);
+            const float tc = tanh_(c);
             const float dc = fmaf(dh * og, 1.f - tc * tc, dc_carry);
             const float di = dc * gg * ig * (1.f - ig);
             const float df = dc * cp * fg * (1.f - fg);
@@ -261,21 +259,23 @@ __global__ __launch_bounds__(512) void bwd_kernel(int T, int H, int G, int rever
         }
         lds_barrier();
         gu64* slot = pbuf + ((int64_t)(s & 1) * B + b) * G * H;
-        if (tid < H) {                                    // partial dh_{t-1}[tid] over the own gate rows
-            const float4* w4 = reinterpret_cast<const float4*>(s_wt + tid * RS4);
+        {                                                 // partial dh_{t-1}[col] over the own gate rows:
+            const float4* w4 = reinterpret_cast<const float4*>(s_wt + (colok ? col : 0) * RS4);
             const float4* d4 = reinterpret_cast<const float4*>(s_dg);
-            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);    // 4 independent fma chains
-#pragma unroll 11
-            for (int r4 = 0; r4 < RS4 / 4; ++r4) {
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);    // 2 lanes per column, 4 fma chains each
+#pragma unroll 9
+            for (int r4 = r4lo; r4 < r4hi; ++r4) {
                 const float4 w = w4[r4], d = d4[r4];
                 a.x = fmaf(w.x, d.x, a.x);
                 a.y = fmaf(w.y, d.y, a.y);
                 a.z = fmaf(w.z, d.z, a.z);
                 a.w = fmaf(w.w, d.w, a.w);
             }
-            const float acc = (a.x + a.y) + (a.z + a.w);
-            __hip_atomic_store(slot + (int64_t)g * H + tid, granule((unsigned)s + 1u, acc), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            float acc = (a.x + a.y) + (a.z + a.w);
+            acc += __shfl_xor(acc, 32, 64);
+            if (colok && hr == 0)
+                __hip_atomic_store(slot + (int64_t)g * H + col, granule((unsigned)s + 1u, acc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
         if (tid < 64 && alive) {                          // wave 0, lane = own unit: dh = sum of the G partials
             float acc = 0.f;                               // in group order (deterministic)
@@ -298,8 +298,9 @@ using namespace avse;
 namespace {
 
 // smallest G in {1, 2, 4, 8, 16} whose forward and backward LDS fit 160 KiB with H / G <= 64 units per workgroup
+// (H <= 384)
 int group_size(int64_t H) {
-    if (H <= 0 || H > lstmg::MAXH) return 0;
+    if (H <= 0 || H > 384) return 0;                  // backward: 2 lanes per unit column in <= 768 threads
     for (int G = 1; G <= lstmg::MAXG; G *= 2) {
         const int64_t U = (H + G - 1) / G, RS = (H + 3) & ~3LL, RS4 = (4 * U + 3) & ~3LL;
         const int64_t fwd = 4 * (4 * U * RS + RS + 4 * U), bwd = 4 * (H * RS4 + RS4 + U);
@@ -344,23 +345,16 @@ int avse_lstm_fwd_group(int64_t B, int64_t T, int64_t H, int32_t reverse, const 
     const size_t lds = fwd_lds(H, G);
     static bool attr = false;
     if (!attr) {
-        for (const void* f : {reinterpret_cast<const void*>(&lstmg::fwd_kernel<0>),
-                              reinterpret_cast<const void*>(&lstmg::fwd_kernel<1>),
-                              reinterpret_cast<const void*>(&lstmg::fwd_kernel<2>),
-                              reinterpret_cast<const void*>(&lstmg::fwd_kernel<3>)})
-            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-                return AVSE_ELAUNCH;
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lstmg::fwd_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+            return AVSE_ELAUNCH;
         attr = true;
     }
     const int64_t U = (H + G - 1) / G;
     const int threads = (int)std::max<int64_t>(64, (4 * U + 31) / 32 * 64);        // 32 gate rows per wave
     auto* status = reinterpret_cast<unsigned*>(workspace);
     auto* hbuf = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + 16);
-    const char* dbg = getenv("AVSE_LSTM_DBG");
-    const int d = dbg ? atoi(dbg) : 0;
-    auto kern = d == 1 ? lstmg::fwd_kernel<1> : d == 2 ? lstmg::fwd_kernel<2> : d == 3 ? lstmg::fwd_kernel<3>
-                                                                                   : lstmg::fwd_kernel<0>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)(B * G)), dim3(threads), lds, st, (int)T, (int)H, G,
+    hipLaunchKernelGGL(lstmg::fwd_kernel, dim3((unsigned)(B * G)), dim3(threads), lds, st, (int)T, (int)H, G,
                        (int)reverse, gx, whh, hout, hout_bs, hout_ts, c_all, gates, hbuf, status);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
@@ -383,7 +377,8 @@ int avse_lstm_bwd_group(int64_t B, int64_t T, int64_t H, int32_t reverse, const 
             return AVSE_ELAUNCH;
         attr = true;
     }
-    const int threads = (int)((H + 63) / 64 * 64);
+    const int threads = (int)((H + 31) / 32 * 64);                      // 32 columns per wave
+    if (threads > 768) return AVSE_ESHAPE;
     auto* status = reinterpret_cast<unsigned*>(workspace);
     auto* pbuf = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + 16);
     hipLaunchKernelGGL(lstmg::bwd_kernel, dim3((unsigned)(B * G)), dim3(threads), lds, st, (int)T, (int)H, G,

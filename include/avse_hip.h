@@ -307,7 +307,7 @@ int avse_lstm_fwd(int64_t B, int64_t T, int64_t H, int32_t reverse, const float*
 int avse_lstm_bwd(int64_t B, int64_t T, int64_t H, int32_t reverse, const float* dh_out, int64_t dh_bs, int64_t dh_ts,
                   const float* gates, const float* c_all, const float* whh_pad, float* dgates, avse_stream_t stream);
 /* The same recurrences with each sequence spread over G = avse_lstm_group_size(B, H) workgroups (0: not available
- * for this shape: B * G > 256 or H > 512), W_hh resident in their LDS, h / dh exchanged through data-tagged
+ * for this shape: B * G > 256 or H > 384), W_hh resident in their LDS, h / dh exchanged through data-tagged
  * granules in `workspace` (avse_lstm_group_workspace_bytes; zeroed by the call; its first uint32 is a status word,
  * 0 = every hand-off completed, else 0x71000000 + step of a timed-out wait: the sequence's workgroups were not
  * co-resident and the outputs are invalid).  whh = W_hh (4H, H) contiguous for both directions; other arguments and

@@ -36,20 +36,6 @@ def main():
         key = "grouped" if mode == "1" else "one_wg_per_sequence"
         out[key] = {"fwd_ms": round(f, 3), "bwd_ms": round(b, 3), "fwd_us_per_step": round(1e3 * f / T, 2),
                     "bwd_us_per_step": round(1e3 * b / T, 2)}
-    os.environ["AVSE_LSTM_GROUP"] = "1"
-    for dbg in ("1", "2"):      # timing split (wrong results): 1 = no hand-off wait, 2 = no gate dot products
-        os.environ["AVSE_LSTM_DBG"] = dbg
-        out[f"fwd_dbg{dbg}_ms"] = round(timeit(lambda: K.lstm_fwd(gx, w), a.iters), 3)
-    os.environ["AVSE_LSTM_DBG"] = "3"      # per-phase wall clocks (100 MHz) of block 0, steps 100..115
-    K.lstm_fwd(gx, w)
-    torch.cuda.synchronize()
-    ws = K._LSTM_GROUP_WS[-1]
-    off = (16 + 2 * B * H * 8) // 8 + 64
-    pr = ws.view(torch.int64)[off:off + 64].view(16, 4).cpu()
-    d = (pr[:, 1:] - pr[:, :-1]).double() * 10.0            # ns: dots, cell+stores, hand-off
-    out["probe_ns_dots_cell_handoff"] = [round(float(v), 0) for v in d.median(0).values]
-    out["probe_ns_step"] = round(float((pr[1:, 0] - pr[:-1, 0]).double().median()) * 10.0, 0)
-    os.environ["AVSE_LSTM_DBG"] = "0"
     out["status"] = K.lstm_group_status()
     print(json.dumps(out), flush=True)
 
