@@ -17,6 +17,7 @@ namespace avse {
 namespace gln {
 
 constexpr int THREADS = 256;
+constexpr int DW_U = 8, DW_UB = 4;          // elements per thread in flight (forward, backward passes)
 
 __device__ inline float prelu(float x, float a) { return x > 0.f ? x : a * x; }
 
@@ -49,35 +50,46 @@ __global__ __launch_bounds__(THREADS) void stats_kernel(int C, int K, const floa
     if (threadIdx.x == 0) ws[row] = make_float2(s1, s2);
 }
 
-// per sample: mean, rstd = 1/sqrt(var + EPS)
-__global__ void stats_finalize(int B, int C, int K, const float* __restrict__ x, const float* __restrict__ alpha,
-                               const float2* __restrict__ ws, float eps, float2* __restrict__ stats) {
-    __shared__ double red1[4], red2[4];
-    const int b = blockIdx.x;
+// sample b's (sum_c v.x, sum_c v.y) over its C row partials, in double, by a 256-thread block (fixed order:
+// every caller gets the same bits)
+__device__ inline double2 sample_sums(const float2* __restrict__ ws, int b, int C, double* red /* [8] */,
+                                      const float* __restrict__ wgt = nullptr) {
     double s1 = 0.0, s2 = 0.0;
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
         const float2 v = ws[(int64_t)b * C + c];
-        s1 += v.x;
-        s2 += v.y;
+        const double g = wgt ? (double)wgt[c] : 1.0;
+        s1 += g * v.x;
+        s2 += g * v.y;
     }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
         s1 += __shfl_xor(s1, m, 64);
         s2 += __shfl_xor(s2, m, 64);
     }
+    __syncthreads();                                   // red may still be read by a previous call
     if ((threadIdx.x & 63) == 0) {
-        red1[threadIdx.x >> 6] = s1;
-        red2[threadIdx.x >> 6] = s2;
+        red[threadIdx.x >> 6] = s1;
+        red[4 + (threadIdx.x >> 6)] = s2;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const double n = (double)C * K;
-        const double m1 = (red1[0] + red1[1] + red1[2] + red1[3]) / n;
-        const double m2 = (red2[0] + red2[1] + red2[2] + red2[3]) / n;
-        const double var = fmax(m2 - m1 * m1, 0.0);
-        const float shift = prelu(x[(int64_t)b * C * K], alpha[0]);
-        stats[b] = make_float2((float)(m1 + shift), (float)(1.0 / sqrt(var + (double)eps)));
-    }
+    return make_double2((red[0] + red[1]) + (red[2] + red[3]), (red[4] + red[5]) + (red[6] + red[7]));
+}
+
+// mean, rstd = 1 / sqrt(var + EPS) of sample b from its shifted row sums
+__device__ inline float2 sample_stats(double2 sums, int C, int K, float shift, float eps) {
+    const double n = (double)C * K;
+    const double m1 = sums.x / n, m2 = sums.y / n;
+    const double var = fmax(m2 - m1 * m1, 0.0);
+    return make_float2((float)(m1 + shift), (float)(1.0 / sqrt(var + (double)eps)));
+}
+
+// per sample: mean, rstd = 1/sqrt(var + EPS)
+__global__ void stats_finalize(int B, int C, int K, const float* __restrict__ x, const float* __restrict__ alpha,
+                               const float2* __restrict__ ws, float eps, float2* __restrict__ stats) {
+    __shared__ double red[8];
+    const int b = blockIdx.x;
+    const double2 sums = sample_sums(ws, b, C, red);
+    if (threadIdx.x == 0) stats[b] = sample_stats(sums, C, K, prelu(x[(int64_t)b * C * K], alpha[0]), eps);
 }
 
 __global__ __launch_bounds__(THREADS) void apply_kernel(int C, int K, const float* __restrict__ x,
@@ -87,6 +99,26 @@ __global__ __launch_bounds__(THREADS) void apply_kernel(int C, int K, const floa
     const int row = blockIdx.x, b = row / C, c = row % C;
     const float a = alpha[0];
     const float2 st = stats[b];
+    const float g = gamma[c] * st.y, o = beta[c] - gamma[c] * st.y * st.x;
+    const float* xr = x + (int64_t)row * K;
+    float* yr = y + (int64_t)row * K;
+    for (int t = threadIdx.x; t < K; t += THREADS) yr[t] = g * prelu(xr[t], a) + o;
+}
+
+// apply with the finalize folded in: every row block re-derives its sample's statistics from the row partials (the
+// same sums in the same order as stats_finalize: bitwise equal), the channel-0 block stores them for the backward.
+// shift_src: the tensor whose (b, 0, 0) element defines the shift (y1 here)
+__global__ __launch_bounds__(THREADS) void apply_fused_kernel(int C, int K, const float* __restrict__ x,
+                                                              const float* __restrict__ alpha,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta,
+                                                              const float2* __restrict__ ws, float eps,
+                                                              float2* __restrict__ stats, float* __restrict__ y) {
+    __shared__ double red[8];
+    const int row = blockIdx.x, b = row / C, c = row % C;
+    const float a = alpha[0];
+    const float2 st = sample_stats(sample_sums(ws, b, C, red), C, K, prelu(x[(int64_t)b * C * K], a), eps);
+    if (c == 0 && threadIdx.x == 0) stats[b] = st;
     const float g = gamma[c] * st.y, o = beta[c] - gamma[c] * st.y * st.x;
     const float* xr = x + (int64_t)row * K;
     float* yr = y + (int64_t)row * K;
@@ -104,11 +136,22 @@ __global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int C, int K, const
     const float* xr = x + (int64_t)row * K;
     const float* gr = dy + (int64_t)row * K;
     float s1 = 0.f, s2 = 0.f;
-    for (int t = threadIdx.x; t < K; t += THREADS) {
-        const float g = gr[t];
-        const float xh = (prelu(xr[t], a) - st.x) * st.y;
-        s1 += g;
-        s2 += g * xh;
+    for (int t0 = 0; t0 < K; t0 += DW_U * THREADS) {  // DW_U elements per thread in flight
+        float gv[DW_U], xv[DW_U];
+#pragma unroll
+        for (int j = 0; j < DW_U; ++j) {
+            const int t = min(t0 + j * THREADS + (int)threadIdx.x, K - 1);
+            gv[j] = gr[t];
+            xv[j] = xr[t];
+        }
+#pragma unroll
+        for (int j = 0; j < DW_U; ++j) {
+            if (t0 + j * THREADS + (int)threadIdx.x < K) {
+                const float xh = (prelu(xv[j], a) - st.x) * st.y;
+                s1 += gv[j];
+                s2 += gv[j] * xh;
+            }
+        }
     }
     s1 = block_sum(s1, red);
     s2 = block_sum(s2, red);
@@ -198,19 +241,23 @@ __global__ void alpha_finalize(int rows, const float* __restrict__ ws_alpha, flo
 
 // ----------------------------------------------------------------------------------------------------------
 // Fused depthwise dilated conv1d <-> PReLU -> gLN (DepthwiseSeparableConv.net[:3], model.py:278-292)
-//   fwd: ONE pass computes y1 = dwconv(x) per row tile (LDS tile + dilation halo, as dwconv.hip) and, from the
-//        registers, the row's shifted PReLU statistics; finalize; the apply pass reads y1 once (apply_kernel).
-//   bwd: the row reduction of (y1, dy) (bwd_reduce_kernel); finalize; ONE pass whose tile loader turns (y1, dy)
-//        into the gLN/PReLU input gradient on the fly (halo included) and runs the dwconv backward on it
-//        (dx, dW row partials) plus the PReLU-slope partial over the tile's own elements.
-constexpr int DW_PER = 8, DW_TILE = THREADS * DW_PER, DW_MAXP = 7, DW_MAXHALO = 512;
+//   fwd: ONE pass computes y1 = dwconv(x) per row (streaming: the taps' neighbours come from the cache lines the
+//        row's workgroup just loaded) and, from the registers, the row's shifted PReLU statistics; the apply pass
+//        re-derives the sample statistics from the row partials (finalize folded in) and reads y1 once.
+//   bwd: the row reduction of (y1, dy) (bwd_reduce_kernel); ONE pass (finalize folded in) that recomputes the
+//        gLN/PReLU input gradient at each tap's position from (y1, dy) and runs the dwconv backward on it (dx, dW
+//        row partials) plus the PReLU-slope partial of the own elements; one tail launch for dW, dgamma / dbeta and
+//        the slope.
+constexpr int DW_MAXP = 7, DW_MAXHALO = 512;
 
 template <int P>
 __global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int C, int K, int dil, const float* __restrict__ x,
                                                                const float* __restrict__ w,
                                                                const float* __restrict__ alpha, float* __restrict__ y1,
                                                                float2* __restrict__ ws) {
-    __shared__ float s[DW_TILE + 2 * DW_MAXHALO];
+    // streaming form, no LDS: thread t-loop over the row with the taps' neighbours (+-halo) read straight from the
+    // cache lines this workgroup just brought in (each x line leaves HBM once); the same k-ordered sums as the tiled
+    // form (bitwise equal y1, same per-thread element order for the statistics)
     __shared__ float red[4];
     const int row = blockIdx.x, b = row / C, c = row % C;
     const int halo = (P - 1) / 2 * dil;
@@ -232,22 +279,22 @@ __global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int C, int K, int
     }
     const float shift = prelu(y00, a);
     float s1 = 0.f, s2 = 0.f;
-    for (int t0 = 0; t0 < K; t0 += DW_TILE) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < DW_TILE + 2 * halo; i += THREADS) {
-            const int t = t0 - halo + i;
-            s[i] = (t >= 0 && t < K) ? xr[t] : 0.f;
+    const auto rx = make_rsrc(xr, K);                 // taps outside the row load 0 (buffer range check, no branch)
+    for (int t0 = 0; t0 < K; t0 += DW_U * THREADS) {  // DW_U elements per thread in flight
+        float acc[DW_U];
+#pragma unroll
+        for (int j = 0; j < DW_U; ++j) {
+            const int t = t0 + j * THREADS + threadIdx.x;
+            acc[j] = 0.f;
+#pragma unroll
+            for (int k = 0; k < P; ++k) acc[j] += wk[k] * bufld<float>::ld(rx, t + k * dil - halo, 0);
         }
-        __syncthreads();
 #pragma unroll
-        for (int p = 0; p < DW_PER; ++p) {
-            const int i = threadIdx.x + p * THREADS, t = t0 + i;
+        for (int j = 0; j < DW_U; ++j) {
+            const int t = t0 + j * THREADS + threadIdx.x;
             if (t < K) {
-                float acc = 0.f;
-#pragma unroll
-                for (int k = 0; k < P; ++k) acc += wk[k] * s[i + k * dil];
-                yr[t] = acc;
-                const float v = prelu(acc, a) - shift;
+                yr[t] = acc[j];
+                const float v = prelu(acc[j], a) - shift;
                 s1 += v;
                 s2 += v * v;
             }
@@ -264,16 +311,22 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd_kernel(int C, int K, i
                                                                  const float* __restrict__ alpha,
                                                                  const float* __restrict__ gamma,
                                                                  const float2* __restrict__ stats,
-                                                                 const float2* __restrict__ smeans,
+                                                                 const float2* __restrict__ ws_rows,
                                                                  const float* __restrict__ dy, float* __restrict__ dx,
                                                                  float* __restrict__ ws_dw, float* __restrict__ ws_alpha) {
-    __shared__ float sx[DW_TILE + 2 * DW_MAXHALO];
-    __shared__ float sg[DW_TILE + 2 * DW_MAXHALO];
+    // streaming form, no LDS: the PReLU -> gLN input gradient g1(u) is recomputed at each of the P taps' positions
+    // from (y1, dy) cache lines (each line leaves HBM once), then dx = the transposed conv of g1 and the row's dW /
+    // PReLU-slope partials
     __shared__ float red[THREADS / 64][DW_MAXP + 1];
+    __shared__ double dred[8];
     const int row = blockIdx.x, b = row / C, c = row % C;
     const int halo = (P - 1) / 2 * dil;
     const float a = alpha[0];
-    const float2 st = stats[b], sm = smeans[b];
+    const float2 st = stats[b];
+    // the sample's (mean_g, mean_gxh) with g = dy * gamma, from the row partials of bwd_reduce_kernel
+    const double2 sg12 = sample_sums(ws_rows, b, C, dred, gamma);
+    const double nn = (double)C * K;
+    const float2 sm = make_float2((float)(sg12.x / nn), (float)(sg12.y / nn));
     const float gm = gamma[c];
     const float* xr = x + (int64_t)row * K;
     const float* yr = y1 + (int64_t)row * K;
@@ -285,35 +338,38 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd_kernel(int C, int K, i
         wk[k] = w[c * P + k];
         dw[k] = 0.f;
     }
-    for (int t0 = 0; t0 < K; t0 += DW_TILE) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < DW_TILE + 2 * halo; i += THREADS) {
-            const int t = t0 - halo + i;
-            const bool ok = t >= 0 && t < K;
-            float g1 = 0.f;
-            if (ok) {   // d(gLN(PReLU(y1)))/dy1 applied to dy: the PReLU -> gLN backward of gln.hip bwd_apply_kernel
-                const float yv = yr[t];
+    const auto rx = make_rsrc(xr, K), ry = make_rsrc(yr, K), rg = make_rsrc(gr, K);   // outside the row: 0
+    for (int t0 = 0; t0 < K; t0 += DW_UB * THREADS) {
+        float acc[DW_UB], gown[DW_UB];
+#pragma unroll
+        for (int j = 0; j < DW_UB; ++j) {
+            const int t = t0 + j * THREADS + threadIdx.x;
+            acc[j] = 0.f;
+            gown[j] = 0.f;
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                // d(gLN(PReLU(y1)))/dy1 applied to dy at u (0 outside the row: y1 = dy = 0 there gives dp = -rstd
+                // mean_g..., so mask it)
+                const int u = t + halo - k * dil;
+                const float yv = bufld<float>::ld(ry, u, 0), gv = bufld<float>::ld(rg, u, 0);
                 const float xh = (prelu(yv, a) - st.x) * st.y;
-                const float dp = st.y * (gr[t] * gm - sm.x - xh * sm.y);
-                g1 = yv > 0.f ? dp : a * dp;
-                if (i >= halo && i < halo + DW_TILE && yv <= 0.f) da += dp * yv;   // own elements only
-            }
-            sx[i] = ok ? xr[t] : 0.f;
-            sg[i] = g1;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int p = 0; p < DW_PER; ++p) {
-            const int i = threadIdx.x + p * THREADS, t = t0 + i;
-            if (t < K) {
-                float acc = 0.f;
-                const float g = sg[i + halo];
-#pragma unroll
-                for (int k = 0; k < P; ++k) {
-                    acc += wk[k] * sg[i + 2 * halo - k * dil];
-                    dw[k] += g * sx[i + k * dil];
+                float dp = st.y * (gv * gm - sm.x - xh * sm.y);
+                dp = (u >= 0 && u < K) ? dp : 0.f;
+                const float gk = yv > 0.f ? dp : a * dp;
+                acc[j] += wk[k] * gk;
+                if (k == (P - 1) / 2) {                   // the own element: g for dW, the slope partial
+                    gown[j] = gk;
+                    if (t < K && yv <= 0.f) da += dp * yv;
                 }
-                dr[t] = acc;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < DW_UB; ++j) {
+            const int t = t0 + j * THREADS + threadIdx.x;
+            if (t < K) {
+                dr[t] = acc[j];
+#pragma unroll
+                for (int k = 0; k < P; ++k) dw[k] += gown[j] * bufld<float>::ld(rx, t + k * dil - halo, 0);
             }
         }
     }
@@ -339,6 +395,52 @@ __global__ void dw_sum_kernel(const float* __restrict__ ws, int B, int C, int P,
     float v = 0.f;
     for (int b = 0; b < B; ++b) v += ws[((int64_t)b * C + c) * DW_MAXP + k];
     dw[i] = v;
+}
+
+// the fused backward's tail, one launch: block 0 = dalpha (alpha_finalize), the next blocks dW (dw_sum_kernel) and
+// per channel dgamma / dbeta (sum over b of the row partials: bwd_finalize's channel blocks)
+__global__ void dw_tail_kernel(const float* __restrict__ ws_dw, const float2* __restrict__ ws_rows,
+                               const float* __restrict__ ws_alpha, int B, int C, int P, float* __restrict__ dw,
+                               float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dalpha) {
+    if (blockIdx.x == 0) {
+        __shared__ double red[4];
+        double s = 0.0;
+        for (int i0 = 0; i0 < B * C; i0 += 8 * blockDim.x) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = i0 + j * blockDim.x + threadIdx.x;
+                v[j] = i < B * C ? ws_alpha[i] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += v[j];
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) dalpha[0] = (float)(red[0] + red[1] + red[2] + red[3]);
+        return;
+    }
+    const int i = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
+    if (i < C * P) {
+        const int c = i / P, k = i % P;
+        float v = 0.f;
+#pragma unroll 16
+        for (int b = 0; b < B; ++b) v += ws_dw[((int64_t)b * C + c) * DW_MAXP + k];
+        dw[i] = v;
+    } else if (i < C * P + C) {
+        const int c = i - C * P;
+        double g = 0.0, bt = 0.0;
+#pragma unroll 16
+        for (int b = 0; b < B; ++b) {
+            const float2 v = ws_rows[(int64_t)b * C + c];
+            bt += v.x;
+            g += v.y;
+        }
+        dgamma[c] = (float)g;
+        dbeta[c] = (float)bt;
+    }
 }
 
 }  // namespace gln
@@ -427,11 +529,8 @@ int avse_dwconv_gln_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     AVSE_DW_P_SWITCH(P, L_)
 #undef L_
     AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(stats_finalize, dim3((unsigned)B), dim3(256), 0, st, (int)B, (int)C, (int)K, y1, alpha, ws, eps,
-                       (float2*)stats);
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(apply_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, y1, alpha, gamma, beta,
-                       (const float2*)stats, y);
+    hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, y1, alpha, gamma, beta,
+                       (const float2*)ws, eps, (float2*)stats, y);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
@@ -447,24 +546,18 @@ int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     const unsigned rows = (unsigned)(B * C);
     float2* ws = (float2*)workspace;
     float* ws_a = (float*)(ws + B * C);
-    float2* smeans = (float2*)(ws_a + B * C);
-    float* ws_dw = (float*)(smeans + B);
+    float* ws_dw = (float*)((float2*)(ws_a + B * C) + B);
     hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, y1, alpha,
                        (const float2*)stats, dy, ws);
     AVSE_CHECK_LAUNCH();
-    const unsigned cblocks = (unsigned)((C + 255) / 256);
-    hipLaunchKernelGGL(bwd_finalize, dim3((unsigned)B + cblocks), dim3(256), 0, st, (int)B, (int)C, (int)K, ws, gamma,
-                       smeans, dgamma, dbeta);
-    AVSE_CHECK_LAUNCH();
 #define L_(PP) hipLaunchKernelGGL(dwconv_gln_bwd_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, (int)dil, \
-                                  x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)smeans, dy, dx, ws_dw, ws_a)
+                                  x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, ws_a)
     AVSE_DW_P_SWITCH(P, L_)
 #undef L_
     AVSE_CHECK_LAUNCH();
-    const int n = (int)(C * P);
-    hipLaunchKernelGGL(dw_sum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ws_dw, (int)B, (int)C, (int)P, dw);
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(alpha_finalize, dim3(1), dim3(256), 0, st, (int)rows, ws_a, dalpha);
+    const int n = (int)(C * P + C);
+    hipLaunchKernelGGL(dw_tail_kernel, dim3(1 + (n + 255) / 256), dim3(256), 0, st, ws_dw, (const float2*)ws, ws_a,
+                       (int)B, (int)C, (int)P, dw, dgamma, dbeta, dalpha);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
