@@ -3,8 +3,8 @@
 // Replaces nn.Conv1d(C, C, P, padding=(P-1)*dil/2, dilation=dil, groups=C, bias=False) of
 // /root/reference/baseline/avse4/model.py:278-285 (DepthwiseSeparableConv, P=3, dil 2^x) and
 // model.py:191-198 (VisualConv1D, P=3, dil 1):  y[t] = sum_k w[c,k] x[t + (k - (P-1)/2) * dil].
-// One workgroup per (b, c) row; the row streams through LDS in TILE pieces with a (P-1)/2*dil
-// halo each side, so each HBM byte moves once (fwd: 8 B/elem, bwd: 12 B/elem — the SURVEY §8d
+// One workgroup per (b, c) row; forward: the row streams through LDS in TILE pieces with a (P-1)/2*dil
+// halo each side; backward: streaming loads (below); each HBM byte moves once (fwd: 8 B/elem, bwd: 12 B/elem — the SURVEY §8d
 // algorithmic bytes).  dW is reduced per row in registers/LDS and summed over the batch by a
 // second kernel (deterministic).
 #include "common.h"
@@ -46,12 +46,14 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(int C, int K, int dil, con
 }
 
 // dx[t] = sum_k w[k] dy[t - (k - h) * dil];  dw[k] += dy[t] * x[t + (k - h) * dil]
+// Streaming form, no LDS: thread t-loop over the row, BU elements per thread in flight; the taps' neighbours come
+// from the cache lines this workgroup just brought in (buffer loads: outside the row reads 0, no branches), so each
+// HBM byte still moves once (tools/avse4 TCN profile: the LDS-tiled form ran at 3.8 TB/s, latency-bound).
 template <int P>
 __global__ __launch_bounds__(THREADS) void bwd_kernel(int C, int K, int dil, const float* __restrict__ x,
                                                       const float* __restrict__ w, const float* __restrict__ dy,
                                                       float* __restrict__ dx, float* __restrict__ ws) {
-    __shared__ float sx[TILE + 2 * MAXHALO];
-    __shared__ float sg[TILE + 2 * MAXHALO];
+    constexpr int BU = 4;
     __shared__ float red[THREADS / 64][MAXP];
     const int row = blockIdx.x, c = row % C;
     const int halo = (P - 1) / 2 * dil;
@@ -64,27 +66,28 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int C, int K, int dil, con
         wk[k] = w[c * P + k];
         dw[k] = 0.f;
     }
-    for (int t0 = 0; t0 < K; t0 += TILE) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < TILE + 2 * halo; i += THREADS) {
-            const int t = t0 - halo + i;
-            const bool ok = t >= 0 && t < K;
-            sx[i] = ok ? xr[t] : 0.f;
-            sg[i] = ok ? gr[t] : 0.f;
+    const auto rx = make_rsrc(xr, K), rg = make_rsrc(gr, K);
+    for (int t0 = 0; t0 < K; t0 += BU * THREADS) {
+        float acc[BU], g[BU], xv[BU][P];
+#pragma unroll
+        for (int j = 0; j < BU; ++j) {
+            const int t = t0 + j * THREADS + threadIdx.x;
+            acc[j] = 0.f;
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                const float gk = bufld<float>::ld(rg, t + halo - k * dil, 0);
+                acc[j] += wk[k] * gk;
+                if (k == (P - 1) / 2) g[j] = gk;
+                xv[j][k] = bufld<float>::ld(rx, t + k * dil - halo, 0);
+            }
         }
-        __syncthreads();
 #pragma unroll
-        for (int p = 0; p < PER; ++p) {
-            const int i = threadIdx.x + p * THREADS, t = t0 + i;
+        for (int j = 0; j < BU; ++j) {
+            const int t = t0 + j * THREADS + threadIdx.x;
             if (t < K) {
-                float acc = 0.f;
-                const float g = sg[i + halo];
+                dr[t] = acc[j];
 #pragma unroll
-                for (int k = 0; k < P; ++k) {
-                    acc += wk[k] * sg[i + 2 * halo - k * dil];
-                    dw[k] += g * sx[i + k * dil];
-                }
-                dr[t] = acc;
+                for (int k = 0; k < P; ++k) dw[k] += g[j] * xv[j][k];
             }
         }
     }
@@ -105,6 +108,7 @@ __global__ void dw_reduce_kernel(const float* __restrict__ ws, int B, int C, int
     if (i >= C * P) return;
     const int c = i / P, k = i % P;
     float v = 0.f;
+#pragma unroll 16
     for (int b = 0; b < B; ++b) v += ws[((int64_t)b * C + c) * MAXP + k];
     dw[i] = v;
 }
