@@ -103,6 +103,17 @@ __device__ inline float softplus(float x) {
     const float r = (u == 1.f) ? t : lp;
     return (x > 20.f) ? x : r;
 }
+// The same value with two transcendentals instead of three: log1p(t) = log(u + c) with u = fl(1 + t) and
+// c = t - (u - 1) the rounding error of that sum (u - 1 is exact for t < 3), so log1p(t) = log(u) + c/u + O(c^2);
+// taking c for c/u errs by |c| t / (1 + t) <= 2^-24 t, i.e. below one ulp of log1p(t) ~ t for tiny t (u == 1 gives
+// log(u) = 0 and c = t exactly) and far below it for t ~ 1.  No rcp, no u == 1 select.
+__device__ inline float softplus2(float x) {
+    const float t = fast_exp(x);
+    const float u = 1.f + t;
+    const float c = t - (u - 1.f);
+    const float r = __builtin_fmaf(__builtin_amdgcn_logf(u), AVSE_LN2, c);
+    return (x > 20.f) ? x : r;
+}
 __device__ inline float sigmoidf_(float x) { return fast_rcp(1.f + fast_exp(-x)); }
 __device__ inline float siluf_(float x) { return x * sigmoidf_(x); }
 

@@ -130,18 +130,47 @@ struct BCRegs {
 
 // (u, dt) rows: dt = softplus(delta + bias) applied once per element here; bias_r holds the
 // thread's 16 row biases (loaded once per kernel, so no global load sits in the chunk loop)
-template <typename Tin, bool SOFTPLUS, bool HAS_BIAS>
+template <typename Tin, bool SOFTPLUS, bool HAS_BIAS, bool FULL>
 __device__ inline void store_ud(float* s_ud, const RowRegs<Tin>& ru, const RowRegs<Tin>& rd, const float* bias_r,
                                 int tn, int nrow) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-        const bool ok = lane < tn && wave + 4 * i < nrow;
         float dt = rd.at(i);
         if (HAS_BIAS) dt += bias_r[i];
-        if (SOFTPLUS) dt = softplus(dt);
-        *reinterpret_cast<float2*>(&s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]) =
-            make_float2(ok ? ru.at(i) : 0.f, ok ? dt : 0.f);
+        if (SOFTPLUS) dt = softplus2(dt);     // the forward's dt bit for bit (its replay restarts from the forward's states)
+        float uv = ru.at(i);
+        if (!FULL) {
+            const bool ok = lane < tn && wave + 4 * i < nrow;
+            dt = ok ? dt : 0.f;
+            uv = ok ? uv : 0.f;
+        }
+        *reinterpret_cast<float2*>(&s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]) = make_float2(uv, dt);
+    }
+}
+
+// Forward staging: (dt u, dt) rows with dt = softplus(delta + bias), and D u kept in the thread's registers for
+// the flush (the flush thread owns the same (row, step) elements), so the recurrence does neither the dt u
+// product nor the D u skip term per lane and step.  FULL: every step and row of the chunk is real data, no
+// selects (all chunks but the row's last one).
+template <typename Tin, bool SOFTPLUS, bool HAS_BIAS, bool HAS_D, bool FULL>
+__device__ inline void store_fwd(float* s_ud, const RowRegs<Tin>& ru, const RowRegs<Tin>& rd, const float2* s_par,
+                                 float* du_keep, int tn, int nrow) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        const float2 par = s_par[wave + 4 * i];         // (bias, D) of the row: one broadcast LDS read
+        float dt = rd.at(i);
+        if (HAS_BIAS) dt += par.x;
+        if (SOFTPLUS) dt = softplus2(dt);
+        float uv = ru.at(i);
+        if (!FULL) {
+            const bool ok = lane < tn && wave + 4 * i < nrow;
+            dt = ok ? dt : 0.f;
+            uv = ok ? uv : 0.f;
+        }
+        du_keep[i] = HAS_D ? par.y * uv : 0.f;
+        *reinterpret_cast<float2*>(&s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]) = make_float2(dt * uv, dt);
     }
 }
 
@@ -163,6 +192,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     // there.  That keeps LDS at 42 KB and VGPRs under 168, i.e. 3 workgroups (12 waves) per CU.
     __shared__ __attribute__((aligned(16))) float s_ud[CPB * UD_STRIDE];
     __shared__ __attribute__((aligned(16))) float s_bc[TC * BC_STRIDE];
+    __shared__ float2 s_par[CPB];                      // (delta_bias, D) per row of the block
 
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int b = bid / nblk_d, d0 = (bid % nblk_d) * CPB;
@@ -172,6 +202,10 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     const int d = d0 + id.c;
     const bool dvalid = d < D;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x < CPB) {
+        const int r = d0 + (int)threadIdx.x;
+        s_par[threadIdx.x] = make_float2((HAS_BIAS && r < D) ? a.delta_bias[r] : 0.f, (HAS_D && r < D) ? a.D[r] : 0.f);
+    }
 
     // the lane's 4 states as 2 packed pairs: every state update is v_pk_mul / v_pk_fma on pairs
     f2_t A2v[NS / 2], h2[NS / 2];
@@ -181,7 +215,6 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
         A2v[p] = dvalid ? f2_t{a.A[(int64_t)d * NSTATE + j], a.A[(int64_t)d * NSTATE + j + 1]} * AVSE_LOG2E : f2_t{0.f, 0.f};
         h2[p] = f2_t{0.f, 0.f};
     }
-    const float Dv = (HAS_D && dvalid) ? a.D[d] : 0.f;
 
     const Tin* u = (const Tin*)a.u;
     const Tin* dl = (const Tin*)a.delta;
@@ -191,18 +224,21 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     float* xrow = a.x + ((int64_t)b * D + (dvalid ? d : 0)) * nck32 * (2 * NSTATE) + 2 * id.g * NS;
 
     const int nrow = min(CPB, D - d0);
-    float bias_r[RPT];
-    load_bias_rows<HAS_BIAS>(bias_r, a.delta_bias, d0, D);
     RowRegs<Tin> ru, rd;
     BCRegs<Tin> rbc;
     ru.load(u, a.u_bs, a.u_ds, b, d0, D, 0, min(TC, L), L, rev);
     rd.load(dl, a.delta_bs, a.delta_ds, b, d0, D, 0, min(TC, L), L, rev);
     rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, 0, min(TC, L), L, rev);
+    __syncthreads();                                   // s_par
+    float du_keep[RPT];                                // D u of the thread's staged elements, added at the flush
 
     for (int k = 0; k < nck; ++k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
         // registers -> LDS (chunk k)
-        store_ud<Tin, SOFTPLUS, HAS_BIAS>(s_ud, ru, rd, bias_r, tn, nrow);
+        if (tn == TC && nrow == CPB)
+            store_fwd<Tin, SOFTPLUS, HAS_BIAS, HAS_D, true>(s_ud, ru, rd, s_par, du_keep, tn, nrow);
+        else
+            store_fwd<Tin, SOFTPLUS, HAS_BIAS, HAS_D, false>(s_ud, ru, rd, s_par, du_keep, tn, nrow);
         rbc.store(s_bc, tn);
         __syncthreads();
         // prefetch chunk k + 1 while chunk k computes
@@ -223,16 +259,15 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
         constexpr int U = 8;
         auto steps = [&](int t, auto UNR) {
             constexpr int NU = decltype(UNR)::value;
-            float yv[NU], uv[NU];
+            float yv[NU];
 #pragma unroll
             for (int q = 0; q < NU; ++q) {
-                const float2 ud = *reinterpret_cast<const float2*>(&my_ud[2 * (t + q)]);
+                const float2 ud = *reinterpret_cast<const float2*>(&my_ud[2 * (t + q)]);   // (dt u, dt)
                 const float4 bq = *reinterpret_cast<const float4*>(&s_bc[(t + q) * BC_STRIDE + id.g * NS]);
                 const float4 cq = *reinterpret_cast<const float4*>(&s_bc[(t + q) * BC_STRIDE + NSTATE + id.g * NS]);
                 const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
                 const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
-                const float dt = ud.y, dtu = ud.y * ud.x;
-                const f2_t dt2 = f2_t{dt, dt}, dtu2 = f2_t{dtu, dtu};
+                const f2_t dt2 = f2_t{ud.y, ud.y}, dtu2 = f2_t{ud.x, ud.x};
                 f2_t y2 = f2_t{0.f, 0.f};
 #pragma unroll
                 for (int p = 0; p < NS / 2; ++p) {
@@ -240,17 +275,13 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                     y2 += h2[p] * cp[p];
                 }
                 yv[q] = y2.x + y2.y;
-                uv[q] = ud.x;
             }
 #pragma unroll
             for (int q = 0; q < NU; ++q) yv[q] = group_sum<G>(yv[q]);
             // every lane of the channel's quad holds the same sum and writes it to the same LDS word:
             // no exec-mask branch per step, so the NU reductions and stores schedule together
 #pragma unroll
-            for (int q = 0; q < NU; ++q) {
-                const float out = yv[q] + Dv * uv[q];
-                my_ud[2 * (t + q)] = out;                              // u slot <- out
-            }
+            for (int q = 0; q < NU; ++q) my_ud[2 * (t + q)] = yv[q];   // dt u slot <- y (D u added at the flush)
         };
         // always the full 64 steps: the staged tail of the last chunk is zero (dt = 0, u = 0, B = C = 0), which
         // leaves h unchanged, so no step needs a bounds test; the state is checkpointed every 16 steps
@@ -280,10 +311,13 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
             const auto ro = make_rsrc((Tin*)a.out + b * a.out_bs + (int64_t)d0 * a.out_ds,
                                       (int64_t)(nrow - 1) * a.out_ds + L);
             const int vo = wave * (int)a.out_ds + tpos(t0 + lane, L, rev);
+            float outv[RPT];
+#pragma unroll
+            for (int i = 0; i < RPT; ++i) outv[i] = s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane] + du_keep[i];
             if (a.out && lane < tn) {      // out is optional when z is given (training fwd: the bwd recomputes it)
 #pragma unroll
                 for (int i = 0; i < RPT; ++i)
-                    if (wave + 4 * i < nrow) bufst<Tin>::st(ro, vo, 4 * i * (int)a.out_ds, s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]);
+                    if (wave + 4 * i < nrow) bufst<Tin>::st(ro, vo, 4 * i * (int)a.out_ds, outv[i]);
             }
             if (HAS_Z) {
                 const auto rz_ = make_rsrc((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d0 * a.out_z_ds,
@@ -293,8 +327,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
 #pragma unroll
                     for (int i = 0; i < RPT; ++i)
                         if (wave + 4 * i < nrow)
-                            bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds,
-                                           s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane] * siluf_(rz.at(i)));
+                            bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds, outv[i] * siluf_(rz.at(i)));
                 }
             }
         }
@@ -319,10 +352,20 @@ __device__ inline void rs8_swap(const float v[8], float r[2]) {
     for (int j = 0; j < 2; ++j) {
         auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[j]), __float_as_uint(w[j + 2]), false, false);
         float x = __uint_as_float(p[0]) + __uint_as_float(p[1]);
-        x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, false));   // row_ror:8
-        x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, false));   // row_ror:4
+        x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, true));   // row_ror:8
+        x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, true));   // row_ror:4
         r[j] = x;
     }
+}
+
+// Reduce-scatter over a channel's quad (lanes g = 0..3): lane g returns the quad's sum of v[g].  Two DPP stages
+// (xor 2, then xor 1), each lane keeping the half its partner does not: 9 VALU for 4 sums (4 group_sums: 8)
+__device__ inline float quad_rs4(const float v[4], int g) {
+    const bool b1 = (g & 2) != 0, b0 = (g & 1) != 0;
+    float k[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) k[j] = (b1 ? v[j + 2] : v[j]) + dpp_xor2(b1 ? v[j] : v[j + 2]);
+    return (b0 ? k[1] : k[0]) + dpp_xor1(b0 ? k[0] : k[1]);
 }
 
 constexpr int RED = 8;   // adjoint steps buffered per cross-wave dB/dC flush
@@ -342,7 +385,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
     __shared__ __attribute__((aligned(16))) float s_ud[CPB * UD_STRIDE];   // (u, dt) -> (du, ddelta)
     __shared__ __attribute__((aligned(16))) float s_zg[CPB * Z_STRIDE];    // (F, g) -> (dz, g)  [(z, dout) unfolded]
     __shared__ __attribute__((aligned(16))) float s_bc[TC * BC_STRIDE];
-    __shared__ float s_red[4 * RED * 2 * NSTATE];
+    __shared__ __attribute__((aligned(16))) float s_red[4 * RED * 2 * NSTATE];
     __shared__ float s_bias[CPB];              // delta_bias of the block's rows (LDS, not 16 VGPRs per thread)
 
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -399,17 +442,17 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
             if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t0, tn, L, rev);
             rg.load(dout, a.dout_bs, a.dout_ds, b, d0, D, t0, tn, L, rev);
             rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t0, tn, L, rev);
+            __builtin_amdgcn_sched_barrier(0);   // no bf16 decode scheduled between the loads (each would wait for its load)
             __syncthreads();
+            // with z (and no out_z recompute) the gate is folded here, once per element instead of once
+            // per lane per step: s_zg = (F, g) with g = dout silu(z) and F = dout sg (1 + z (1 - sg)),
+            // so dz = out F in the replay; otherwise s_zg = (z, dout)
             {
                 float bias_r[RPT];
 #pragma unroll
                 for (int i = 0; i < RPT; ++i) bias_r[i] = s_bias[wave + 4 * i];
-                store_ud<Tin, SOFTPLUS, HAS_BIAS>(s_ud, ru, rd, bias_r, tn, nrow_b);
+                store_ud<Tin, SOFTPLUS, HAS_BIAS, false>(s_ud, ru, rd, bias_r, tn, nrow_b);
             }
-            rbc.store(s_bc, tn);
-            // with z (and no out_z recompute) the gate is folded here, once per element instead of once
-            // per lane per step: s_zg = (F, g) with g = dout silu(z) and F = dout sg (1 + z (1 - sg)),
-            // so dz = out F in the replay; otherwise s_zg = (z, dout)
 #pragma unroll
             for (int i = 0; i < RPT; ++i) {
                 const float zv = HAS_Z ? rz.get(i, tn, nrow_b) : 0.f, gd = rg.get(i, tn, nrow_b);
@@ -420,6 +463,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                 }
                 *reinterpret_cast<float2*>(&s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane]) = v;
             }
+            rbc.store(s_bc, tn);
         }
         __syncthreads();
 
@@ -451,17 +495,16 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                 float2 ud_n = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * ts]);
                 float4 bq_n = *reinterpret_cast<const float4*>(&s_bc[ts * BC_STRIDE + id.g * NS]);
                 float4 cq_n = *reinterpret_cast<const float4*>(&s_bc[ts * BC_STRIDE + NSTATE + id.g * NS]);
-                float2 zg_n = *reinterpret_cast<const float2*>(&s_zg[id.c * Z_STRIDE + 2 * ts]);
+                float y_q[4];          // the quad partials of y = sum_n C h of the group's 4 steps
 #pragma unroll
                 for (int i = 0; i < TS; ++i) {
                     const int t = ts + i;
-                    const float2 ud = ud_n, zg = zg_n;
+                    const float2 ud = ud_n;
                     const float4 bq = bq_n, cq = cq_n;
                     if (i + 1 < TS) {
                         ud_n = *reinterpret_cast<const float2*>(&s_ud[id.c * UD_STRIDE + 2 * (t + 1)]);
                         bq_n = *reinterpret_cast<const float4*>(&s_bc[(t + 1) * BC_STRIDE + id.g * NS]);
                         cq_n = *reinterpret_cast<const float4*>(&s_bc[(t + 1) * BC_STRIDE + NSTATE + id.g * NS]);
-                        zg_n = *reinterpret_cast<const float2*>(&s_zg[id.c * Z_STRIDE + 2 * (t + 1)]);
                     }
                     const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
                     const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
@@ -473,26 +516,27 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                         hist[i][p] = h[p];
                         y2 = pkfma(h[p], cp[p], y2);
                     }
-                    const float y = group_sum<G>(y2.x + y2.y);
-                    const float out = y + Dv * ud.x;
-                    float* zg_p = &s_zg[id.c * Z_STRIDE + 2 * t];
-                    float gv, dzv = 0.f, oz = out;
-                    if (HAS_Z && fold_gate) {
-                        dzv = out * zg.x;
-                        gv = zg.y;
-                    } else if (HAS_Z) {
-                        const float sg = sigmoidf_(zg.x);
-                        const float sl = zg.x * sg;
-                        gv = zg.y * sl;
-                        dzv = zg.y * out * sg * (1.f + zg.x * (1.f - sg));
-                        oz = out * sl;
-                    } else {
-                        gv = zg.y;
+                    y_q[i & 3] = y2.x + y2.y;
+                    if ((i & 3) == 3 && HAS_Z) {
+                        // the gate of steps i-3 .. i, one step per lane of the quad: lane g reduce-scatters y of step
+                        // i - 3 + g, forms out = y + D u and dz = out F (folded) or the full silu gate (s_zg = (z, dout))
+                        const float y = quad_rs4(y_q, id.g);
+                        const int tg = t - 3 + id.g;
+                        const float out = y + Dv * s_ud[id.c * UD_STRIDE + 2 * tg];
+                        float* zg_p = &s_zg[id.c * Z_STRIDE + 2 * tg];
+                        if (fold_gate) {
+                            zg_p[0] = out * zg_p[0];                      // (F, g) -> (dz, g)
+                        } else {
+                            const float2 zg = *reinterpret_cast<const float2*>(zg_p);
+                            const float sg = sigmoidf_(zg.x);
+                            const float sl = zg.x * sg;
+                            *reinterpret_cast<float2*>(zg_p) =
+                                make_float2(zg.y * out * sg * (1.f + zg.x * (1.f - sg)), zg.y * sl);   // (dz, g)
+                            if (!FOLD && a.recompute_out_z && dvalid && tg < tn)   // direct (uncoalesced) store
+                                io<Tin>::st((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d * a.out_z_ds + tpos(t0 + tg, L, rev),
+                                            out * sl);
+                        }
                     }
-                    *reinterpret_cast<float2*>(zg_p) = make_float2(dzv, gv);   // same value from the quad
-                    if (!FOLD && HAS_Z && a.recompute_out_z && id.g == 0 && t < tn)   // direct (uncoalesced) store
-                        io<Tin>::st((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d * a.out_z_ds + tpos(t0 + t, L, rev),
-                                    oz);
                     SCHED_FENCE();
                 }
             }
@@ -501,12 +545,12 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
             float gv_n = s_zg[id.c * Z_STRIDE + 2 * (ts + TS - 1) + 1];
             float4 bq_n = *reinterpret_cast<const float4*>(&s_bc[(ts + TS - 1) * BC_STRIDE + id.g * NS]);
             float4 cq_n = *reinterpret_cast<const float4*>(&s_bc[(ts + TS - 1) * BC_STRIDE + NSTATE + id.g * NS]);
+            float dus_q[4], ddt_q[4];     // quad partials of sum_n lam B and sum_n A lam dA h of the group's 4 steps
 #pragma unroll
             for (int i = TS - 1; i >= 0; --i) {
                 const int t = ts + i;
                 float part[8];
                 {
-                    float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * t];
                     const float2 ud = ud_n;
                     const float gv = gv_n;
                     const float4 bq = bq_n, cq = cq_n;
@@ -540,14 +584,8 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                         part[4 + 2 * p + 1] = pc.y;
                         dAn[p] = ldA;
                     }
-                    const float dus = group_sum<G>(dus2.x + dus2.y);
-                    const float ddt = group_sum<G>(ddt2.x + ddt2.y) * AVSE_LN2 + uu * dus;
-                    const float du = dus * dt + gv * Dv;
-                    const float sig = SOFTPLUS ? (1.f - fast_exp(-dt)) : 1.f;
-                    const float ddr = ddt * sig;
-                    dD_acc += gv * uu;
-                    dbias_acc += ddr;
-                    *reinterpret_cast<float2*>(ud_p) = make_float2(du, ddr);   // same value from the quad
+                    dus_q[i & 3] = dus2.x + dus2.y;               // lane partials; summed over the quad below
+                    ddt_q[i & 3] = ddt2.x + ddt2.y;
                 }
                 SCHED_FENCE();
 #ifdef AVSE_EXP_BWD_NORED
@@ -556,12 +594,33 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
 #endif
                 float r2[2];
                 rs8_swap(part, r2);
-                if ((id.lane & 12) == 0) {
-                    // vi = 4 b5 + 2 b4 + j: slot = (b5 ? C : B) + g * 4 + 2 b4 + j
+                {
+                    // vi = 4 b5 + 2 b4 + j: slot = (b5 ? C : B) + g * 4 + 2 b4 + j.  The slot does not depend on lane
+                    // bits 2-3 and those four lanes hold the same sums, so all of them store (same word, same value):
+                    // no exec-mask branch, and the reduction stays in the step's basic block for the scheduler
                     const int slot = ((id.lane >> 5) & 1) * NSTATE + id.g * NS + ((id.lane >> 4) & 1) * 2;
                     float* dst = &s_red[(id.wave * RED + (i & (RED - 1))) * 2 * NSTATE + slot];
-                    dst[0] = r2[0];
-                    dst[1] = r2[1];
+#ifdef AVSE_EXP_CONDRED
+                    if ((id.lane & 12) == 0)
+#endif
+                    *reinterpret_cast<float2*>(dst) = make_float2(r2[0], r2[1]);
+                }
+                if ((i & 3) == 0) {
+                    // per-channel epilogue of steps i .. i+3, one step per lane of the quad (not 4 copies of each):
+                    // lane g reduce-scatters the quad's partials to the sums of step i + g and finishes that step's
+                    // du, ddelta (the softplus derivative included) and its dD / ddelta_bias terms
+                    const float dus = quad_rs4(dus_q, id.g), ddt_s = quad_rs4(ddt_q, id.g);
+                    const int tg = ts + i + id.g;
+                    float* ud_p = &s_ud[id.c * UD_STRIDE + 2 * tg];
+                    const float2 ud = *reinterpret_cast<const float2*>(ud_p);
+                    const float gv = s_zg[id.c * Z_STRIDE + 2 * tg + 1];
+                    const float ddt = ddt_s * AVSE_LN2 + ud.x * dus;
+                    const float du = dus * ud.y + gv * Dv;
+                    const float sig = SOFTPLUS ? (1.f - fast_exp(-ud.y)) : 1.f;
+                    const float ddr = ddt * sig;
+                    dD_acc += gv * ud.x;
+                    dbias_acc += ddr;
+                    *reinterpret_cast<float2*>(ud_p) = make_float2(du, ddr);
                 }
                 if ((i & (RED - 1)) == 0) {
                     // cross-wave sum of steps ts+i .. ts+i+RED-1 -> partial slab
@@ -620,6 +679,8 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
             p[id.g * NS + 2 * q] = dA_acc[q].x;
             p[id.g * NS + 2 * q + 1] = dA_acc[q].y;
         }
+        dD_acc = group_sum<G>(dD_acc);                  // each lane of the quad finished a quarter of the steps
+        dbias_acc = group_sum<G>(dbias_acc);
         if (id.g == 0) {
             p[NSTATE] = dD_acc;
             p[NSTATE + 1] = dbias_acc;
