@@ -311,23 +311,24 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
             const auto ro = make_rsrc((Tin*)a.out + b * a.out_bs + (int64_t)d0 * a.out_ds,
                                       (int64_t)(nrow - 1) * a.out_ds + L);
             const int vo = wave * (int)a.out_ds + tpos(t0 + lane, L, rev);
+            // rows past D need no test: their offsets lie beyond the resource's range, whose stores the hardware
+            // drops; steps past L do (inside the range they would land in the row padding), one exec mask for all
             float outv[RPT];
 #pragma unroll
             for (int i = 0; i < RPT; ++i) outv[i] = s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane] + du_keep[i];
             if (a.out && lane < tn) {      // out is optional when z is given (training fwd: the bwd recomputes it)
 #pragma unroll
-                for (int i = 0; i < RPT; ++i)
-                    if (wave + 4 * i < nrow) bufst<Tin>::st(ro, vo, 4 * i * (int)a.out_ds, outv[i]);
+                for (int i = 0; i < RPT; ++i) bufst<Tin>::st(ro, vo, 4 * i * (int)a.out_ds, outv[i]);
             }
             if (HAS_Z) {
                 const auto rz_ = make_rsrc((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d0 * a.out_z_ds,
                                            (int64_t)(nrow - 1) * a.out_z_ds + L);
                 const int vz = wave * (int)a.out_z_ds + tpos(t0 + lane, L, rev);
+#pragma unroll
+                for (int i = 0; i < RPT; ++i) outv[i] *= siluf_(rz.at(i));   // 16 independent gates (ILP)
                 if (lane < tn) {
 #pragma unroll
-                    for (int i = 0; i < RPT; ++i)
-                        if (wave + 4 * i < nrow)
-                            bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds, outv[i] * siluf_(rz.at(i)));
+                    for (int i = 0; i < RPT; ++i) bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds, outv[i]);
                 }
             }
         }
@@ -342,16 +343,23 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
 // the full sums of value indices vi = 4 b5 + 2 b4 + j in r[j], j = 0, 1, for its own state group
 // (bits 0-1); lanes with b2 = b3 = 0 carry the unique copy.  16 VALU, no LDS swizzles.
 __device__ inline void rs8_swap(const float v[8], float r[2]) {
-    float w[4];
+    // the swapped pairs of two adjacent value indices are added as one v_pk_add_f32 (3 packed adds for the 6
+    // scalar ones of the two swap stages)
+    f2_t w[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 4]), false, false);
-        w[i] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    for (int i = 0; i < 2; ++i) {
+        auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2 * i]), __float_as_uint(v[2 * i + 4]), false, false);
+        auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2 * i + 1]), __float_as_uint(v[2 * i + 5]), false, false);
+        w[i] = f2_t{__uint_as_float(p[0]), __uint_as_float(q[0])} + f2_t{__uint_as_float(p[1]), __uint_as_float(q[1])};
     }
+    // w[0] = (w_0, w_1), w[1] = (w_2, w_3) in the notation of the scalar form
+    auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[0].x), __float_as_uint(w[1].x), false, false);
+    auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[0].y), __float_as_uint(w[1].y), false, false);
+    const f2_t xy = f2_t{__uint_as_float(p[0]), __uint_as_float(q[0])} + f2_t{__uint_as_float(p[1]), __uint_as_float(q[1])};
+    float xs[2] = {xy.x, xy.y};
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[j]), __float_as_uint(w[j + 2]), false, false);
-        float x = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+        float x = xs[j];
         x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, true));   // row_ror:8
         x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, true));   // row_ror:4
         r[j] = x;
@@ -485,7 +493,10 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     for (int p = 0; p < NP; ++p) h0[p] = f2_t{0.f, 0.f};
                 }
             }
-            f2_t hist[TS][NP];
+            // the replay keeps each step's dA = exp(dt A) (the adjoint re-evaluates no exponential) and the state after
+            // every odd step; the adjoint gets h(t-1) dA(t) at odd steps as h(t) - dt u B(t), and at even steps
+            // recomputes h(t) = dA(t) h(t-1) + dt u B(t) from the stored odd state (96 VGPRs instead of 64 for h alone)
+            f2_t dAs[TS][NP], hodd[TS / 2][NP];
             {
                 f2_t h[NP];
 #pragma unroll
@@ -512,8 +523,10 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     f2_t y2 = f2_t{0.f, 0.f};
 #pragma unroll
                     for (int p = 0; p < NP; ++p) {
-                        h[p] = pkfma(exp2_2(dt2 * A2v[p]), h[p], dtu2 * bp[p]);
-                        hist[i][p] = h[p];
+                        const f2_t dA = exp2_2(dt2 * A2v[p]);
+                        dAs[i][p] = dA;
+                        h[p] = pkfma(dA, h[p], dtu2 * bp[p]);
+                        if (i & 1) hodd[i >> 1][p] = h[p];
                         y2 = pkfma(h[p], cp[p], y2);
                     }
                     y_q[i & 3] = y2.x + y2.y;
@@ -568,16 +581,23 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     f2_t ddt2 = f2_t{0.f, 0.f}, dus2 = f2_t{0.f, 0.f};
 #pragma unroll
                     for (int p = 0; p < NP; ++p) {
-                        const f2_t hp = (i == 0) ? h0[p] : hist[i > 0 ? i - 1 : 0][p];
                         // dAn holds lam(t + 1) dA(t + 1): the product the previous step formed for its lhp
                         lam[p] = pkfma(gv2, cp[p], dAn[p]);
-                        const f2_t dA = exp2_2(dt2 * A2v[p]);
+                        const f2_t dA = dAs[i][p];
                         const f2_t ldA = lam[p] * dA;
-                        const f2_t lhp = ldA * hp;
+                        f2_t ht, lhp;                              // h(t) and lam dA h(t - 1)
+                        if (i & 1) {
+                            ht = hodd[i >> 1][p];
+                            lhp = lam[p] * pkfma(-dtu2, bp[p], ht);
+                        } else {
+                            const f2_t hp = (i == 0) ? h0[p] : hodd[i > 0 ? (i - 1) >> 1 : 0][p];
+                            ht = pkfma(dA, hp, dtu2 * bp[p]);
+                            lhp = ldA * hp;
+                        }
                         ddt2 = pkfma(A2v[p], lhp, ddt2);           // x ln 2 and + u * sum(lam B) once per lane, below
                         dus2 = pkfma(lam[p], bp[p], dus2);
                         dA_acc[p] = pkfma(dt2, lhp, dA_acc[p]);
-                        const f2_t pb = lam[p] * dtu2, pc = gv2 * hist[i][p];
+                        const f2_t pb = lam[p] * dtu2, pc = gv2 * ht;
                         part[2 * p] = pb.x;
                         part[2 * p + 1] = pb.y;
                         part[4 + 2 * p] = pc.x;
@@ -647,24 +667,26 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
             const auto r_dd = make_rsrc((Tin*)a.ddelta + b * a.ddelta_bs + (int64_t)d0 * a.ddelta_ds,
                                         (int64_t)(nrow - 1) * a.ddelta_ds + L);
             const int v_du = wave * (int)a.du_ds + pos, v_dd = wave * (int)a.ddelta_ds + pos;
+            // rows past D: beyond the resources' ranges (stores dropped by the hardware); steps past L: exec mask
+            float2 v[RPT];
+#pragma unroll
+            for (int i = 0; i < RPT; ++i) v[i] = *reinterpret_cast<const float2*>(&s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]);
             if (lane < tn) {
 #pragma unroll
                 for (int i = 0; i < RPT; ++i) {
-                    if (wave + 4 * i < nrow) {
-                        const float2 v = *reinterpret_cast<const float2*>(&s_ud[(wave + 4 * i) * UD_STRIDE + 2 * lane]);
-                        bufst<Tin>::st(r_du, v_du, 4 * i * (int)a.du_ds, v.x);
-                        bufst<Tin>::st(r_dd, v_dd, 4 * i * (int)a.ddelta_ds, v.y);
-                    }
+                    bufst<Tin>::st(r_du, v_du, 4 * i * (int)a.du_ds, v[i].x);
+                    bufst<Tin>::st(r_dd, v_dd, 4 * i * (int)a.ddelta_ds, v[i].y);
                 }
             }
             if (HAS_Z) {
                 const auto r_dz = make_rsrc((Tin*)a.dz + b * a.dz_bs + (int64_t)d0 * a.dz_ds, (int64_t)(nrow - 1) * a.dz_ds + L);
                 const int v_dz = wave * (int)a.dz_ds + pos;
+                float dzv[RPT];
+#pragma unroll
+                for (int i = 0; i < RPT; ++i) dzv[i] = s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane];
                 if (lane < tn) {
 #pragma unroll
-                    for (int i = 0; i < RPT; ++i)
-                        if (wave + 4 * i < nrow)
-                            bufst<Tin>::st(r_dz, v_dz, 4 * i * (int)a.dz_ds, s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane]);
+                    for (int i = 0; i < RPT; ++i) bufst<Tin>::st(r_dz, v_dz, 4 * i * (int)a.dz_ds, dzv[i]);
                 }
             }
         }
