@@ -43,7 +43,7 @@ def main():
     es = 4 if dt == torch.float32 else 2
     dev = "cuda"
     for cfg in args.cfg:
-        b, d, l = map(int, cfg.split(","))
+        b, d, l = map(int, cfg.replace("x", ",").split(","))   # BxDxL also accepted
         g = torch.Generator(device=dev).manual_seed(0)
         per = 128 // es
         lp = -(-l // per) * per if args.pad else l
