@@ -610,8 +610,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                 SCHED_FENCE();
 #ifdef AVSE_EXP_BWD_NORED
                 if (part[0] == 12345.f) a.dB[0] = part[1] + part[2] + part[3] + part[4] + part[5] + part[6] + part[7];
-                continue;
-#endif
+#else
                 float r2[2];
                 rs8_swap(part, r2);
                 {
@@ -625,6 +624,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
 #endif
                     *reinterpret_cast<float2*>(dst) = make_float2(r2[0], r2[1]);
                 }
+#endif
                 if ((i & 3) == 0) {
                     // per-channel epilogue of steps i .. i+3, one step per lane of the quad (not 4 copies of each):
                     // lane g reduce-scatters the quad's partials to the sums of step i + g and finishes that step's
@@ -642,6 +642,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     dbias_acc += ddr;
                     *reinterpret_cast<float2*>(ud_p) = make_float2(du, ddr);
                 }
+#if !defined(AVSE_EXP_BWD_NORED) && !defined(AVSE_EXP_BWD_NOFLUSH)
                 if ((i & (RED - 1)) == 0) {
                     // cross-wave sum of steps ts+i .. ts+i+RED-1 -> partial slab
                     __syncthreads();
@@ -656,6 +657,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     }
                     __syncthreads();
                 }
+#endif
             }
         }
         __syncthreads();
