@@ -779,7 +779,7 @@ def test_lstm_group_kernels_at_the_avse1_shape(monkeypatch):
 # ------------------------------------------------------------------ fused dwconv <-> PReLU -> gLN (avse4 TCN)
 
 @pytest.mark.parametrize("B,C,Kn,P,dil", [(2, 512, 3999, 3, 128), (3, 64, 300, 3, 4), (2, 40, 2500, 3, 1), (1, 8, 17, 5, 2),
-                                          (2, 16, 5000, 3, 256)])
+                                          (2, 16, 5000, 3, 256), (2, 24, 1001, 5, 4), (1, 8, 13, 3, 4), (2, 8, 2050, 7, 64)])
 def test_dwconv_prelu_gln_fused_vs_fp64(B, C, Kn, P, dil):
     """layers.dwconv_prelu_gln (two fused passes each way) vs the fp64 composition of the reference ops
     (model.py:278-292: depthwise conv1d, PReLU, gLN with EPS 1e-8 inside the sqrt): output and the gradients of
