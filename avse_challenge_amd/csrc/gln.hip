@@ -137,31 +137,42 @@ __global__ __launch_bounds__(THREADS) void apply_fused_kernel(int C, int K, cons
     for (int t = threadIdx.x; t < K; t += THREADS) yr[t] = g * prelu(xr[t], a) + o;
 }
 
-// backward pass 1: per row S1 = sum dy, S2 = sum dy * xhat
+typedef unsigned int u4_t __attribute__((ext_vector_type(4)));
+__device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, int voff_elems) {
+    const u4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff_elems * 4, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ inline float f4at(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
+
+// backward pass 1: per row S1 = sum dy, S2 = sum dy * xhat.  4 consecutive elements per thread (dwordx4 loads, rows
+// need only dword alignment; the row's last partial quadruple is masked per element), 2 quadruples in flight
 __global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int C, int K, const float* __restrict__ x,
                                                              const float* __restrict__ alpha, const float2* __restrict__ stats,
                                                              const float* __restrict__ dy, float2* __restrict__ ws) {
+    constexpr int V = 4, UB = 2;
     __shared__ float red[4];
     const int row = blockIdx.x, b = row / C;
     const float a = alpha[0];
     const float2 st = stats[b];
-    const float* xr = x + (int64_t)row * K;
-    const float* gr = dy + (int64_t)row * K;
+    const auto rx = make_rsrc(x + (int64_t)row * K, K), rg = make_rsrc(dy + (int64_t)row * K, K);
     float s1 = 0.f, s2 = 0.f;
-    for (int t0 = 0; t0 < K; t0 += DW_U * THREADS) {  // DW_U elements per thread in flight
-        float gv[DW_U], xv[DW_U];
+    for (int t0 = 0; t0 < K; t0 += UB * V * THREADS) {
+        float4 gv[UB], xv[UB];
 #pragma unroll
-        for (int j = 0; j < DW_U; ++j) {
-            const int t = min(t0 + j * THREADS + (int)threadIdx.x, K - 1);
-            gv[j] = gr[t];
-            xv[j] = xr[t];
+        for (int j = 0; j < UB; ++j) {
+            const int t = t0 + (j * THREADS + (int)threadIdx.x) * V;
+            gv[j] = ld4(rg, t);
+            xv[j] = ld4(rx, t);
         }
 #pragma unroll
-        for (int j = 0; j < DW_U; ++j) {
-            if (t0 + j * THREADS + (int)threadIdx.x < K) {
-                const float xh = (prelu(xv[j], a) - st.x) * st.y;
-                s1 += gv[j];
-                s2 += gv[j] * xh;
+        for (int j = 0; j < UB; ++j) {
+            const int t = t0 + (j * THREADS + (int)threadIdx.x) * V;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const float g = (t + e < K) ? f4at(gv[j], e) : 0.f;
+                const float xh = (prelu(f4at(xv[j], e), a) - st.x) * st.y;
+                s1 += g;
+                s2 += g * xh;
             }
         }
     }
@@ -404,13 +415,6 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd_kernel(int C, int K, i
 // quadruple is either wholly before the row or starts inside it; the row's tail is clipped dword by dword by the
 // buffer range check): 4x fewer VMEM instructions than the scalar form, which was VMEM-issue bound (10 dword
 // accesses per element: 3 taps of y1 and dy, 3 of x, the dx store).  Same per-element arithmetic and tap order.
-typedef unsigned int u4_t __attribute__((ext_vector_type(4)));
-__device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, int voff_elems) {
-    const u4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff_elems * 4, 0, 0);
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ inline float f4at(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
-
 template <int P>
 __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int C, int K, int dil, const float* __restrict__ x,
                                                                   const float* __restrict__ w, const float* __restrict__ y1,
@@ -521,15 +525,15 @@ __global__ void dw_tail_kernel(const float* __restrict__ ws_dw, const float2* __
     if (blockIdx.x == 0) {
         // 32 loads per thread in flight: the row partials were written by workgroups on every XCD, so each pass of
         // this loop is a round trip to the memory-side cache (8 in flight: 4 round trips, 12.8 us for C4's 8192 rows)
+        // (a guarded load per element had become a branch + wait per load: 32 serial round trips, 13.5 us; the buffer
+        // range check returns 0 past the end without a branch)
         __shared__ double red[4];
         double s = 0.0;
+        const auto ra = make_rsrc(ws_alpha, (int64_t)B * C);
         for (int i0 = 0; i0 < B * C; i0 += 32 * blockDim.x) {
             float v[32];
 #pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                const int i = i0 + j * blockDim.x + threadIdx.x;
-                v[j] = i < B * C ? ws_alpha[i] : 0.f;
-            }
+            for (int j = 0; j < 32; ++j) v[j] = bufld<float>::ld(ra, i0 + j * (int)blockDim.x + (int)threadIdx.x, 0);
 #pragma unroll
             for (int j = 0; j < 32; ++j) s += v[j];
         }
@@ -540,21 +544,37 @@ __global__ void dw_tail_kernel(const float* __restrict__ ws_dw, const float2* __
         if (threadIdx.x == 0) dalpha[0] = (float)(red[0] + red[1] + red[2] + red[3]);
         return;
     }
+    // sums over the batch with 16 loads in flight per thread (buffer loads: no per-load branch)
     const int i = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
     if (i < C * P) {
         const int c = i / P, k = i % P;
+        const auto rw = make_rsrc(ws_dw, (int64_t)B * C * DW_MAXP);
         float v = 0.f;
-#pragma unroll 16
-        for (int b = 0; b < B; ++b) v += ws_dw[((int64_t)b * C + c) * DW_MAXP + k];
+        for (int b0 = 0; b0 < B; b0 += 16) {
+            float t[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) t[j] = bufld<float>::ld(rw, (b0 + j < B ? (b0 + j) * C + c : B * C) * DW_MAXP + k, 0);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v += t[j];
+        }
         dw[i] = v;
     } else if (i < C * P + C) {
         const int c = i - C * P;
+        const auto rr = make_rsrc(reinterpret_cast<const float*>(ws_rows), (int64_t)2 * B * C);
         double g = 0.0, bt = 0.0;
-#pragma unroll 16
-        for (int b = 0; b < B; ++b) {
-            const float2 v = ws_rows[(int64_t)b * C + c];
-            bt += v.x;
-            g += v.y;
+        for (int b0 = 0; b0 < B; b0 += 16) {
+            float t[16][2];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int e = (b0 + j < B ? (b0 + j) * C + c : B * C) * 2;
+                t[j][0] = bufld<float>::ld(rr, e, 0);
+                t[j][1] = bufld<float>::ld(rr, e + 1, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                bt += t[j][0];
+                g += t[j][1];
+            }
         }
         dgamma[c] = (float)g;
         dbeta[c] = (float)bt;
