@@ -437,6 +437,21 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
     if (threadIdx.x < CPB) s_bias[threadIdx.x] = (HAS_BIAS && d0 + (int)threadIdx.x < D) ? a.delta_bias[d0 + threadIdx.x] : 0.f;
     __syncthreads();
     constexpr bool fold_gate = FOLD;        // = !recompute_out_z (the drop-in's reference call recomputes out_z)
+    // the 16-step checkpoint (state after step ts - 1) of the sub-chunk starting at logical step ts, into ck_nx; slot
+    // j < 0 (the row's first sub-chunk) restarts from zero.  Clamped address, select at use: no branch, no wait here
+    f2_t ck_nx[NP];
+    bool ck_ok = false;
+    // (the prefetch also runs for sub-chunks past the row's end, which are skipped: the slot is clamped to the row's
+    // 2 nck32 checkpoints, whose last one is the last element of the tensor for the last (b, d))
+    auto ck_load = [&](int ts_abs) {
+        const int j = ts_abs / TS - 1;
+        ck_ok = ts_abs >= 0 && j >= 0 && j < 2 * nck32 && dvalid;
+        const int jc = min(max(j, 0), 2 * nck32 - 1);
+        const float* xp = xrow + (int64_t)(jc >> 1) * (2 * NSTATE) + (jc & 1);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) ck_nx[p] = f2_t{xp[4 * p], xp[4 * p + 2]};
+    };
+    ck_load((nck - 1) * TC + (TC / TS - 1) * TS);
 
     for (int k = nck - 1; k >= 0; --k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
@@ -480,19 +495,16 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
 #pragma unroll 1
         for (int s = TC / TS - 1; s >= 0; --s) {
             const int ts = s * TS;
-            if (ts >= tn) continue;                 // wholly past the row's end: lam stays 0, nothing to add
+            // this sub-chunk's checkpoint was loaded one sub-chunk ago; issue the next one's now, so its global-memory
+            // latency overlaps this sub-chunk's replay and adjoint (waited on where it was used: ~1-2 us per 16 steps)
             f2_t h0[NP];
             {
-                const int j = (t0 + ts) / TS - 1;   // checkpoint slot = state after step t0 + ts - 1
-                if (j >= 0 && dvalid) {
-                    const float* xp = xrow + (int64_t)(j >> 1) * (2 * NSTATE) + (j & 1);
+                const bool ok = ck_ok;
 #pragma unroll
-                    for (int p = 0; p < NP; ++p) h0[p] = f2_t{xp[4 * p], xp[4 * p + 2]};
-                } else {
-#pragma unroll
-                    for (int p = 0; p < NP; ++p) h0[p] = f2_t{0.f, 0.f};
-                }
+                for (int p = 0; p < NP; ++p) h0[p] = ok ? ck_nx[p] : f2_t{0.f, 0.f};
+                ck_load(s > 0 ? t0 + ts - TS : t0 - TS);
             }
+            if (ts >= tn) continue;                 // wholly past the row's end: lam stays 0, nothing to add
             // the replay keeps each step's dA = exp(dt A) (the adjoint re-evaluates no exponential) and the state after
             // every odd step; the adjoint gets h(t-1) dA(t) at odd steps as h(t) - dt u B(t), and at even steps
             // recomputes h(t) = dA(t) h(t-1) + dt u B(t) from the stored odd state (96 VGPRs instead of 64 for h alone)
