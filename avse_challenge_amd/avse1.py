@@ -169,6 +169,7 @@ class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 conv
         pay a transpose in and out of every conv (needs PYTORCH_MIOPEN_SUGGEST_NHWC=1)."""
         self.channels_last = on
         self.to(memory_format=torch.channels_last if on else torch.contiguous_format)
+        self.conv1.nhwc_out = on          # the 1 -> 64 conv as GEMMs into channels-last memory (layers._Conv1Fn)
         return self
 
     def forward(self, spec):              # (B, 1, T, F) -> (B, T, 4F)

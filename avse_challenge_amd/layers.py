@@ -237,6 +237,57 @@ class _DilatedConvFn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+class _Conv1Fn(torch.autograd.Function):
+    """AudioFeatNet.conv1 = Conv2d(1, 64, 5, padding=2) (model.py:199-215) as GEMMs over all B·T·F pixels, writing its
+    output straight into channels-last memory.  MIOpen ran this single-input-channel conv in NCHW (for C = 1 the
+    input is both NCHW- and NHWC-contiguous, and the library picks NCHW): its output and its incoming gradient were
+    each copied between layouts (2 x 791 MB per step), the bias was a separate pass, and the input gradient took
+    ~3.6 ms behind transposes.  Here: A = the (B·T·F, 26) im2col rows with a ones column (the bias); y = A @ [W^T; b]
+    (K = 26); dW and db in ONE GEMM dy^T @ A; dx = col2im of (W^T @ dy^T) as 25 shifted adds of contiguous tap
+    planes.  add_bias=False leaves b out of y (a training-mode BatchNorm consumer: DilatedConv2d) but returns db."""
+
+    @staticmethod
+    def _rows(x):
+        n, _, h, w = x.shape
+        xp = F.pad(x.reshape(n, h, w), (2, 2, 2, 2))                               # (n, h + 4, w + 4)
+        hp, wp = h + 4, w + 4
+        a = x.new_empty((n, h, w, 26))
+        a[..., :25].view(n, h, w, 5, 5).copy_(xp.as_strided((n, h, w, 5, 5), (hp * wp, wp, 1, wp, 1)))
+        a[..., 25] = 1.0
+        return a.view(n * h * w, 26)
+
+    @staticmethod
+    def forward(ctx, x, w, b, add_bias):
+        n, _, h, ww = x.shape
+        a = _Conv1Fn._rows(x)
+        wb = torch.cat([w.reshape(w.shape[0], 25), (b if add_bias else torch.zeros_like(b)).reshape(-1, 1)], 1)
+        y = a @ wb.t()                                                                # (n h w, 64): NHWC memory
+        ctx.save_for_backward(a, w)
+        ctx.shape = (n, h, ww)
+        return y.view(n, h, ww, -1).permute(0, 3, 1, 2)                               # channels-last view
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, w = ctx.saved_tensors
+        n, h, ww = ctx.shape
+        cout = w.shape[0]
+        dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)                                # a view for channels-last dy
+        dx = dw = db = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            g = dy2.t() @ a                                                           # (64, 26): dW | db
+            dw = g[:, :25].reshape(w.shape) if ctx.needs_input_grad[1] else None
+            db = g[:, 25].contiguous() if ctx.needs_input_grad[2] else None
+        if ctx.needs_input_grad[0]:
+            gt = w.reshape(cout, 25).t() @ dy2.t()                                    # (25, n h w): tap planes
+            gt = gt.view(5, 5, n, h, ww)
+            dxp = dy2.new_zeros((n, h + 4, ww + 4))
+            for i in range(5):
+                for j in range(5):
+                    dxp[:, i:i + h, j:j + ww] += gt[i, j]
+            dx = dxp[:, 2:-2, 2:-2].reshape(n, 1, h, ww).contiguous()
+        return dx, dw, db, None
+
+
 class DilatedConv2d(nn.Conv2d):
     """nn.Conv2d(cin, cout, 5, padding=2*dilation, dilation) — the avse1 AudioFeatNet convs (same parameters and
     state_dict keys).  The 64 -> 64 ones on GPU tensors in channels-last memory (the benchmarked layout) take their
@@ -252,12 +303,22 @@ class DilatedConv2d(nn.Conv2d):
         super().__init__(cin, cout, kernel_size, padding=padding, dilation=dilation)
         assert self.padding == (2 * self.dilation[0],) * 2 and self.kernel_size == (5, 5)
 
+    nhwc_out = False          # set by AudioFeatNet.use_channels_last: conv1 (1 -> 64) writes channels-last output
+
+    def conv1_ok(self, x):
+        return (self.nhwc_out and os.environ.get("AVSE_CONV1_GEMM", "1") == "1" and x.is_cuda and self.in_channels == 1
+                and self.dilation[0] == 1 and self.bias is not None and x.dtype == torch.float32 and x.is_contiguous())
+
     def hip_ok(self, x):
+        if self.conv1_ok(x):
+            return True
         return (os.environ.get("AVSE_DCONV_WGRAD", "1") == "1" and x.is_cuda and self.in_channels == 64
                 and self.out_channels == 64 and self.dilation[0] <= K.DCONV_WGRAD_MAX_DIL
                 and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last))
 
     def forward(self, x, bias_to_bn=False):
+        if self.conv1_ok(x):
+            return _Conv1Fn.apply(x, self.weight, self.bias, not (bias_to_bn and self.bias is not None))
         if self.hip_ok(x):
             add_bias = not (bias_to_bn and self.bias is not None)
             return _DilatedConvFn.apply(x, self.weight, self.bias, self.dilation[0], add_bias)

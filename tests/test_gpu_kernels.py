@@ -904,6 +904,35 @@ def test_dilated_conv2d_module_grads_vs_torch():
     close(ours.bias.grad, ref.bias.grad, 2e-5 * sc(ref.bias.grad), 0, "db")
 
 
+def test_conv1_module_nhwc_vs_torch():
+    """AudioFeatNet.conv1 (DilatedConv2d(1, 64, 5, padding=2) with nhwc_out: layers._Conv1Fn on hipBLASLt) at an avse1
+    spectrogram shape: channels-last output, and output / input / weight / bias gradients vs nn.Conv2d in fp64; with
+    bias_to_bn the bias is left out of the output and its gradient is unchanged."""
+    from avse_challenge_amd.layers import DilatedConv2d
+    torch.manual_seed(4)
+    ref = torch.nn.Conv2d(1, 64, 5, padding=2).double()
+    ours = DilatedConv2d(1, 64, 5, padding=2, dilation=1).to(DEV)
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    ours.nhwc_out = True
+    x = det_input((2, 1, 376, 257), 1860)
+    gy = det_input((2, 64, 376, 257), 1861)
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr)
+    (yr * gy.double()).sum().backward()
+    sc = lambda t: max(1e-6, float(t.abs().max()))                                                 # noqa: E731
+    for bias_to_bn in (False, True):
+        ours.zero_grad()
+        xg = x.to(DEV).requires_grad_(True)
+        y = ours(xg, bias_to_bn=bias_to_bn)
+        assert y.is_contiguous(memory_format=torch.channels_last)
+        want = yr - ref.bias.view(1, -1, 1, 1) if bias_to_bn else yr
+        close(y, want, 2e-6 * sc(want), 0, "y")
+        (y * gy.to(DEV)).sum().backward()
+        close(xg.grad, xr.grad, 2e-5 * sc(xr.grad), 0, "dx")
+        close(ours.weight.grad, ref.weight.grad, 2e-5 * sc(ref.weight.grad), 0, "dw")
+        close(ours.bias.grad, ref.bias.grad, 2e-5 * sc(ref.bias.grad), 0, "db")
+
+
 # ------------------------------------------------------------------ ResNet trunk 3x3 Conv2d weight gradient
 
 @pytest.mark.parametrize("N,cin,cout,H,W,stride", [(6, 64, 64, 24, 24, 1), (5, 64, 128, 24, 24, 2),

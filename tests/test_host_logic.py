@@ -87,3 +87,26 @@ def test_gemm_conv_matches_conv2d_fp64(k, stride, hw, cl):
     dxr, dwr = torch.autograd.grad(yr, (x, w), gy)
     torch.testing.assert_close(dx, dxr, rtol=1e-12, atol=1e-12)
     torch.testing.assert_close(dw, dwr, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("add_bias", [True, False])
+def test_conv1_gemm_matches_conv2d_fp64(add_bias):
+    """layers._Conv1Fn (AudioFeatNet.conv1, Conv2d(1, 64, 5, padding=2), model.py:199-215, as im2col GEMMs with the bias
+    as a ones column and a 25-plane col2im backward) equals F.conv2d in fp64: output (channels-last memory), input /
+    weight / bias gradients.  add_bias=False leaves the bias out of the output (BatchNorm-folded) but returns db."""
+    import torch.nn.functional as F
+    from avse_challenge_amd.layers import _Conv1Fn
+    g = torch.Generator().manual_seed(11 + add_bias)
+    x = torch.randn(3, 1, 11, 17, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(8, 1, 5, 5, generator=g, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(8, generator=g, dtype=torch.float64, requires_grad=True)
+    y = _Conv1Fn.apply(x, w, b, add_bias)
+    yr = F.conv2d(x, w, b if add_bias else None, padding=2)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y, yr, rtol=1e-12, atol=1e-12)
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    got = torch.autograd.grad(y, (x, w, b), gy)
+    xr, wr, br = (t.detach().requires_grad_(True) for t in (x, w, b))
+    ref = torch.autograd.grad(F.conv2d(xr, wr, br, padding=2), (xr, wr, br), gy)
+    for a_, r_ in zip(got, ref):
+        torch.testing.assert_close(a_, r_, rtol=1e-12, atol=1e-12)
