@@ -100,6 +100,7 @@ SIGNATURES = {
     "avse_maxpool2d_out_size": (c_i64, [c_i64] * 4),
     "avse_maxpool2d_fwd": (c_i32, [c_i64] * 9 + [c_vp, c_vp, c_vp, c_vp]),
     "avse_maxpool2d_bwd": (c_i32, [c_i64] * 9 + [c_vp, c_vp, c_vp, c_vp]),
+    "avse_transpose_cp": (c_i32, [c_i64] * 3 + [c_vp, c_vp, c_vp]),
     "avse_bnact_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "avse_bnact_fwd": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_f32, c_f32,
                                c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -22,7 +22,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .layers import DilatedConv2d, HipLSTM, LipConv3d, PointwiseConv2d, PReLU, TrunkConv2d, bn_act, maxpool3d
+from .layers import (DilatedConv2d, HipLSTM, LipConv3d, PointwiseConv2d, PReLU, TrunkConv2d, bn_act, frames_nhwc,
+                     maxpool3d)
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
@@ -143,7 +144,7 @@ class VisualFeatNet(nn.Module):           # model.py:17-58
         x = maxpool3d(bn_act(conv(lips), bn, act), pool)
         Tn, C, H, W = x.shape[2], x.shape[1], x.shape[3], x.shape[4]
         if self.channels_last:            # (B, C, T, H, W) -> (B*T, H, W, C) in memory, viewed as NCHW
-            x = x.permute(0, 2, 3, 4, 1).reshape(Bn * Tn, H, W, C).permute(0, 3, 1, 2)
+            x = frames_nhwc(x)
         else:
             x = x.transpose(1, 2).reshape(Bn * Tn, C, H, W)
         x = self.trunk(x).view(Bn, Tn, -1)

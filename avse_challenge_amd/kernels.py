@@ -501,6 +501,17 @@ def maxpool_planes_fwd(x, k, s, p):
     return y, idx
 
 
+def transpose_cp(x):
+    """x (N, C, P) contiguous fp32 -> y (N, P, C) contiguous with y[n, p, c] = x[n, c, p] (csrc/transpose.hip)."""
+    _need_gpu(x)
+    if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 3:
+        raise ValueError("transpose_cp: (N, C, P) contiguous fp32 expected")
+    N, C, P = x.shape
+    y = torch.empty((N, P, C), device=x.device, dtype=torch.float32)
+    check(_lib.lib().avse_transpose_cp(N, C, P, ptr(x), ptr(y), stream_ptr(x.device)), "avse_transpose_cp")
+    return y
+
+
 def maxpool_planes_bwd(dy, idx, in_shape, k, s, p):
     _need_gpu(dy, idx)
     dy = dy.float().contiguous()

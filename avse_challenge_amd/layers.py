@@ -237,6 +237,33 @@ class _DilatedConvFn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+class _FramesNHWC(torch.autograd.Function):
+    """(B, C, T, H, W) contiguous -> (B*T, C, H, W) in channels-last memory (the frames of the lip front-end as the
+    batch of the channels-last ResNet trunk, baseline/avse1/model.py:46-50), and the gradient back, as one batched
+    64 x 64-tile transpose each way (csrc/transpose.hip) instead of torch's strided copies (~0.35 TB/s)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        B, C, T, H, W = x.shape
+        ctx.shape = x.shape
+        y = K.transpose_cp(x.contiguous().view(B, C, T * H * W))                  # (B, T*H*W, C)
+        return y.view(B * T, H, W, C).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, C, T, H, W = ctx.shape
+        d = dy.permute(0, 2, 3, 1).contiguous().view(B, T * H * W, C)           # a view for channels-last dy
+        return K.transpose_cp(d).view(B, C, T, H, W)
+
+
+def frames_nhwc(x):
+    """(B, C, T, H, W) -> (B*T, C, H, W) channels-last; HIP transpose for fp32 GPU tensors, torch elsewhere."""
+    B, C, T, H, W = x.shape
+    if x.is_cuda and x.dtype == torch.float32:
+        return _FramesNHWC.apply(x)
+    return x.permute(0, 2, 3, 4, 1).reshape(B * T, H, W, C).permute(0, 3, 1, 2)
+
+
 class _Conv1Fn(torch.autograd.Function):
     """AudioFeatNet.conv1 = Conv2d(1, 64, 5, padding=2) (model.py:199-215) as GEMMs over all B·T·F pixels, writing its
     output straight into channels-last memory.  MIOpen ran this single-input-channel conv in NCHW (for C = 1 the

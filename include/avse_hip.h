@@ -255,6 +255,13 @@ int avse_maxpool2d_fwd(int64_t planes, int64_t H, int64_t W, int64_t KH, int64_t
 int avse_maxpool2d_bwd(int64_t planes, int64_t H, int64_t W, int64_t KH, int64_t KW, int64_t SH, int64_t SW, int64_t PH,
                        int64_t PW, const float* dy, const uint8_t* idx, float* dx, avse_stream_t stream);
 
+/* ---------------------------------------------------------------- batched transpose ------------
+ * y[n][p][c] = x[n][c][p], fp32, x and y (N, C, P) / (N, P, C) contiguous, y must not alias x.  The avse1 lip front-end
+ * output (B, C, T, H, W) -> (B*T, H, W, C) for the channels-last ResNet trunk and its gradient back (the reference
+ * folds frames into the batch at baseline/avse1/model.py:46-50).  64 x 64 LDS tiles.
+ */
+int avse_transpose_cp(int64_t N, int64_t C, int64_t P, const float* x, float* y, avse_stream_t stream);
+
 /* ---------------------------------------------------------------- PReLU -> gLN (avse4) ----
  * y = gLN(PReLU(x)) of baseline/avse4/model.py:259-266,284-292 (PReLU with one slope; gLN
  * :225-252, EPS inside the sqrt).  x, y: (B, C, K) contiguous; gamma, beta: (C); stats: (B, 2)

@@ -904,6 +904,21 @@ def test_dilated_conv2d_module_grads_vs_torch():
     close(ours.bias.grad, ref.bias.grad, 2e-5 * sc(ref.bias.grad), 0, "db")
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 75, 24, 24), (3, 5, 7, 9, 11), (1, 70, 3, 5, 13)])
+def test_frames_nhwc_transpose(shape):
+    """layers.frames_nhwc on csrc/transpose.hip: (B, C, T, H, W) -> (B*T, C, H, W) channels-last equals torch's
+    permute exactly, and its backward is the exact inverse permutation (tiles not dividing C or T*H*W included)."""
+    from avse_challenge_amd.layers import frames_nhwc
+    B, C, T, H, W = shape
+    x = det_input(shape, 1870).to(DEV).requires_grad_(True)
+    y = frames_nhwc(x)
+    ref = x.detach().permute(0, 2, 3, 4, 1).reshape(B * T, H, W, C).permute(0, 3, 1, 2)
+    assert y.is_contiguous(memory_format=torch.channels_last) and torch.equal(y, ref)
+    gy = det_input((B * T, C, H, W), 1871).to(DEV).contiguous(memory_format=torch.channels_last)
+    (gx,) = torch.autograd.grad(y, x, gy)
+    assert torch.equal(gx, gy.view(B, T, C, H, W).permute(0, 2, 1, 3, 4))
+
+
 def test_conv1_module_nhwc_vs_torch():
     """AudioFeatNet.conv1 (DilatedConv2d(1, 64, 5, padding=2) with nhwc_out: layers._Conv1Fn on hipBLASLt) at an avse1
     spectrogram shape: channels-last output, and output / input / weight / bias gradients vs nn.Conv2d in fp64; with
