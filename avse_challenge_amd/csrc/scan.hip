@@ -302,8 +302,8 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
             }
         }
 #endif
-        RowRegs<Tin> rz;       // this chunk's z for the gate, issued before the barrier wait
-        if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t0, tn, L, rev);
+        RowRegs<Tin> rz;       // this chunk's z for the gate, issued before the barrier wait (issuing it with the
+        if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t0, tn, L, rev);   // prefetch measured the same, round 3)
         __syncthreads();
         // flush chunk k outputs (lane = time column, rows wave + 4i): buffer stores, row step in soffset
         {

@@ -7,7 +7,8 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/build/exp/$name
 mkdir -p "$out" "$root/expso"
 for f in "$root"/avse_challenge_amd/csrc/*.hip; do
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w -I"$root/include" $flags -c "$f" -o "$out/$(basename "$f" .hip).o" &
+    extra=""; [ "$(basename "$f")" = scan.hip ] && extra="-fno-slp-vectorize"    # as the Makefile builds it
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w -I"$root/include" $extra $flags -c "$f" -o "$out/$(basename "$f" .hip).o" &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/expso/$name.so" "$out"/*.o
