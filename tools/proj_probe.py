@@ -56,6 +56,19 @@ def main():
                 ms = ev_ms(fn)
                 res[f"{name}_{lib}"] = {"ms": round(ms, 4), "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4)}
         torch.backends.cuda.preferred_blas_library("cublaslt")
+        # flat: the (channel, batch, time) layout makes every projection ONE GEMM over N = b*l (no batch, no stride 0)
+        hf = h.reshape(b * l, dm)
+        xzf = torch.empty(2 * di, b * l, device="cuda", dtype=dt)
+        yf = torch.randn(di, b * l, device="cuda").to(dt)
+        of = torch.empty(b * l, dm, device="cuda", dtype=dt)
+        dxzf = torch.randn(2 * di, b * l, device="cuda").to(dt)
+        for name, fn, fl in (("in_proj_flat", lambda: torch.mm(w_in, hf.t(), out=xzf), fl_in),
+                             ("out_proj_flat", lambda: torch.mm(yf.t(), w_out_t, out=of), fl_out),
+                             ("in_proj_dW_flat", lambda: torch.mm(dxzf, hf), fl_in),
+                             ("in_proj_dh_flat", lambda: torch.mm(dxzf.t(), w_in), fl_in)):
+            ms = ev_ms(fn)
+            res[name] = {"ms": round(ms, 4), "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4)}
+        del hf, xzf, yf, of, dxzf
         print(json.dumps(res), flush=True)
         del h, y, xz, o, w_in_m, w_out_m
         torch.cuda.empty_cache()
