@@ -673,7 +673,7 @@ def roofline_hip(dev):
     for tag, b, l, dt in (("C3", 64, 3999, torch.float32), ("C5", 32, 5999, torch.bfloat16)):
         d, s = 1024, (2 if dt == torch.bfloat16 else 4)
         name = "fp32" if s == 4 else "bf16"
-        pmcf = "r03b_scan_pmc_c3_fp32.txt" if tag == "C3" else "r02c_scan_pmc_c5_bf16.txt"   # C5: round-2 PMC
+        pmcf = "r03b_scan_pmc_c3_fp32.txt" if tag == "C3" else "r03e_scan_pmc_c5_bf16.txt"
         ktype = "float" if s == 4 else "avse::bf16_t"
         u, z, dout = rnd(b, d, l, dtype=dt), rnd(b, d, l, dtype=dt), rnd(b, d, l, dtype=dt)
         delta = rnd(b, d, l, dtype=dt, scale=0.1)
