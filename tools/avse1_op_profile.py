@@ -7,6 +7,8 @@ import argparse
 import collections
 import os
 import sys
+import threading
+import time
 
 import torch
 
@@ -27,6 +29,9 @@ def main():
     p.add_argument("--top", type=int, default=40)
     p.add_argument("--kernels", default=None)
     a = p.parse_args()
+    # the profiler's post-processing (with stacks) can run for minutes without output: keep a heartbeat on stdout
+    threading.Thread(target=lambda: [print(f"alive {i * 30}s", flush=True) or time.sleep(30) for i in range(10 ** 6)],
+                     daemon=True).start()
     st = bench.Avse1Step(a.batch, torch.device("cuda"), 0, 1, 96)
     params = [q for q in st.model.parameters()]
 
