@@ -121,8 +121,11 @@ SIGNATURES = {
     "avse_lstm_padded_hidden": (c_i64, [c_i64]),
     "avse_lstm_group_size": (c_i64, [c_i64, c_i64]),
     "avse_lstm_group_workspace_bytes": (c_i64, [c_i64, c_i64]),
-    "avse_lstm_fwd_group": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
-    "avse_lstm_bwd_group": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_lstm_group_capacity": (c_i64, [c_i64, c_i32]),
+    "avse_lstm_fwd_group": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp]),
+    "avse_lstm_bwd_group": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp]),
     "avse_lstm_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "avse_lstm_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }

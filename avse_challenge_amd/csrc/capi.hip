@@ -13,6 +13,7 @@ const char* avse_strerror(int code) {
         case AVSE_EDTYPE: return "unsupported dtype";
         case AVSE_ELAUNCH: return "kernel launch failed";
         case AVSE_EALIGN: return "misaligned pointer or stride";
+        case AVSE_ENORESIDENT: return "grid cannot be co-resident on this device (use the single-workgroup kernels)";
         default: return "unknown error";
     }
 }

@@ -18,10 +18,13 @@
 //
 // Granule slots alternate by step parity, so a producer one step ahead never overwrites a slot a slower consumer of
 // the previous step still has to read.  Every slot is zeroed by the launch function (a memset node under graph
-// capture).  Residency: a sequence's G workgroups must run concurrently; they are consecutive block ids and the grid
-// is at most 256 workgroups of one per CU, and every spin is bounded: on timeout the workgroup writes a code into
-// the status word and every later wait of the launch gives up at once (the outputs are then garbage; the host reads
-// the status word, the workspace's first uint32: kernels.lstm_group_status).
+// capture).  Residency: a sequence's G workgroups must run concurrently.  They are consecutive block ids, and the
+// launch refuses (AVSE_ENORESIDENT, nothing enqueued) a grid larger than the workgroups of that kernel the device can
+// hold at once (occupancy x CUs), so with in-order dispatch every sequence's group eventually runs together even
+// when other work holds CUs.  Every spin is still bounded (a CU mask, or persistent kernels of another process that
+// never yield): on timeout the workgroup writes a code into the launch's status word (every later wait of the launch
+// then gives up at once) AND into the caller's sticky error flag, which the host checks (kernels.lstm_group_status /
+// raise_if_kernel_error; ddp.Trainer after every step), so a timed-out launch raises instead of training on garbage.
 #include <algorithm>
 
 #include "common.h"
@@ -46,7 +49,7 @@ __device__ inline unsigned long long granule(unsigned tag, float v) {
 // one wave: re-read the granules g[idx(lane, k)] (k < NK; idx < 0: none) until every tag == tag, then hand each value
 // to out(lane, k, v) in ascending k.  Returns false on timeout or once another workgroup has timed out (status set).
 template <int NK, typename Idx, typename Out>
-__device__ inline bool sweep(const gu64* g, unsigned tag, gu32* status, Idx idx, Out out) {
+__device__ inline bool sweep(const gu64* g, unsigned tag, gu32* status, gu32* errflag, Idx idx, Out out) {
     const int lane = threadIdx.x & 63;
     unsigned long long v[NK];
     for (unsigned spins = 0;; ++spins) {
@@ -63,8 +66,10 @@ __device__ inline bool sweep(const gu64* g, unsigned tag, gu32* status, Idx idx,
         if ((spins & 63) == 63) {
             const unsigned st = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (st != 0u || spins >= SPIN_MAX) {
-                if (st == 0u && lane == 0)
+                if (st == 0u && lane == 0) {
                     __hip_atomic_store(status, 0x71000000u + tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(errflag, 0x71000000u + tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 return false;
             }
         }
@@ -100,9 +105,11 @@ __device__ inline Geo geo(int H, int G, int g) {
 __global__ __launch_bounds__(512) void fwd_kernel(int T, int H, int G, int reverse, const float* __restrict__ gx,
                                                   const float* __restrict__ whh, float* __restrict__ hout,
                                                   int64_t hout_bs, int64_t hout_ts, float* __restrict__ c_all,
-                                                  float* __restrict__ gates, unsigned long long* hbuf_, unsigned* status_) {
+                                                  float* __restrict__ gates, unsigned long long* hbuf_, unsigned* status_,
+                                                  unsigned* errflag_) {
     gu64* hbuf = (gu64*)hbuf_;                        // global address space: agent-scope atomics
     gu32* status = (gu32*)status_;
+    gu32* errflag = (gu32*)errflag_;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int b = blockIdx.x / G, g = blockIdx.x % G, tid = threadIdx.x;
     const int B = gridDim.x / G;
@@ -172,7 +179,7 @@ __global__ __launch_bounds__(512) void fwd_kernel(int T, int H, int G, int rever
             gt[3 * H + j] = og;
         }
         if (tid < 64 && alive) {                          // wave 0 gathers h_t of all units (own ones included)
-            alive = sweep<MAXH / 64>(slot, (unsigned)s + 1u, status,
+            alive = sweep<MAXH / 64>(slot, (unsigned)s + 1u, status, errflag,
                                      [&](int l, int k) -> int64_t { return l + 64 * k < H ? l + 64 * k : -1; },
                                      [&](int l, int k, float v) { s_h[l + 64 * k] = v; });
         }
@@ -185,9 +192,11 @@ __global__ __launch_bounds__(512) void fwd_kernel(int T, int H, int G, int rever
 __global__ __launch_bounds__(768) void bwd_kernel(int T, int H, int G, int reverse, const float* __restrict__ dh_out,
                                                   int64_t dh_bs, int64_t dh_ts, const float* __restrict__ gates,
                                                   const float* __restrict__ c_all, const float* __restrict__ whh,
-                                                  float* __restrict__ dgp, unsigned long long* pbuf_, unsigned* status_) {
+                                                  float* __restrict__ dgp, unsigned long long* pbuf_, unsigned* status_,
+                                                  unsigned* errflag_) {
     gu64* pbuf = (gu64*)pbuf_;
     gu32* status = (gu32*)status_;
+    gu32* errflag = (gu32*)errflag_;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int b = blockIdx.x / G, g = blockIdx.x % G, tid = threadIdx.x;
     const int B = gridDim.x / G;
@@ -279,7 +288,7 @@ __global__ __launch_bounds__(768) void bwd_kernel(int T, int H, int G, int rever
         }
         if (tid < 64 && alive) {                          // wave 0, lane = own unit: dh = sum of the G partials
             float acc = 0.f;                               // in group order (deterministic)
-            alive = sweep<MAXG>(slot, (unsigned)s + 1u, status,
+            alive = sweep<MAXG>(slot, (unsigned)s + 1u, status, errflag,
                                 [&](int l, int k) -> int64_t {
                                     return (l < q.nu && k < G) ? (int64_t)k * H + q.u0 + l : -1;
                                 },
@@ -317,6 +326,37 @@ size_t bwd_lds(int64_t H, int G) {
     const int64_t U = (H + G - 1) / G, RS4 = (4 * U + 3) & ~3LL;
     return 4 * (size_t)(H * RS4 + RS4 + U);
 }
+int fwd_threads(int64_t H, int G) {
+    const int64_t U = (H + G - 1) / G;
+    return (int)std::max<int64_t>(64, (4 * U + 31) / 32 * 64);          // 32 gate rows per wave
+}
+int bwd_threads(int64_t H) { return (int)((H + 31) / 32 * 64); }        // 32 columns per wave
+
+// the kernels take up to 160 KiB of dynamic LDS (set once per process; thread-safe static init)
+bool lds_attr_set() {
+    static const bool ok =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&lstmg::fwd_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&lstmg::bwd_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    return ok;
+}
+
+// workgroups of the forward (backward) kernel the current device holds at once at hidden size H: occupancy per CU
+// x CUs; 0 when it cannot be determined
+int64_t capacity(int64_t H, bool backward) {
+    const int G = group_size(H);
+    if (G == 0 || !lds_attr_set()) return 0;
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    const hipError_t e = backward
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstmg::bwd_kernel, bwd_threads(H), bwd_lds(H, G))
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstmg::fwd_kernel, fwd_threads(H, G), fwd_lds(H, G));
+    if (e != hipSuccess) return 0;
+    return (int64_t)per_cu * cus;
+}
 
 }  // namespace
 
@@ -333,56 +373,43 @@ int64_t avse_lstm_group_workspace_bytes(int64_t B, int64_t H) {
     return 16 + 2 * B * G * H * 8;                    // status block + the backward's granules (>= the forward's)
 }
 
+int64_t avse_lstm_group_capacity(int64_t H, int32_t backward) { return capacity(H, backward != 0); }
+
 int avse_lstm_fwd_group(int64_t B, int64_t T, int64_t H, int32_t reverse, const float* gx, const float* whh,
                         float* hout, int64_t hout_bs, int64_t hout_ts, float* c_all, float* gates, void* workspace,
-                        avse_stream_t stream) {
-    if (!gx || !whh || !hout || !c_all || !gates || !workspace) return AVSE_EINVAL;
+                        uint32_t* error_flag, avse_stream_t stream) {
+    if (!gx || !whh || !hout || !c_all || !gates || !workspace || !error_flag) return AVSE_EINVAL;
     const int G = (int)avse_lstm_group_size(B, H);
     if (G == 0 || T <= 0 || T >= (1LL << 31)) return AVSE_ESHAPE;
+    if (B * G > capacity(H, false)) return AVSE_ENORESIDENT;
     hipStream_t st = (hipStream_t)stream;
     const int64_t used = 16 + 2 * B * H * 8;
     if (hipMemsetAsync(workspace, 0, (size_t)((used + 15) & ~15LL), st) != hipSuccess) return AVSE_ELAUNCH;
-    const size_t lds = fwd_lds(H, G);
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lstmg::fwd_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-            return AVSE_ELAUNCH;
-        attr = true;
-    }
-    const int64_t U = (H + G - 1) / G;
-    const int threads = (int)std::max<int64_t>(64, (4 * U + 31) / 32 * 64);        // 32 gate rows per wave
     auto* status = reinterpret_cast<unsigned*>(workspace);
     auto* hbuf = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + 16);
-    hipLaunchKernelGGL(lstmg::fwd_kernel, dim3((unsigned)(B * G)), dim3(threads), lds, st, (int)T, (int)H, G,
-                       (int)reverse, gx, whh, hout, hout_bs, hout_ts, c_all, gates, hbuf, status);
+    hipLaunchKernelGGL(lstmg::fwd_kernel, dim3((unsigned)(B * G)), dim3(fwd_threads(H, G)), fwd_lds(H, G), st, (int)T,
+                       (int)H, G, (int)reverse, gx, whh, hout, hout_bs, hout_ts, c_all, gates, hbuf, status,
+                       reinterpret_cast<unsigned*>(error_flag));
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
 
 int avse_lstm_bwd_group(int64_t B, int64_t T, int64_t H, int32_t reverse, const float* dh_out, int64_t dh_bs,
                         int64_t dh_ts, const float* gates, const float* c_all, const float* whh, float* dgates,
-                        void* workspace, avse_stream_t stream) {
-    if (!dh_out || !gates || !c_all || !whh || !dgates || !workspace) return AVSE_EINVAL;
+                        void* workspace, uint32_t* error_flag, avse_stream_t stream) {
+    if (!dh_out || !gates || !c_all || !whh || !dgates || !workspace || !error_flag) return AVSE_EINVAL;
     const int G = (int)avse_lstm_group_size(B, H);
     if (G == 0 || T <= 0 || T >= (1LL << 31)) return AVSE_ESHAPE;
+    if (bwd_threads(H) > 768) return AVSE_ESHAPE;
+    if (B * G > capacity(H, true)) return AVSE_ENORESIDENT;
     hipStream_t st = (hipStream_t)stream;
     const int64_t used = 16 + 2 * B * G * H * 8;
     if (hipMemsetAsync(workspace, 0, (size_t)((used + 15) & ~15LL), st) != hipSuccess) return AVSE_ELAUNCH;
-    const size_t lds = bwd_lds(H, G);
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lstmg::bwd_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-            return AVSE_ELAUNCH;
-        attr = true;
-    }
-    const int threads = (int)((H + 31) / 32 * 64);                      // 32 columns per wave
-    if (threads > 768) return AVSE_ESHAPE;
     auto* status = reinterpret_cast<unsigned*>(workspace);
     auto* pbuf = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + 16);
-    hipLaunchKernelGGL(lstmg::bwd_kernel, dim3((unsigned)(B * G)), dim3(threads), lds, st, (int)T, (int)H, G,
-                       (int)reverse, dh_out, dh_bs, dh_ts, gates, c_all, whh, dgates, pbuf, status);
+    hipLaunchKernelGGL(lstmg::bwd_kernel, dim3((unsigned)(B * G)), dim3(bwd_threads(H)), bwd_lds(H, G), st, (int)T,
+                       (int)H, G, (int)reverse, dh_out, dh_bs, dh_ts, gates, c_all, whh, dgates, pbuf, status,
+                       reinterpret_cast<unsigned*>(error_flag));
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

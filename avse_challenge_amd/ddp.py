@@ -22,6 +22,10 @@ buffer instead of DDP's reducer:
 With ``use_graph`` (single GPU) the forward/backward and the optimizer step are each replayed as a captured
 HIP graph; with world > 1 the forward/backward stays eager (the collectives are launched from autograd hooks)
 and only the optimizer step is captured.
+Kernel errors: the grouped LSTM recurrence (csrc/lstm_group.hip) writes a sticky device flag when its workgroups
+were not co-resident (its outputs are then invalid).  Every step enqueues a 4-byte copy of that flag into pinned
+memory and checks the previous copy once it has landed (no synchronisation); ``check_kernel_errors()`` is the
+blocking form.  Either raises ``kernels.HipKernelError``.
 """
 import functools
 
@@ -65,6 +69,30 @@ class Trainer:
         self.opt = torch.optim.Adam(self.params, lr=step.lr, capturable=self.use_graph, foreach=True)
         self.g_fb = self.g_opt = None
         self.loss = None
+        self._err_host = self._err_ev = None
+
+    # ------------------------------------------------------------------ kernel error flag
+    def _poll_kernel_errors(self):
+        """Lagged, non-blocking check of the device's sticky kernel-error flag (ddp module docstring)."""
+        if self.dev.type != "cuda":
+            return
+        from . import kernels
+        flag = kernels._ERROR_FLAGS.get(self.dev.index if self.dev.index is not None else torch.cuda.current_device())
+        if flag is None:
+            return
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._err_ev = torch.cuda.Event()
+        elif self._err_ev.query() and int(self._err_host[0]) != 0:
+            kernels.raise_if_kernel_error(self.dev)
+        self._err_host.copy_(flag, non_blocking=True)      # the flag is sticky: a later copy misses nothing
+        self._err_ev.record()
+
+    def check_kernel_errors(self):
+        """Blocking: raise kernels.HipKernelError if any kernel of the steps so far reported invalid outputs."""
+        if self.dev.type == "cuda":
+            from . import kernels
+            kernels.raise_if_kernel_error(self.dev)
 
     # ------------------------------------------------------------------ buckets
     def _make_buckets(self, ranges, bucket_mb):
@@ -193,6 +221,7 @@ class Trainer:
         if self.world > 1:
             self._finish_allreduce()
         self._opt()
+        self._poll_kernel_errors()
         return self.loss
 
     def capture(self):
@@ -239,6 +268,7 @@ class Trainer:
             self.loss = self._fwd_bwd()
             self._finish_allreduce()
         self.g_opt.replay()
+        self._poll_kernel_errors()
         return self.loss
 
 

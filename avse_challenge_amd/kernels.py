@@ -715,11 +715,11 @@ def lstm_fwd(gx, w_hh, hout=None, reverse=False):
     c_all = torch.empty((Bn, T, H), device=gx.device, dtype=torch.float32)
     gates = torch.empty((Bn, T, H4), device=gx.device, dtype=torch.float32)
     L = _lib.lib()
-    ws = _lstm_group_ws(L, Bn, H, gx.device)
+    ws = _lstm_group_ws(L, Bn, H, gx.device, backward=False)
     if ws is not None:      # W_hh resident in LDS, each sequence over G workgroups (csrc/lstm_group.hip)
         check(L.avse_lstm_fwd_group(Bn, T, H, int(bool(reverse)), ptr(gx), ptr(w_hh.float().contiguous()), ptr(hout),
                                     hout.stride(0), hout.stride(1), ptr(c_all), ptr(gates), ptr(ws),
-                                    stream_ptr(gx.device)), "avse_lstm_fwd_group")
+                                    ptr(_kernel_error_flag(gx.device)), stream_ptr(gx.device)), "avse_lstm_fwd_group")
         return hout, c_all, gates
     whhT = w_hh.float().t().contiguous()
     check(L.avse_lstm_fwd(Bn, T, H, int(bool(reverse)), ptr(gx), ptr(whhT), ptr(hout), hout.stride(0),
@@ -727,27 +727,66 @@ def lstm_fwd(gx, w_hh, hout=None, reverse=False):
     return hout, c_all, gates
 
 
-_LSTM_GROUP_WS = []     # the workspaces of the grouped launches (status word at offset 0), for lstm_group_status
+_GROUP_CAPACITY = {}     # (device index, H, backward) -> workgroups of that grouped kernel the device holds at once
+_ERROR_FLAGS = {}        # device index -> int32 sticky error flag of the grouped LSTM launches (never freed)
 
 
-def _lstm_group_ws(L, Bn, H, device):
-    """Workspace of the grouped LSTM kernels, or None when they do not apply (AVSE_LSTM_GROUP=0, or B * G > 256
-    workgroups, or H > 512): those shapes run lstm.hip's one-workgroup-per-sequence kernels."""
+def _lstm_group_ws(L, Bn, H, device, backward):
+    """Workspace of the grouped LSTM kernels, or None when they do not apply: AVSE_LSTM_GROUP=0; B * G > 256 or
+    H > 384 (avse_lstm_group_size); or B * G workgroups cannot be co-resident on this device
+    (avse_lstm_group_capacity).  Those cases run lstm.hip's one-workgroup-per-sequence kernels."""
     if os.environ.get("AVSE_LSTM_GROUP", "1") != "1":
         return None
-    nb = int(L.avse_lstm_group_workspace_bytes(Bn, H))
-    if nb <= 0:
+    G = int(L.avse_lstm_group_size(Bn, H))
+    if G == 0:
         return None
-    ws = torch.empty((nb + 15) // 16 * 4, device=device, dtype=torch.int32)
-    _LSTM_GROUP_WS.append(ws)
-    del _LSTM_GROUP_WS[:-8]
-    return ws
+    key = (device.index, H, bool(backward))
+    if key not in _GROUP_CAPACITY:
+        with torch.cuda.device(device):
+            _GROUP_CAPACITY[key] = int(L.avse_lstm_group_capacity(H, int(bool(backward))))
+    cap = _GROUP_CAPACITY[key]
+    if os.environ.get("AVSE_LSTM_GROUP_CAPACITY"):      # test hook: pretend the device holds fewer workgroups
+        cap = min(cap, int(os.environ["AVSE_LSTM_GROUP_CAPACITY"]))
+    if Bn * G > cap:
+        return None
+    nb = int(L.avse_lstm_group_workspace_bytes(Bn, H))
+    return torch.empty((nb + 15) // 16 * 4, device=device, dtype=torch.int32)
 
 
-def lstm_group_status():
-    """0 when every recent grouped LSTM launch completed its hand-offs; else the timeout code one of them wrote
-    (0x71000000 + step): a sequence's workgroups were not co-resident (synchronises the device)."""
-    return max([int(w[0].item()) & 0xFFFFFFFF for w in _LSTM_GROUP_WS] + [0])
+def _kernel_error_flag(device):
+    """The device's sticky error flag (int32, 0 = no error) that the grouped LSTM kernels write a timeout code into.
+    Allocated once per device outside any graph pool and never freed, so captured launches keep a valid pointer."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _ERROR_FLAGS:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("the grouped LSTM error flag must be created before graph capture (run the step "
+                               "eagerly first)")
+        _ERROR_FLAGS[idx] = torch.zeros(1, device=torch.device("cuda", idx), dtype=torch.int32)
+    return _ERROR_FLAGS[idx]
+
+
+class HipKernelError(RuntimeError):
+    """A hand-written kernel reported invalid outputs through its sticky error flag."""
+
+
+def lstm_group_status(device=None):
+    """0 when every grouped LSTM launch on `device` (default: all used devices) since the last reset completed its
+    hand-offs; else the timeout code one of them wrote (0x71000000 + step): a sequence's workgroups were not
+    co-resident and that launch's outputs are invalid.  Synchronises with the flag's device."""
+    flags = _ERROR_FLAGS.values() if device is None else         [f for i, f in _ERROR_FLAGS.items() if i == torch.device(device).index]
+    return max([int(f.item()) & 0xFFFFFFFF for f in flags] + [0])
+
+
+def raise_if_kernel_error(device=None, reset=True):
+    """Raise HipKernelError when a grouped LSTM launch timed out (see lstm_group_status); with ``reset`` clear the
+    flag afterwards (a raised error is reported once)."""
+    code = lstm_group_status(device)
+    if code and reset:
+        for f in _ERROR_FLAGS.values():
+            f.zero_()
+    if code:
+        raise HipKernelError(f"grouped LSTM recurrence timed out waiting for its workgroups (code {code:#x}): the "
+                             "grid was not co-resident on the GPU; the step's outputs and gradients are invalid")
 
 
 def lstm_bwd(dh, gates, c_all, w_hh, reverse=False):
@@ -760,11 +799,12 @@ def lstm_bwd(dh, gates, c_all, w_hh, reverse=False):
     Bn, T, H = dh.shape
     L = _lib.lib()
     dg = torch.empty((Bn, T, 4 * H), device=dh.device, dtype=torch.float32)
-    ws = _lstm_group_ws(L, Bn, H, dh.device)
+    ws = _lstm_group_ws(L, Bn, H, dh.device, backward=True)
     if ws is not None:
         check(L.avse_lstm_bwd_group(Bn, T, H, int(bool(reverse)), ptr(dh), dh.stride(0), dh.stride(1),
                                     ptr(gates.contiguous()), ptr(c_all.contiguous()), ptr(w_hh.float().contiguous()),
-                                    ptr(dg), ptr(ws), stream_ptr(dh.device)), "avse_lstm_bwd_group")
+                                    ptr(dg), ptr(ws), ptr(_kernel_error_flag(dh.device)), stream_ptr(dh.device)),
+              "avse_lstm_bwd_group")
         return dg
     Hp = int(L.avse_lstm_padded_hidden(H))
     w_pad = torch.nn.functional.pad(w_hh.float(), (0, Hp - H)).contiguous()

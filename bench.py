@@ -846,6 +846,7 @@ def main():
         dt = float(t)
     if not torch.isfinite(loss.detach()).all():
         raise RuntimeError("non-finite loss in the timed region")
+    step.check_kernel_errors()          # a grouped-LSTM launch that was not co-resident raises here (ddp.py)
 
     cuda = dev.type == "cuda"
     roof = None if args.no_roofline or rank != 0 or not cuda else work.roofline(dev)

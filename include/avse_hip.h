@@ -25,7 +25,8 @@ extern "C" {
 
 typedef void* avse_stream_t; /* a hipStream_t */
 
-enum { AVSE_OK = 0, AVSE_EINVAL = -1, AVSE_ESHAPE = -2, AVSE_EDTYPE = -3, AVSE_ELAUNCH = -4, AVSE_EALIGN = -5 };
+enum { AVSE_OK = 0, AVSE_EINVAL = -1, AVSE_ESHAPE = -2, AVSE_EDTYPE = -3, AVSE_ELAUNCH = -4, AVSE_EALIGN = -5,
+       AVSE_ENORESIDENT = -6 };
 enum { AVSE_F32 = 0, AVSE_BF16 = 1, AVSE_U8 = 2 };
 
 const char* avse_strerror(int code);
@@ -315,18 +316,22 @@ int avse_lstm_bwd(int64_t B, int64_t T, int64_t H, int32_t reverse, const float*
                   const float* gates, const float* c_all, const float* whh_pad, float* dgates, avse_stream_t stream);
 /* The same recurrences with each sequence spread over G = avse_lstm_group_size(B, H) workgroups (0: not available
  * for this shape: B * G > 256 or H > 384), W_hh resident in their LDS, h / dh exchanged through data-tagged
- * granules in `workspace` (avse_lstm_group_workspace_bytes; zeroed by the call; its first uint32 is a status word,
- * 0 = every hand-off completed, else 0x71000000 + step of a timed-out wait: the sequence's workgroups were not
- * co-resident and the outputs are invalid).  whh = W_hh (4H, H) contiguous for both directions; other arguments and
- * outputs as avse_lstm_fwd / avse_lstm_bwd. */
+ * granules in `workspace` (avse_lstm_group_workspace_bytes; zeroed by the call).  A sequence's G workgroups must be
+ * co-resident: the call returns AVSE_ENORESIDENT without enqueueing anything when B * G exceeds
+ * avse_lstm_group_capacity(H, backward) (that kernel's workgroups the current device holds at once; the caller then
+ * runs avse_lstm_fwd / avse_lstm_bwd).  Every inter-workgroup wait is bounded: a wait that times out (e.g. CUs held
+ * by another process's persistent kernels) writes 0x71000000 + step into *error_flag (device memory, never cleared
+ * by the call; the outputs of that launch are invalid) — the caller checks it after the step and raises.
+ * whh = W_hh (4H, H) contiguous for both directions; other arguments and outputs as avse_lstm_fwd / avse_lstm_bwd. */
 int64_t avse_lstm_group_size(int64_t B, int64_t H);
 int64_t avse_lstm_group_workspace_bytes(int64_t B, int64_t H);
+int64_t avse_lstm_group_capacity(int64_t H, int32_t backward);
 int avse_lstm_fwd_group(int64_t B, int64_t T, int64_t H, int32_t reverse, const float* gx, const float* whh,
                         float* hout, int64_t hout_bs, int64_t hout_ts, float* c_all, float* gates, void* workspace,
-                        avse_stream_t stream);
+                        uint32_t* error_flag, avse_stream_t stream);
 int avse_lstm_bwd_group(int64_t B, int64_t T, int64_t H, int32_t reverse, const float* dh_out, int64_t dh_bs,
                         int64_t dh_ts, const float* gates, const float* c_all, const float* whh, float* dgates,
-                        void* workspace, avse_stream_t stream);
+                        void* workspace, uint32_t* error_flag, avse_stream_t stream);
 
 #ifdef __cplusplus
 }

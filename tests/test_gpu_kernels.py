@@ -4,6 +4,8 @@ Tolerances (fp32 path): the reference arithmetic is fp32; our kernels use fp32 w
 summation order and exp2-based exponentials, so element-wise agreement is ~1e-6 relative.
 Stated per test; BASELINE north_star bar for waveforms is RMS <= 1e-4.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -746,7 +748,7 @@ def test_lstm_vs_torch_fp64(B, T, I, H, bidir, group, monkeypatch):
     rp = dict(ref.named_parameters())
     for k, p in ours.named_parameters():
         close(p.grad, rp[k].grad, 5e-5 * sc(rp[k].grad), 0, k)
-    assert K().lstm_group_status() == 0
+    K().raise_if_kernel_error()
 
 
 def test_lstm_group_kernels_at_the_avse1_shape(monkeypatch):
@@ -765,7 +767,7 @@ def test_lstm_group_kernels_at_the_avse1_shape(monkeypatch):
     for rev in (False, True):
         hr, cr, gr = K().lstm_fwd(gx, w, reverse=rev)
         dr = K().lstm_bwd(dh, gr, cr, w, reverse=rev)
-        assert K().lstm_group_status() == 0
+        K().raise_if_kernel_error()
         monkeypatch.setenv("AVSE_LSTM_GROUP", "0")
         h0, c0, g0 = K().lstm_fwd(gx, w, reverse=rev)
         d0 = K().lstm_bwd(dh, g0, c0, w, reverse=rev)
@@ -774,6 +776,66 @@ def test_lstm_group_kernels_at_the_avse1_shape(monkeypatch):
             close(a_, b_, 1e-5 * float(b_.abs().max()), 0, f"{n_} reverse={rev}")
         close(dr, d0, 1e-5 * float(d0.abs().max()), 0, f"dgates reverse={rev}")
     assert torch.equal(K().lstm_fwd(gx, w)[0], h1) and torch.equal(K().lstm_bwd(dh, g1, c1, w), d1)   # deterministic
+
+
+def test_lstm_group_residency_guard(monkeypatch):
+    """The grouped kernels run only when a launch's B * G workgroups fit the device at once: the capacity query
+    (occupancy x CUs) covers the avse1 grid (32 x 8 = 256, one 136 KB-LDS workgroup per CU); a device that holds fewer
+    (AVSE_LSTM_GROUP_CAPACITY stands in for it) takes lstm.hip's kernels instead, with their exact results."""
+    L = K()._lib.lib()
+    B, T, H = 32, 24, 257
+    assert L.avse_lstm_group_capacity(H, 0) >= 256 and L.avse_lstm_group_capacity(H, 1) >= 256
+    gx = det_input((B, T, 4 * H), 1630).to(DEV)
+    w = (0.06 * det_input((4 * H, H), 1631)).to(DEV)
+    dh = det_input((B, T, H), 1632).to(DEV)
+    monkeypatch.setenv("AVSE_LSTM_GROUP", "0")
+    h0, c0, g0 = K().lstm_fwd(gx, w)
+    d0 = K().lstm_bwd(dh, g0, c0, w)
+    monkeypatch.setenv("AVSE_LSTM_GROUP", "1")
+    monkeypatch.setenv("AVSE_LSTM_GROUP_CAPACITY", "255")
+    h1, c1, g1 = K().lstm_fwd(gx, w)
+    d1 = K().lstm_bwd(dh, g1, c1, w)
+    assert torch.equal(h1, h0) and torch.equal(c1, c0) and torch.equal(d1, d0)      # the single-workgroup kernels
+    monkeypatch.delenv("AVSE_LSTM_GROUP_CAPACITY")
+    h2, _, _ = K().lstm_fwd(gx, w)
+    assert not torch.equal(h2, h0)          # the grouped kernels again (different summation order)
+    close(h2, h0, 1e-5 * float(h0.abs().max()), 0, "h")
+    K().raise_if_kernel_error()
+
+
+_TIMEOUT_CHILD = r"""
+import json, sys, time, torch
+sys.path.insert(0, sys.argv[1])
+from avse_challenge_amd import kernels as K
+B, T, H = 32, 4, 257
+gx = torch.randn(B, T, 4 * H, device="cuda")
+w = 0.06 * torch.randn(4 * H, H, device="cuda")
+t = time.time()
+K.lstm_fwd(gx, w)
+torch.cuda.synchronize()
+try:
+    K.raise_if_kernel_error()
+    raised = ""
+except K.HipKernelError as e:
+    raised = str(e)
+print(json.dumps({"raised": raised, "s": time.time() - t}))
+"""
+
+
+def test_lstm_group_not_coresident_raises():
+    """A grouped LSTM launch whose workgroups cannot all be resident (the process restricted to 4 CUs with
+    HSA_CU_MASK, so only 4 of a sequence's 8 workgroups ever run at once) times out its hand-offs and the host
+    raises HipKernelError — the step never returns those outputs as if they were valid."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_CU_MASK="0:0-3")
+    r = subprocess.run([sys.executable, "-c", _TIMEOUT_CHILD, root], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "timed out" in out["raised"], out
 
 
 # ------------------------------------------------------------------ fused dwconv <-> PReLU -> gLN (avse4 TCN)
