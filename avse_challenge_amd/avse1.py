@@ -180,7 +180,8 @@ class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 conv
             x = x.contiguous(memory_format=torch.channels_last)
         for i in range(1, self.num_conv + 1):
             conv, bn = getattr(self, f"conv{i}"), getattr(self, f"bn{i}")
-            if bn.training and bn.track_running_stats and conv.bias is not None and conv.hip_ok(x):
+            if bn.training and bn.track_running_stats and bn.momentum is not None and conv.bias is not None \
+                    and conv.hip_ok(x):
                 # the conv bias goes into the BatchNorm (no separate bias-add pass): DilatedConv2d docstring
                 x = bn_act(conv(x, bias_to_bn=True), bn, "relu", folded_bias=conv.bias)
             else:

@@ -96,13 +96,7 @@ __global__ void stats_finalize(int B, int C, int K, const float* __restrict__ x,
 // still in the Infinity Cache / L2 when it starts ((y1, dy) of C4 is 262 MB against the 256 MB memory-side cache):
 // C4 dwconv_gln_bwd 0.193 -> 0.186 ms.  The forward's apply pass keeps the launch order (reversed it measured
 // 0.0965 -> 0.101 ms).
-__device__ inline int second_pass_row() {
-#ifdef AVSE_EXP_NOREV
-    return blockIdx.x;
-#else
-    return gridDim.x - 1 - blockIdx.x;
-#endif
-}
+__device__ inline int second_pass_row() { return gridDim.x - 1 - blockIdx.x; }
 
 __global__ __launch_bounds__(THREADS) void apply_kernel(int C, int K, const float* __restrict__ x,
                                                         const float* __restrict__ alpha, const float* __restrict__ gamma,
@@ -692,12 +686,9 @@ int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
                                   x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, ws_a)
 #define L4_(PP) hipLaunchKernelGGL(dwconv_gln_bwd4_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, (int)dil, \
                                    x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, ws_a)
-#ifndef AVSE_EXP_DWB_SCALAR
     if (dil % 4 == 0) {
         AVSE_DW_P_SWITCH(P, L4_)
-    } else
-#endif
-    {
+    } else {
         AVSE_DW_P_SWITCH(P, L_)
     }
 #undef L_

@@ -242,11 +242,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
         rbc.store(s_bc, tn);
         __syncthreads();
         // prefetch chunk k + 1 while chunk k computes
-#ifdef AVSE_EXP_NOLOAD
-        if (false) {
-#else
         if (k + 1 < nck) {
-#endif
             const int t1 = t0 + TC, tn1 = min(TC, L - t1);
             ru.load(u, a.u_bs, a.u_ds, b, d0, D, t1, tn1, L, rev);
             rd.load(dl, a.delta_bs, a.delta_ds, b, d0, D, t1, tn1, L, rev);
@@ -286,7 +282,6 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
         // always the full 64 steps: the staged tail of the last chunk is zero (dt = 0, u = 0, B = C = 0), which
         // leaves h unchanged, so no step needs a bounds test; the state is checkpointed every 16 steps
         // (x slot j = state after logical step 16 j + 15, clamped to the last step)
-#ifndef AVSE_EXP_NOCOMPUTE
 #pragma unroll 1
         for (int q32 = 0; q32 < TC / 32; ++q32) {
             steps(q32 * 32, std::integral_constant<int, U>());
@@ -301,7 +296,6 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                 xp[1] = make_float4(ha1.x, h2[1].x, ha1.y, h2[1].y);
             }
         }
-#endif
         RowRegs<Tin> rz;       // this chunk's z for the gate, issued before the barrier wait (issuing it with the
         if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t0, tn, L, rev);   // prefetch measured the same, round 3)
         __syncthreads();
@@ -382,11 +376,7 @@ constexpr int RED = 8;   // adjoint steps buffered per cross-wave dB/dC flush
 // on top of the 64 of the state history and spills); the other wave of the SIMD covers the LDS latency
 // (session-3 A/B, tools/gpu_round2z2.sh: masks letting VALU / SALU / transcendentals cross the fence moved the
 // C3 and C5 backward by -0.7 .. +1.8 %: the kernel is VALU-throughput bound, not latency bound)
-#ifndef AVSE_NO_SCHED_FENCE
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define SCHED_FENCE() do {} while (0)
-#endif
 
 template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS, bool FOLD>
 __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, int nblk_d) {
@@ -620,9 +610,6 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     ddt_q[i & 3] = ddt2.x + ddt2.y;
                 }
                 SCHED_FENCE();
-#ifdef AVSE_EXP_BWD_NORED
-                if (part[0] == 12345.f) a.dB[0] = part[1] + part[2] + part[3] + part[4] + part[5] + part[6] + part[7];
-#else
                 float r2[2];
                 rs8_swap(part, r2);
                 {
@@ -631,12 +618,8 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     // no exec-mask branch, and the reduction stays in the step's basic block for the scheduler
                     const int slot = ((id.lane >> 5) & 1) * NSTATE + id.g * NS + ((id.lane >> 4) & 1) * 2;
                     float* dst = &s_red[(id.wave * RED + (i & (RED - 1))) * 2 * NSTATE + slot];
-#ifdef AVSE_EXP_CONDRED
-                    if ((id.lane & 12) == 0)
-#endif
                     *reinterpret_cast<float2*>(dst) = make_float2(r2[0], r2[1]);
                 }
-#endif
                 if ((i & 3) == 0) {
                     // per-channel epilogue of steps i .. i+3, one step per lane of the quad (not 4 copies of each):
                     // lane g reduce-scatters the quad's partials to the sums of step i + g and finishes that step's
@@ -654,7 +637,6 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     dbias_acc += ddr;
                     *reinterpret_cast<float2*>(ud_p) = make_float2(du, ddr);
                 }
-#if !defined(AVSE_EXP_BWD_NORED) && !defined(AVSE_EXP_BWD_NOFLUSH)
                 if ((i & (RED - 1)) == 0) {
                     // cross-wave sum of steps ts+i .. ts+i+RED-1 -> partial slab
                     __syncthreads();
@@ -669,7 +651,6 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     }
                     __syncthreads();
                 }
-#endif
             }
         }
         __syncthreads();

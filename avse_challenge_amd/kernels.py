@@ -12,6 +12,25 @@ from ._lib import AVSE_BF16, AVSE_F32, ScanBwdArgs, ScanFwdArgs, check, ptr, str
 
 NSTATE = 16
 
+# Launch timing taps (bench.py's in-step roofline): while ``LAUNCH_TAPS`` maps a C entry point's name to a list, each
+# eager launch of that entry point appends a (start, end) pair of HIP timing events recorded on its launch stream.
+LAUNCH_TAPS = {}
+
+
+def _tap_begin(name, device):
+    taps = LAUNCH_TAPS.get(name)
+    if taps is None or torch.cuda.is_current_stream_capturing():
+        return None
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(torch.cuda.current_stream(device))
+    taps.append((e0, e1))
+    return e1, device
+
+
+def _tap_end(tap):
+    if tap is not None:
+        tap[0].record(torch.cuda.current_stream(tap[1]))
+
 
 def _need_gpu(*ts):
     for t in ts:
@@ -343,6 +362,7 @@ def conv3d_fwd_supported(x, w, stride, padding):
     return (tuple(stride) == (1, 2, 2) and tuple(padding) == (2, 3, 3) and tuple(w.shape[0:1]) == (64,)
             and tuple(w.shape[2:]) == (5, 7, 7) and x.dim() == 5 and x.shape[1] == w.shape[1]
             and x.dtype in (torch.uint8, torch.float32)
+            and x.numel() * x.element_size() < (1 << 31)          # the kernel's 32-bit buffer offsets
             and _lib.lib().avse_conv3d_fwd_workspace_bytes(x.shape[1], x.shape[3], x.shape[4]) > 0)
 
 
@@ -389,8 +409,10 @@ def dconv_wgrad(x, dy, dilation, bias_grad=False):
     ws = torch.empty((L.avse_dconv_wgrad_workspace_bytes(Bn, H, W, dilation) + 3) // 4, device=x.device,
                      dtype=torch.float32)
     db = torch.empty(64, device=x.device, dtype=torch.float32) if bias_grad else None
+    tap = _tap_begin("avse_dconv_wgrad", x.device)
     check(L.avse_dconv_wgrad(Bn, H, W, dilation, ptr(x), ptr(dy), ptr(out), ptr(db) if bias_grad else None, ptr(ws),
                              stream_ptr(x.device)), "avse_dconv_wgrad")
+    _tap_end(tap)
     return (out, db) if bias_grad else out
 
 

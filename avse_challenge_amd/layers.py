@@ -81,8 +81,9 @@ def bn_act(x, bn, act=None, res=None, folded_bias=None):
     act(bn(x + bias)) — equal to act(bn(x)), the batch statistics shift with the bias — and the running mean takes
     the bias in (momentum * bias)."""
     if folded_bias is not None:
-        if not (bn.training and bn.track_running_stats) or res is not None:
-            raise RuntimeError("bn_act: folded_bias needs a training-mode BatchNorm with running stats, no residual")
+        if not (bn.training and bn.track_running_stats) or res is not None or bn.momentum is None:
+            raise RuntimeError("bn_act: folded_bias needs a training-mode BatchNorm with running stats and a momentum "
+                               "(not the cumulative average), no residual")
         y = bn_act(x, bn, act)
         # through .data, as the kernel's own running-stat update: no version bump (under DDP the BatchNorm buffers are
         # views of one flat tensor, and a bump would invalidate every library BatchNorm's saved running stats)
@@ -339,9 +340,12 @@ class DilatedConv2d(nn.Conv2d):
     def hip_ok(self, x):
         if self.conv1_ok(x):
             return True
+        # x.numel() < 2^29: the kernel's 32-bit buffer offsets (csrc/dconv_wgrad.hip; B >= ~87 at 3 s clips exceeds
+        # it, and those shapes take the library path instead of failing in the backward)
         return (os.environ.get("AVSE_DCONV_WGRAD", "1") == "1" and x.is_cuda and self.in_channels == 64
                 and self.out_channels == 64 and self.dilation[0] <= K.DCONV_WGRAD_MAX_DIL
-                and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last))
+                and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+                and x.numel() < (1 << 29))
 
     def forward(self, x, bias_to_bn=False):
         if self.conv1_ok(x):

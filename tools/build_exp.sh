@@ -1,14 +1,22 @@
 #!/bin/bash
-# Build experiment variants of libavse_hip.so into build/exp/<name>.so with extra -D flags.
-# usage: tools/build_exp.sh NAME "-DFLAG1 -DFLAG2"
+# Build an experiment variant of libavse_hip.so into expso/<name>.so from a PATCHED COPY of the kernel sources:
+# the product sources carry no experiment switches.  PATCH is a unified diff (git diff format, paths relative to the
+# repo root) applied to the copy, e.g. one that compiles out the scan backward's dB/dC reduction for an A/B timing.
+# usage: tools/build_exp.sh NAME [PATCH] ["-DFLAG ..."]
 set -e
-name=$1; flags=$2
+name=$1; patch=${2:-}; flags=${3:-}
 root=$(cd "$(dirname "$0")/.." && pwd)
+src=$root/build/exp/$name/src
 out=$root/build/exp/$name
-mkdir -p "$out" "$root/expso"
-for f in "$root"/avse_challenge_amd/csrc/*.hip; do
+rm -rf "$src"; mkdir -p "$src" "$root/expso"
+cp -r "$root/avse_challenge_amd/csrc" "$root/include" "$src/"
+if [ -n "$patch" ]; then
+    (cd "$src" && sed -e 's#avse_challenge_amd/csrc/#csrc/#g' "$root/$patch" | patch -p1)
+fi
+for f in "$src"/csrc/*.hip; do
     extra=""; [ "$(basename "$f")" = scan.hip ] && extra="-fno-slp-vectorize"    # as the Makefile builds it
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w -I"$root/include" $extra $flags -c "$f" -o "$out/$(basename "$f" .hip).o" &
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w -I"$src/include" $extra $flags -c "$f" \
+        -o "$out/$(basename "$f" .hip).o" &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/expso/$name.so" "$out"/*.o
