@@ -213,6 +213,28 @@ def _branch_stream(device):
     return _STREAMS[device]
 
 
+class _JoinFromSide(torch.autograd.Function):
+    """Identity at the point where the lip branch (side stream) joins the main stream (model.py:124-126's concat).
+    Backward (on the main stream, where the join ran): the gradient it hands to the lip branch's backward was
+    allocated on the main stream; the side stream reads it, so it is recorded on the side stream (the caching
+    allocator then keeps its block until the side stream's reads have completed) and the side stream is ordered
+    after the main stream's production of it."""
+
+    @staticmethod
+    def forward(ctx, x, side):
+        ctx.side = side
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        side = ctx.side
+        main = torch.cuda.current_stream(g.device)
+        if side is not None and side != main:
+            side.wait_stream(main)
+            g.record_stream(side)
+        return g, None
+
+
 class AVNet(nn.Module):
     """LightningModule surface of baseline/avse1/model.py:AVNet (forward / training_step / cal_loss)."""
 
@@ -248,6 +270,8 @@ class AVNet(nn.Module):
         if side is not None:
             main.wait_stream(side)
             vis.record_stream(main)
+            if os.environ.get("AVSE_AVSE1_JOIN_HOLD", "1") == "1":
+                vis = _JoinFromSide.apply(vis, side)
         if self.a_only:
             comb = audio
         else:

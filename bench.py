@@ -66,7 +66,39 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of captured HIP graphs")
+    p.add_argument("--secondary", default="mamba,avse4,avmamba",
+                   help="with the default avse1 workload at one rank: also time these BASELINE configs (C3 Mamba-TasNet-L "
+                        "B=64, C4 avse4 B=16, C5 AV Mamba-TasNet-L bf16 B=32), each as a child bench run after the "
+                        "headline's measurement, reported under 'secondary' in the same JSON line ('' = none)")
+    p.add_argument("--secondary-steps", type=int, default=4)
     return p.parse_args()
+
+
+def run_secondary(args):
+    """The other BASELINE configs, each in a child process (fresh device memory; a failure is reported, not raised)
+    started after this process's measurement is complete; returns one record per config."""
+    out = []
+    for wl in [w for w in args.secondary.split(",") if w]:
+        cmd = [sys.executable, os.path.abspath(__file__), "--workload", wl, "--steps", str(args.secondary_steps),
+               "--warmup", "1", "--secondary", "", "--no-cpu-baseline", "--no-roofline-hip"]
+        t = time.perf_counter()
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode != 0 or not lines:
+                out.append({"workload": wl, "error": f"rc {r.returncode}: {r.stderr[-400:]}"})
+                continue
+            rec = json.loads(lines[-1])
+            keep = {k: rec.get(k) for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype")}
+            keep["config"] = {k: rec["config"].get(k) for k in ("workload", "global_batch", "hip_graph", "max_mem_gb")
+                              if k in rec["config"]}
+            keep["roofline"] = rec.get("roofline")
+            keep["wall_s"] = round(time.perf_counter() - t, 1)
+            out.append({"workload": wl, **keep})
+        except Exception as e:      # noqa: BLE001 - the headline line must still print
+            out.append({"workload": wl, "error": f"{type(e).__name__}: {e}"})
+        print(f"[bench] secondary {wl}: {out[-1].get('value', out[-1].get('error'))}", file=sys.stderr, flush=True)
+    return out
 
 
 def _free_port():
@@ -876,6 +908,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = work.cpu_baseline()
+    secondary = None
+    if rank == 0 and world == 1 and cuda and args.workload == "avse1" and args.secondary:
+        secondary = run_secondary(args)
     if rank == 0:
         value = world * B * args.steps / dt
         cfg = {**work.config(world), "hip_graph": graph}
@@ -897,6 +932,8 @@ def main():
                "data": "synthetic (speech-like noise with 4 Hz envelope at SNR {0,3,6,9} dB, uint8 lips; "
                        "random-init weights)",
                "config": cfg, "roofline": roof, "roofline_hip": hbm_list, "projections": proj, "cpu_baseline": cpu}
+        if secondary is not None:
+            rec["secondary"] = secondary
         if not cuda:
             rec["device"] = "cpu (gloo ranks; n_gpus counts ranks)"
         print(json.dumps(rec), flush=True)

@@ -5,7 +5,8 @@ first serial run, the bitwise / relative differences of the lip-branch forward a
 layers, TCN output = vis), of the gradients arriving at those points, and of each parameter group's gradient.
 
   serial        AVSE_AVSE1_STREAMS=0
-  stream        lip branch on the side stream (product default)
+  stream        lip branch on the side stream (product default: the join hands its gradient over with record_stream)
+  stream_nohold as stream, without avse1._JoinFromSide (round 3's join)
   stream_sync   as stream, with torch.cuda.synchronize() after the lip forward and around the backward
   det           serial / stream with torch.backends.cudnn.deterministic = True
 
@@ -25,6 +26,7 @@ DEV = torch.device("cuda:0")
 
 def run(mode):
     os.environ["AVSE_AVSE1_STREAMS"] = "0" if mode.startswith("serial") else "1"
+    os.environ["AVSE_AVSE1_JOIN_HOLD"] = "0" if "nohold" in mode else "1"
     torch.backends.cudnn.deterministic = mode.endswith("_det")
     torch.manual_seed(5)
     st = bench.Avse1Step(2, DEV, 0, 1, 96)
@@ -87,7 +89,8 @@ def group(k):
 
 
 def main():
-    modes = sys.argv[1:] or ["serial", "serial", "stream", "stream", "stream_sync", "serial"]
+    modes = sys.argv[1:] or ["serial", "serial", "stream_nohold", "stream_nohold", "stream", "stream", "stream_sync",
+                             "serial"]
     base = None
     for i, mode in enumerate(modes):
         r = run(mode)
