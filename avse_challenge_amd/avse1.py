@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import kernels as K
 from .layers import (DilatedConv2d, HipLSTM, LipConv3d, PointwiseConv2d, PReLU, TrunkConv2d, bn_act, frames_nhwc,
-                     maxpool3d)
+                     maxpool3d, time_conv1d, time_major_4d)
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
@@ -80,6 +80,12 @@ class _Chomp(nn.Module):
 
 
 class _TemporalBlock(nn.Module):          # utils/tcn.py:144-243 (dwpw=False, symm_chomp=True)
+    """net = conv1 -> batchnorm1 -> chomp1 -> relu1 (PReLU) -> dropout1 -> conv2 -> ... -> dropout2; out = relu(net(x) + x)
+    (same modules and state_dict keys).  Runs TIME-MAJOR (B, T, C): each Conv1d as one GEMM over im2col rows
+    (layers._TimeConv1dFn, bit-reproducible), BatchNorm1d -> PReLU as ONE bnact pass over the conv's whole (T + pad)
+    output (BatchNorm statistics over the unchomped output, as the reference; the PReLU is elementwise, so applying it
+    before the symmetric chomp is the same), the chomp a slice, the final add + PReLU on the NHWC kernels."""
+
     def __init__(self, c, k, dil, p_drop):
         super().__init__()
         pad = (k - 1) * dil
@@ -97,9 +103,20 @@ class _TemporalBlock(nn.Module):          # utils/tcn.py:144-243 (dwpw=False, sy
                                  self.conv2, self.batchnorm2, self.chomp2, self.relu2, self.dropout2)
         self.downsample = None
         self.relu = _prelu(c)
+        self.pad = pad
 
-    def forward(self, x):
-        return self.relu(self.net(x) + x)
+    def _half(self, x, conv, bn, act, drop):
+        y = time_conv1d(x, conv)                                          # (B, T + pad, C)
+        y = bn_act(time_major_4d(y), bn, act)                             # BatchNorm1d -> PReLU, same memory layout
+        h = self.pad // 2
+        y = y.squeeze(3).transpose(1, 2)[:, h:y.shape[2] - h]             # (B, T, C) view: symmetric chomp
+        return drop(y)
+
+    def forward(self, x):                 # x: (B, T, C) time-major
+        y = self._half(x, self.conv1, self.batchnorm1, self.relu1, self.dropout1)
+        y = self._half(y, self.conv2, self.batchnorm2, self.relu2, self.dropout2)
+        z = (y + x).contiguous()
+        return self.relu(time_major_4d(z)).squeeze(3).transpose(1, 2)
 
 
 class _TCNTrunk(nn.Module):
@@ -117,8 +134,8 @@ class _TCN(nn.Module):                    # utils/nn.py:106-128 (extract_feats=T
         self.tcn_trunk = _TCNTrunk()
         self.tcn_output = nn.Linear(512, 500)   # present in checkpoints, unused on the feature path
 
-    def forward(self, x):
-        return self.tcn_trunk(x.transpose(1, 2))
+    def forward(self, x):                 # (B, T, 512) -> (B, T, 512); the reference's (B, 512, T) transposes are not made
+        return self.tcn_trunk(x.contiguous())
 
 
 class VisualFeatNet(nn.Module):           # model.py:17-58
@@ -148,7 +165,7 @@ class VisualFeatNet(nn.Module):           # model.py:17-58
         else:
             x = x.transpose(1, 2).reshape(Bn * Tn, C, H, W)
         x = self.trunk(x).view(Bn, Tn, -1)
-        return self.tcn(x).transpose(1, 2)
+        return self.tcn(x)
 
 
 class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 convs + 1x1 -> 4)

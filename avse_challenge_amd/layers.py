@@ -451,6 +451,59 @@ def gemm_conv_ok(x, k, stride):
     return mode == "all" and ho * wo <= 36
 
 
+class _TimeConv1dFn(torch.autograd.Function):
+    """Conv1d(C, C', k, dilation, padding=(k - 1) * dilation) with bias on TIME-MAJOR activations (B, T, C) ->
+    (B, T + pad, C') as ONE GEMM: im2col rows [x(t + j d)]_{j < k} (B * T', k * C) built from k shifted slices of the
+    zero-padded input, times the (C', k * C) weight re-laid [co][j][ci]; backward = two GEMMs + col2im (k shifted slice
+    adds).  hipBLASLt GEMMs and slice copies only: bit-reproducible run to run (MIOpen's conv1d forward is not; its
+    rounding-level jitter flipped PReLU signs in the avse1 TCN and moved the lip-branch gradients by up to 7e-3 between
+    identical steps, profiles/r04a_avse1_stream_diag.txt)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, dil):
+        B, T, C = x.shape
+        Co, _, k = w.shape
+        pad = (k - 1) * dil
+        To = T + pad
+        xp = F.pad(x, (0, 0, pad, pad))                                   # (B, T + 2 pad, C)
+        cols = torch.cat([xp[:, j * dil:j * dil + To] for j in range(k)], dim=2).reshape(B * To, k * C)
+        wm = w.permute(0, 2, 1).reshape(Co, k * C)
+        y = torch.addmm(b, cols, wm.t()) if b is not None else cols @ wm.t()
+        ctx.save_for_backward(cols, wm)
+        ctx.shape = (B, T, C, k, dil, b is not None)
+        return y.view(B, To, Co)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, wm = ctx.saved_tensors
+        B, T, C, k, dil, has_b = ctx.shape
+        pad = (k - 1) * dil
+        To = T + pad
+        Co = wm.shape[0]
+        dy2 = dy.reshape(B * To, Co)
+        dw = (dy2.t() @ cols).view(Co, k, C).permute(0, 2, 1)
+        db = dy2.sum(0) if has_b else None
+        dcols = (dy2 @ wm).view(B, To, k, C)
+        dxp = torch.zeros((B, T + 2 * pad, C), device=dy.device, dtype=dy.dtype)
+        for j in range(k):
+            dxp[:, j * dil:j * dil + To] += dcols[:, :, j]
+        return dxp[:, pad:pad + T], dw, db, None
+
+
+def time_conv1d(x, conv):
+    """nn.Conv1d ``conv`` (padding (k - 1) * dilation, stride 1, groups 1) applied to TIME-MAJOR x (B, T, C):
+    returns (B, T + pad, C') time-major (_TimeConv1dFn)."""
+    assert conv.stride == (1,) and conv.groups == 1 and conv.padding == ((conv.kernel_size[0] - 1) * conv.dilation[0],)
+    return _TimeConv1dFn.apply(x, conv.weight, conv.bias, conv.dilation[0])
+
+
+def time_major_4d(x):
+    """(B, T, C) contiguous -> the same memory as a (B, C, T, 1) channels-last 4-D view (what bn_act and the NHWC
+    PReLU kernels read as (B * T, C) rows)."""
+    B, T, C = x.shape
+    return x.as_strided((B, C, T, 1), (T * C, 1, C, C))
+
+
 class PointwiseConv2d(nn.Conv2d):
     """nn.Conv2d(cin, cout, 1, stride, bias=False) — the ResNet shortcut (utils/resnet.py:86-95 downsample): one GEMM
     (same parameters and state_dict keys)."""

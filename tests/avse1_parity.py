@@ -54,6 +54,16 @@ def capture_masks(model):
         avse1.bn_act = orig
         for h in handles:
             h.remove()
+        # the TCN runs time-major: its activations are (B, C, T, 1) channels-last views, and relu1 / relu2 are applied
+        # (fused with the BatchNorm) BEFORE the symmetric chomp — bring those masks to the oracle's (B, C, T) sites
+        for key in list(masks):
+            m = masks[key]
+            if ".tcn." in key and m.dim() == 4 and m.shape[3] == 1:
+                m = m.squeeze(3)
+                if key.endswith(".relu1") or key.endswith(".relu2"):
+                    h = model.get_submodule(key.rsplit(".", 1)[0]).pad // 2
+                    m = m[:, :, h:m.shape[2] - h]
+                masks[key] = m.contiguous()
 
 
 def impose_masks(ref, masks, flips):

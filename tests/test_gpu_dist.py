@@ -102,7 +102,8 @@ def _worker(rank, world, port, q, workload, bucket_mb):
             off += n
         tot = (float((torch.tensor([e for e, _ in errs]) ** 2).sum().sqrt()),
                float((torch.tensor([r for _, r in errs]) ** 2).sum().sqrt()))
-        q.put((rank, {"errs": errs, "total": tot, "n_buckets": n_buckets, "in_hooks": in_hooks}))
+        names = [n for n, p in ref.model.named_parameters() if p.requires_grad]
+        q.put((rank, {"errs": errs, "names": names, "total": tot, "n_buckets": n_buckets, "in_hooks": in_hooks}))
     except Exception as e:                                # surface the failure instead of a queue timeout
         import traceback
         q.put((rank, {"error": repr(e) + "\n" + traceback.format_exc()}))
@@ -134,7 +135,16 @@ def test_two_ranks_one_gpu_side_stream_buckets(workload):
         # library noise: MIOpen may pick another solver for the same shape when the caching allocator hands it less
         # workspace, so the two runs' activations differ by fp32 rounding and L1 / ReLU signs near 0 can flip
         # (measured 3e-5 .. 3e-4 of the norm); a bucket reduced before a side stream's gradients landed holds zeros
-        # or stale partial sums for whole parameters: O(1) of their norm
-        assert e <= 2e-3 * n, (workload, r, e, n)
+        # or stale partial sums for whole parameters: O(1) of their norm.  Per branch (the avse1 lip / audio / fusion
+        # nets, the Mamba encoder / masknet / decoder): an error of 0.5 % on a whole branch fails the 1e-3 bar
+        assert e <= 5e-4 * n, (workload, r, e, n)
+        branches = {}
+        for name, (ei, ni) in zip(rec["names"], rec["errs"]):
+            key = ".".join(name.split(".")[:2]) if workload == "mamba" else name.split(".")[0]
+            be, bn = branches.get(key, (0.0, 0.0))
+            branches[key] = (be + ei ** 2, bn + ni ** 2)
+        for key, (be, bn) in branches.items():
+            print(f"    branch {key}: rel err {(be / max(bn, 1e-60)) ** 0.5:.2e}")
+            assert be ** 0.5 <= 1e-3 * bn ** 0.5 + 1e-6 * n, (workload, r, key, be ** 0.5, bn ** 0.5)
         for i, (ei, ni) in enumerate(rec["errs"]):
             assert ei <= 5e-2 * ni + 1e-4 * n, (workload, r, i, ei, ni)

@@ -832,15 +832,24 @@ def test_lstm_group_residency_guard(monkeypatch):
 
 
 _TIMEOUT_CHILD = r"""
-import json, sys, time, torch
+import ctypes, json, sys, time, torch
 sys.path.insert(0, sys.argv[1])
 from avse_challenge_amd import kernels as K
 B, T, H = 32, 4, 257
 gx = torch.randn(B, T, 4 * H, device="cuda")
 w = 0.06 * torch.randn(4 * H, H, device="cuda")
-t = time.time()
-K.lstm_fwd(gx, w)
+K.lstm_fwd(gx, w)                       # grouped launch on the full device: completes
 torch.cuda.synchronize()
+K.raise_if_kernel_error()
+hip = ctypes.CDLL("libamdhip64.so")
+raw = ctypes.c_void_p()
+mask = (ctypes.c_uint32 * 1)(0xF)       # a stream restricted to 4 CUs: 4 of a sequence's 8 workgroups at a time
+assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(raw), 1, mask) == 0
+s = torch.cuda.ExternalStream(raw.value)
+t = time.time()
+with torch.cuda.stream(s):
+    h, _, _ = K.lstm_fwd(gx, w)
+s.synchronize()
 try:
     K.raise_if_kernel_error()
     raised = ""
@@ -851,16 +860,14 @@ print(json.dumps({"raised": raised, "s": time.time() - t}))
 
 
 def test_lstm_group_not_coresident_raises():
-    """A grouped LSTM launch whose workgroups cannot all be resident (the process restricted to 4 CUs with
-    HSA_CU_MASK, so only 4 of a sequence's 8 workgroups ever run at once) times out its hand-offs and the host
-    raises HipKernelError — the step never returns those outputs as if they were valid."""
+    """A grouped LSTM launch whose workgroups cannot all be resident (launched on a stream restricted to 4 CUs with
+    hipExtStreamCreateWithCUMask, so only 4 of a sequence's 8 workgroups ever run at once) times out its hand-offs
+    (bounded spins, seconds) and the host raises HipKernelError — the step never returns those outputs as valid."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, HSA_CU_MASK="0:0-3")
-    r = subprocess.run([sys.executable, "-c", _TIMEOUT_CHILD, root], env=env, capture_output=True, text=True,
-                       timeout=110)
+    r = subprocess.run([sys.executable, "-c", _TIMEOUT_CHILD, root], capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert "timed out" in out["raised"], out

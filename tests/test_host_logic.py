@@ -110,3 +110,44 @@ def test_conv1_gemm_matches_conv2d_fp64(add_bias):
     ref = torch.autograd.grad(F.conv2d(xr, wr, br, padding=2), (xr, wr, br), gy)
     for a_, r_ in zip(got, ref):
         torch.testing.assert_close(a_, r_, rtol=1e-12, atol=1e-12)
+
+
+def test_time_conv1d_matches_conv1d_fp64():
+    """layers._TimeConv1dFn (the avse1 TCN conv: im2col GEMM on time-major activations) == nn.Conv1d with padding
+    (k-1)*dil (utils/tcn.py:163-166) in fp64: output and the input / weight / bias gradients, dilations 1..8."""
+    import torch.nn as nn
+    from avse_challenge_amd.layers import time_conv1d
+    torch.manual_seed(0)
+    for dil in (1, 2, 4, 8):
+        conv = nn.Conv1d(12, 10, 3, padding=2 * dil, dilation=dil).double()
+        x = torch.randn(2, 12, 19, dtype=torch.float64, requires_grad=True)
+        y_ref = conv(x)                                           # (B, C', T + pad)
+        g = torch.randn_like(y_ref)
+        gx_ref, gw_ref, gb_ref = torch.autograd.grad((y_ref * g).sum(), (x, conv.weight, conv.bias))
+        xt = x.detach().transpose(1, 2).contiguous().requires_grad_(True)     # (B, T, C) time-major
+        y = time_conv1d(xt, conv)
+        assert y.shape == (2, 19 + 2 * dil, 10)
+        assert torch.allclose(y.transpose(1, 2), y_ref, atol=1e-12)
+        gx, gw, gb = torch.autograd.grad((y * g.transpose(1, 2)).sum(), (xt, conv.weight, conv.bias))
+        assert torch.allclose(gx.transpose(1, 2), gx_ref, atol=1e-12)
+        assert torch.allclose(gw, gw_ref, atol=1e-12) and torch.allclose(gb, gb_ref, atol=1e-12)
+
+
+def test_time_major_tcn_chomp_matches_reference_order():
+    """The avse1 TCN's time-major half-block order — BatchNorm statistics over the whole (T + pad) conv output, the
+    elementwise PReLU before the symmetric chomp — equals the reference's conv -> BN -> chomp -> PReLU (fp64, torch
+    ops standing in for the bnact kernel)."""
+    import torch.nn as nn
+    import torch.nn.functional as F
+    torch.manual_seed(1)
+    dil, C, T = 2, 8, 15
+    conv = nn.Conv1d(C, C, 3, padding=2 * dil, dilation=dil).double()
+    bn = nn.BatchNorm1d(C).double().train()
+    a = torch.full((C,), 0.25, dtype=torch.float64)
+    x = torch.randn(2, C, T, dtype=torch.float64)
+    ref = F.prelu(bn(conv(x))[:, :, dil:T + 2 * dil - dil], a)          # reference: chomp then PReLU
+    from avse_challenge_amd.layers import time_conv1d
+    y = time_conv1d(x.transpose(1, 2).contiguous(), conv)                # (B, T + pad, C)
+    bn2 = nn.BatchNorm1d(C).double().train()
+    z = F.prelu(bn2(y.transpose(1, 2)), a)[:, :, dil:y.shape[1] - dil]   # ours: BN + PReLU, then chomp
+    assert torch.allclose(z, ref, atol=1e-12)
