@@ -69,7 +69,6 @@ SIGNATURES = {
     "avse_scan_n_chunks": (c_i64, [c_i64]),
     "avse_scan_bwd_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "avse_scan_fwd": (c_i32, [ctypes.POINTER(ScanFwdArgs), c_vp]),
-    "avse_scan_fwd_variant": (c_i32, [ctypes.POINTER(ScanFwdArgs), c_i32, c_vp]),
     "avse_scan_bwd": (c_i32, [ctypes.POINTER(ScanBwdArgs), c_vp]),
     "avse_cconv_bwd_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "avse_cconv_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,

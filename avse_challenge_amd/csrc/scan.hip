@@ -330,221 +330,6 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     }
 }
 
-// ------------------------------------------------------------------------------- forward, pipelined (round 4)
-// The same recurrence with ONE workgroup barrier per 32-step chunk and no global-memory latency between chunks:
-// LDS holds two chunk buffers; in iteration k every thread (1) runs chunk k's 32 steps from buffer k&1, (2) flushes
-// chunk k-1's outputs from buffer (k+1)&1 and stages chunk k+1 (loaded one iteration earlier) into the SAME elements
-// of that buffer — the flush and the staging of a thread touch the same (row, step) elements, so they need no barrier
-// between them — (3) issues the loads of chunk k+2 and of chunk k's z, then (4) meets the others at one barrier that
-// waits for LDS only (lgkmcnt), never for the loads in flight.  A chunk is one checkpoint row (states after its steps
-// 15 and 31).  Staging / flush map: lane = (h, t), t = lane & 31, rows 8 i + 2 wave + h: one wave-instruction covers
-// two rows x 32 consecutive steps (two 128-B lines).
-constexpr int TC2 = 32;
-constexpr int UD2 = 2 * TC2 + 2;                 // float2 rows: the 16 channels of a wave start on distinct banks
-constexpr int EPT = CPB * TC2 / THREADS;         // 8 rows per thread per tensor per chunk
-constexpr int BPT2 = NSTATE * TC2 / THREADS;     // 2 B (and C) rows per thread
-
-__device__ inline void lds_barrier_() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-template <typename Tin>
-struct Rows8 {
-    typename rawv<Tin>::R v[EPT];
-    // rows past D lie beyond the resource's range (read as 0); steps past L are masked at staging
-    __device__ inline void load(const Tin* p, int64_t bs, int64_t ds, int b, int d0, int D, int t0, int L, bool rev) {
-        const int lane = threadIdx.x & 63, wave = wave_u();
-        const int nrow = min(CPB, D - d0);
-        const auto rs = make_rsrc(p + b * bs + (int64_t)d0 * ds, (int64_t)(nrow - 1) * ds + L);
-        const int voff = (2 * wave + (lane >> 5)) * (int)ds + tpos(t0 + (lane & 31), L, rev);
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) v[i] = rawv<Tin>::ld(rs, voff, 8 * i * (int)ds);
-    }
-    __device__ inline float at(int i) const { return rawv<Tin>::f(v[i]); }
-};
-
-template <typename Tin>
-struct BC2 {
-    typename rawv<Tin>::R bv[BPT2], cv[BPT2];
-    __device__ inline void load(const Tin* B, int64_t B_bs, int64_t B_ns, const Tin* C, int64_t C_bs, int64_t C_ns,
-                                int b, int t0, int L, bool rev) {
-        const int lane = threadIdx.x & 63, wave = wave_u();
-        const int pos = tpos(t0 + (lane & 31), L, rev);
-        const auto rb = make_rsrc(B + b * B_bs, (int64_t)(NSTATE - 1) * B_ns + L);
-        const auto rc = make_rsrc(C + b * C_bs, (int64_t)(NSTATE - 1) * C_ns + L);
-        const int n0 = 2 * wave + (lane >> 5);
-        const int vb = n0 * (int)B_ns + pos, vc = n0 * (int)C_ns + pos;
-#pragma unroll
-        for (int i = 0; i < BPT2; ++i) {
-            bv[i] = rawv<Tin>::ld(rb, vb, 8 * i * (int)B_ns);
-            cv[i] = rawv<Tin>::ld(rc, vc, 8 * i * (int)C_ns);
-        }
-    }
-    __device__ inline void store(float* s_bc, int tn) const {
-        const int lane = threadIdx.x & 63, wave = wave_u();
-        const int t = lane & 31, n0 = 2 * wave + (lane >> 5);
-        const bool tv = t < tn;
-#pragma unroll
-        for (int i = 0; i < BPT2; ++i) {
-            s_bc[t * BC_STRIDE + n0 + 8 * i] = tv ? rawv<Tin>::f(bv[i]) : 0.f;
-            s_bc[t * BC_STRIDE + NSTATE + n0 + 8 * i] = tv ? rawv<Tin>::f(cv[i]) : 0.f;
-        }
-    }
-};
-
-template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS>
-__global__ __launch_bounds__(THREADS) void fwd2_kernel(avse_scan_fwd_args a, int nblk_d) {
-    __shared__ __attribute__((aligned(16))) float s_ud[2][CPB * UD2];
-    __shared__ __attribute__((aligned(16))) float s_bc[2][TC2 * BC_STRIDE];
-    __shared__ float2 s_par[CPB];                      // (delta_bias, D) per row of the block
-
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int b = bid / nblk_d, d0 = (bid % nblk_d) * CPB;
-    const int D = (int)a.dim, L = (int)a.seqlen;
-    const bool rev = a.reverse != 0;
-    const Lane id = lane_ids();
-    const int d = d0 + id.c;
-    const bool dvalid = d < D;
-    const int lane = threadIdx.x & 63, wave = wave_u();
-    const int st_t = lane & 31, st_r0 = 2 * wave + (lane >> 5);     // staging / flush element map
-    const int nrow = min(CPB, D - d0);
-    if (threadIdx.x < CPB) {
-        const int r = d0 + (int)threadIdx.x;
-        s_par[threadIdx.x] = make_float2((HAS_BIAS && r < D) ? a.delta_bias[r] : 0.f, (HAS_D && r < D) ? a.D[r] : 0.f);
-    }
-    f2_t A2v[NS / 2], h2[NS / 2];
-#pragma unroll
-    for (int p = 0; p < NS / 2; ++p) {
-        const int j = id.g * NS + 2 * p;
-        A2v[p] = dvalid ? f2_t{a.A[(int64_t)d * NSTATE + j], a.A[(int64_t)d * NSTATE + j + 1]} * AVSE_LOG2E : f2_t{0.f, 0.f};
-        h2[p] = f2_t{0.f, 0.f};
-    }
-    const Tin* u = (const Tin*)a.u;
-    const Tin* dl = (const Tin*)a.delta;
-    const Tin* z = (const Tin*)a.z;
-    const int nck = (L + TC2 - 1) / TC2;
-    float* xrow = a.x + ((int64_t)b * D + (dvalid ? d : 0)) * nck * (2 * NSTATE) + 2 * id.g * NS;
-    const auto ro = make_rsrc((Tin*)a.out + b * a.out_bs + (int64_t)d0 * a.out_ds, (int64_t)(nrow - 1) * a.out_ds + L);
-    const auto rzo = make_rsrc((Tin*)a.out_z + b * a.out_z_bs + (int64_t)d0 * a.out_z_ds,
-                               (int64_t)(nrow - 1) * a.out_z_ds + L);
-
-    Rows8<Tin> ru, rd, rz;
-    BC2<Tin> rbc;
-    float duk0[EPT], duk1[EPT];                        // D u of the staged elements, per buffer (added at the flush)
-
-    // (u, delta) of chunk kk (in ru / rd) -> (dt u, dt) rows of buffer P; D u -> duk
-    auto stage = [&](int kk, float* sud, float* sbc, float* duk) {
-        const int tn = min(TC2, L - kk * TC2);
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) {
-            const int r = st_r0 + 8 * i;
-            const float2 par = s_par[r];
-            float dt = rd.at(i);
-            if (HAS_BIAS) dt += par.x;
-            if (SOFTPLUS) dt = softplus2(dt);
-            float uv = ru.at(i);
-            const bool ok = st_t < tn && r < nrow;
-            dt = ok ? dt : 0.f;
-            uv = ok ? uv : 0.f;
-            duk[i] = HAS_D ? par.y * uv : 0.f;
-            *reinterpret_cast<float2*>(&sud[r * UD2 + 2 * st_t]) = make_float2(dt * uv, dt);
-        }
-        rbc.store(sbc, tn);
-    };
-    auto load_in = [&](int kk) {
-        const int t0 = kk * TC2;
-        ru.load(u, a.u_bs, a.u_ds, b, d0, D, t0, L, rev);
-        rd.load(dl, a.delta_bs, a.delta_ds, b, d0, D, t0, L, rev);
-        rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, t0, L, rev);
-    };
-    // outputs of chunk kk from buffer sud (y in the dt u slots) + duk; z of chunk kk in rz
-    auto flush = [&](int kk, const float* sud, const float* duk) {
-        const int tn = min(TC2, L - kk * TC2);
-        const int pos = tpos(kk * TC2 + st_t, L, rev);
-        float outv[EPT];
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) outv[i] = sud[(st_r0 + 8 * i) * UD2 + 2 * st_t] + duk[i];
-        if (st_t < tn) {            // rows past D: beyond the resources' ranges (stores dropped)
-            if (a.out) {
-                const int vo = st_r0 * (int)a.out_ds + pos;
-#pragma unroll
-                for (int i = 0; i < EPT; ++i) bufst<Tin>::st(ro, vo, 8 * i * (int)a.out_ds, outv[i]);
-            }
-            if (HAS_Z) {
-                const int vz = st_r0 * (int)a.out_z_ds + pos;
-#pragma unroll
-                for (int i = 0; i < EPT; ++i) bufst<Tin>::st(rzo, vz, 8 * i * (int)a.out_z_ds, outv[i] * siluf_(rz.at(i)));
-            }
-        }
-    };
-    // the 32 steps of chunk kk from buffer (sud, sbc); y into the dt u slots; checkpoint row kk
-    auto compute = [&](int kk, float* sud, const float* sbc) {
-        float* my_ud = &sud[id.c * UD2];
-        constexpr int U = 8;
-        auto steps = [&](int t) {
-            float yv[U];
-#pragma unroll
-            for (int q = 0; q < U; ++q) {
-                const float2 ud = *reinterpret_cast<const float2*>(&my_ud[2 * (t + q)]);   // (dt u, dt)
-                const float4 bq = *reinterpret_cast<const float4*>(&sbc[(t + q) * BC_STRIDE + id.g * NS]);
-                const float4 cq = *reinterpret_cast<const float4*>(&sbc[(t + q) * BC_STRIDE + NSTATE + id.g * NS]);
-                const f2_t bp[2] = {f2_t{bq.x, bq.y}, f2_t{bq.z, bq.w}};
-                const f2_t cp[2] = {f2_t{cq.x, cq.y}, f2_t{cq.z, cq.w}};
-                const f2_t dt2 = f2_t{ud.y, ud.y}, dtu2 = f2_t{ud.x, ud.x};
-                f2_t y2 = f2_t{0.f, 0.f};
-#pragma unroll
-                for (int p = 0; p < NS / 2; ++p) {
-                    h2[p] = exp2_2(dt2 * A2v[p]) * h2[p] + dtu2 * bp[p];
-                    y2 += h2[p] * cp[p];
-                }
-                yv[q] = y2.x + y2.y;
-            }
-#pragma unroll
-            for (int q = 0; q < U; ++q) yv[q] = group_sum<G>(yv[q]);
-#pragma unroll
-            for (int q = 0; q < U; ++q) my_ud[2 * (t + q)] = yv[q];
-        };
-        steps(0);
-        steps(U);
-        const f2_t ha0 = h2[0], ha1 = h2[1];          // state after step 15 of the chunk
-        steps(2 * U);
-        steps(3 * U);
-        if (dvalid) {
-            float4* xp = reinterpret_cast<float4*>(xrow + (int64_t)kk * (2 * NSTATE));
-            xp[0] = make_float4(ha0.x, h2[0].x, ha0.y, h2[0].y);
-            xp[1] = make_float4(ha1.x, h2[1].x, ha1.y, h2[1].y);
-        }
-    };
-
-    load_in(0);
-    __syncthreads();                                   // s_par
-    stage(0, s_ud[0], s_bc[0], duk0);
-    if (nck > 1) load_in(1);
-    lds_barrier_();
-    // iteration k: compute k | flush k-1, stage k+1 (same buffer, same elements) | loads k+2, z(k) | barrier
-    auto iter = [&](int k, float* sud_k, float* sbc_k, float* sud_o, float* sbc_o, float* duk_k, float* duk_o) {
-        compute(k, sud_k, sbc_k);
-        if (k >= 1) flush(k - 1, sud_o, duk_o);
-        if (k + 1 < nck) stage(k + 1, sud_o, sbc_o, duk_o);
-        if (k + 2 < nck) load_in(k + 2);
-        if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, k * TC2, L, rev);
-        lds_barrier_();
-    };
-#pragma unroll 1
-    for (int k = 0; k < nck; k += 2) {
-        iter(k, s_ud[0], s_bc[0], s_ud[1], s_bc[1], duk0, duk1);
-        if (k + 1 < nck) iter(k + 1, s_ud[1], s_bc[1], s_ud[0], s_bc[0], duk1, duk0);
-    }
-    if ((nck - 1) & 1) flush(nck - 1, s_ud[1], duk1);
-    else flush(nck - 1, s_ud[0], duk0);
-}
-
-template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS>
-static void launch_fwd2(const avse_scan_fwd_args& a, int nblk_d, int nblocks, hipStream_t st) {
-    if (a.delta_softplus)
-        hipLaunchKernelGGL((fwd2_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, true>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
-    else
-        hipLaunchKernelGGL((fwd2_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, false>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
-}
-
 // ------------------------------------------------------------------------------- backward
 // Sum of 8 values over the 16 channel lanes (lane bits 2..5) of a wave without selects: a
 // permlane32_swap + add per pair halves 8 -> 4 values (bit 5), permlane16_swap + add halves 4 -> 2
@@ -1026,8 +811,7 @@ static int check_common(int64_t batch, int64_t dim, int64_t seqlen, int64_t dsta
     return AVSE_OK;
 }
 
-// variant 1: the 64-step chunk kernel (three barriers per chunk); 2: the pipelined 32-step kernel (fwd2_kernel)
-int avse_scan_fwd_variant(const avse_scan_fwd_args* a, int32_t variant, avse_stream_t stream) {
+int avse_scan_fwd(const avse_scan_fwd_args* a, avse_stream_t stream) {
     if (!a || !a->u || !a->delta || !a->A || !a->B || !a->C || !a->x) return AVSE_EINVAL;
     if (a->z ? !a->out_z : !a->out) return AVSE_EINVAL;
     int rc = check_common(a->batch, a->dim, a->seqlen, a->dstate, a->in_dtype);
@@ -1035,18 +819,11 @@ int avse_scan_fwd_variant(const avse_scan_fwd_args* a, int32_t variant, avse_str
     const int nblk_d = (int)((a->dim + CPB - 1) / CPB);
     const int nblocks = (int)(a->batch * nblk_d);
     hipStream_t st = (hipStream_t)stream;
-    if (variant == 2) {
-        if (a->in_dtype == AVSE_F32) AVSE_DISPATCH_FLAGS(launch_fwd2, float, (*a), nblk_d, nblocks, st);
-        else AVSE_DISPATCH_FLAGS(launch_fwd2, bf16_t, (*a), nblk_d, nblocks, st);
-    } else {
-        if (a->in_dtype == AVSE_F32) AVSE_DISPATCH_FLAGS(launch_fwd, float, (*a), nblk_d, nblocks, st);
-        else AVSE_DISPATCH_FLAGS(launch_fwd, bf16_t, (*a), nblk_d, nblocks, st);
-    }
+    if (a->in_dtype == AVSE_F32) AVSE_DISPATCH_FLAGS(launch_fwd, float, (*a), nblk_d, nblocks, st);
+    else AVSE_DISPATCH_FLAGS(launch_fwd, bf16_t, (*a), nblk_d, nblocks, st);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
-
-int avse_scan_fwd(const avse_scan_fwd_args* a, avse_stream_t stream) { return avse_scan_fwd_variant(a, 1, stream); }
 
 int avse_scan_bwd(const avse_scan_bwd_args* a, avse_stream_t stream) {
     if (!a || !a->u || !a->delta || !a->A || !a->B || !a->C || !a->dout || !a->x || !a->du || !a->ddelta ||

@@ -11,8 +11,6 @@ from . import _lib
 from ._lib import AVSE_BF16, AVSE_F32, ScanBwdArgs, ScanFwdArgs, check, ptr, stream_ptr
 
 NSTATE = 16
-# selective-scan forward kernel (csrc/scan.hip avse_scan_fwd_variant): 1 = 64-step chunks, 2 = pipelined 32-step chunks
-SCAN_FWD_VARIANT = int(os.environ.get("AVSE_SCAN_FWD_VARIANT", "1"))
 
 # Launch timing taps (bench.py's in-step roofline): while ``LAUNCH_TAPS`` maps a C entry point's name to a list, each
 # eager launch of that entry point appends a (start, end) pair of HIP timing events recorded on its launch stream.
@@ -130,7 +128,7 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
     if out is not None:
         a.out, a.out_bs, a.out_ds = out.data_ptr(), out.stride(0), out.stride(1)
     a.x = x.data_ptr()
-    check(L.avse_scan_fwd_variant(a, SCAN_FWD_VARIANT, stream_ptr(u.device)), "avse_scan_fwd")
+    check(L.avse_scan_fwd(a, stream_ptr(u.device)), "avse_scan_fwd")
     return out, x, out_z
 
 

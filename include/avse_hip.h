@@ -94,10 +94,6 @@ typedef struct {
 int64_t avse_scan_n_chunks(int64_t seqlen);
 int64_t avse_scan_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t seqlen, int64_t dstate);
 int avse_scan_fwd(const avse_scan_fwd_args* a, avse_stream_t stream);
-/* avse_scan_fwd with an explicit kernel choice (A/B measurement): 1 = 64-step chunks with three workgroup barriers per
- * chunk (avse_scan_fwd's), 2 = two LDS chunk buffers of 32 steps, one barrier per chunk (compute of chunk k overlaps
- * the flush of k-1 and the staging of k+1).  Same results bit for bit; same checkpoint layout. */
-int avse_scan_fwd_variant(const avse_scan_fwd_args* a, int32_t variant, avse_stream_t stream);
 int avse_scan_bwd(const avse_scan_bwd_args* a, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- causal conv1d -------

@@ -714,34 +714,6 @@ def test_c5_cconv_bf16_production_shape_vs_oracle():
     close(db, bias.grad, 1e-5 * sb, 1e-5, "dbias")
 
 
-@pytest.mark.parametrize("b,d,l,dtype,rev,flags", [(2, 64, 300, torch.float32, False, "zdb"),
-                                                    (1, 100, 33, torch.float32, True, "zdb"),
-                                                    (3, 70, 65, torch.bfloat16, False, "zd"),
-                                                    (2, 128, 5, torch.float32, True, ""),
-                                                    (1, 64, 1, torch.float32, False, "z"),
-                                                    (2, 1024, 3999, torch.bfloat16, True, "zdb")])
-def test_scan_fwd_variants_bitwise_equal(b, d, l, dtype, rev, flags, monkeypatch):
-    """avse_scan_fwd_variant 2 (pipelined 32-step chunks) returns the out / out_z and the 16-step checkpoints of
-    variant 1 bit for bit (same per-element arithmetic in the same order), including ragged L, D not a multiple of the
-    64-channel block, reverse, bf16, no z / D / bias."""
-    torch.manual_seed(l + d)
-    u = det_input((b, d, l), 1900 + l).to(DEV, dtype)
-    dl = (0.5 * det_input((b, d, l), 1901)).to(DEV, dtype)
-    z = det_input((b, d, l), 1902).to(DEV, dtype) if "z" in flags else None
-    A = -torch.exp(0.5 * det_input((d, 16), 1903)).to(DEV)
-    Bm, Cm = det_input((b, 1, 16, l), 1904).to(DEV, dtype), det_input((b, 1, 16, l), 1905).to(DEV, dtype)
-    D = det_input((d,), 1906).to(DEV) if "d" in flags else None
-    bias = (0.1 * det_input((d,), 1907)).to(DEV) if "b" in flags else None
-    outs = []
-    for v in (1, 2):
-        monkeypatch.setattr(K(), "SCAN_FWD_VARIANT", v)
-        outs.append(K().selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, reverse=rev))
-    for a_, b_ in zip(outs[0], outs[1]):
-        assert (a_ is None) == (b_ is None)
-        if a_ is not None:
-            assert torch.equal(a_, b_)
-
-
 # ------------------------------------------------------------------ LSTM recurrence (avse1 FusionNet, avse2 DPRNN)
 
 @pytest.mark.parametrize("group", ["1", "0"])
