@@ -804,44 +804,53 @@ def test_lstm_group_residency_guard(monkeypatch):
 
 
 _TIMEOUT_CHILD = r"""
-import ctypes, json, sys, time, torch
+import ctypes, json, os, sys, time, torch
 sys.path.insert(0, sys.argv[1])
 from avse_challenge_amd import kernels as K
 B, T, H = 32, 4, 257
 gx = torch.randn(B, T, 4 * H, device="cuda")
 w = 0.06 * torch.randn(4 * H, H, device="cuda")
-K.lstm_fwd(gx, w)                       # grouped launch on the full device: completes
+K.lstm_fwd(gx, w)                       # grouped launch on the idle device: completes
 torch.cuda.synchronize()
 K.raise_if_kernel_error()
-hip = ctypes.CDLL("libamdhip64.so")
-raw = ctypes.c_void_p()
-mask = (ctypes.c_uint32 * 1)(0xF)       # a stream restricted to 4 CUs: 4 of a sequence's 8 workgroups at a time
-assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(raw), 1, mask) == 0
-s = torch.cuda.ExternalStream(raw.value)
+occ = ctypes.CDLL(os.path.join(sys.argv[1], "tests", "hip", "libocc.so"))
+ncu = torch.cuda.get_device_properties(0).multi_processor_count
+arrived = torch.zeros(1, dtype=torch.int32, device="cuda")
+hog = torch.cuda.Stream()
+assert occ.occupy_cus(ncu - 4, ctypes.c_void_p(arrived.data_ptr()), ctypes.c_double(8.0),
+                      ctypes.c_void_p(hog.cuda_stream)) == 0
+side = torch.cuda.Stream()
 t = time.time()
-with torch.cuda.stream(s):
-    h, _, _ = K.lstm_fwd(gx, w)
-s.synchronize()
+with torch.cuda.stream(side):
+    while int(arrived.item()) < ncu - 4 and time.time() - t < 3.0:   # the hog holds all CUs but 4
+        time.sleep(0.01)
+    held = int(arrived.item())
+    K.lstm_fwd(gx, w)                   # 4 of a sequence's 8 workgroups fit: hand-offs time out
+side.synchronize()
+hog.synchronize()
 try:
     K.raise_if_kernel_error()
     raised = ""
 except K.HipKernelError as e:
     raised = str(e)
-print(json.dumps({"raised": raised, "s": time.time() - t}))
+print(json.dumps({"raised": raised, "held": held, "ncu": ncu, "s": time.time() - t}))
 """
 
 
 def test_lstm_group_not_coresident_raises():
-    """A grouped LSTM launch whose workgroups cannot all be resident (launched on a stream restricted to 4 CUs with
-    hipExtStreamCreateWithCUMask, so only 4 of a sequence's 8 workgroups ever run at once) times out its hand-offs
-    (bounded spins, seconds) and the host raises HipKernelError — the step never returns those outputs as valid."""
+    """A grouped LSTM launch whose workgroups cannot all be resident — a bounded test kernel (tests/hip/occupy.hip)
+    holds all CUs but 4 with 160 KB of LDS each for 8 s (longer than the kernel's bounded spin), so only 4 of a sequence's 8 workgroups can run — times out its
+    hand-offs (bounded spins) and the host raises HipKernelError: the outputs are never returned as valid."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "tests", "hip", "libocc.so")):
+        pytest.fail("tests/hip/libocc.so missing: run __graft_entry__.build()")
     r = subprocess.run([sys.executable, "-c", _TIMEOUT_CHILD, root], capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["held"] == out["ncu"] - 4, out
     assert "timed out" in out["raised"], out
 
 
