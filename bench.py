@@ -44,7 +44,7 @@ os.environ.setdefault("PYTORCH_MIOPEN_SUGGEST_NHWC_BATCHNORM", "1")
 METRIC = "utterances/sec (3s@16kHz + 75 lip frames)"
 # HBM bytes per launch of each roofline kernel, from rocprofv3 PMC passes (tools/pmc_traffic.sh:
 # FETCH_SIZE and WRITE_SIZE in separate passes, corrected as MI355X_MICROARCH.md prescribes)
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r04_traffic.json")
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFS = 157.3          # FP32 matrix (= vector) peak, spec
 
@@ -736,13 +736,13 @@ def roofline_hip(dev):
         # training fwd: reads u, delta, z, B, C; writes out_z
         add_hbm(f"avse_scan_fwd ({tag}, training fwd, out_z only)", [b, d, l], name, s * b * l * (4 * d + 2 * n),
                 lambda: K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, return_out=False),
-                "scan" if tag == "C3" else None, (pmcf, f"void avse::scan::fwd_kernel<{ktype},"))
+                "scan" if tag == "C3" else "scan_c5", (pmcf, f"void avse::scan::fwd_kernel<{ktype},"))
         # bwd as the model calls it (out=None, no out_z recompute): reads u, delta, z, dout, B, C; writes du,
         # ddelta, dz (input dtype) and fp32 dB, dC
         add_hbm(f"avse_scan_bwd ({tag}, as MambaInnerNoOutProj calls it)", [b, d, l], name,
                 b * l * (7 * s * d + 2 * s * n + 2 * 4 * n),
                 lambda: K.selective_scan_bwd(u, delta, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False),
-                "scan_bwd" if tag == "C3" else None,
+                "scan_bwd" if tag == "C3" else "scan_bwd_c5",
                 (pmcf, f"void avse::scan::bwd_kernel<{ktype},"))
         if tag == "C3":
             w, cb = rnd(d, 4, scale=0.5), rnd(d)
@@ -762,9 +762,9 @@ def roofline_hip(dev):
     gm, bt = 1 + 0.1 * torch.randn(1, 512, 1, device=dev, generator=g), 0.1 * torch.randn(1, 512, 1, device=dev, generator=g)
     _, y1, st = K.dwconv_gln_fwd(xd, wd, 128, al, gm, bt)
     add_hbm("avse_dwconv_gln_fwd (C4 TCN fused dwconv -> PReLU -> gLN: x read, y1 + y written)", [16, 512, 3999], "fp32",
-            12 * xd.numel(), lambda: K.dwconv_gln_fwd(xd, wd, 128, al, gm, bt))
+            12 * xd.numel(), lambda: K.dwconv_gln_fwd(xd, wd, 128, al, gm, bt), "dwconv_gln")
     add_hbm("avse_dwconv_gln_bwd (C4 TCN fused: x, y1, dy read, dx written)", [16, 512, 3999], "fp32",
-            16 * xd.numel(), lambda: K.dwconv_gln_bwd(xd, wd, 128, y1, al, gm, st, gy))
+            16 * xd.numel(), lambda: K.dwconv_gln_bwd(xd, wd, 128, y1, al, gm, st, gy), "dwconv_gln_bwd")
     del xd, gy, y1
     # avse1 C2 lip front-end: BatchNorm3d -> PReLU (bnact) and the (1,3,3) max pool on (32, 64, 75, 48, 48), and the
     # ResNet layer4 bn2 + shortcut -> PReLU site on (2400, 512, 3, 3).  Two passes each way: fwd reads x twice and

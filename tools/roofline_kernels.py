@@ -18,12 +18,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from avse_challenge_amd import kernels as K  # noqa: E402
 
 SHAPES = {"scan": (64, 1024, 3999), "scan_bwd": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999),
-          "conv3": (32, 64, 376, 257), "dconv_wgrad": (32, 64, 376, 257)}
+          "conv3": (32, 64, 376, 257), "dconv_wgrad": (32, 64, 376, 257),
+          "scan_c5": (32, 1024, 5999), "scan_bwd_c5": (32, 1024, 5999),
+          "dwconv_gln": (16, 512, 3999), "dwconv_gln_bwd": (16, 512, 3999)}
 
 
-def aligned(b, d, l, g, scale=1.0):
-    """(b, d, l) fp32 with the product's 128-B aligned time stride (kernels.bdl_empty), filled N(0, scale^2)."""
-    t = K.bdl_empty(b, d, l, torch.float32, "cuda")
+def aligned(b, d, l, g, scale=1.0, dtype=torch.float32):
+    """(b, d, l) with the product's 128-B aligned time stride (kernels.bdl_empty), filled N(0, scale^2)."""
+    t = K.bdl_empty(b, d, l, dtype, "cuda")
     t.copy_(scale * torch.randn(b, d, l, device="cuda", generator=g))
     return t
 
@@ -35,17 +37,27 @@ def main():
     a = p.parse_args()
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
-    if a.phase in ("scan", "scan_bwd"):
-        b, d, l = SHAPES["scan"]
-        u, dl, z = aligned(b, d, l, g), aligned(b, d, l, g, 0.1), aligned(b, d, l, g)
+    if a.phase.startswith("scan"):
+        b, d, l = SHAPES[a.phase]
+        dt = torch.bfloat16 if a.phase.endswith("_c5") else torch.float32
+        u, dl, z = aligned(b, d, l, g, dtype=dt), aligned(b, d, l, g, 0.1, dt), aligned(b, d, l, g, dtype=dt)
         A = -torch.rand(d, 16, device=dev, generator=g) - 0.5
-        Bm, Cm = aligned(b, 16, l, g), aligned(b, 16, l, g)
+        Bm, Cm = aligned(b, 16, l, g, dtype=dt), aligned(b, 16, l, g, dtype=dt)
         D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
         fn = lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False)  # noqa: E731
-        if a.phase == "scan_bwd":
+        if a.phase.startswith("scan_bwd"):
             _, x, _ = fn()
-            dout = aligned(b, d, l, g)
+            dout = aligned(b, d, l, g, dtype=dt)
             fn = lambda: K.selective_scan_bwd(u, dl, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False)  # noqa: E731
+    elif a.phase.startswith("dwconv_gln"):
+        x = torch.randn(*SHAPES["dwconv_gln"], device=dev, generator=g)
+        w = 0.5 * torch.randn(512, 1, 3, device=dev, generator=g)
+        al, gm, bt = torch.full((1,), 0.25, device=dev), torch.ones(1, 512, 1, device=dev), torch.zeros(1, 512, 1, device=dev)
+        fn = lambda: K.dwconv_gln_fwd(x, w, 128, al, gm, bt)  # noqa: E731
+        if a.phase == "dwconv_gln_bwd":
+            _, y1, st = fn()
+            gy = torch.randn(*SHAPES["dwconv_gln"], device=dev, generator=g)
+            fn = lambda: K.dwconv_gln_bwd(x, w, 128, y1, al, gm, st, gy)  # noqa: E731
     elif a.phase == "dwconv":
         x = torch.randn(*SHAPES["dwconv"], device=dev, generator=g)
         w = torch.randn(512, 1, 3, device=dev, generator=g)
