@@ -21,6 +21,26 @@ constexpr int DW_U = 8, DW_UB = 4;          // elements per thread in flight (fo
 
 __device__ inline float prelu(float x, float a) { return x > 0.f ? x : a * x; }
 
+// 4 consecutive fp32 per thread: dwordx4 buffer loads (rows need only dword alignment; outside the row's range: 0)
+typedef unsigned int u4_t __attribute__((ext_vector_type(4)));
+__device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, int voff_elems) {
+    const u4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff_elems * 4, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ inline float f4at(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
+// a row's quadruple t..t+3: one dwordx4 store, the row's last partial quadruple element by element
+__device__ inline void st4_row(__amdgpu_buffer_rsrc_t r, float* row, int t, int K, const float (&v)[4]) {
+    if (t + 4 <= K) {
+        const u4_t o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(o, r, t * 4, 0, 0);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (t + e < K) row[t + e] = v[e];
+    }
+}
+constexpr int V4 = 4, UB4 = 2;                  // elements per thread per access, accesses in flight
+
 template <typename T>
 __device__ inline T block_sum(T v, T* red) {
 #pragma unroll
@@ -31,19 +51,29 @@ __device__ inline T block_sum(T v, T* red) {
     return red[0] + red[1] + red[2] + red[3];
 }
 
-// row partials of shifted sums: ws[row] = (sum(p - s), sum((p - s)^2)), s = p(x[b, 0, 0])
-__global__ __launch_bounds__(THREADS) void stats_kernel(int C, int K, const float* __restrict__ x,
+// row partials of shifted sums: ws[row] = (sum(p - s), sum((p - s)^2)), s = p(x[b, 0, 0]); rows row0 + blockIdx.x
+__global__ __launch_bounds__(THREADS) void stats_kernel(int row0, int C, int K, const float* __restrict__ x,
                                                         const float* __restrict__ alpha, float2* __restrict__ ws) {
     __shared__ float red[4];
-    const int row = blockIdx.x, b = row / C;
+    const int row = row0 + (int)blockIdx.x, b = row / C;
     const float a = alpha[0];
     const float shift = prelu(x[(int64_t)b * C * K], a);
-    const float* xr = x + (int64_t)row * K;
+    const auto rx = make_rsrc(x + (int64_t)row * K, K);
     float s1 = 0.f, s2 = 0.f;
-    for (int t = threadIdx.x; t < K; t += THREADS) {
-        const float v = prelu(xr[t], a) - shift;
-        s1 += v;
-        s2 += v * v;
+    for (int t0 = 0; t0 < K; t0 += UB4 * V4 * THREADS) {
+        float4 xv[UB4];
+#pragma unroll
+        for (int j = 0; j < UB4; ++j) xv[j] = ld4(rx, t0 + (j * THREADS + (int)threadIdx.x) * V4);
+#pragma unroll
+        for (int j = 0; j < UB4; ++j) {
+            const int t = t0 + (j * THREADS + (int)threadIdx.x) * V4;
+#pragma unroll
+            for (int e = 0; e < V4; ++e) {
+                const float v = (t + e < K) ? prelu(f4at(xv[j], e), a) - shift : 0.f;
+                s1 += v;
+                s2 += v * v;
+            }
+        }
     }
     s1 = block_sum(s1, red);
     s2 = block_sum(s2, red);
@@ -83,69 +113,54 @@ __device__ inline float2 sample_stats(double2 sums, int C, int K, float shift, f
     return make_float2((float)(m1 + shift), (float)(1.0 / sqrt(var + (double)eps)));
 }
 
-// per sample: mean, rstd = 1/sqrt(var + EPS)
-__global__ void stats_finalize(int B, int C, int K, const float* __restrict__ x, const float* __restrict__ alpha,
-                               const float2* __restrict__ ws, float eps, float2* __restrict__ stats) {
-    __shared__ double red[8];
-    const int b = blockIdx.x;
-    const double2 sums = sample_sums(ws, b, C, red);
-    if (threadIdx.x == 0) stats[b] = sample_stats(sums, C, K, prelu(x[(int64_t)b * C * K], alpha[0]), eps);
-}
-
 // The backward's second pass walks the rows in reverse: its first rows are the ones the reduction pass read last,
 // still in the Infinity Cache / L2 when it starts ((y1, dy) of C4 is 262 MB against the 256 MB memory-side cache):
 // C4 dwconv_gln_bwd 0.193 -> 0.186 ms.  The forward's apply pass keeps the launch order (reversed it measured
 // 0.0965 -> 0.101 ms).
 __device__ inline int second_pass_row() { return gridDim.x - 1 - blockIdx.x; }
 
-__global__ __launch_bounds__(THREADS) void apply_kernel(int C, int K, const float* __restrict__ x,
-                                                        const float* __restrict__ alpha, const float* __restrict__ gamma,
-                                                        const float* __restrict__ beta, const float2* __restrict__ stats,
-                                                        float* __restrict__ y) {
-    const int row = blockIdx.x, b = row / C, c = row % C;
-    const float a = alpha[0];
-    const float2 st = stats[b];
-    const float g = gamma[c] * st.y, o = beta[c] - gamma[c] * st.y * st.x;
-    const float* xr = x + (int64_t)row * K;
-    float* yr = y + (int64_t)row * K;
-    for (int t = threadIdx.x; t < K; t += THREADS) yr[t] = g * prelu(xr[t], a) + o;
-}
-
 // apply with the finalize folded in: every row block re-derives its sample's statistics from the row partials (the
-// same sums in the same order as stats_finalize: bitwise equal), the channel-0 block stores them for the backward.
+// same sums in the same order in every block: bitwise equal), the channel-0 block stores them for the backward.
 // shift_src: the tensor whose (b, 0, 0) element defines the shift (y1 here)
-__global__ __launch_bounds__(THREADS) void apply_fused_kernel(int C, int K, const float* __restrict__ x,
+__global__ __launch_bounds__(THREADS) void apply_fused_kernel(int row0, int C, int K, const float* __restrict__ x,
                                                               const float* __restrict__ alpha,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta,
                                                               const float2* __restrict__ ws, float eps,
                                                               float2* __restrict__ stats, float* __restrict__ y) {
     __shared__ double red[8];
-    const int row = blockIdx.x, b = row / C, c = row % C;
+    const int row = row0 + (int)blockIdx.x, b = row / C, c = row % C;
     const float a = alpha[0];
     const float2 st = sample_stats(sample_sums(ws, b, C, red), C, K, prelu(x[(int64_t)b * C * K], a), eps);
     if (c == 0 && threadIdx.x == 0) stats[b] = st;
     const float g = gamma[c] * st.y, o = beta[c] - gamma[c] * st.y * st.x;
     const float* xr = x + (int64_t)row * K;
     float* yr = y + (int64_t)row * K;
-    for (int t = threadIdx.x; t < K; t += THREADS) yr[t] = g * prelu(xr[t], a) + o;
+    const auto rx = make_rsrc(xr, K), ry = make_rsrc(yr, K);
+    for (int t0 = 0; t0 < K; t0 += UB4 * V4 * THREADS) {
+        float4 xv[UB4];
+#pragma unroll
+        for (int jj = 0; jj < UB4; ++jj) xv[jj] = ld4(rx, t0 + (jj * THREADS + (int)threadIdx.x) * V4);
+#pragma unroll
+        for (int jj = 0; jj < UB4; ++jj) {
+            const int t = t0 + (jj * THREADS + (int)threadIdx.x) * V4;
+            float o4[4];
+#pragma unroll
+            for (int e = 0; e < V4; ++e) o4[e] = g * prelu(f4at(xv[jj], e), a) + o;
+            st4_row(ry, yr, t, K, o4);
+        }
+    }
 }
 
-typedef unsigned int u4_t __attribute__((ext_vector_type(4)));
-__device__ inline float4 ld4(__amdgpu_buffer_rsrc_t r, int voff_elems) {
-    const u4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff_elems * 4, 0, 0);
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ inline float f4at(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
 
 // backward pass 1: per row S1 = sum dy, S2 = sum dy * xhat.  4 consecutive elements per thread (dwordx4 loads, rows
 // need only dword alignment; the row's last partial quadruple is masked per element), 2 quadruples in flight
-__global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int C, int K, const float* __restrict__ x,
+__global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int row0, int C, int K, const float* __restrict__ x,
                                                              const float* __restrict__ alpha, const float2* __restrict__ stats,
                                                              const float* __restrict__ dy, float2* __restrict__ ws) {
     constexpr int V = 4, UB = 2;
     __shared__ float red[4];
-    const int row = blockIdx.x, b = row / C;
+    const int row = row0 + (int)blockIdx.x, b = row / C;
     const float a = alpha[0];
     const float2 st = stats[b];
     const auto rx = make_rsrc(x + (int64_t)row * K, K), rg = make_rsrc(dy + (int64_t)row * K, K);
@@ -219,27 +234,51 @@ __global__ void bwd_finalize(int B, int C, int K, const float2* __restrict__ ws,
     }
 }
 
-// backward pass 2: dx = (x > 0 ? 1 : a) * rstd * (dy*gamma - mean_g - xhat*mean_gxh); dalpha row partial
-__global__ __launch_bounds__(THREADS) void bwd_apply_kernel(int C, int K, const float* __restrict__ x,
+// backward pass 2: dx = (x > 0 ? 1 : a) * rstd * (dy*gamma - mean_g - xhat*mean_gxh); dalpha row partial.  The
+// sample's (mean_g, mean_gxh) re-derived per row block from the row partials (as dwconv_gln_bwd does), so a sample
+// group needs no finalize launch between its two passes
+__global__ __launch_bounds__(THREADS) void bwd_apply_kernel(int row0, int C, int K, const float* __restrict__ x,
                                                             const float* __restrict__ alpha, const float* __restrict__ gamma,
-                                                            const float2* __restrict__ stats, const float2* __restrict__ smeans,
+                                                            const float2* __restrict__ stats,
+                                                            const float2* __restrict__ ws_rows,
                                                             const float* __restrict__ dy, float* __restrict__ dx,
                                                             float* __restrict__ ws_alpha) {
     __shared__ float red[4];
-    const int row = second_pass_row(), b = row / C, c = row % C;
+    __shared__ double dred[8];
+    const int row = row0 + second_pass_row(), b = row / C, c = row % C;
     const float a = alpha[0];
-    const float2 st = stats[b], sm = smeans[b];
+    const float2 st = stats[b];
+    const double2 sg12 = sample_sums(ws_rows, b, C, dred, gamma);
+    const double nn = (double)C * K;
+    const float2 sm = make_float2((float)(sg12.x / nn), (float)(sg12.y / nn));
     const float gm = gamma[c];
     const float* xr = x + (int64_t)row * K;
     const float* gr = dy + (int64_t)row * K;
     float* dr = dx + (int64_t)row * K;
+    const auto rx = make_rsrc(xr, K), rg = make_rsrc(gr, K), rd = make_rsrc(dr, K);
     float da = 0.f;
-    for (int t = threadIdx.x; t < K; t += THREADS) {
-        const float xv = xr[t];
-        const float xh = (prelu(xv, a) - st.x) * st.y;
-        const float dp = st.y * (gr[t] * gm - sm.x - xh * sm.y);
-        dr[t] = xv > 0.f ? dp : a * dp;
-        da += xv > 0.f ? 0.f : dp * xv;
+    for (int t0 = 0; t0 < K; t0 += UB4 * V4 * THREADS) {
+        float4 xv[UB4], gv[UB4];
+#pragma unroll
+        for (int j = 0; j < UB4; ++j) {
+            const int t = t0 + (j * THREADS + (int)threadIdx.x) * V4;
+            xv[j] = ld4(rx, t);
+            gv[j] = ld4(rg, t);
+        }
+#pragma unroll
+        for (int j = 0; j < UB4; ++j) {
+            const int t = t0 + (j * THREADS + (int)threadIdx.x) * V4;
+            float o4[4];
+#pragma unroll
+            for (int e = 0; e < V4; ++e) {
+                const float xvv = f4at(xv[j], e);
+                const float xh = (prelu(xvv, a) - st.x) * st.y;
+                const float dp = st.y * (f4at(gv[j], e) * gm - sm.x - xh * sm.y);
+                o4[e] = xvv > 0.f ? dp : a * dp;
+                da += (xvv > 0.f || t + e >= K) ? 0.f : dp * xvv;
+            }
+            st4_row(rd, dr, t, K, o4);
+        }
     }
     da = block_sum(da, red);
     if (threadIdx.x == 0) ws_alpha[row] = da;
@@ -268,7 +307,7 @@ __global__ void alpha_finalize(int rows, const float* __restrict__ ws_alpha, flo
 constexpr int DW_MAXP = 7, DW_MAXHALO = 512;
 
 template <int P>
-__global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int C, int K, int dil, const float* __restrict__ x,
+__global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int row0, int C, int K, int dil, const float* __restrict__ x,
                                                                const float* __restrict__ w,
                                                                const float* __restrict__ alpha, float* __restrict__ y1,
                                                                float2* __restrict__ ws) {
@@ -276,7 +315,7 @@ __global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int C, int K, int
     // cache lines this workgroup just brought in (each x line leaves HBM once); the same k-ordered sums as the tiled
     // form (bitwise equal y1, same per-thread element order for the statistics)
     __shared__ float red[4];
-    const int row = blockIdx.x, b = row / C, c = row % C;
+    const int row = row0 + (int)blockIdx.x, b = row / C, c = row % C;
     const int halo = (P - 1) / 2 * dil;
     const float a = alpha[0];
     const float* xr = x + (int64_t)row * K;
@@ -323,7 +362,7 @@ __global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int C, int K, int
 }
 
 template <int P>
-__global__ __launch_bounds__(THREADS) void dwconv_gln_bwd_kernel(int C, int K, int dil, const float* __restrict__ x,
+__global__ __launch_bounds__(THREADS) void dwconv_gln_bwd_kernel(int row0, int C, int K, int dil, const float* __restrict__ x,
                                                                  const float* __restrict__ w, const float* __restrict__ y1,
                                                                  const float* __restrict__ alpha,
                                                                  const float* __restrict__ gamma,
@@ -336,7 +375,7 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd_kernel(int C, int K, i
     // PReLU-slope partials
     __shared__ float red[THREADS / 64][DW_MAXP + 1];
     __shared__ double dred[8];
-    const int row = second_pass_row(), b = row / C, c = row % C;
+    const int row = row0 + second_pass_row(), b = row / C, c = row % C;
     const int halo = (P - 1) / 2 * dil;
     const float a = alpha[0];
     const float2 st = stats[b];
@@ -410,7 +449,7 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd_kernel(int C, int K, i
 // buffer range check): 4x fewer VMEM instructions than the scalar form, which was VMEM-issue bound (10 dword
 // accesses per element: 3 taps of y1 and dy, 3 of x, the dx store).  Same per-element arithmetic and tap order.
 template <int P>
-__global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int C, int K, int dil, const float* __restrict__ x,
+__global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int C, int K, int dil, const float* __restrict__ x,
                                                                   const float* __restrict__ w, const float* __restrict__ y1,
                                                                   const float* __restrict__ alpha,
                                                                   const float* __restrict__ gamma,
@@ -421,7 +460,7 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int C, int K, 
     constexpr int V = 4, UB = 2;                  // 4 consecutive elements per thread, 2 quadruples in flight
     __shared__ float red[THREADS / 64][DW_MAXP + 1];
     __shared__ double dred[8];
-    const int row = second_pass_row(), b = row / C, c = row % C;
+    const int row = row0 + second_pass_row(), b = row / C, c = row % C;
     const int halo = (P - 1) / 2 * dil;
     const float a = alpha[0];
     const float2 st = stats[b];
@@ -580,6 +619,15 @@ __global__ void dw_tail_kernel(const float* __restrict__ ws_dw, const float2* __
 
 using namespace avse::gln;
 
+// samples per launch group of the two-pass PReLU -> gLN kernels (fused dwconv or not): the group's two fp32 tensors a pass pair re-reads
+// (fwd: y1; bwd: y1, dy) plus what streams past them stay well inside the 256 MB Infinity Cache (<= ~64 MB per
+// re-read tensor pair), split evenly; one group when everything fits anyway
+static int sample_group(int64_t B, int64_t C, int64_t K) {
+    const int64_t per = 8 * C * K;                          // bytes of two fp32 (C, K) tensors of one sample
+    const int64_t ngroups = std::max<int64_t>(1, (B * per + (64LL << 20) - 1) / (64LL << 20));
+    return (int)((B + ngroups - 1) / ngroups);
+}
+
 extern "C" {
 
 int64_t avse_prelu_gln_workspace_bytes(int64_t B, int64_t C) { return 8 * B * C + 4 * B * C + 16 * B; }
@@ -589,16 +637,19 @@ int avse_prelu_gln_fwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     if (!x || !alpha || !gamma || !beta || !y || !stats || !workspace) return AVSE_EINVAL;
     if (B <= 0 || C <= 0 || K <= 0 || B * C > (1LL << 31) - 1) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
-    const unsigned rows = (unsigned)(B * C);
     float2* ws = (float2*)workspace;
-    hipLaunchKernelGGL(stats_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, x, alpha, ws);
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(stats_finalize, dim3((unsigned)B), dim3(256), 0, st, (int)B, (int)C, (int)K, x, alpha, ws, eps,
-                       (float2*)stats);
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(apply_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, x, alpha, gamma, beta,
-                       (const float2*)stats, y);
-    AVSE_CHECK_LAUNCH();
+    // per sample group: row statistics, then the apply pass with the finalize folded in; its second read of x finds
+    // the group's lines in the Infinity Cache
+    const int gsz = sample_group(B, C, K);
+    for (int64_t b0 = 0; b0 < B; b0 += gsz) {
+        const int row0 = (int)(b0 * C);
+        const unsigned rows = (unsigned)(std::min<int64_t>(gsz, B - b0) * C);
+        hipLaunchKernelGGL(stats_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, ws);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
+                           beta, (const float2*)ws, eps, (float2*)stats, y);
+        AVSE_CHECK_LAUNCH();
+    }
     return AVSE_OK;
 }
 
@@ -608,21 +659,27 @@ int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     if (!x || !alpha || !gamma || !stats || !dy || !dx || !dalpha || !dgamma || !dbeta || !workspace) return AVSE_EINVAL;
     if (B <= 0 || C <= 0 || K <= 0 || B * C > (1LL << 31) - 1) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
-    const unsigned rows = (unsigned)(B * C);
+    const unsigned all_rows = (unsigned)(B * C);
     float2* ws = (float2*)workspace;
     float* ws_a = (float*)(ws + B * C);
     float2* smeans = (float2*)(ws_a + B * C);
-    hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, x, alpha,
-                       (const float2*)stats, dy, ws);
-    AVSE_CHECK_LAUNCH();
+    const int gsz = sample_group(B, C, K);
+    for (int64_t b0 = 0; b0 < B; b0 += gsz) {
+        const int row0 = (int)(b0 * C);
+        const unsigned rows = (unsigned)(std::min<int64_t>(gsz, B - b0) * C);
+        hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha,
+                           (const float2*)stats, dy, ws);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(bwd_apply_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
+                           (const float2*)stats, (const float2*)ws, dy, dx, ws_a);
+        AVSE_CHECK_LAUNCH();
+    }
+    // dgamma / dbeta (sum over samples of the row partials) and the PReLU slope, after every group
     const unsigned cblocks = (unsigned)((C + 255) / 256);
     hipLaunchKernelGGL(bwd_finalize, dim3((unsigned)B + cblocks), dim3(256), 0, st, (int)B, (int)C, (int)K, ws, gamma,
                        smeans, dgamma, dbeta);
     AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(bwd_apply_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, x, alpha, gamma,
-                       (const float2*)stats, smeans, dy, dx, ws_a);
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(alpha_finalize, dim3(1), dim3(256), 0, st, (int)rows, ws_a, dalpha);
+    hipLaunchKernelGGL(alpha_finalize, dim3(1), dim3(256), 0, st, (int)all_rows, ws_a, dalpha);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
@@ -654,16 +711,22 @@ int avse_dwconv_gln_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     if (!x || !w || !alpha || !gamma || !beta || !y1 || !y || !stats || !workspace) return AVSE_EINVAL;
     if (int rc = dw_check(B, C, K, P, dil)) return rc;
     hipStream_t st = (hipStream_t)stream;
-    const unsigned rows = (unsigned)(B * C);
     float2* ws = (float2*)workspace;
-#define L_(PP) hipLaunchKernelGGL(dwconv_stats_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, (int)dil, \
-                                  x, w, alpha, y1, ws)
-    AVSE_DW_P_SWITCH(P, L_)
+    // sample groups (gLN statistics are per sample): the apply pass of a group runs right after its stats pass, so
+    // the y1 it reads was written a group ago and is served by the 256 MB Infinity Cache, not HBM
+    const int gsz = sample_group(B, C, K);
+    for (int64_t b0 = 0; b0 < B; b0 += gsz) {
+        const int row0 = (int)(b0 * C);
+        const unsigned rows = (unsigned)(std::min<int64_t>(gsz, B - b0) * C);
+#define L_(PP) hipLaunchKernelGGL(dwconv_stats_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, \
+                                  (int)dil, x, w, alpha, y1, ws)
+        AVSE_DW_P_SWITCH(P, L_)
 #undef L_
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, y1, alpha, gamma, beta,
-                       (const float2*)ws, eps, (float2*)stats, y);
-    AVSE_CHECK_LAUNCH();
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha, gamma,
+                           beta, (const float2*)ws, eps, (float2*)stats, y);
+        AVSE_CHECK_LAUNCH();
+    }
     return AVSE_OK;
 }
 
@@ -679,21 +742,30 @@ int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     float2* ws = (float2*)workspace;
     float* ws_a = (float*)(ws + B * C);
     float* ws_dw = (float*)((float2*)(ws_a + B * C) + B);
-    hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, y1, alpha,
-                       (const float2*)stats, dy, ws);
-    AVSE_CHECK_LAUNCH();
-#define L_(PP) hipLaunchKernelGGL(dwconv_gln_bwd_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, (int)dil, \
-                                  x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, ws_a)
-#define L4_(PP) hipLaunchKernelGGL(dwconv_gln_bwd4_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, (int)C, (int)K, (int)dil, \
-                                   x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, ws_a)
-    if (dil % 4 == 0) {
-        AVSE_DW_P_SWITCH(P, L4_)
-    } else {
-        AVSE_DW_P_SWITCH(P, L_)
-    }
+    // sample groups: the (y1, dy) lines the fused pass re-reads were read by the group's reduction pass just before
+    // (it walks the group's rows in reverse, most recent first), so they come from the Infinity Cache
+    const int gsz = sample_group(B, C, K);
+    for (int64_t b0 = 0; b0 < B; b0 += gsz) {
+        const int row0 = (int)(b0 * C);
+        const unsigned rows = (unsigned)(std::min<int64_t>(gsz, B - b0) * C);
+        hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha,
+                           (const float2*)stats, dy, ws);
+        AVSE_CHECK_LAUNCH();
+#define L_(PP) hipLaunchKernelGGL(dwconv_gln_bwd_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, \
+                                  (int)dil, x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, \
+                                  ws_a)
+#define L4_(PP) hipLaunchKernelGGL(dwconv_gln_bwd4_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, \
+                                   (int)dil, x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, \
+                                   ws_dw, ws_a)
+        if (dil % 4 == 0) {
+            AVSE_DW_P_SWITCH(P, L4_)
+        } else {
+            AVSE_DW_P_SWITCH(P, L_)
+        }
 #undef L_
 #undef L4_
-    AVSE_CHECK_LAUNCH();
+        AVSE_CHECK_LAUNCH();
+    }
     const int n = (int)(C * P + C);
     hipLaunchKernelGGL(dw_tail_kernel, dim3(1 + (n + 255) / 256), dim3(256), 0, st, ws_dw, (const float2*)ws, ws_a,
                        (int)B, (int)C, (int)P, dw, dgamma, dbeta, dalpha);

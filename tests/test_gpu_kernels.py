@@ -572,9 +572,10 @@ def test_encoder_decoder_framing_gemm_vs_golden():
 
 # ------------------------------------------------------------------ avse4 TCN: fused PReLU->gLN, depthwise dilated conv1d
 
-@pytest.mark.parametrize("shape", [(2, 256, 300), (1, 512, 4001), (3, 8, 1), (2, 64, 2049)])
+@pytest.mark.parametrize("shape", [(2, 256, 300), (1, 512, 4001), (3, 8, 1), (2, 64, 2049), (6, 512, 4001)])
 def test_prelu_gln_vs_fp64(shape):
-    """gLN(PReLU(x)) of baseline/avse4/model.py:225-252 (eps 1e-8) vs the fp64 oracle; fwd + all grads."""
+    """gLN(PReLU(x)) of baseline/avse4/model.py:225-252 (eps 1e-8) vs the fp64 oracle; fwd + all grads.  (6, 512, 4001)
+    runs as two sample groups of 3 (csrc/gln.hip sample_group: > 64 MB of a pass pair's re-read tensors)."""
     from avse_challenge_amd.layers import prelu_gln
     from oracle.avse4_ref import GlobalLayerNorm
     C = shape[1]
@@ -857,7 +858,8 @@ def test_lstm_group_not_coresident_raises():
 # ------------------------------------------------------------------ fused dwconv <-> PReLU -> gLN (avse4 TCN)
 
 @pytest.mark.parametrize("B,C,Kn,P,dil", [(2, 512, 3999, 3, 128), (3, 64, 300, 3, 4), (2, 40, 2500, 3, 1), (1, 8, 17, 5, 2),
-                                          (2, 16, 5000, 3, 256), (2, 24, 1001, 5, 4), (1, 8, 13, 3, 4), (2, 8, 2050, 7, 64)])
+                                          (2, 16, 5000, 3, 256), (2, 24, 1001, 5, 4), (1, 8, 13, 3, 4), (2, 8, 2050, 7, 64),
+                                          (6, 512, 3999, 3, 128)])
 def test_dwconv_prelu_gln_fused_vs_fp64(B, C, Kn, P, dil):
     """layers.dwconv_prelu_gln (two fused passes each way) vs the fp64 composition of the reference ops
     (model.py:278-292: depthwise conv1d, PReLU, gLN with EPS 1e-8 inside the sqrt): output and the gradients of
