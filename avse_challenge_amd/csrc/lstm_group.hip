@@ -36,7 +36,9 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
 constexpr int MAXG = 16, MAXU = 64, MAXH = 512;
-constexpr unsigned SPIN_MAX = 1u << 22;           // ~ seconds of polling before giving up
+// a hand-off wait gives up after 1 s of the 100 MHz realtime counter (a legitimate wait is one step, microseconds, or
+// at most the time other work holds CUs the group still needs)
+constexpr uint64_t WAIT_TICKS = 100000000ull;
 
 // hardware exp / rcp (a few ulp; the step's dot products carry more rounding than that)
 __device__ inline float sigm(float x) { return fast_rcp(1.f + fast_exp(-x)); }
@@ -52,6 +54,7 @@ template <int NK, typename Idx, typename Out>
 __device__ inline bool sweep(const gu64* g, unsigned tag, gu32* status, gu32* errflag, Idx idx, Out out) {
     const int lane = threadIdx.x & 63;
     unsigned long long v[NK];
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     for (unsigned spins = 0;; ++spins) {
         bool ok = true;
 #pragma unroll
@@ -65,7 +68,7 @@ __device__ inline bool sweep(const gu64* g, unsigned tag, gu32* status, gu32* er
         if (__all(ok)) break;
         if ((spins & 63) == 63) {
             const unsigned st = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (st != 0u || spins >= SPIN_MAX) {
+            if (st != 0u || __builtin_amdgcn_s_memrealtime() - t_start > WAIT_TICKS) {
                 if (st == 0u && lane == 0) {
                     __hip_atomic_store(status, 0x71000000u + tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(errflag, 0x71000000u + tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -818,7 +818,7 @@ occ = ctypes.CDLL(os.path.join(sys.argv[1], "tests", "hip", "libocc.so"))
 ncu = torch.cuda.get_device_properties(0).multi_processor_count
 arrived = torch.zeros(1, dtype=torch.int32, device="cuda")
 hog = torch.cuda.Stream()
-assert occ.occupy_cus(ncu - 4, ctypes.c_void_p(arrived.data_ptr()), ctypes.c_double(8.0),
+assert occ.occupy_cus(ncu - 4, ctypes.c_void_p(arrived.data_ptr()), ctypes.c_double(4.0),
                       ctypes.c_void_p(hog.cuda_stream)) == 0
 side = torch.cuda.Stream()
 t = time.time()
@@ -840,7 +840,7 @@ print(json.dumps({"raised": raised, "held": held, "ncu": ncu, "s": time.time() -
 
 def test_lstm_group_not_coresident_raises():
     """A grouped LSTM launch whose workgroups cannot all be resident — a bounded test kernel (tests/hip/occupy.hip)
-    holds all CUs but 4 with 160 KB of LDS each for 8 s (longer than the kernel's bounded spin), so only 4 of a sequence's 8 workgroups can run — times out its
+    holds all CUs but 4 with 160 KB of LDS each for 4 s (longer than the kernel's 1 s bound on a hand-off wait), so only 4 of a sequence's 8 workgroups can run — times out its
     hand-offs (bounded spins) and the host raises HipKernelError: the outputs are never returned as valid."""
     import json
     import subprocess

@@ -8,16 +8,19 @@ name=$1; patch=${2:-}; flags=${3:-}
 root=$(cd "$(dirname "$0")/.." && pwd)
 src=$root/build/exp/$name/src
 out=$root/build/exp/$name
-rm -rf "$src"; mkdir -p "$src" "$root/expso"
-cp -r "$root/avse_challenge_amd/csrc" "$root/include" "$src/"
+rm -rf "$src"; mkdir -p "$src/avse_challenge_amd" "$root/expso"
+cp -r "$root/avse_challenge_amd/csrc" "$src/avse_challenge_amd/"      # same relative layout: common.h includes
+cp -r "$root/include" "$src/"                                        # ../../include/avse_hip.h
 if [ -n "$patch" ]; then
-    (cd "$src" && sed -e 's#avse_challenge_amd/csrc/#csrc/#g' "$root/$patch" | patch -p1)
+    (cd "$src" && patch -p1 < "$root/$patch")
 fi
-for f in "$src"/csrc/*.hip; do
+status=0
+for f in "$src"/avse_challenge_amd/csrc/*.hip; do
     extra=""; [ "$(basename "$f")" = scan.hip ] && extra="-fno-slp-vectorize"    # as the Makefile builds it
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w -I"$src/include" $extra $flags -c "$f" \
         -o "$out/$(basename "$f" .hip).o" &
 done
-wait
+for j in $(jobs -p); do wait "$j" || status=1; done
+[ $status -eq 0 ] || { echo "compile failed"; exit 1; }
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/expso/$name.so" "$out"/*.o
 echo "built expso/$name.so"
