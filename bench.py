@@ -186,10 +186,15 @@ class Avse1Step:
         from avse_challenge_amd import kernels as K
         cl = torch.channels_last
         flops = 2.0 * self.B * 64 * 64 * 25 * 376 * 257
+        mark = bool(int(os.environ.get("AVSE_PROFILE_MARK", "0")))    # tools/ktrace_window.py OUT_ROOF.csv
         K.LAUNCH_TAPS["avse_dconv_wgrad"] = taps = []
         try:
+            if mark:
+                torch.cuda._sleep(1000)
             for _ in range(3):
                 self.loss().backward()
+            if mark:
+                torch.cuda._sleep(1000)
             torch.cuda.synchronize()
         finally:
             K.LAUNCH_TAPS.pop("avse_dconv_wgrad", None)

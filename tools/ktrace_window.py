@@ -1,10 +1,12 @@
 """Per-kernel summary of the timed steps only: reads a rocprofv3 kernel_trace.csv, keeps the kernels
 between the two marker kernels bench.py launches when AVSE_PROFILE_MARK=1 (torch.cuda._sleep -> spin_kernel), and
 prints / writes the same columns as rocprofv3's kernel_stats.csv.
-usage: ktrace_window.py TRACE.csv STEPS OUT_STATS.csv [OUT_POST.csv]
+usage: ktrace_window.py TRACE.csv STEPS OUT_STATS.csv [OUT_POST.csv [OUT_ROOF.csv]]
 OUT_POST.csv: the same summary for the kernels after the second marker -- bench.py's isolated roofline /
 roofline_hip measurements, which run after the timed steps (their averages are the live numbers' counterpart;
-the whole-run rocprof average mixes them with the in-step calls, which overlap the avse1 lip stream)."""
+the whole-run rocprof average mixes them with the in-step calls, which overlap the avse1 lip stream).
+OUT_ROOF.csv: with the avse1 workload's in-step roofline (bench.py Avse1Step.roofline brackets its 3 eager train
+steps with markers 3 and 4), the summary of those steps: the kernel averages the line's `roofline.avg_ms` is."""
 import csv
 import sys
 from collections import defaultdict
@@ -19,7 +21,7 @@ rows.sort()
 marks = [i for i, r in enumerate(rows) if "spin_kernel" in r[2]]
 if len(marks) < 2:
     sys.exit(f"expected 2 marker kernels, found {len(marks)}")
-win = rows[marks[-2] + 1:marks[-1]]
+win = rows[marks[0] + 1:marks[1]]
 
 
 def write_stats(sel, path):
@@ -38,6 +40,9 @@ def write_stats(sel, path):
 tot = write_stats(win, out)
 span = win[-1][1] - win[0][0]
 if post_out:
-    write_stats(rows[marks[-1] + 1:], post_out)
+    write_stats(rows[marks[1] + 1:], post_out)
+roof_out = sys.argv[5] if len(sys.argv) > 5 else None
+if roof_out and len(marks) >= 4:
+    write_stats(rows[marks[2] + 1:marks[3]], roof_out)
 print(f"timed window: {span / 1e6:.2f} ms wall, {tot / 1e6:.2f} ms kernel busy "
       f"({tot / 1e6 / steps:.2f} ms/step over {steps:g} steps, {len(win)} launches)")
