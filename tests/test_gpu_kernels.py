@@ -820,7 +820,7 @@ arrived = torch.zeros(1, dtype=torch.int32, device="cuda")
 hog = torch.cuda.Stream()
 assert occ.occupy_cus(ncu - 4, ctypes.c_void_p(arrived.data_ptr()), ctypes.c_double(4.0),
                       ctypes.c_void_p(hog.cuda_stream)) == 0
-side = torch.cuda.Stream()
+side = torch.cuda.Stream(priority=-1)    # a high-priority stream: its own hardware queue, not behind the hog's
 t = time.time()
 with torch.cuda.stream(side):
     while int(arrived.item()) < ncu - 4 and time.time() - t < 3.0:   # the hog holds all CUs but 4
