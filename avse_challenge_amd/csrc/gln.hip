@@ -619,15 +619,6 @@ __global__ void dw_tail_kernel(const float* __restrict__ ws_dw, const float2* __
 
 using namespace avse::gln;
 
-// samples per launch group of the two-pass PReLU -> gLN kernels (fused dwconv or not): the group's two fp32 tensors a pass pair re-reads
-// (fwd: y1; bwd: y1, dy) plus what streams past them stay well inside the 256 MB Infinity Cache (<= ~64 MB per
-// re-read tensor pair), split evenly; one group when everything fits anyway
-static int sample_group(int64_t B, int64_t C, int64_t K) {
-    (void)C;
-    (void)K;
-    return (int)B;      // one group: 4 groups of 4 samples measured slower at C4 (profiles/r04e_gln_ab.txt)
-}
-
 extern "C" {
 
 int64_t avse_prelu_gln_workspace_bytes(int64_t B, int64_t C) { return 8 * B * C + 4 * B * C + 16 * B; }
@@ -638,18 +629,14 @@ int avse_prelu_gln_fwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     if (B <= 0 || C <= 0 || K <= 0 || B * C > (1LL << 31) - 1) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     float2* ws = (float2*)workspace;
-    // per sample group: row statistics, then the apply pass with the finalize folded in; its second read of x finds
-    // the group's lines in the Infinity Cache
-    const int gsz = sample_group(B, C, K);
-    for (int64_t b0 = 0; b0 < B; b0 += gsz) {
-        const int row0 = (int)(b0 * C);
-        const unsigned rows = (unsigned)(std::min<int64_t>(gsz, B - b0) * C);
-        hipLaunchKernelGGL(stats_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, ws);
-        AVSE_CHECK_LAUNCH();
-        hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
-                           beta, (const float2*)ws, eps, (float2*)stats, y);
-        AVSE_CHECK_LAUNCH();
-    }
+    // row statistics, then the apply pass with the finalize folded in (no finalize launch between them)
+    const int row0 = 0;
+    const unsigned rows = (unsigned)(B * C);
+    hipLaunchKernelGGL(stats_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, ws);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
+                       beta, (const float2*)ws, eps, (float2*)stats, y);
+    AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
 
@@ -663,18 +650,15 @@ int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     float2* ws = (float2*)workspace;
     float* ws_a = (float*)(ws + B * C);
     float2* smeans = (float2*)(ws_a + B * C);
-    const int gsz = sample_group(B, C, K);
-    for (int64_t b0 = 0; b0 < B; b0 += gsz) {
-        const int row0 = (int)(b0 * C);
-        const unsigned rows = (unsigned)(std::min<int64_t>(gsz, B - b0) * C);
-        hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha,
-                           (const float2*)stats, dy, ws);
-        AVSE_CHECK_LAUNCH();
-        hipLaunchKernelGGL(bwd_apply_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
-                           (const float2*)stats, (const float2*)ws, dy, dx, ws_a);
-        AVSE_CHECK_LAUNCH();
-    }
-    // dgamma / dbeta (sum over samples of the row partials) and the PReLU slope, after every group
+    const int row0 = 0;
+    const unsigned rows = (unsigned)(B * C);
+    hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha,
+                       (const float2*)stats, dy, ws);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bwd_apply_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
+                       (const float2*)stats, (const float2*)ws, dy, dx, ws_a);
+    AVSE_CHECK_LAUNCH();
+    // dgamma / dbeta (sum over samples of the row partials) and the PReLU slope
     const unsigned cblocks = (unsigned)((C + 255) / 256);
     hipLaunchKernelGGL(bwd_finalize, dim3((unsigned)B + cblocks), dim3(256), 0, st, (int)B, (int)C, (int)K, ws, gamma,
                        smeans, dgamma, dbeta);
@@ -712,21 +696,16 @@ int avse_dwconv_gln_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     if (int rc = dw_check(B, C, K, P, dil)) return rc;
     hipStream_t st = (hipStream_t)stream;
     float2* ws = (float2*)workspace;
-    // sample groups (gLN statistics are per sample): the apply pass of a group runs right after its stats pass, so
-    // the y1 it reads was written a group ago and is served by the 256 MB Infinity Cache, not HBM
-    const int gsz = sample_group(B, C, K);
-    for (int64_t b0 = 0; b0 < B; b0 += gsz) {
-        const int row0 = (int)(b0 * C);
-        const unsigned rows = (unsigned)(std::min<int64_t>(gsz, B - b0) * C);
+    const int row0 = 0;
+    const unsigned rows = (unsigned)(B * C);
 #define L_(PP) hipLaunchKernelGGL(dwconv_stats_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, \
-                                  (int)dil, x, w, alpha, y1, ws)
-        AVSE_DW_P_SWITCH(P, L_)
+                              (int)dil, x, w, alpha, y1, ws)
+    AVSE_DW_P_SWITCH(P, L_)
 #undef L_
-        AVSE_CHECK_LAUNCH();
-        hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha, gamma,
-                           beta, (const float2*)ws, eps, (float2*)stats, y);
-        AVSE_CHECK_LAUNCH();
-    }
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha, gamma,
+                       beta, (const float2*)ws, eps, (float2*)stats, y);
+    AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
 
@@ -742,30 +721,24 @@ int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     float2* ws = (float2*)workspace;
     float* ws_a = (float*)(ws + B * C);
     float* ws_dw = (float*)((float2*)(ws_a + B * C) + B);
-    // sample groups: the (y1, dy) lines the fused pass re-reads were read by the group's reduction pass just before
-    // (it walks the group's rows in reverse, most recent first), so they come from the Infinity Cache
-    const int gsz = sample_group(B, C, K);
-    for (int64_t b0 = 0; b0 < B; b0 += gsz) {
-        const int row0 = (int)(b0 * C);
-        const unsigned rows = (unsigned)(std::min<int64_t>(gsz, B - b0) * C);
-        hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha,
-                           (const float2*)stats, dy, ws);
-        AVSE_CHECK_LAUNCH();
+    const int row0 = 0;
+    hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha,
+                       (const float2*)stats, dy, ws);
+    AVSE_CHECK_LAUNCH();
 #define L_(PP) hipLaunchKernelGGL(dwconv_gln_bwd_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, \
-                                  (int)dil, x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, \
-                                  ws_a)
+                              (int)dil, x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, \
+                              ws_a)
 #define L4_(PP) hipLaunchKernelGGL(dwconv_gln_bwd4_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, \
-                                   (int)dil, x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, \
-                                   ws_dw, ws_a)
-        if (dil % 4 == 0) {
-            AVSE_DW_P_SWITCH(P, L4_)
-        } else {
-            AVSE_DW_P_SWITCH(P, L_)
-        }
+                               (int)dil, x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, \
+                               ws_dw, ws_a)
+    if (dil % 4 == 0) {
+        AVSE_DW_P_SWITCH(P, L4_)
+    } else {
+        AVSE_DW_P_SWITCH(P, L_)
+    }
 #undef L_
 #undef L4_
-        AVSE_CHECK_LAUNCH();
-    }
+    AVSE_CHECK_LAUNCH();
     const int n = (int)(C * P + C);
     hipLaunchKernelGGL(dw_tail_kernel, dim3(1 + (n + 255) / 256), dim3(256), 0, st, ws_dw, (const float2*)ws, ws_a,
                        (int)B, (int)C, (int)P, dw, dgamma, dbeta, dalpha);

@@ -574,8 +574,8 @@ def test_encoder_decoder_framing_gemm_vs_golden():
 
 @pytest.mark.parametrize("shape", [(2, 256, 300), (1, 512, 4001), (3, 8, 1), (2, 64, 2049), (6, 512, 4001)])
 def test_prelu_gln_vs_fp64(shape):
-    """gLN(PReLU(x)) of baseline/avse4/model.py:225-252 (eps 1e-8) vs the fp64 oracle; fwd + all grads.  (6, 512, 4001)
-    runs as two sample groups of 3 (csrc/gln.hip sample_group: > 64 MB of a pass pair's re-read tensors)."""
+    """gLN(PReLU(x)) of baseline/avse4/model.py:225-252 (eps 1e-8) vs the fp64 oracle; fwd + all grads (K = 1, odd K:
+    the vectorized passes' partial last quadruple)."""
     from avse_challenge_amd.layers import prelu_gln
     from oracle.avse4_ref import GlobalLayerNorm
     C = shape[1]
