@@ -795,7 +795,12 @@ def lstm_group_status(device=None):
     """0 when every grouped LSTM launch on `device` (default: all used devices) since the last reset completed its
     hand-offs; else the timeout code one of them wrote (0x71000000 + step): a sequence's workgroups were not
     co-resident and that launch's outputs are invalid.  Synchronises with the flag's device."""
-    flags = _ERROR_FLAGS.values() if device is None else         [f for i, f in _ERROR_FLAGS.items() if i == torch.device(device).index]
+    if device is None:
+        flags = list(_ERROR_FLAGS.values())
+    else:
+        idx = torch.device(device).index
+        idx = torch.cuda.current_device() if idx is None else idx
+        flags = [f for i, f in _ERROR_FLAGS.items() if i == idx]
     return max([int(f.item()) & 0xFFFFFFFF for f in flags] + [0])
 
 
