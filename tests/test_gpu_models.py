@@ -363,6 +363,59 @@ def test_avse4_full_train_step_vs_oracle():
         assert e_gpu <= max(3 * e_torch, floor) and cos > 1 - 1e-4, (k, e_gpu, e_torch, float(cos))
 
 
+def test_avse4_full_train_step_vs_masked_oracle():
+    """The reduced AVSE4BaselineModule train step (lip front-end included) vs the fp64 oracle with OUR activation
+    masks imposed (tests/avse4_parity.py): every sign disagreement at a rounding-level pre-activation; loss within
+    1e-5; per parameter the max error relative to the masked fp64 gradient's max within max(3x the stock PyTorch-ROCm
+    fp32 oracle run's, 10x the fp32 CPU oracle run's (both vs the unmasked fp64 truth, their own flips included),
+    1e-3); cosine > 1 - 1e-6.  Replaces the 1e-2 .. 1e-1 floors of test_avse4_full_train_step_vs_oracle with a bar that
+    separates fp32 error from sign flips."""
+    from avse4_parity import capture_masks, check_flips, impose_masks
+    from avse_challenge_amd import avse4
+    from oracle import avse4_ref
+    from oracle.losses_ref import avse4_loss
+    kw = dict(N=64, L=40, B=64, H=128, P=3, X=3, R=2, C=2)
+    batch = {"noisy_audio": 0.1 * det_input((2, 2, 8000), 611), "vis_feat": det_input((2, 1, 13, 112, 112), 612, "uniform"),
+             "clean": 0.1 * det_input((2, 2, 8000), 613)}
+    bg = {k: v.to(DEV) for k, v in batch.items()}
+    b64 = {k: v.double() for k, v in batch.items()}
+    ours = det_init_(avse4.AVSE4BaselineModule(num_channels=2, **kw), 61).to(DEV).train()
+    with capture_masks(ours) as masks:
+        loss = ours.training_step(bg)
+    loss.backward()
+    ref64 = det_init_(avse4_ref.AVSE4BaselineModule(num_channels=2, **kw), 61).double().train()
+    flips = {}
+    remove = impose_masks(ref64, masks, flips)
+    l64 = avse4_loss(b64["clean"], ref64.model(b64["noisy_audio"], ref64.visual_frontend(b64["vis_feat"])))
+    l64.backward()
+    remove()
+    n_flips = check_flips(flips)
+    assert len(flips) >= 30, sorted(flips)               # every site took its mask (front-end, ResNet, TCN, visual)
+    close(loss, l64, 1e-5 * max(1.0, abs(float(l64))), 0, "loss")
+    ref64u = det_init_(avse4_ref.AVSE4BaselineModule(num_channels=2, **kw), 61).double().train()
+    avse4_loss(b64["clean"], ref64u.model(b64["noisy_audio"], ref64u.visual_frontend(b64["vis_feat"]))).backward()
+    tg = det_init_(avse4_ref.AVSE4BaselineModule(num_channels=2, **kw), 61).to(DEV).train()
+    tg.cal_loss(bg).backward()
+    c32 = det_init_(avse4_ref.AVSE4BaselineModule(num_channels=2, **kw), 61).train()
+    c32.cal_loss(batch).backward()
+    pm, pu = dict(ref64.named_parameters()), dict(ref64u.named_parameters())
+    pt, pc = dict(tg.named_parameters()), dict(c32.named_parameters())
+    worst = []
+    for k, p in ours.named_parameters():
+        q = pm[k].grad
+        if q is None:                                  # layer1.downsample: unused at stride 1 (utils.py:62)
+            assert p.grad is None, k
+            continue
+        scale, scale_u = max(1e-12, float(q.abs().max())), max(1e-12, float(pu[k].grad.abs().max()))
+        e = float((p.grad.double().cpu() - q).abs().max()) / scale
+        e_tg = float((pt[k].grad.double().cpu() - pu[k].grad).abs().max()) / scale_u
+        e_c = float((pc[k].grad.double() - pu[k].grad).abs().max()) / scale_u
+        cos = float(torch.nn.functional.cosine_similarity(p.grad.double().cpu().reshape(-1), q.reshape(-1), 0))
+        worst.append((e, k))
+        assert e <= max(3 * e_tg, 10 * e_c, 1e-3) and cos > 1 - 1e-6, (k, e, e_tg, e_c, cos)
+    print(f"avse4 masked: {n_flips} rounding-level flips; worst {sorted(worst, reverse=True)[:3]}")
+
+
 def test_bench_trainer_graph_replay_equals_eager():
     """bench.Trainer: a step replayed from the captured HIP graphs == the same step launched eagerly."""
     import bench
