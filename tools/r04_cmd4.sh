@@ -1,6 +1,6 @@
 mkdir -p gpurun_out; export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 200 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_models.py -x -v -s -m gpu -k "error_flag or avse4_full_train_step_vs_masked" --timeout 150 --timeout-method thread > gpurun_out/r04d_occ.log 2>&1; rc=$?
-echo "occ rc=$rc"; grep -E "PASS|FAIL|assert|held" gpurun_out/r04d_occ.log | tail -8
+timeout -k 10 200 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_dist.py -v -s -m gpu -k "error_flag or two_ranks" --timeout 150 --timeout-method thread > gpurun_out/r04d_occ.log 2>&1; rc=$?
+echo "occ rc=$rc"; grep -E "PASS|FAIL|assert|branch|rank " gpurun_out/r04d_occ.log | tail -20
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/r04c_tests.log 2>&1; rc=$?
 echo "tests rc=$rc"; grep -E "FAILED|ERROR|passed|failed" gpurun_out/r04c_tests.log | tail -8
