@@ -772,9 +772,9 @@ def roofline_hip(dev):
             16 * xd.numel(), lambda: K.dwconv_gln_bwd(xd, wd, 128, y1, al, gm, st, gy), "dwconv_gln_bwd")
     _, st2 = K.prelu_gln_fwd(xd, al, gm, bt)
     add_hbm("avse_prelu_gln_fwd (C4 TCN PReLU -> gLN after the 1x1 conv: x read, y written)", [16, 512, 3999], "fp32",
-            8 * xd.numel(), lambda: K.prelu_gln_fwd(xd, al, gm, bt))
+            8 * xd.numel(), lambda: K.prelu_gln_fwd(xd, al, gm, bt), "prelu_gln")
     add_hbm("avse_prelu_gln_bwd (C4 TCN: x, dy read, dx written)", [16, 512, 3999], "fp32",
-            12 * xd.numel(), lambda: K.prelu_gln_bwd(xd, al, gm, st2, gy))
+            12 * xd.numel(), lambda: K.prelu_gln_bwd(xd, al, gm, st2, gy), "prelu_gln_bwd")
     del xd, gy, y1
     # avse1 C2 lip front-end: BatchNorm3d -> PReLU (bnact) and the (1,3,3) max pool on (32, 64, 75, 48, 48), and the
     # ResNet layer4 bn2 + shortcut -> PReLU site on (2400, 512, 3, 3).  Two passes each way: fwd reads x twice and

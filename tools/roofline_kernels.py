@@ -20,7 +20,8 @@ from avse_challenge_amd import kernels as K  # noqa: E402
 SHAPES = {"scan": (64, 1024, 3999), "scan_bwd": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999),
           "conv3": (32, 64, 376, 257), "dconv_wgrad": (32, 64, 376, 257),
           "scan_c5": (32, 1024, 5999), "scan_bwd_c5": (32, 1024, 5999),
-          "dwconv_gln": (16, 512, 3999), "dwconv_gln_bwd": (16, 512, 3999)}
+          "dwconv_gln": (16, 512, 3999), "dwconv_gln_bwd": (16, 512, 3999),
+          "prelu_gln": (16, 512, 3999), "prelu_gln_bwd": (16, 512, 3999)}
 
 
 def aligned(b, d, l, g, scale=1.0, dtype=torch.float32):
@@ -49,6 +50,14 @@ def main():
             _, x, _ = fn()
             dout = aligned(b, d, l, g, dtype=dt)
             fn = lambda: K.selective_scan_bwd(u, dl, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False)  # noqa: E731
+    elif a.phase.startswith("prelu_gln"):
+        x = torch.randn(*SHAPES["prelu_gln"], device=dev, generator=g)
+        al, gm, bt = torch.full((1,), 0.25, device=dev), torch.ones(1, 512, 1, device=dev), torch.zeros(1, 512, 1, device=dev)
+        fn = lambda: K.prelu_gln_fwd(x, al, gm, bt)  # noqa: E731
+        if a.phase == "prelu_gln_bwd":
+            _, st = fn()
+            gy = torch.randn(*SHAPES["prelu_gln"], device=dev, generator=g)
+            fn = lambda: K.prelu_gln_bwd(x, al, gm, st, gy)  # noqa: E731
     elif a.phase.startswith("dwconv_gln"):
         x = torch.randn(*SHAPES["dwconv_gln"], device=dev, generator=g)
         w = 0.5 * torch.randn(512, 1, 3, device=dev, generator=g)

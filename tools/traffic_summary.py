@@ -19,7 +19,8 @@ root = sys.argv[1]
 SHAPES = {"scan": (64, 1024, 3999), "scan_bwd": (64, 1024, 3999), "dwconv": (16, 512, 3999), "cconv": (64, 1024, 3999),
           "conv3": (32, 64, 376, 257), "dconv_wgrad": (32, 64, 376, 257),
           "scan_c5": (32, 1024, 5999), "scan_bwd_c5": (32, 1024, 5999),
-          "dwconv_gln": (16, 512, 3999), "dwconv_gln_bwd": (16, 512, 3999)}
+          "dwconv_gln": (16, 512, 3999), "dwconv_gln_bwd": (16, 512, 3999),
+          "prelu_gln": (16, 512, 3999), "prelu_gln_bwd": (16, 512, 3999)}
 
 
 def per_launch(phase, counter):
