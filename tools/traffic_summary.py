@@ -23,7 +23,20 @@ SHAPES = {"scan": (64, 1024, 3999), "scan_bwd": (64, 1024, 3999), "dwconv": (16,
           "prelu_gln": (16, 512, 3999), "prelu_gln_bwd": (16, 512, 3999)}
 
 
+# the kernels one call of a multi-launch op consists of (name substrings); other phases: the dominant kernel.  A bwd
+# phase's setup call of the forward runs the forward's kernels once — they are not in these sets
+OPS = {"scan_bwd": ("scan::bwd_kernel", "scan::reduce_bc_kernel", "scan::reduce_d_kernel"),
+       "scan_bwd_c5": ("scan::bwd_kernel", "scan::reduce_bc_kernel", "scan::reduce_d_kernel"),
+       "dwconv_gln": ("gln::dwconv_stats_kernel", "gln::apply_fused_kernel"),
+       "dwconv_gln_bwd": ("gln::bwd_reduce_kernel", "gln::dwconv_gln_bwd", "gln::dw_tail_kernel"),
+       "prelu_gln": ("gln::stats_kernel", "gln::apply_fused_kernel"),
+       "prelu_gln_bwd": ("gln::bwd_reduce_kernel", "gln::bwd_apply_kernel", "gln::bwd_finalize",
+                         "gln::alpha_finalize")}
+
+
 def per_launch(phase, counter):
+    """(bytes per call of the phase's op, kernel label): the per-dispatch average of each of the op's kernels,
+    summed over them (OPS), or of the dominant kernel alone."""
     f = glob.glob(os.path.join(root, phase, counter, "**", "*counter_collection.csv"), recursive=True)
     if not f:
         return None, None
@@ -37,9 +50,15 @@ def per_launch(phase, counter):
         names[r["Dispatch_Id"]] = name
     if not per:
         return None, None
+
+    def avg(n):
+        vals = [per[d] for d in per if names[d] == n]
+        return sum(vals) / len(vals)
+    if phase in OPS:
+        ks = sorted({n for n in names.values() if any(p in n for p in OPS[phase])})
+        return sum(avg(n) for n in ks) * 1024.0, " + ".join(k.split("(")[0].replace("void ", "") for k in ks)
     kern = max(set(names.values()), key=lambda n: sum(per[d] for d in per if names[d] == n))
-    vals = [per[d] for d in per if names[d] == kern]
-    return sum(vals) / len(vals) * 1024.0, kern.split("(")[0]     # KB -> bytes
+    return avg(kern) * 1024.0, kern.split("(")[0]     # KB -> bytes
 
 
 res = {}
