@@ -62,6 +62,16 @@ class ScanBwdArgs(ctypes.Structure):
     ]
 
 
+class GemmBf16Args(ctypes.Structure):
+    _fields_ = [
+        ("batch", c_i64), ("mp", c_i64), ("mq", c_i64), ("k", c_i64),
+        ("p", c_vp), ("p_bs", c_i64), ("p_sx", c_i64), ("p_sk", c_i64), ("p_extent", c_i64),
+        ("q", c_vp), ("q_bs", c_i64), ("q_sx", c_i64), ("q_sk", c_i64), ("q_extent", c_i64),
+        ("c", c_vp), ("c_bs", c_i64), ("c_sq", c_i64),
+        ("alpha", c_f32), ("c_dtype", c_i32),
+    ]
+
+
 # name -> (restype, argtypes); every symbol include/avse_hip.h declares
 SIGNATURES = {
     "avse_strerror": (ctypes.c_char_p, [c_i32]),
@@ -128,6 +138,7 @@ SIGNATURES = {
                                     c_vp]),
     "avse_lstm_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "avse_lstm_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_gemm_bf16": (c_i32, [ctypes.POINTER(GemmBf16Args), c_vp]),
 }
 
 _lib = None

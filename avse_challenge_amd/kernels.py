@@ -838,3 +838,61 @@ def lstm_bwd(dh, gates, c_all, w_hh, reverse=False):
     check(L.avse_lstm_bwd(Bn, T, H, int(bool(reverse)), ptr(dh), dh.stride(0), dh.stride(1), ptr(gates.contiguous()),
                           ptr(c_all.contiguous()), ptr(w_pad), ptr(dg), stream_ptr(dh.device)), "avse_lstm_bwd")
     return dg
+
+
+# ------------------------------------------------------------------------ bf16 projection GEMM (Mamba in/out_proj)
+
+GEMM_BK = 64        # projgemm.hip: the reduction length must be a multiple of one LDS stage
+
+
+def _extent(t):
+    """Elements readable from t.data_ptr() to the end of t's storage."""
+    return t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()
+
+
+def _gemm_operand(t):
+    """(batch stride, stride of the row index, stride of k) of a (b|1, rows, k) operand; None when neither of the
+    last two strides is 1 or the other one is not a multiple of 8 elements (16 B)."""
+    bs = 0 if t.shape[0] == 1 else t.stride(0)
+    sx, sk = t.stride(1), t.stride(2)
+    if t.shape[1] == 1:                     # one row: either layout reads it
+        sx = 8 if sk == 1 else 1
+    if sk == 1 and sx % 8 == 0 and sx > 0:
+        return bs, sx, sk
+    if sx == 1 and sk % 8 == 0 and sk > 0:
+        return bs, sx, sk
+    return None
+
+
+def gemm_bf16_supported(P, Q, out):
+    """True when avse_gemm_bf16 takes out[b, q, p] = sum_k P[b, p, k] Q[b, q, k] as laid out (see gemm_bf16)."""
+    if not (P.is_cuda and P.dtype == Q.dtype == out.dtype == torch.bfloat16):
+        return False
+    if P.dim() != 3 or Q.dim() != 3 or out.dim() != 3 or P.shape[2] != Q.shape[2] or P.shape[2] % GEMM_BK:
+        return False
+    b = out.shape[0]
+    if out.shape[1:] != (Q.shape[1], P.shape[1]) or P.shape[0] not in (1, b) or Q.shape[0] not in (1, b):
+        return False
+    if out.stride(2) != 1 or out.stride(1) % 4 or out.data_ptr() % 8 or P.data_ptr() % 16 or Q.data_ptr() % 16:
+        return False
+    return _gemm_operand(P) is not None and _gemm_operand(Q) is not None
+
+
+def gemm_bf16(P, Q, out, alpha=1.0):
+    """out[b, q, p] = alpha * sum_k P[b, p, k] * Q[b, q, k] on the bf16 MFMA GEMM (csrc/projgemm.hip): bf16 operands,
+    fp32 accumulation, bf16 out.  P (b or 1, mp, k), Q (b or 1, mq, k) are strided views whose k or row stride is 1
+    (a batch of 1 is shared by every output batch); out (b, mq, mp) with stride(2) == 1.  Returns out."""
+    _need_gpu(P, Q, out)
+    if not gemm_bf16_supported(P, Q, out):
+        raise RuntimeError(f"avse_gemm_bf16: unsupported operands P {tuple(P.shape)}/{P.stride()} "
+                           f"Q {tuple(Q.shape)}/{Q.stride()} out {tuple(out.shape)}/{out.stride()} ({P.dtype})")
+    a = _lib.GemmBf16Args()
+    a.batch, a.mp, a.mq, a.k = out.shape[0], P.shape[1], Q.shape[1], P.shape[2]
+    a.p, (a.p_bs, a.p_sx, a.p_sk), a.p_extent = P.data_ptr(), _gemm_operand(P), _extent(P)
+    a.q, (a.q_bs, a.q_sx, a.q_sk), a.q_extent = Q.data_ptr(), _gemm_operand(Q), _extent(Q)
+    a.c, a.c_bs, a.c_sq = out.data_ptr(), out.stride(0), out.stride(1)
+    a.alpha, a.c_dtype = float(alpha), AVSE_BF16
+    tap = _tap_begin("avse_gemm_bf16", out.device)
+    check(_lib.lib().avse_gemm_bf16(a, stream_ptr(out.device)), "avse_gemm_bf16")
+    _tap_end(tap)
+    return out

@@ -9,7 +9,9 @@ Mirrors, with identical parameter names / state_dict keys (checkpoints load unch
   Encoder / Decoder    speechbrain dual_path Encoder/Decoder (hparams mambatasnet_*.yaml)
   MambaTasNet.forward  train_wsj0mix.py:86-111 compute_forward
 The scan, the causal conv and the add+RMSNorm run in libavse_hip.so; the dense projections
-are GEMMs (torch.matmul -> hipBLASLt MFMA).  No CPU fallback: CPU tensors raise.
+are GEMMs: bf16 (autocast) in_proj / out_proj / x_proj and their input gradients on the HIP MFMA GEMM
+(csrc/projgemm.hip), the fp32 ones, dt_proj (K = dt_rank) and the weight gradients on hipBLASLt
+(torch.matmul).  No CPU fallback: CPU tensors raise.
 """
 import math
 import os
@@ -28,17 +30,37 @@ _FWD = torch.amp.custom_fwd(device_type="cuda")
 _BWD = torch.amp.custom_bwd(device_type="cuda")
 
 
-def _wbmm(w, x):
-    """(m, k) weight @ (b, k, n) -> (b, m, n) as one strided-batched GEMM (weight batch stride 0).
+# bf16 projections (BASELINE configs[4]) on the HIP MFMA GEMM (csrc/projgemm.hip) where it takes the operands;
+# AVSE_PROJ_GEMM=0 keeps them on the library (torch.bmm -> hipBLASLt), which every fp32 GEMM uses.
+_HIP_GEMM = os.environ.get("AVSE_PROJ_GEMM", "1") == "1"
+
+
+def _autocast_dtype():
+    return torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
+
+
+def _hip_gemm(P, Q, out, alpha=1.0):
+    """out[b, q, p] = alpha sum_k P[b, p, k] Q[b, q, k] on the HIP bf16 GEMM; None when it does not take them."""
+    if _HIP_GEMM and K.gemm_bf16_supported(P, Q, out):
+        return K.gemm_bf16(P, Q, out, alpha)
+    return None
+
+
+def _wbmm(w, x, alpha=1.0):
+    """alpha (m, k) weight @ (b, k, n) -> (b, m, n) as one strided-batched GEMM (weight batch stride 0).
     Keeping every projection in the scan's (b, channels, l) layout means no layout copies.  The output rows get
-    the kernels' cache-line-aligned time stride (kernels.TIME_ALIGN_BYTES; hipBLASLt writes with ldc = the padded
+    the kernels' cache-line-aligned time stride (kernels.TIME_ALIGN_BYTES; the GEMM writes with ldc = the padded
     stride), so every (b, d, l) operand of the conv / scan kernels starts its rows on a 128-B line."""
-    if torch.is_autocast_enabled("cuda"):
-        dt = torch.get_autocast_dtype("cuda")
+    dt = _autocast_dtype()
+    if dt is not None:
         w, x = w.to(dt), x.to(dt)
     else:
         dt = torch.result_type(w, x)
     out = K.bdl_empty(x.shape[0], w.shape[0], x.shape[2], dt, x.device)
+    if _hip_gemm(x.transpose(1, 2), w[None], out, alpha) is not None:
+        return out
+    if alpha != 1.0:
+        w = alpha * w
     with torch.autocast("cuda", enabled=False):
         return torch.bmm(w.expand(x.shape[0], *w.shape), x, out=out)
 
@@ -162,7 +184,14 @@ class _InProj(torch.autograd.Function):
     @_BWD
     def backward(ctx, dxz):
         h, w = ctx.saved_tensors
-        dh = torch.bmm(dxz.transpose(1, 2), w.expand(dxz.shape[0], *w.shape))
+        dt = _autocast_dtype()
+        dh = None
+        if dt is not None:
+            wc, dxc = w.to(dt), dxz.to(dt)
+            dh = _hip_gemm(wc.t()[None], dxc.transpose(1, 2),
+                           torch.empty(dxz.shape[0], dxz.shape[2], w.shape[1], device=dxz.device, dtype=dt))
+        if dh is None:
+            dh = torch.bmm(dxz.transpose(1, 2), w.expand(dxz.shape[0], *w.shape))
         dw = _bsum_mm(dxz, h)
         return dh, dw
 
@@ -177,6 +206,13 @@ class _BiOutProj(torch.autograd.Function):
     def forward(ctx, f, bk, w):
         y = _padded_add(f, bk)
         ctx.save_for_backward(y, w)
+        dt = _autocast_dtype()
+        if dt is not None:
+            wc, yc = w.to(dt), y.to(dt)
+            out = _hip_gemm(wc[None], yc.transpose(1, 2),
+                            torch.empty(y.shape[0], y.shape[2], w.shape[0], device=y.device, dtype=dt), 0.5)
+            if out is not None:
+                return out
         wt = 0.5 * w.t()
         return torch.bmm(y.transpose(1, 2), wt.expand(y.shape[0], *wt.shape))
 
@@ -184,7 +220,7 @@ class _BiOutProj(torch.autograd.Function):
     @_BWD
     def backward(ctx, dout):
         y, w = ctx.saved_tensors
-        dy = _wbmm(0.5 * w.t(), dout.transpose(1, 2))                            # (b, d_inner, l)
+        dy = _wbmm(w.t(), dout.transpose(1, 2), 0.5)                             # (b, d_inner, l)
         dw = 0.5 * _bsum_mm(dout.transpose(1, 2), y.transpose(1, 2))               # (d_model, d_inner)
         return dy, dy, dw
 

@@ -1,0 +1,90 @@
+"""bf16 projection GEMM (csrc/projgemm.hip, kernels.gemm_bf16) vs an fp64 matmul of the same bf16 operands.
+
+The op is the bf16 F.linear of the Mamba projections under autocast (Mamba-TasNet/modules/mamba/bimamba.py:190-196,
+250-253): fp32 accumulation, one round to bf16 at the end.  Bar per element: |out - ref| <= 2^-8 |ref| (half a bf16
+ulp, the final rounding) + 1e-5 * sum_k |P Q| (fp32 accumulation in another order).  Outputs outside the logical
+shape (the padded time columns of the model's layout) must stay untouched.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def K():
+    from avse_challenge_amd import kernels
+    return kernels
+
+
+def _operand(b, rows, k, kc, g, shared=False):
+    """A (b or 1, rows, k) bf16 view that is K-contiguous (kc) or contiguous along rows, with padded strides."""
+    nb = 1 if shared else b
+    if kc:
+        base = torch.randn(nb, rows, k + 8, device=DEV, generator=g).to(torch.bfloat16)
+        return base[:, :, :k]
+    base = torch.randn(nb, k, -(-rows // 8) * 8 + 16, device=DEV, generator=g).to(torch.bfloat16)
+    return base[:, :, :rows].transpose(1, 2)
+
+
+def _check(out, P, Q, alpha, mp):
+    ref = alpha * torch.matmul(Q.double(), P.double().transpose(1, 2))              # (b, mq, mp)
+    mag = torch.matmul(Q.double().abs(), P.double().abs().transpose(1, 2)) * abs(alpha)
+    got = out[..., :mp].double()
+    bad = (got - ref).abs() > 2.0 ** -8 * ref.abs() + 1e-5 * mag
+    assert not bool(bad.any()), (int(bad.sum()), float((got - ref).abs().max()))
+
+
+@pytest.mark.parametrize("p_kc", [True, False])
+@pytest.mark.parametrize("q_kc", [True, False])
+@pytest.mark.parametrize("shared", ["p", "q", None])
+def test_gemm_bf16_layouts_ragged(p_kc, q_kc, shared):
+    g = torch.Generator(device=DEV).manual_seed(7 + 2 * p_kc + q_kc)
+    b, mp, mq, k = 3, 300, 200, 192
+    P = _operand(b, mp, k, p_kc, g, shared == "p")
+    Q = _operand(b, mq, k, q_kc, g, shared == "q")
+    out = torch.full((b, mq, mp + 20), float("nan"), device=DEV, dtype=torch.bfloat16)[..., :mp]
+    assert K().gemm_bf16_supported(P, Q, out)
+    K().gemm_bf16(P, Q, out, 0.5)
+    _check(out, P, Q, 0.5, mp)
+    pad = torch.as_strided(out, (b, mq, 20), out.stride(), out.storage_offset() + mp)
+    assert bool(torch.isnan(pad.float()).all()), "the GEMM wrote outside the logical output"
+
+
+@pytest.mark.parametrize("mp,mq,k", [(1, 1, 64), (129, 127, 64), (4, 640, 1024), (640, 4, 2048)])
+def test_gemm_bf16_edge_shapes(mp, mq, k):
+    g = torch.Generator(device=DEV).manual_seed(mp * 31 + mq)
+    P = _operand(2, mp, k, True, g)
+    Q = _operand(2, mq, k, False, g, shared=True)
+    out = torch.empty((2, mq, mp + (-mp) % 4), device=DEV, dtype=torch.bfloat16)[..., :mp]
+    K().gemm_bf16(P, Q, out)
+    _check(out, P, Q, 1.0, mp)
+
+
+def test_gemm_bf16_mamba_layouts_c5_rows():
+    """The four C5 projections as mamba_tasnet lays them out (B = 2, L = 999 with the 128-B padded time stride)."""
+    k = K()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    b, L, dm, di, bf = 2, 999, 512, 1024, torch.bfloat16
+    rnd = lambda *s: torch.randn(*s, device=DEV, generator=g).to(bf)  # noqa: E731
+    w_in, w_out = rnd(2 * di, dm), rnd(dm, di)
+    h, dout = rnd(b, L, dm), rnd(b, L, dm)
+    y = k.bdl_empty(b, di, L, bf, DEV).copy_(torch.randn(b, di, L, device=DEV, generator=g))
+    dxz = k.bdl_empty(b, 2 * di, L, bf, DEV).copy_(torch.randn(b, 2 * di, L, device=DEV, generator=g))
+    xz = k.bdl_empty(b, 2 * di, L, bf, DEV)
+    _check(k.gemm_bf16(h, w_in[None], xz), h, w_in[None], 1.0, L)                                # in_proj
+    o = torch.empty(b, L, dm, device=DEV, dtype=bf)
+    _check(k.gemm_bf16(w_out[None], y.transpose(1, 2), o, 0.5), w_out[None], y.transpose(1, 2), 0.5, dm)
+    dh = torch.empty(b, L, dm, device=DEV, dtype=bf)
+    _check(k.gemm_bf16(w_in.t()[None], dxz.transpose(1, 2), dh), w_in.t()[None], dxz.transpose(1, 2), 1.0, dm)
+    dy = k.bdl_empty(b, di, L, bf, DEV)
+    _check(k.gemm_bf16(dout, w_out.t()[None], dy, 0.5), dout, w_out.t()[None], 0.5, L)
+
+
+def test_gemm_bf16_rejects_unsupported():
+    k = K()
+    a = torch.randn(2, 64, 96, device=DEV).to(torch.bfloat16)                  # k = 96: not a multiple of 64
+    out = torch.empty(2, 64, 64, device=DEV, dtype=torch.bfloat16)
+    assert not k.gemm_bf16_supported(a, a, out)
+    with pytest.raises(RuntimeError):
+        k.gemm_bf16(a, a, out)
