@@ -64,7 +64,7 @@ class ScanBwdArgs(ctypes.Structure):
 
 class GemmBf16Args(ctypes.Structure):
     _fields_ = [
-        ("batch", c_i64), ("mp", c_i64), ("mq", c_i64), ("k", c_i64),
+        ("batch", c_i64), ("mp", c_i64), ("mq", c_i64), ("k", c_i64), ("fold", c_i64),
         ("p", c_vp), ("p_bs", c_i64), ("p_sx", c_i64), ("p_sk", c_i64), ("p_extent", c_i64),
         ("q", c_vp), ("q_bs", c_i64), ("q_sx", c_i64), ("q_sk", c_i64), ("q_extent", c_i64),
         ("c", c_vp), ("c_bs", c_i64), ("c_sq", c_i64),

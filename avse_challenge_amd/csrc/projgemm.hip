@@ -12,17 +12,24 @@
 //
 // P feeds the MFMA's rows, so each lane's accumulator holds 4 consecutive p (one 8-byte bf16 store).
 //
-// Tiling: 256 threads, 128 (p) x 128 (q) per workgroup, 2 x 2 waves of 64 x 64 (2 x 2 MFMA blocks of 32 x 32),
-// K in stages of 64 staged HBM -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds: out-of-range reads land as 0), two
-// stage buffers (64 KB: 2 workgroups per CU, the other one's MFMAs cover a stage's load latency).
+// Shape of the work: K is short (512 .. 2048), so a 128 x 128 tile spends more time fetching its operands from L2
+// than multiplying them (256 KB per 16.8 MFLOP = 75 GB/s per CU at half the MFMA peak, the L2's per-CU rate), and a
+// non-persistent workgroup's epilogue leaves the MFMAs idle.  Hence:
+//   - 256 x 256 tiles, 8 waves (2 per SIMD) of 128 (p) x 64 (q) each: 4 x 2 MFMA blocks, 128 accumulators per lane;
+//     37 GB/s of L2 reads per CU at half the peak;
+//   - persistent workgroups (one per CU) walking a flat sequence of (tile, k-stage) pairs; stages of 32 k staged
+//     HBM/L2 -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds; reads past the operand's extent land as 0) into a ring of
+//     4 buffers (128 KB), issued 3 stages ahead — across tile boundaries, so the next tile's first stages load while
+//     this tile's epilogue stores;
+//   - one barrier per stage: after it, every wave has finished the stage that last used the buffer being refilled.
 // LDS images per operand and stage (16 KB):
-//   K-contiguous: 128 rows x 128 B (64 k); 16-B chunk c of row r stored at c ^ ((r >> 1) & 7), so the fragment
-//     reads (ds_read_b128, lane = row) of a 16-lane group hit 16 distinct 16-B bank slots;
-//   MN-contiguous: 64 k-rows x 256 B (128 p or q); chunk c of k-row r at c ^ ((r & 3) << 2); fragments by
+//   K-contiguous: 256 rows x 64 B (32 k); 16-B chunk c of row r stored at c ^ ((r >> 2) & 3): the fragment reads
+//     (ds_read_b128, lane = row) of each 16-lane group hit 16 distinct 16-B bank slots;
+//   MN-contiguous: 32 k-rows x 512 B (256 p or q); chunk c of k-row r at c ^ ((r & 3) << 2); fragments by
 //     ds_read_b64_tr_b16 (4 k-rows x 16 columns per 16-lane group, delivered column-major), conflict-free per half.
 // The swizzle is applied to the DMA's per-lane SOURCE address (the LDS side of an LDS-DMA is lane-linear).
-// Workgroup order: the tile index of the shared weight (batch stride 0) runs fastest and neighbouring ids share an
-// XCD (xcd_remap), so an activation tile is fetched from HBM once and re-read from that XCD's L2.
+// Tile order: the shared weight's tile index runs fastest, and the 32 workgroups of an XCD take 32 consecutive tiles
+// per round, so an activation block is fetched from HBM once and re-read from that XCD's L2.
 #include "common.h"
 
 namespace avse {
@@ -30,14 +37,17 @@ namespace pg {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef short s8_t __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) s4_t lds_s4_t;
 
-constexpr int BP = 128, BQ = 128, BK = 64, THREADS = 256;
-constexpr int IMG = 16384;                 // one operand's image of one stage
+constexpr int BT = 256, BK = 32, THREADS = 512, WAVES = THREADS / 64;
+constexpr int IMG = BT * BK * 2;           // one operand's image of one stage: 16 KB
 constexpr int STAGE = 2 * IMG;
-constexpr int NSTAGE = 2;
+constexpr int NBUF = 4, AHEAD = 3;         // LDS ring; stages in flight ahead of the one computed
+constexpr int PIECES = IMG / 1024 / WAVES; // LDS-DMA wave-instructions per operand, stage and wave (2)
+constexpr int LOADS = 2 * PIECES;          // per stage and wave
 
 struct Args {
     const uint16_t* p;
@@ -48,50 +58,84 @@ struct Args {
     int32_t p_sx, q_sx;                    // stride of the p / q index (K-contiguous operand) or of k (MN-contiguous)
     int32_t c_sq;
     int32_t mp, mq, k, batch;
-    int32_t tp, tq;                        // tile counts
-    int32_t q_fast;                        // q tile index runs fastest in the workgroup order
+    int32_t tp, tq;                        // tile counts per batch group
+    int32_t ntiles, ntb;                   // tiles in all; k-stages per batch
+    int32_t fold;                          // batches summed into one output (weight gradients), batch % fold == 0
+    int32_t kv_last;                       // valid k in a batch's last stage (BK unless k % BK)
+    int32_t q_fast;                        // q tile index runs fastest in the tile order
+    int32_t c_vec16;                       // bf16 out: rows 16-B aligned (c and c_sq * 2 multiples of 16)
     float alpha;
 };
 
-__device__ inline __amdgpu_buffer_rsrc_t rsrc_from(const uint16_t* base, int64_t elems) {
+typedef int i4_t __attribute__((ext_vector_type(4)));
+
+// Buffer resource (wave-uniform) over [base, base + elems): reads past it return 0.
+__device__ inline i4_t rsrc_from(const uint16_t* base, int64_t elems) {
     int64_t bytes = elems * 2;
     if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
     if (bytes < 0) bytes = 0;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+    const uint64_t a = (uint64_t)base;
+    return i4_t{__builtin_amdgcn_readfirstlane((int)(uint32_t)a), __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff)),
+                __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
 }
 
-// One operand's stage (BK k x 128 rows) HBM -> LDS image.  KC: the operand is K-contiguous (row x0 + r has stride sx,
-// k is contiguous); otherwise k-row k0 + r has stride sx and the 128 rows are contiguous.  Rows past mx are clamped
+// One 16-B-per-lane LDS-DMA wave-instruction: LDS[lds_addr + 16 lane] = buffer[voff].  Inline asm on purpose: the
+// compiler tracks its own LDS-DMA builtins as pending writes to the whole staging array and then waits vmcnt(0)
+// before every ds_read of it, which drains the stages in flight; the ring's counted waits are done by hand instead.
+// Nothing else in these kernels uses M0.
+__device__ inline void dma16(i4_t r, uint32_t lds_addr, uint32_t voff) {
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds_addr)
+                 : "memory");
+}
+
+__device__ inline uint32_t lds_u32(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_void_t*)p);
+}
+
+struct Tile {
+    int b, p0, q0;
+};
+
+// b: the batch group (the output batch); its batches are b * fold .. b * fold + fold - 1
+__device__ inline Tile tile_of(const Args& a, int T) {
+    const int per_b = a.tp * a.tq;
+    const int b = T / per_b, t = T - b * per_b;
+    const int tpi = a.q_fast ? t / a.tq : t % a.tp;
+    const int tqi = a.q_fast ? t % a.tq : t / a.tp;
+    return Tile{b, tpi * BT, tqi * BT};
+}
+
+// One operand's stage (BK k x 256 rows) -> LDS image.  KC: the operand is K-contiguous (row x0 + r has stride sx, k
+// is contiguous); otherwise k-row k0 + r has stride sx and the 256 rows are contiguous.  Rows past mx are clamped
 // (KC) or read whatever lies there / 0 past the buffer (MN); they only feed outputs that are never stored.
 template <bool KC>
-__device__ inline void stage_load(__amdgpu_buffer_rsrc_t r, uint8_t* img, int x0, int k0, int sx, int mx, int wave,
-                                  int lane) {
+__device__ inline void stage_load(i4_t r, uint32_t img, int x0, int k0, int sx, int mx, int wave, int lane) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int piece = wave * 4 + j;                        // 1 KB of the image per wave-instruction
+    for (int j = 0; j < PIECES; ++j) {
+        const int piece = wave * PIECES + j;                  // 1 KB of the image per wave-instruction
         uint32_t voff;
         if constexpr (KC) {
-            const int row = piece * 8 + (lane >> 3);
+            const int row = piece * 16 + (lane >> 2);
             const int xr = min(x0 + row, mx - 1);
-            const int c = (lane & 7) ^ ((row >> 1) & 7);
+            const int c = (lane & 3) ^ ((row >> 2) & 3);
             voff = (uint32_t)(xr * sx + k0 + c * 8) * 2u;
         } else {
-            const int krow = piece * 4 + (lane >> 4);
-            const int c = (lane & 15) ^ ((krow & 3) << 2);
+            const int krow = piece * 2 + (lane >> 5);
+            const int c = (lane & 31) ^ ((krow & 3) << 2);
             voff = (uint32_t)((k0 + krow) * sx + x0 + c * 8) * 2u;
         }
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(img + piece * 1024), 16, voff, 0, 0, 0);
+        dma16(r, img + piece * 1024, voff);
     }
 }
 
 // The 32 x 16 (row x k) MFMA operand fragment of rows rb .. rb + 31, k-substep s (k = 16 s .. 16 s + 15):
-// lane l holds row rb + (l & 31), k = 16 s + 8 (l >> 5) + 0..7.
+// lane l holds row rb + (l & 31), k = 16 s + 8 (l >> 5) + 0..7 (element e <-> k = 16 s + 8 (l >> 5) + e).
 template <bool KC>
-__device__ inline bf16x8 frag(const uint8_t* img, int rb, int s, int lane) {
+__device__ inline bf16x8 frag_raw(const uint8_t* img, int rb, int s, int lane) {
     if constexpr (KC) {
         const int row = rb + (lane & 31);
         const int ch = 2 * s + (lane >> 5);
-        return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * (ch ^ ((row >> 1) & 7)));
+        return *reinterpret_cast<const bf16x8*>(img + row * 64 + 16 * (ch ^ ((row >> 2) & 3)));
     } else {
         const int g = lane >> 4, i = lane & 15;
         const int col = rb + 16 * (g & 1) + 4 * (i & 3);
@@ -100,12 +144,35 @@ __device__ inline bf16x8 frag(const uint8_t* img, int rb, int s, int lane) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int kr = kb + 4 * u;
-            const int off = kr * 256 + 16 * ((col >> 3) ^ ((kr & 3) << 2)) + (col & 7) * 2;
+            const int off = kr * 512 + 16 * ((col >> 3) ^ ((kr & 3) << 2)) + (col & 7) * 2;
             v[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(img + off));
         }
-        typedef short s8_t __attribute__((ext_vector_type(8)));
         const s8_t w = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]};
         return __builtin_bit_cast(bf16x8, w);
+    }
+}
+
+// Zero the k >= kv part of one operand's stage image (the reduction's last, partial stage: what lies past k is
+// another row's data, pad columns or 0, and a non-finite value there must not reach the sums as 0 * inf), so both
+// operands are cleared.  KC image: 16-B chunk c of row r (k = 8 c .. 8 c + 7) at c ^ ((r >> 2) & 3); MN image: whole
+// k-rows.
+template <bool KC>
+__device__ inline void zero_tail(uint8_t* img, int kv, int tid) {
+    if constexpr (KC) {
+        for (int i = tid; i < BT * 4; i += THREADS) {
+            const int row = i >> 2, pos = i & 3, c = pos ^ ((row >> 2) & 3);
+            if (8 * c + 8 <= kv) continue;
+            s8_t* ptr = reinterpret_cast<s8_t*>(img + row * 64 + 16 * pos);
+            s8_t w = *ptr;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] = (8 * c + e < kv) ? w[e] : (short)0;
+            *ptr = w;
+        }
+    } else {
+        for (int i = tid; i < BK * 32; i += THREADS) {          // 32 16-B chunks per 512-B k-row
+            const int kr = i >> 5;
+            if (kr >= kv) *reinterpret_cast<uint4*>(img + kr * 512 + 16 * (i & 31)) = uint4{0u, 0u, 0u, 0u};
+        }
     }
 }
 
@@ -116,92 +183,182 @@ __device__ inline uint32_t pack_bf16x2(float a, float b) {
     return (uint32_t)x.x | ((uint32_t)y.x << 16);
 }
 
+// Wave (wr, wc) = (wave >> 2, wave & 3) owns the p blocks 32 (2 i + wr), i = 0..3 (so an epilogue round i covers the
+// 64 contiguous p of 64 i .. 64 i + 63 over both wave rows) and the q columns 64 wc .. 64 wc + 63.
 template <bool P_KC, bool Q_KC>
-__global__ __launch_bounds__(THREADS, 2) void gemm_kernel(Args a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[NSTAGE * STAGE];
+__device__ inline void mma_stage(floatx16 (&acc)[4][2], const uint8_t* img, int wr, int wq, int lane) {
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+        bf16x8 fa[4], fb[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = frag_raw<P_KC>(img, 32 * (2 * i + wr), ks, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j] = frag_raw<Q_KC>(img + IMG, wq + 32 * j, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+template <bool P_KC, bool Q_KC, bool OUT_F32>
+__global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * STAGE];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nwg = gridDim.x;
-    const int id = xcd_remap(blockIdx.x, nwg);
-    const int per_b = a.tp * a.tq;
-    const int b = id / per_b, t = id % per_b;
-    const int tpi = a.q_fast ? t / a.tq : t % a.tp;
-    const int tqi = a.q_fast ? t % a.tq : t / a.tp;
-    const int p0 = tpi * BP, q0 = tqi * BQ;
+    // tiles of this workgroup: round r takes tile r * G + xcd * (G / 8) + slot (G % 8 == 0), so the workgroups of
+    // one XCD (blockIdx % 8) work on consecutive tiles
+    const int G = gridDim.x;
+    const int base = (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8;
+    const int my_tiles = base < a.ntiles ? (a.ntiles - base + G - 1) / G : 0;
+    const int per_tile = a.ntb * a.fold;
+    const int total = my_tiles * per_tile;
+    const int wr = wave >> 2, wc = wave & 3, wq = wc * 64;
+    const uint32_t lds0 = lds_u32(lds);
 
-    const uint16_t* pb = a.p + (int64_t)b * a.p_bs;
-    const uint16_t* qb = a.q + (int64_t)b * a.q_bs;
-    const auto rp = rsrc_from(pb, a.p_ext - (int64_t)b * a.p_bs);
-    const auto rq = rsrc_from(qb, a.q_ext - (int64_t)b * a.q_bs);
-
-    floatx16 acc[2][2];
+    // load cursor: the stage issued next = (tile ld_T, batch ld_f of its group, k-stage ld_kt)
+    int ld_s = 0, ld_kt = 0, ld_f = 0, ld_T = base;
+    Tile ld_tile = tile_of(a, base);
+    i4_t rp, rq;
+    auto set_rsrc = [&](int b) {
+        rp = rsrc_from(a.p + (int64_t)b * a.p_bs, a.p_ext - (int64_t)b * a.p_bs);
+        rq = rsrc_from(a.q + (int64_t)b * a.q_bs, a.q_ext - (int64_t)b * a.q_bs);
+    };
+    if (total > 0) set_rsrc(ld_tile.b * a.fold);
+    auto issue = [&]() {
+        if (ld_s >= total) return;
+        const uint32_t img = lds0 + (ld_s % NBUF) * STAGE;
+        stage_load<P_KC>(rp, img, ld_tile.p0, ld_kt * BK, a.p_sx, a.mp, wave, lane);
+        stage_load<Q_KC>(rq, img + IMG, ld_tile.q0, ld_kt * BK, a.q_sx, a.mq, wave, lane);
+        ++ld_s;
+        if (++ld_kt == a.ntb) {
+            ld_kt = 0;
+            if (++ld_f == a.fold) {
+                ld_f = 0;
+                ld_T += G;
+                if (ld_s < total) ld_tile = tile_of(a, ld_T);
+            }
+            if (ld_s < total) set_rsrc(ld_tile.b * a.fold + ld_f);
+        }
+    };
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < AHEAD; ++i) issue();
+
+    floatx16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-    const int wp = (wave >> 1) * 64, wq = (wave & 1) * 64;
-    const int nt = a.k / BK;
-    stage_load<P_KC>(rp, lds, p0, 0, a.p_sx, a.mp, wave, lane);
-    stage_load<Q_KC>(rq, lds + IMG, q0, 0, a.q_sx, a.mq, wave, lane);
-    for (int kt = 0; kt < nt; ++kt) {
-        const uint8_t* img = lds + (kt & 1) * STAGE;
-        if (kt + 1 < nt) {
-            uint8_t* nxt = lds + ((kt + 1) & 1) * STAGE;
-            stage_load<P_KC>(rp, nxt, p0, (kt + 1) * BK, a.p_sx, a.mp, wave, lane);
-            stage_load<Q_KC>(rq, nxt + IMG, q0, (kt + 1) * BK, a.q_sx, a.mq, wave, lane);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");          // this stage's 8 DMAs landed, the next 8 fly
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+    int kt = 0, f = 0, T = base;
+    for (int s = 0; s < total; ++s) {
+        // stage s has landed when at most the stages issued after it are still in flight
+        const int after = ld_s - s - 1;
+        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // this wave's reads of stage s - 1 are done
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-#pragma unroll
-        for (int s = 0; s < BK / 16; ++s) {
-            bf16x8 fa[2], fb[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) fa[i] = frag<P_KC>(img, wp + 32 * i, s, lane);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) fb[j] = frag<Q_KC>(img + IMG, wq + 32 * j, s, lane);
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        issue();                                                // into the buffer of stage s - 1
+        uint8_t* img = lds + (s % NBUF) * STAGE;
+        if (kt == a.ntb - 1 && a.kv_last < BK) {                  // workgroup-uniform
+            zero_tail<P_KC>(img, a.kv_last, threadIdx.x);
+            zero_tail<Q_KC>(img + IMG, a.kv_last, threadIdx.x);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();                                  // the buffer is re-filled next iteration
-        asm volatile("" ::: "memory");
-    }
-
-    // epilogue: lane holds C rows p = p0 + wp + 32 i + 8 g + 4 (lane >> 5) + 0..3 at column q = q0 + wq + 32 j + (lane & 31)
-    uint16_t* cb = reinterpret_cast<uint16_t*>(a.c) + (int64_t)b * a.c_bs;
+        mma_stage<P_KC, Q_KC>(acc, img, wr, wq, lane);
+        if (++kt < a.ntb) continue;
+        kt = 0;
+        if (++f < a.fold) continue;
+        f = 0;
+        // epilogue of tile T.  acc[i][j]: rows p = p0 + 32 (2 i + wr) + 8 g + 4 (lane >> 5) + 0..3 (register 4 g + 0..3),
+        // column q = q0 + wq + 32 j + (lane & 31)
+        const Tile t = tile_of(a, T);
+        T += G;
+        if constexpr (OUT_F32) {
+            // the weight gradients: small outputs, written straight from the accumulators (16 B per lane)
+            float* cf = reinterpret_cast<float*>(a.c) + (int64_t)t.b * a.c_bs;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int q = q0 + wq + 32 * j + (lane & 31);
-        if (q >= a.mq) continue;
-        uint16_t* crow = cb + (int64_t)q * a.c_sq;
+            for (int j = 0; j < 2; ++j) {
+                const int q = t.q0 + wq + 32 * j + (lane & 31);
+                float* crow = cf + (int64_t)min(q, a.mq - 1) * a.c_sq;
+                const bool qok = q < a.mq;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int p = p0 + wp + 32 * i + 8 * g + 4 * (lane >> 5);
-                const float v0 = a.alpha * acc[i][j][4 * g], v1 = a.alpha * acc[i][j][4 * g + 1];
-                const float v2 = a.alpha * acc[i][j][4 * g + 2], v3 = a.alpha * acc[i][j][4 * g + 3];
-                if (p + 3 < a.mp) {
-                    uint2 w;
-                    w.x = pack_bf16x2(v0, v1);
-                    w.y = pack_bf16x2(v2, v3);
-                    *reinterpret_cast<uint2*>(crow + p) = w;
-                } else {
-                    const float v[4] = {v0, v1, v2, v3};
+                    for (int g = 0; g < 4; ++g) {
+                        const int p = t.p0 + 32 * (2 * i + wr) + 8 * g + 4 * (lane >> 5);
+                        const float4 v = {a.alpha * acc[i][j][4 * g], a.alpha * acc[i][j][4 * g + 1],
+                                          a.alpha * acc[i][j][4 * g + 2], a.alpha * acc[i][j][4 * g + 3]};
+                        if (qok && p + 3 < a.mp) {
+                            *reinterpret_cast<float4*>(crow + p) = v;
+                        } else if (qok) {
+                            const float w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (p + e < a.mp) io<bf16_t>::st(reinterpret_cast<bf16_t*>(crow + p + e), v[e]);
-                }
+                            for (int e = 0; e < 4; ++e)
+                                if (p + e < a.mp) crow[p + e] = w[e];
+                        }
+                    }
             }
+        } else {
+            // bf16 out through the buffer of stage s (free until the next stage's barrier) in 4 rounds of 64 p x
+            // 256 q: each q row's 64 p leave as one 128-B line (8 lanes x 16 B) instead of 16-B pieces of 32 lines
+            uint8_t* stg = lds + (s % NBUF) * STAGE;              // [256 q][128 B], 16-B chunk c of row q at c ^ (q & 7)
+            uint16_t* cb = reinterpret_cast<uint16_t*>(a.c) + (int64_t)t.b * a.c_bs;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                __builtin_amdgcn_s_barrier();                       // all waves are done reading the buffer
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int q = wq + 32 * j + (lane & 31);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int pl = 32 * wr + 8 * g + 4 * (lane >> 5);       // p within the round's 64
+                        uint2 w;
+                        w.x = pack_bf16x2(a.alpha * acc[i][j][4 * g], a.alpha * acc[i][j][4 * g + 1]);
+                        w.y = pack_bf16x2(a.alpha * acc[i][j][4 * g + 2], a.alpha * acc[i][j][4 * g + 3]);
+                        *reinterpret_cast<uint2*>(stg + q * 128 + 16 * ((pl >> 3) ^ (q & 7)) + (pl & 7) * 2) = w;
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int r = 0; r < 256 / 64; ++r) {                // 8 rows per wave-instruction, 4 per wave
+                    const int ql = (r * WAVES + wave) * 8 + (lane >> 3), c = lane & 7;
+                    const uint4 v = *reinterpret_cast<const uint4*>(stg + ql * 128 + 16 * (c ^ (ql & 7)));
+                    const int q = t.q0 + ql, p = t.p0 + 64 * i + 8 * c;
+                    if (q < a.mq) {
+                        uint16_t* dst = cb + (int64_t)q * a.c_sq + p;
+                        if (p + 7 < a.mp && a.c_vec16) {
+                            *reinterpret_cast<uint4*>(dst) = v;
+                        } else if (p + 7 < a.mp) {
+                            reinterpret_cast<uint2*>(dst)[0] = uint2{v.x, v.y};
+                            reinterpret_cast<uint2*>(dst)[1] = uint2{v.z, v.w};
+                        } else {
+                            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                            for (int e = 0; e < 8; ++e)
+                                if (p + e < a.mp) dst[e] = (uint16_t)(u[e >> 1] >> (16 * (e & 1)));
+                        }
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
     }
 }
 
@@ -214,21 +371,24 @@ extern "C" {
 
 int avse_gemm_bf16(const avse_gemm_bf16_args* g, avse_stream_t stream) {
     if (!g || !g->p || !g->q || !g->c) return AVSE_EINVAL;
-    if (g->c_dtype != AVSE_BF16) return AVSE_EDTYPE;
-    if (g->batch <= 0 || g->mp <= 0 || g->mq <= 0 || g->k <= 0) return AVSE_ESHAPE;
-    if (g->k % BK) return AVSE_ESHAPE;
+    if (g->c_dtype != AVSE_BF16 && g->c_dtype != AVSE_F32) return AVSE_EDTYPE;
+    const int64_t fold = g->fold > 0 ? g->fold : 1;
+    if (g->batch <= 0 || g->mp <= 0 || g->mq <= 0 || g->k <= 0 || g->batch % fold) return AVSE_ESHAPE;
     const bool p_kc = g->p_sk == 1, q_kc = g->q_sk == 1;
     if (!p_kc && g->p_sx != 1) return AVSE_ESHAPE;
     if (!q_kc && g->q_sx != 1) return AVSE_ESHAPE;
     const int64_t p_s = p_kc ? g->p_sx : g->p_sk, q_s = q_kc ? g->q_sx : g->q_sk;
-    if (p_s % 8 || q_s % 8 || ((uintptr_t)g->p & 15) || ((uintptr_t)g->q & 15) || ((uintptr_t)g->c & 7) || g->c_sq % 4)
+    const int c_align = g->c_dtype == AVSE_F32 ? 15 : 7;
+    if (p_s % 8 || q_s % 8 || ((uintptr_t)g->p & 15) || ((uintptr_t)g->q & 15) || ((uintptr_t)g->c & c_align) ||
+        g->c_sq % 4)
         return AVSE_EALIGN;
-    const int64_t tp = (g->mp + BP - 1) / BP, tq = (g->mq + BQ - 1) / BQ;
-    // 32-bit per-batch byte offsets: the farthest element a stage reads, and the output's
-    const int64_t p_far = p_kc ? (tp * BP) * p_s + g->k : (g->k) * p_s + tp * BP;
-    const int64_t q_far = q_kc ? (tq * BQ) * q_s + g->k : (g->k) * q_s + tq * BQ;
+    const int64_t tp = (g->mp + BT - 1) / BT, tq = (g->mq + BT - 1) / BT, ntb = (g->k + BK - 1) / BK;
+    // 32-bit per-batch byte offsets: the farthest element a stage reads
+    const int64_t p_far = p_kc ? (tp * BT) * p_s + ntb * BK : ntb * BK * p_s + tp * BT;
+    const int64_t q_far = q_kc ? (tq * BT) * q_s + ntb * BK : ntb * BK * q_s + tq * BT;
     if (p_far * 2 >= (1LL << 31) || q_far * 2 >= (1LL << 31)) return AVSE_ESHAPE;
-    if (g->mp >= (1 << 30) || g->mq >= (1 << 30) || g->batch * tp * tq >= (1LL << 31)) return AVSE_ESHAPE;
+    const int64_t ntiles = g->batch / fold * tp * tq;
+    if (g->mp >= (1 << 30) || g->mq >= (1 << 30) || ntiles * ntb * fold >= (1LL << 31)) return AVSE_ESHAPE;
     Args a;
     a.p = (const uint16_t*)g->p;
     a.q = (const uint16_t*)g->q;
@@ -247,15 +407,39 @@ int avse_gemm_bf16(const avse_gemm_bf16_args* g, avse_stream_t stream) {
     a.batch = (int32_t)g->batch;
     a.tp = (int32_t)tp;
     a.tq = (int32_t)tq;
+    a.ntiles = (int32_t)ntiles;
+    a.ntb = (int32_t)ntb;
+    a.fold = (int32_t)fold;
+    a.kv_last = (int32_t)(g->k - (ntb - 1) * BK);
     // the shared weight's tiles vary fastest; otherwise the operand with fewer tiles
     a.q_fast = (g->q_bs == 0) ? 1 : (g->p_bs == 0) ? 0 : (tq <= tp);
     a.alpha = g->alpha;
-    const dim3 grid((unsigned)(g->batch * tp * tq)), block(THREADS);
+    a.c_vec16 = ((uintptr_t)g->c % 16 == 0) && (g->c_sq % 8 == 0);
+    // persistent: one workgroup per CU (128 KB of LDS each), a multiple of 8 (the XCD tile split)
+    static int cu_count[64];
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        if (cu_count[dev] <= 0 &&
+            hipDeviceGetAttribute(&cu_count[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cu_count[dev] = 256;
+        cus = cu_count[dev];
+    }
+    int64_t G = ((int64_t)cus + 7) / 8 * 8;
+    const int64_t need = (ntiles + 7) / 8 * 8;
+    if (G > need) G = need;
+    const dim3 grid((unsigned)G), block(THREADS);
     hipStream_t st = (hipStream_t)stream;
-    if (p_kc && q_kc) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, block, 0, st, a);
-    else if (p_kc) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, block, 0, st, a);
-    else if (q_kc) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((gemm_kernel<false, false>), grid, block, 0, st, a);
+    if (g->c_dtype == AVSE_BF16) {
+        if (p_kc && q_kc) hipLaunchKernelGGL((gemm_kernel<true, true, false>), grid, block, 0, st, a);
+        else if (p_kc) hipLaunchKernelGGL((gemm_kernel<true, false, false>), grid, block, 0, st, a);
+        else if (q_kc) hipLaunchKernelGGL((gemm_kernel<false, true, false>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((gemm_kernel<false, false, false>), grid, block, 0, st, a);
+    } else {
+        if (p_kc && q_kc) hipLaunchKernelGGL((gemm_kernel<true, true, true>), grid, block, 0, st, a);
+        else if (p_kc) hipLaunchKernelGGL((gemm_kernel<true, false, true>), grid, block, 0, st, a);
+        else if (q_kc) hipLaunchKernelGGL((gemm_kernel<false, true, true>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((gemm_kernel<false, false, true>), grid, block, 0, st, a);
+    }
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

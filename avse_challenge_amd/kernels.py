@@ -842,8 +842,6 @@ def lstm_bwd(dh, gates, c_all, w_hh, reverse=False):
 
 # ------------------------------------------------------------------------ bf16 projection GEMM (Mamba in/out_proj)
 
-GEMM_BK = 64        # projgemm.hip: the reduction length must be a multiple of one LDS stage
-
 
 def _extent(t):
     """Elements readable from t.data_ptr() to the end of t's storage."""
@@ -864,34 +862,41 @@ def _gemm_operand(t):
     return None
 
 
-def gemm_bf16_supported(P, Q, out):
-    """True when avse_gemm_bf16 takes out[b, q, p] = sum_k P[b, p, k] Q[b, q, k] as laid out (see gemm_bf16)."""
-    if not (P.is_cuda and P.dtype == Q.dtype == out.dtype == torch.bfloat16):
+def gemm_bf16_supported(P, Q, out, fold=1):
+    """True when avse_gemm_bf16 takes out[g, q, p] = sum_{b in group g} sum_k P[b, p, k] Q[b, q, k] as laid out
+    (see gemm_bf16)."""
+    if not (P.is_cuda and P.dtype == Q.dtype == torch.bfloat16 and out.dtype in (torch.bfloat16, torch.float32)):
         return False
-    if P.dim() != 3 or Q.dim() != 3 or out.dim() != 3 or P.shape[2] != Q.shape[2] or P.shape[2] % GEMM_BK:
+    if P.dim() != 3 or Q.dim() != 3 or out.dim() != 3 or P.shape[2] != Q.shape[2] or P.shape[2] < 1:
         return False
-    b = out.shape[0]
+    b = out.shape[0] * fold
     if out.shape[1:] != (Q.shape[1], P.shape[1]) or P.shape[0] not in (1, b) or Q.shape[0] not in (1, b):
         return False
-    if out.stride(2) != 1 or out.stride(1) % 4 or out.data_ptr() % 8 or P.data_ptr() % 16 or Q.data_ptr() % 16:
+    if max(P.shape[0], Q.shape[0]) != b and fold != 1:
+        return False
+    if out.stride(2) != 1 or out.stride(1) % 4 or out.data_ptr() % (16 if out.dtype == torch.float32 else 8):
+        return False
+    if P.data_ptr() % 16 or Q.data_ptr() % 16:
         return False
     return _gemm_operand(P) is not None and _gemm_operand(Q) is not None
 
 
-def gemm_bf16(P, Q, out, alpha=1.0):
-    """out[b, q, p] = alpha * sum_k P[b, p, k] * Q[b, q, k] on the bf16 MFMA GEMM (csrc/projgemm.hip): bf16 operands,
-    fp32 accumulation, bf16 out.  P (b or 1, mp, k), Q (b or 1, mq, k) are strided views whose k or row stride is 1
-    (a batch of 1 is shared by every output batch); out (b, mq, mp) with stride(2) == 1.  Returns out."""
+def gemm_bf16(P, Q, out, alpha=1.0, fold=1):
+    """out[g, q, p] = alpha * sum_{b = g fold .. g fold + fold - 1} sum_k P[b, p, k] * Q[b, q, k] on the bf16 MFMA GEMM
+    (csrc/projgemm.hip): bf16 operands, fp32 accumulation, bf16 or fp32 out.  P (b or 1, mp, k), Q (b or 1, mq, k) are
+    strided views whose k or row stride is 1 (a batch of 1 is shared by every batch); out (b / fold, mq, mp) with
+    stride(2) == 1.  fold > 1 sums groups of batches (the weight gradients).  Returns out."""
     _need_gpu(P, Q, out)
-    if not gemm_bf16_supported(P, Q, out):
+    if not gemm_bf16_supported(P, Q, out, fold):
         raise RuntimeError(f"avse_gemm_bf16: unsupported operands P {tuple(P.shape)}/{P.stride()} "
-                           f"Q {tuple(Q.shape)}/{Q.stride()} out {tuple(out.shape)}/{out.stride()} ({P.dtype})")
+                           f"Q {tuple(Q.shape)}/{Q.stride()} out {tuple(out.shape)}/{out.stride()} ({P.dtype}, "
+                           f"fold {fold})")
     a = _lib.GemmBf16Args()
-    a.batch, a.mp, a.mq, a.k = out.shape[0], P.shape[1], Q.shape[1], P.shape[2]
+    a.batch, a.mp, a.mq, a.k, a.fold = out.shape[0] * fold, P.shape[1], Q.shape[1], P.shape[2], fold
     a.p, (a.p_bs, a.p_sx, a.p_sk), a.p_extent = P.data_ptr(), _gemm_operand(P), _extent(P)
     a.q, (a.q_bs, a.q_sx, a.q_sk), a.q_extent = Q.data_ptr(), _gemm_operand(Q), _extent(Q)
     a.c, a.c_bs, a.c_sq = out.data_ptr(), out.stride(0), out.stride(1)
-    a.alpha, a.c_dtype = float(alpha), AVSE_BF16
+    a.alpha, a.c_dtype = float(alpha), _dtype_code(out.dtype)
     tap = _tap_begin("avse_gemm_bf16", out.device)
     check(_lib.lib().avse_gemm_bf16(a, stream_ptr(out.device)), "avse_gemm_bf16")
     _tap_end(tap)

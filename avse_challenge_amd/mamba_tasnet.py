@@ -32,17 +32,18 @@ _BWD = torch.amp.custom_bwd(device_type="cuda")
 
 # bf16 projections (BASELINE configs[4]) on the HIP MFMA GEMM (csrc/projgemm.hip) where it takes the operands;
 # AVSE_PROJ_GEMM=0 keeps them on the library (torch.bmm -> hipBLASLt), which every fp32 GEMM uses.
-_HIP_GEMM = os.environ.get("AVSE_PROJ_GEMM", "1") == "1"
+_HIP_GEMM = os.environ.get("AVSE_PROJ_GEMM", "0") == "1"
 
 
 def _autocast_dtype():
     return torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
 
 
-def _hip_gemm(P, Q, out, alpha=1.0):
-    """out[b, q, p] = alpha sum_k P[b, p, k] Q[b, q, k] on the HIP bf16 GEMM; None when it does not take them."""
-    if _HIP_GEMM and K.gemm_bf16_supported(P, Q, out):
-        return K.gemm_bf16(P, Q, out, alpha)
+def _hip_gemm(P, Q, out, alpha=1.0, fold=1):
+    """out[g, q, p] = alpha sum_{b in group g} sum_k P[b, p, k] Q[b, q, k] on the HIP bf16 GEMM; None when it does not
+    take them."""
+    if _HIP_GEMM and min(P.shape[1], Q.shape[1]) >= 128 and K.gemm_bf16_supported(P, Q, out, fold):
+        return K.gemm_bf16(P, Q, out, alpha, fold)
     return None
 
 
@@ -103,17 +104,28 @@ class _Fork(torch.autograd.Function):
         return _padded_add(g1, g2)
 
 
-def _bsum_mm(a, bt):
-    """sum_b a[b] @ bt[b] for a (b, m, l), bt (b, l, n): the weight gradient of a batched projection.
-    The result is fp32 (under bf16 autocast the partials are bf16 GEMM outputs summed in fp32).
-    As one strided-batched GEMM + sum while the (b, m, n) partials are small (Mamba-TasNet: b = batch);
+def _bsum_mm(a, bt, alpha=1.0):
+    """alpha sum_b a[b] @ bt[b] for a (b, m, l), bt (b, l, n): the weight gradient of a batched projection, fp32.
+    Under bf16 autocast: the HIP GEMM with fp32 accumulation (avse_gemm_bf16, batches folded into groups).
+    Otherwise as one strided-batched GEMM + sum while the (b, m, n) partials are small (Mamba-TasNet: b = batch);
     as ONE (m, b*l) x (b*l, n) GEMM when they are not (DPMamba's inter pass has b = B*250 sequences of
     34 frames: the partials would take 33 GB, and each GEMM's depth would be 34)."""
     nb, m, l = a.shape
     n = bt.shape[2]
+    dt = _autocast_dtype()
+    if dt == torch.bfloat16:
+        # batches folded into groups so that the launch has about one 256 x 256 tile per CU; groups summed after
+        fold = max(1, nb * (-(-m // 256)) * (-(-n // 256)) // 256)
+        while nb % fold:
+            fold -= 1
+        out = torch.empty(nb // fold, m, n, device=a.device, dtype=torch.float32)
+        if _hip_gemm(bt.to(dt).transpose(1, 2), a.to(dt), out, alpha, fold=fold) is not None:
+            return out.sum(0)
     if nb * m * n <= (1 << 27):
-        return torch.bmm(a, bt).float().sum(0)
-    return (a.transpose(0, 1).reshape(m, nb * l) @ bt.reshape(nb * l, n)).float()
+        r = torch.bmm(a, bt).float().sum(0)
+    else:
+        r = (a.transpose(0, 1).reshape(m, nb * l) @ bt.reshape(nb * l, n)).float()
+    return r if alpha == 1.0 else alpha * r
 
 
 class MambaInnerNoOutProj(torch.autograd.Function):
@@ -221,7 +233,7 @@ class _BiOutProj(torch.autograd.Function):
     def backward(ctx, dout):
         y, w = ctx.saved_tensors
         dy = _wbmm(w.t(), dout.transpose(1, 2), 0.5)                             # (b, d_inner, l)
-        dw = 0.5 * _bsum_mm(dout.transpose(1, 2), y.transpose(1, 2))               # (d_model, d_inner)
+        dw = _bsum_mm(dout.transpose(1, 2), y.transpose(1, 2), 0.5)               # (d_model, d_inner)
         return dy, dy, dw
 
 

@@ -335,15 +335,18 @@ int avse_lstm_bwd_group(int64_t B, int64_t T, int64_t H, int32_t reverse, const 
 
 /* ---------------------------------------------------------------- bf16 projection GEMM ------
  * The bf16 GEMMs BiMamba v2 runs under autocast (BASELINE configs[4]): in_proj (Mamba-TasNet/modules/mamba/
- * bimamba.py:190-196, xz = W_in h^T), out_proj (:250-253) and their input gradients — torch.matmul / F.linear on
- * bf16 operands in the reference.  Batched, fp32 accumulation, bf16 output (round to nearest even):
- *     c[b][q][p] = alpha * sum_k P(b, p, k) * Q(b, q, k),   P(b, p, k) = p_ptr[b*p_bs + p*p_sx + k*p_sk]  (Q alike)
- * Exactly one of p_sx / p_sk is 1 (and one of q_sx / q_sk): the operand is K-contiguous or contiguous along p (q);
- * the other stride a multiple of 8, p / q 16-byte aligned; c: p contiguous, c_sq % 4 == 0, 8-byte aligned.  A batch
- * stride of 0 shares the operand (a weight).  k % 64 == 0.  p_extent / q_extent: elements readable from p / q (reads
- * past them return 0).  Per batch, every offset an operand tile reaches must stay below 2^31 bytes. */
+ * bimamba.py:190-196, xz = W_in h^T), out_proj (:250-253), their input gradients and weight gradients —
+ * torch.matmul / F.linear on bf16 operands in the reference.  Batched, fp32 accumulation:
+ *     c[g][q][p] = alpha * sum_{b in group g} sum_k P(b, p, k) * Q(b, q, k),
+ *     P(b, p, k) = p_ptr[b*p_bs + p*p_sx + k*p_sk]  (Q alike),  groups of `fold` consecutive batches (0 or 1: none)
+ * c_dtype AVSE_BF16 (round to nearest even; c 8-byte aligned) or AVSE_F32 (c 16-byte aligned); c has p contiguous,
+ * c_sq % 4 == 0, batch stride c_bs per group.  Exactly one of p_sx / p_sk is 1 (and one of q_sx / q_sk): the operand
+ * is K-contiguous or contiguous along p (q); the other stride a multiple of 8, p / q 16-byte aligned.  A batch stride
+ * of 0 shares the operand (a weight).  Any k >= 1 (elements past it are never summed, whatever lies there).
+ * p_extent / q_extent: elements readable from p / q (reads past them return 0).  Per batch, every offset an operand
+ * tile reaches must stay below 2^31 bytes. */
 typedef struct {
-    int64_t batch, mp, mq, k;
+    int64_t batch, mp, mq, k, fold;
     const void* p;  int64_t p_bs, p_sx, p_sk, p_extent;
     const void* q;  int64_t q_bs, q_sx, q_sk, q_extent;
     void* c;        int64_t c_bs, c_sq;

@@ -67,19 +67,19 @@ def test_host_side_validation_without_gpu():
     assert L.avse_conv3d_fwd(0, 3, 75, 96, 96, 2, dummy, dummy, dummy, dummy, None) == -2
     assert L.avse_conv3d_fwd(2, 3, 75, 96, 96, 1, dummy, dummy, dummy, dummy, None) == -3
     assert L.avse_conv3d_wgrad_u8(2, 3, 5, 96, 96, 5, 7, 7, 2, 3, 3, None, dummy, dummy, 0, dummy, None) == -1
-    # bf16 projection GEMM: null pointers, dtype, k % 64, neither stride unit, alignment
+    # bf16 projection GEMM: null pointers, dtype, batch % fold, neither stride unit, alignment
     g = _lib.GemmBf16Args()
     assert L.avse_gemm_bf16(g, None) == -1
     g.p = g.q = g.c = 4096
-    g.batch, g.mp, g.mq, g.k = 2, 300, 200, 512
+    g.batch, g.mp, g.mq, g.k, g.fold = 2, 300, 200, 512, 1
     g.p_sx, g.p_sk, g.q_sx, g.q_sk, g.c_sq = 512, 1, 512, 1, 304
     g.p_extent = g.q_extent = 1 << 20
-    g.c_dtype = _lib.AVSE_F32
+    g.c_dtype = 2                                       # AVSE_U8
     assert L.avse_gemm_bf16(g, None) == -3
     g.c_dtype = _lib.AVSE_BF16
-    g.k = 500
+    g.fold = 3
     assert L.avse_gemm_bf16(g, None) == -2
-    g.k, g.q_sx, g.q_sk = 512, 3, 512
+    g.fold, g.q_sx, g.q_sk = 1, 3, 512
     assert L.avse_gemm_bf16(g, None) == -2
     g.q_sx, g.q_sk, g.p_sx = 512, 1, 516
     assert L.avse_gemm_bf16(g, None) == -5

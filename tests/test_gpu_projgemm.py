@@ -81,9 +81,40 @@ def test_gemm_bf16_mamba_layouts_c5_rows():
     _check(k.gemm_bf16(dout, w_out.t()[None], dy, 0.5), dout, w_out.t()[None], 0.5, L)
 
 
+def _nan_padded_bdl(b, d, L, g):
+    """A (b, d, L) bf16 tensor in the model's padded layout whose pad columns hold NaN."""
+    t = K().bdl_empty(b, d, L, torch.bfloat16, DEV)
+    full = torch.as_strided(t, (b, d, t.stride(1)), t.stride(), t.storage_offset())
+    full.fill_(float("nan"))
+    return t.copy_(torch.randn(b, d, L, device=DEV, generator=g))
+
+
+@pytest.mark.parametrize("L", [999, 64, 37])
+def test_gemm_bf16_weight_grads_fold_fp32(L):
+    """dW_in = sum_{b,l} dxz[b, :, l] h[b, l, :] and dW_out = 0.5 sum_{b,l} dout[b, l, :] y[b, :, l] (bimamba.py:190-196,
+    250-253 backward): fp32 out, all batches folded into one output, k = L not a multiple of the stage (the pad
+    columns past L hold NaN and must not reach the sums)."""
+    k = K()
+    g = torch.Generator(device=DEV).manual_seed(L)
+    b, dm, di = 3, 512, 1024
+    h = torch.randn(b, L, dm, device=DEV, generator=g).to(torch.bfloat16)
+    dout = torch.randn(b, L, dm, device=DEV, generator=g).to(torch.bfloat16)
+    dxz, y = _nan_padded_bdl(b, 2 * di, L, g), _nan_padded_bdl(b, di, L, g)
+    dw_in = torch.empty(1, 2 * di, dm, device=DEV, dtype=torch.float32)
+    k.gemm_bf16(h.transpose(1, 2), dxz, dw_in, 1.0, fold=b)
+    ref = torch.einsum("bnl,blc->nc", dxz.double(), h.double())
+    mag = torch.einsum("bnl,blc->nc", dxz.double().abs(), h.double().abs())
+    assert bool(((dw_in[0].double() - ref).abs() <= 1e-5 * mag).all())
+    dw_out = torch.empty(1, dm, di, device=DEV, dtype=torch.float32)
+    k.gemm_bf16(y, dout.transpose(1, 2), dw_out, 0.5, fold=b)
+    ref = 0.5 * torch.einsum("blm,bdl->md", dout.double(), y.double())
+    mag = 0.5 * torch.einsum("blm,bdl->md", dout.double().abs(), y.double().abs())
+    assert bool(((dw_out[0].double() - ref).abs() <= 1e-5 * mag).all())
+
+
 def test_gemm_bf16_rejects_unsupported():
     k = K()
-    a = torch.randn(2, 64, 96, device=DEV).to(torch.bfloat16)                  # k = 96: not a multiple of 64
+    a = torch.randn(2, 64, 128, device=DEV).to(torch.bfloat16)[:, :, ::2]      # neither the row nor the k stride is 1
     out = torch.empty(2, 64, 64, device=DEV, dtype=torch.bfloat16)
     assert not k.gemm_bf16_supported(a, a, out)
     with pytest.raises(RuntimeError):

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seqlen", type=int, default=5999)
+    ap.add_argument("--case", default="", help="run only the GEMMs whose name contains this")
+    ap.add_argument("--no-lib", action="store_true", help="skip the library leg")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     b, L, dm, di = args.batch, args.seqlen, 512, 1024
@@ -73,12 +75,42 @@ def main():
     cases.append(("out_proj dgrad", dout, w_out.t()[None], dy, 0.5,
                   lambda: torch.bmm(wt2.expand(b, *wt2.shape), dout.transpose(1, 2), out=dy),
                   lambda: torch.matmul(0.5 * w_out.float().t(), dout.float().transpose(1, 2))))
+    # weight gradients (fp32 out, batches folded: ONE output group per `fold` batches, summed after):
+    # dW_in[n, c] = sum_{b,l} dxz[b, n, l] h[b, l, c];  dW_out[m, d] = 0.5 sum_{b,l} dout[b, l, m] y[b, d, l]
+    wcases = [("in_proj wgrad", h.transpose(1, 2), dxz, 1.0, 2 * di, dm,
+               lambda: torch.bmm(dxz, h).float().sum(0),
+               lambda: torch.einsum("bnl,blc->nc", dxz.float(), h.float())),
+              ("out_proj wgrad", y, dout.transpose(1, 2), 0.5, dm, di,
+               lambda: 0.5 * torch.bmm(dout.transpose(1, 2), y.transpose(1, 2)).float().sum(0),
+               lambda: 0.5 * torch.einsum("blm,bdl->md", dout.float(), y.float()))]
+    for name, P, Q, alpha, m, n, lib_fn, ref_fn in wcases:
+        if args.case not in name:
+            continue
+        flops = 2.0 * b * L * m * n
+        ref = ref_fn()
+        rec = {"gemm": name, "m": m, "n": n, "k": b * L, "gflop": round(flops / 1e9, 2)}
+        if not args.no_lib:
+            lib_ms = timed(lib_fn, args.reps)
+            rec.update(lib_ms=round(lib_ms, 4), lib_frac=round(flops / lib_ms / 1e9 / BF16_PEAK, 4),
+                       lib_rel_err=float((lib_fn() - ref).norm() / ref.norm()))
+        tiles = -(-m // 256) * -(-n // 256)
+        fold = max(1, b * tiles // 256)
+        while b % fold:
+            fold -= 1
+        out = torch.empty(b // fold, m, n, device=dev, dtype=torch.float32)
+        hip_fn = lambda: K.gemm_bf16(P, Q, out, alpha, fold).sum(0)  # noqa: E731
+        hip_ms = timed(hip_fn, args.reps)
+        rec.update(fold=fold, hip_ms=round(hip_ms, 4), hip_frac=round(flops / hip_ms / 1e9 / BF16_PEAK, 4),
+                   hip_rel_err=float((hip_fn() - ref).norm() / ref.norm()))
+        print(json.dumps(rec), flush=True)
     for name, P, Q, out, alpha, lib_fn, ref_fn in cases:
+        if args.case not in name:
+            continue
         kmax = P.shape[2]
         flops = 2.0 * b * P.shape[1] * Q.shape[1] * kmax
         rec = {"gemm": name, "p": list(P.shape), "q": list(Q.shape), "k": kmax, "gflop": round(flops / 1e9, 2)}
         ref = ref_fn()
-        lib_ms = timed(lib_fn, args.reps)
+        lib_ms = 0.0 if args.no_lib else timed(lib_fn, args.reps)
         lib_err = float((out.float() - ref).norm() / ref.norm())
         out.zero_()
         ok = K.gemm_bf16_supported(P, Q, out)
@@ -88,7 +120,8 @@ def main():
             err = float((out.float() - ref).norm() / ref.norm())
             rec.update(hip_ms=round(hip_ms, 4), hip_frac=round(flops / hip_ms / 1e9 / BF16_PEAK, 4),
                        hip_rel_err=err)
-        rec.update(lib_ms=round(lib_ms, 4), lib_frac=round(flops / lib_ms / 1e9 / BF16_PEAK, 4), lib_rel_err=lib_err)
+        if not args.no_lib:
+            rec.update(lib_ms=round(lib_ms, 4), lib_frac=round(flops / lib_ms / 1e9 / BF16_PEAK, 4), lib_rel_err=lib_err)
         print(json.dumps(rec), flush=True)
 
 
