@@ -446,11 +446,14 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd_kernel(int row0, int C
 
 // The backward pass with 4 consecutive elements per thread and dwordx4 tap loads (dil % 4 == 0, so every tap
 // quadruple is either wholly before the row or starts inside it; the row's tail is clipped dword by dword by the
-// buffer range check): 4x fewer VMEM instructions than the scalar form, which was VMEM-issue bound (10 dword
-// accesses per element: 3 taps of y1 and dy, 3 of x, the dx store).  Same per-element arithmetic and tap order.
+// buffer range check).  y1 is NOT read: at each of the P tap positions it is recomputed from x with the forward's
+// exact arithmetic (dwconv_stats_kernel: acc = 0, then += w_m x_m for m = 0..P-1), from the 2P - 1 x quadruples
+// t + (m - k) dil that also serve the dW taps, so this pass moves x + dy + dx (12 B per element) instead of
+// x + y1 + dy + dx (16): the x quadruples of the neighbouring taps come from the lines this row's workgroup just
+// loaded.  Same per-element arithmetic and tap order as the y1-reading form.
 template <int P>
 __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int C, int K, int dil, const float* __restrict__ x,
-                                                                  const float* __restrict__ w, const float* __restrict__ y1,
+                                                                  const float* __restrict__ w,
                                                                   const float* __restrict__ alpha,
                                                                   const float* __restrict__ gamma,
                                                                   const float2* __restrict__ stats,
@@ -458,10 +461,11 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int 
                                                                   const float* __restrict__ dy, float* __restrict__ dx,
                                                                   float* __restrict__ ws_dw, float* __restrict__ ws_alpha) {
     constexpr int V = 4, UB = 2;                  // 4 consecutive elements per thread, 2 quadruples in flight
+    constexpr int H = (P - 1) / 2, NX = 2 * P - 1;
     __shared__ float red[THREADS / 64][DW_MAXP + 1];
     __shared__ double dred[8];
     const int row = row0 + second_pass_row(), b = row / C, c = row % C;
-    const int halo = (P - 1) / 2 * dil;
+    const int halo = H * dil;
     const float a = alpha[0];
     const float2 st = stats[b];
     const double2 sg12 = sample_sums(ws_rows, b, C, dred, gamma);
@@ -469,7 +473,6 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int 
     const float2 sm = make_float2((float)(sg12.x / nn), (float)(sg12.y / nn));
     const float gm = gamma[c];
     const float* xr = x + (int64_t)row * K;
-    const float* yr = y1 + (int64_t)row * K;
     const float* gr = dy + (int64_t)row * K;
     float* dr = dx + (int64_t)row * K;
     float wk[P], dw[P], da = 0.f;
@@ -478,9 +481,19 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int 
         wk[k] = w[c * P + k];
         dw[k] = 0.f;
     }
-    const auto rx = make_rsrc(xr, K), ry = make_rsrc(yr, K), rg = make_rsrc(gr, K), rd = make_rsrc(dr, K);
+    const auto rx = make_rsrc(xr, K), rg = make_rsrc(gr, K), rd = make_rsrc(dr, K);
     for (int t0 = 0; t0 < K; t0 += UB * V * THREADS) {
         float acc[UB][V], gown[UB][V];
+        float4 xq[UB][NX];                        // x at t + (i - (P - 1)) dil, i = 0 .. 2P - 2
+        float4 gq[UB][P];                         // dy at the tap positions u_k = t + halo - k dil
+#pragma unroll
+        for (int j = 0; j < UB; ++j) {
+            const int t = t0 + (j * THREADS + (int)threadIdx.x) * V;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) xq[j][i] = ld4(rx, t + (i - (P - 1)) * dil);
+#pragma unroll
+            for (int k = 0; k < P; ++k) gq[j][k] = ld4(rg, t + halo - k * dil);
+        }
 #pragma unroll
         for (int j = 0; j < UB; ++j) {
             const int t = t0 + (j * THREADS + (int)threadIdx.x) * V;
@@ -489,25 +502,24 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int 
 #pragma unroll
             for (int k = 0; k < P; ++k) {
                 const int u = t + halo - k * dil;
-                const float4 y4 = ld4(ry, u), g4 = ld4(rg, u);
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
-                    const float yv = f4at(y4, e), gv = f4at(g4, e);
+                    // y1(u + e) = sum_m w_m x(u + e + m dil - halo) = sum_m w_m xq[(P - 1) + m - k]
+                    float yv = 0.f;
+#pragma unroll
+                    for (int m = 0; m < P; ++m) yv += wk[m] * f4at(xq[j][P - 1 + m - k], e);
+                    const float gv = f4at(gq[j][k], e);
                     const float xh = (prelu(yv, a) - st.x) * st.y;
                     float dp = st.y * (gv * gm - sm.x - xh * sm.y);
                     dp = (u + e >= 0 && u + e < K) ? dp : 0.f;
                     const float gk = yv > 0.f ? dp : a * dp;
                     acc[j][e] += wk[k] * gk;
-                    if (k == (P - 1) / 2) {
+                    if (k == H) {
                         gown[j][e] = gk;          // 0 past the row's end (dp masked)
                         if (yv <= 0.f) da += dp * yv;
                     }
                 }
             }
-        }
-#pragma unroll
-        for (int j = 0; j < UB; ++j) {
-            const int t = t0 + (j * THREADS + (int)threadIdx.x) * V;
             if (t + V <= K) {
                 const u4_t o = {__float_as_uint(acc[j][0]), __float_as_uint(acc[j][1]), __float_as_uint(acc[j][2]),
                                 __float_as_uint(acc[j][3])};
@@ -520,9 +532,9 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int 
 #pragma unroll
             for (int k = 0; k < P; ++k) {
                 const int q = t + k * dil - halo;     // x taps outside the row are zero padding
-                const float4 x4 = ld4(rx, q);
 #pragma unroll
-                for (int e = 0; e < V; ++e) dw[k] += (q + e >= 0 && q + e < K) ? gown[j][e] * f4at(x4, e) : 0.f;
+                for (int e = 0; e < V; ++e)
+                    dw[k] += (q + e >= 0 && q + e < K) ? gown[j][e] * f4at(xq[j][P - 1 + k - H], e) : 0.f;
             }
         }
     }
@@ -729,8 +741,7 @@ int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
                               (int)dil, x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, \
                               ws_a)
 #define L4_(PP) hipLaunchKernelGGL(dwconv_gln_bwd4_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, \
-                               (int)dil, x, w, y1, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, \
-                               ws_dw, ws_a)
+                               (int)dil, x, w, alpha, gamma, (const float2*)stats, (const float2*)ws, dy, dx, ws_dw, ws_a)
     if (dil % 4 == 0) {
         AVSE_DW_P_SWITCH(P, L4_)
     } else {

@@ -42,12 +42,25 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) s4_t lds_s4_t;
 
-constexpr int BT = 256, BK = 32, THREADS = 512, WAVES = THREADS / 64;
-constexpr int IMG = BT * BK * 2;           // one operand's image of one stage: 16 KB
+#ifndef AVSE_PG_BK
+#define AVSE_PG_BK 32
+#endif
+#ifndef AVSE_PG_NBUF
+#define AVSE_PG_NBUF 4
+#endif
+constexpr int BT = 256, THREADS = 512, WAVES = THREADS / 64;
+constexpr int BK = AVSE_PG_BK;             // k per stage (32 or 64)
+constexpr int IMG = BT * BK * 2;           // one operand's image of one stage
 constexpr int STAGE = 2 * IMG;
-constexpr int NBUF = 4, AHEAD = 3;         // LDS ring; stages in flight ahead of the one computed
-constexpr int PIECES = IMG / 1024 / WAVES; // LDS-DMA wave-instructions per operand, stage and wave (2)
+constexpr int NBUF = AVSE_PG_NBUF, AHEAD = NBUF - 1;   // LDS ring; stages in flight ahead of the one computed
+constexpr int PIECES = IMG / 1024 / WAVES; // LDS-DMA wave-instructions per operand, stage and wave
 constexpr int LOADS = 2 * PIECES;          // per stage and wave
+// K-contiguous image: rows of RB bytes (CPR 16-B chunks), RPL rows per 256-B bank line
+constexpr int RB = 2 * BK, CPR = BK / 8, RPL = 256 / RB;
+static_assert(NBUF * STAGE <= 160 * 1024, "LDS");
+static_assert(AHEAD >= 1 && AHEAD <= 4, "ring depth");
+
+__device__ inline int kc_swz(int row) { return (row / RPL) % CPR; }
 
 struct Args {
     const uint16_t* p;
@@ -108,24 +121,31 @@ __device__ inline Tile tile_of(const Args& a, int T) {
 // One operand's stage (BK k x 256 rows) -> LDS image.  KC: the operand is K-contiguous (row x0 + r has stride sx, k
 // is contiguous); otherwise k-row k0 + r has stride sx and the 256 rows are contiguous.  Rows past mx are clamped
 // (KC) or read whatever lies there / 0 past the buffer (MN); they only feed outputs that are never stored.
+// piece_offsets: this lane's byte offsets of its PIECES wave-instructions for k0 = 0; stage kt adds kt * stage_step.
 template <bool KC>
-__device__ inline void stage_load(i4_t r, uint32_t img, int x0, int k0, int sx, int mx, int wave, int lane) {
+__device__ inline void piece_offsets(uint32_t (&vo)[PIECES], int x0, int sx, int mx, int wave, int lane) {
 #pragma unroll
     for (int j = 0; j < PIECES; ++j) {
         const int piece = wave * PIECES + j;                  // 1 KB of the image per wave-instruction
-        uint32_t voff;
         if constexpr (KC) {
-            const int row = piece * 16 + (lane >> 2);
+            const int row = piece * (1024 / RB) + lane / CPR;
             const int xr = min(x0 + row, mx - 1);
-            const int c = (lane & 3) ^ ((row >> 2) & 3);
-            voff = (uint32_t)(xr * sx + k0 + c * 8) * 2u;
+            const int c = (lane % CPR) ^ kc_swz(row);
+            vo[j] = (uint32_t)(xr * sx + c * 8) * 2u;
         } else {
             const int krow = piece * 2 + (lane >> 5);
             const int c = (lane & 31) ^ ((krow & 3) << 2);
-            voff = (uint32_t)((k0 + krow) * sx + x0 + c * 8) * 2u;
+            vo[j] = (uint32_t)(krow * sx + x0 + c * 8) * 2u;
         }
-        dma16(r, img + piece * 1024, voff);
     }
+}
+template <bool KC>
+__device__ inline uint32_t stage_step(int sx) { return KC ? (uint32_t)(BK * 2) : (uint32_t)(BK * sx * 2); }
+
+template <bool KC>
+__device__ inline void stage_load(i4_t r, uint32_t img, const uint32_t (&vo)[PIECES], uint32_t koff, int wave) {
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) dma16(r, img + (wave * PIECES + j) * 1024, vo[j] + koff);
 }
 
 // The 32 x 16 (row x k) MFMA operand fragment of rows rb .. rb + 31, k-substep s (k = 16 s .. 16 s + 15):
@@ -135,7 +155,7 @@ __device__ inline bf16x8 frag_raw(const uint8_t* img, int rb, int s, int lane) {
     if constexpr (KC) {
         const int row = rb + (lane & 31);
         const int ch = 2 * s + (lane >> 5);
-        return *reinterpret_cast<const bf16x8*>(img + row * 64 + 16 * (ch ^ ((row >> 2) & 3)));
+        return *reinterpret_cast<const bf16x8*>(img + row * RB + 16 * (ch ^ kc_swz(row)));
     } else {
         const int g = lane >> 4, i = lane & 15;
         const int col = rb + 16 * (g & 1) + 4 * (i & 3);
@@ -154,15 +174,15 @@ __device__ inline bf16x8 frag_raw(const uint8_t* img, int rb, int s, int lane) {
 
 // Zero the k >= kv part of one operand's stage image (the reduction's last, partial stage: what lies past k is
 // another row's data, pad columns or 0, and a non-finite value there must not reach the sums as 0 * inf), so both
-// operands are cleared.  KC image: 16-B chunk c of row r (k = 8 c .. 8 c + 7) at c ^ ((r >> 2) & 3); MN image: whole
+// operands are cleared.  KC image: 16-B chunk c of row r (k = 8 c .. 8 c + 7) at c ^ kc_swz(r); MN image: whole
 // k-rows.
 template <bool KC>
 __device__ inline void zero_tail(uint8_t* img, int kv, int tid) {
     if constexpr (KC) {
-        for (int i = tid; i < BT * 4; i += THREADS) {
-            const int row = i >> 2, pos = i & 3, c = pos ^ ((row >> 2) & 3);
+        for (int i = tid; i < BT * CPR; i += THREADS) {
+            const int row = i / CPR, pos = i % CPR, c = pos ^ kc_swz(row);
             if (8 * c + 8 <= kv) continue;
-            s8_t* ptr = reinterpret_cast<s8_t*>(img + row * 64 + 16 * pos);
+            s8_t* ptr = reinterpret_cast<s8_t*>(img + row * RB + 16 * pos);
             s8_t w = *ptr;
 #pragma unroll
             for (int e = 0; e < 8; ++e) w[e] = (8 * c + e < kv) ? w[e] : (short)0;
@@ -185,23 +205,29 @@ __device__ inline uint32_t pack_bf16x2(float a, float b) {
 
 // Wave (wr, wc) = (wave >> 2, wave & 3) owns the p blocks 32 (2 i + wr), i = 0..3 (so an epilogue round i covers the
 // 64 contiguous p of 64 i .. 64 i + 63 over both wave rows) and the q columns 64 wc .. 64 wc + 63.
+struct Frags {
+    bf16x8 a[4], b[2];
+};
 template <bool P_KC, bool Q_KC>
-__device__ inline void mma_stage(floatx16 (&acc)[4][2], const uint8_t* img, int wr, int wq, int lane) {
+__device__ inline void read_frags(Frags& f, const uint8_t* img, int ks, int wr, int wq, int lane) {
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-        bf16x8 fa[4], fb[2];
+    for (int i = 0; i < 4; ++i) f.a[i] = frag_raw<P_KC>(img, 32 * (2 * i + wr), ks, lane);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = frag_raw<P_KC>(img, 32 * (2 * i + wr), ks, lane);
+    for (int j = 0; j < 2; ++j) f.b[j] = frag_raw<Q_KC>(img + IMG, wq + 32 * j, ks, lane);
+}
+__device__ inline void mma(floatx16 (&acc)[4][2], const Frags& f) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j] = frag_raw<Q_KC>(img + IMG, wq + 32 * j, ks, lane);
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
 }
 
+// Pipeline (one barrier per stage).  Stage s is certified readable by the barrier of iteration s - 1 (its DMAs'
+// counted vmcnt wait precedes that barrier), so its first k-substep's fragments are read at the end of iteration s - 1,
+// across the barrier, and iteration s starts on MFMAs.  Iteration s: wait for stage s + 1's DMAs -> barrier (also: every
+// wave has finished reading stage s - 1) -> DMA stage s + AHEAD into stage s - 1's buffer -> MFMAs of stage s with the
+// next substep's / stage's fragment reads interleaved.  Before the barrier each wave's reads of the stage leaving the
+// ring have completed: an lgkmcnt(0) sits between the last read of stage s and the first prefetch read of stage s + 1.
 template <bool P_KC, bool Q_KC, bool OUT_F32>
 __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * STAGE];
@@ -214,36 +240,65 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
     const int my_tiles = base < a.ntiles ? (a.ntiles - base + G - 1) / G : 0;
     const int per_tile = a.ntb * a.fold;
     const int total = my_tiles * per_tile;
+    if (total == 0) return;                                    // workgroup-uniform: no barrier is skipped by part
     const int wr = wave >> 2, wc = wave & 3, wq = wc * 64;
     const uint32_t lds0 = lds_u32(lds);
+    const uint32_t p_step = stage_step<P_KC>(a.p_sx), q_step = stage_step<Q_KC>(a.q_sx);
 
     // load cursor: the stage issued next = (tile ld_T, batch ld_f of its group, k-stage ld_kt)
     int ld_s = 0, ld_kt = 0, ld_f = 0, ld_T = base;
-    Tile ld_tile = tile_of(a, base);
+    uint32_t vp[PIECES], vq[PIECES];
     i4_t rp, rq;
-    auto set_rsrc = [&](int b) {
+    auto set_tile = [&](int T, int f) {
+        const Tile t = tile_of(a, T);
+        const int b = t.b * a.fold + f;
         rp = rsrc_from(a.p + (int64_t)b * a.p_bs, a.p_ext - (int64_t)b * a.p_bs);
         rq = rsrc_from(a.q + (int64_t)b * a.q_bs, a.q_ext - (int64_t)b * a.q_bs);
+        piece_offsets<P_KC>(vp, t.p0, a.p_sx, a.mp, wave, lane);
+        piece_offsets<Q_KC>(vq, t.q0, a.q_sx, a.mq, wave, lane);
     };
-    if (total > 0) set_rsrc(ld_tile.b * a.fold);
+    set_tile(base, 0);
     auto issue = [&]() {
         if (ld_s >= total) return;
         const uint32_t img = lds0 + (ld_s % NBUF) * STAGE;
-        stage_load<P_KC>(rp, img, ld_tile.p0, ld_kt * BK, a.p_sx, a.mp, wave, lane);
-        stage_load<Q_KC>(rq, img + IMG, ld_tile.q0, ld_kt * BK, a.q_sx, a.mq, wave, lane);
+        stage_load<P_KC>(rp, img, vp, ld_kt * p_step, wave);
+        stage_load<Q_KC>(rq, img + IMG, vq, ld_kt * q_step, wave);
         ++ld_s;
         if (++ld_kt == a.ntb) {
             ld_kt = 0;
             if (++ld_f == a.fold) {
                 ld_f = 0;
                 ld_T += G;
-                if (ld_s < total) ld_tile = tile_of(a, ld_T);
             }
-            if (ld_s < total) set_rsrc(ld_tile.b * a.fold + ld_f);
+            if (ld_s < total) set_tile(ld_T, ld_f);
         }
     };
+    // stage s's position in its tile: partial (masked) stage?  (k-stage index = s % ntb)
+    auto masked = [&](int st) { return a.kv_last < BK && (st % a.ntb) == a.ntb - 1; };
+    auto wait_landed = [&](int st) {   // stage st's DMAs done: only the stages issued after it may still fly
+        const int after = ld_s - st - 1;
+        if (AHEAD >= 4 && after >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LOADS) : "memory");
+        else if (AHEAD >= 3 && after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+        else if (AHEAD >= 2 && after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto barrier = [&]() {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    auto zero_stage = [&](int st) {    // after the barrier that certified stage st; ends with a barrier
+        uint8_t* img = lds + (st % NBUF) * STAGE;
+        zero_tail<P_KC>(img, a.kv_last, threadIdx.x);
+        zero_tail<Q_KC>(img + IMG, a.kv_last, threadIdx.x);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier();
+    };
+
 #pragma unroll
     for (int i = 0; i < AHEAD; ++i) issue();
+    wait_landed(0);
+    barrier();
+    if (masked(0)) zero_stage(0);
 
     floatx16 acc[4][2];
 #pragma unroll
@@ -253,26 +308,29 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
+    Frags f0, f1;
+    read_frags<P_KC, Q_KC>(f0, lds, 0, wr, wq, lane);
+
     int kt = 0, f = 0, T = base;
     for (int s = 0; s < total; ++s) {
-        // stage s has landed when at most the stages issued after it are still in flight
-        const int after = ld_s - s - 1;
-        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
-        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // this wave's reads of stage s - 1 are done
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        issue();                                                // into the buffer of stage s - 1
-        uint8_t* img = lds + (s % NBUF) * STAGE;
-        if (kt == a.ntb - 1 && a.kv_last < BK) {                  // workgroup-uniform
-            zero_tail<P_KC>(img, a.kv_last, threadIdx.x);
-            zero_tail<Q_KC>(img + IMG, a.kv_last, threadIdx.x);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
+        const bool more = s + 1 < total;
+        if (more) wait_landed(s + 1);
+        barrier();                                              // stage s + 1 readable; stage s - 1 released
+        issue();                                                // stage s + AHEAD into stage s - 1's buffer
+        if (more && masked(s + 1)) zero_stage(s + 1);
+        const uint8_t* img = lds + (s % NBUF) * STAGE;
+#pragma unroll
+        for (int ks = 1; ks < BK / 16; ++ks) {
+            Frags& cur = (ks & 1) ? f0 : f1;
+            Frags& nxt = (ks & 1) ? f1 : f0;
+            read_frags<P_KC, Q_KC>(nxt, img, ks, wr, wq, lane);
+            mma(acc, cur);
         }
-        mma_stage<P_KC, Q_KC>(acc, img, wr, wq, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // stage s's reads done before its buffer leaves
+        Frags& last = ((BK / 16) & 1) ? f0 : f1;                // the final substep's fragments
+        Frags& pre = ((BK / 16) & 1) ? f1 : f0;                 // BK / 16 even: f0 again holds substep 0
+        if (more) read_frags<P_KC, Q_KC>(pre, lds + ((s + 1) % NBUF) * STAGE, 0, wr, wq, lane);
+        mma(acc, last);
         if (++kt < a.ntb) continue;
         kt = 0;
         if (++f < a.fold) continue;
@@ -307,14 +365,14 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
                     }
             }
         } else {
-            // bf16 out through the buffer of stage s (free until the next stage's barrier) in 4 rounds of 64 p x
-            // 256 q: each q row's 64 p leave as one 128-B line (8 lanes x 16 B) instead of 16-B pieces of 32 lines
+            // bf16 out through stage s's buffer (free until iteration s + 1's barrier) in 4 rounds of 64 p x 256 q:
+            // each q row's 64 p leave as one 128-B line (8 lanes x 16 B), non-temporal (the output is not re-read
+            // here; it must not evict the operand tiles the next workgroups re-read from L2)
             uint8_t* stg = lds + (s % NBUF) * STAGE;              // [256 q][128 B], 16-B chunk c of row q at c ^ (q & 7)
             uint16_t* cb = reinterpret_cast<uint16_t*>(a.c) + (int64_t)t.b * a.c_bs;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                __builtin_amdgcn_s_barrier();                       // all waves are done reading the buffer
-                asm volatile("" ::: "memory");
+                barrier();                                      // all waves are done reading the buffer
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const int q = wq + 32 * j + (lane & 31);
@@ -328,8 +386,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
                     }
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
+                barrier();
 #pragma unroll
                 for (int r = 0; r < 256 / 64; ++r) {                // 8 rows per wave-instruction, 4 per wave
                     const int ql = (r * WAVES + wave) * 8 + (lane >> 3), c = lane & 7;
@@ -338,7 +395,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
                     if (q < a.mq) {
                         uint16_t* dst = cb + (int64_t)q * a.c_sq + p;
                         if (p + 7 < a.mp && a.c_vec16) {
-                            *reinterpret_cast<uint4*>(dst) = v;
+                            typedef unsigned int u4v_t __attribute__((ext_vector_type(4)));
+                            __builtin_nontemporal_store(u4v_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u4v_t*>(dst));
                         } else if (p + 7 < a.mp) {
                             reinterpret_cast<uint2*>(dst)[0] = uint2{v.x, v.y};
                             reinterpret_cast<uint2*>(dst)[1] = uint2{v.z, v.w};
