@@ -58,7 +58,7 @@ constexpr int LOADS = 2 * PIECES;          // per stage and wave
 // K-contiguous image: rows of RB bytes (CPR 16-B chunks), RPL rows per 256-B bank line
 constexpr int RB = 2 * BK, CPR = BK / 8, RPL = 256 / RB;
 static_assert(NBUF * STAGE <= 160 * 1024, "LDS");
-static_assert(AHEAD >= 1 && AHEAD <= 4, "ring depth");
+static_assert(AHEAD >= 2 && AHEAD <= 4, "ring depth: stage s + 1 is issued before iteration s");
 
 __device__ inline int kc_swz(int row) { return (row / RPL) % CPR; }
 
@@ -325,6 +325,9 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
             Frags& nxt = (ks & 1) ? f1 : f0;
             read_frags<P_KC, Q_KC>(nxt, img, ks, wr, wq, lane);
             mma(acc, cur);
+            // keep these MFMAs ahead of the wait below: the compiler would otherwise sink them past it (they touch
+            // no memory) and the wave would stall on the reads with the MFMA pipe idle
+            __builtin_amdgcn_sched_barrier(0);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // stage s's reads done before its buffer leaves
         Frags& last = ((BK / 16) & 1) ? f0 : f1;                // the final substep's fragments

@@ -30,9 +30,14 @@ _FWD = torch.amp.custom_fwd(device_type="cuda")
 _BWD = torch.amp.custom_bwd(device_type="cuda")
 
 
-# bf16 projections (BASELINE configs[4]) on the HIP MFMA GEMM (csrc/projgemm.hip) where it takes the operands;
-# AVSE_PROJ_GEMM=0 keeps them on the library (torch.bmm -> hipBLASLt), which every fp32 GEMM uses.
-_HIP_GEMM = os.environ.get("AVSE_PROJ_GEMM", "0") == "1"
+# bf16 projections (BASELINE configs[4]) on the HIP MFMA GEMM (csrc/projgemm.hip).  Default ("1"): the sites where it
+# measured faster than hipBLASLt at C5 (profiles/r04g_projgemm_probe_vs_lib.jsonl: in_proj forward 0.26 vs 0.25 of the
+# bf16 peak, in_proj input gradient 0.34 vs 0.32, out_proj input gradient 0.30 vs 0.25); out_proj forward (0.29 vs 0.35)
+# and the weight gradients (0.29-0.32 vs 0.34-0.36) stay on the library.  "all": every bf16 site; "0": none.  fp32
+# GEMMs always run on the library.
+_PROJ_GEMM = os.environ.get("AVSE_PROJ_GEMM", "1")
+_HIP_GEMM = _PROJ_GEMM in ("1", "all")
+_HIP_GEMM_ALL = _PROJ_GEMM == "all"
 
 
 def _autocast_dtype():
@@ -106,14 +111,15 @@ class _Fork(torch.autograd.Function):
 
 def _bsum_mm(a, bt, alpha=1.0):
     """alpha sum_b a[b] @ bt[b] for a (b, m, l), bt (b, l, n): the weight gradient of a batched projection, fp32.
-    Under bf16 autocast: the HIP GEMM with fp32 accumulation (avse_gemm_bf16, batches folded into groups).
+    Under bf16 autocast with AVSE_PROJ_GEMM=all: the HIP GEMM with fp32 accumulation (avse_gemm_bf16, batches folded
+    into groups).
     Otherwise as one strided-batched GEMM + sum while the (b, m, n) partials are small (Mamba-TasNet: b = batch);
     as ONE (m, b*l) x (b*l, n) GEMM when they are not (DPMamba's inter pass has b = B*250 sequences of
     34 frames: the partials would take 33 GB, and each GEMM's depth would be 34)."""
     nb, m, l = a.shape
     n = bt.shape[2]
     dt = _autocast_dtype()
-    if dt == torch.bfloat16:
+    if dt == torch.bfloat16 and _HIP_GEMM_ALL:
         # batches folded into groups so that the launch has about one 256 x 256 tile per CU; groups summed after
         fold = max(1, nb * (-(-m // 256)) * (-(-n // 256)) // 256)
         while nb % fold:
@@ -219,7 +225,7 @@ class _BiOutProj(torch.autograd.Function):
         y = _padded_add(f, bk)
         ctx.save_for_backward(y, w)
         dt = _autocast_dtype()
-        if dt is not None:
+        if dt is not None and _HIP_GEMM_ALL:
             wc, yc = w.to(dt), y.to(dt)
             out = _hip_gemm(wc[None], yc.transpose(1, 2),
                             torch.empty(y.shape[0], y.shape[2], w.shape[0], device=y.device, dtype=dt), 0.5)

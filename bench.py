@@ -817,7 +817,9 @@ def roofline_hip(dev):
                 ms = _event_ms(fn)
             ach = flops / (ms * 1e-3) / 1e12
             proj.append({"gemm": f"BiMambaV2 {pname} ({tag})", "shape": [b, l, dm, di], "dtype": str(dt)[6:],
-                         "path": "avse_gemm_bf16 (csrc/projgemm.hip)" if on and M._HIP_GEMM else "hipBLASLt (torch.bmm)",
+                         "path": ("avse_gemm_bf16 (csrc/projgemm.hip)"
+                                  if on and (M._HIP_GEMM_ALL or (M._HIP_GEMM and pname == "in_proj"))
+                                  else "hipBLASLt (torch.bmm)"),
                          "bound": "mfma", "flops_per_launch": flops, "avg_ms": round(ms, 4),
                          "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4)})
         del h, f, bk
