@@ -136,10 +136,13 @@ def test_two_ranks_one_gpu_side_stream_buckets(workload):
         # workspace, so the two runs' activations differ by fp32 rounding and L1 / ReLU signs near 0 can flip
         # (measured 3e-5 .. 3e-4 of the norm); a bucket reduced before a side stream's gradients landed holds zeros
         # or stale partial sums for whole parameters: O(1) of their norm.  Per branch (the avse1 lip / audio / fusion
-        # nets, the Mamba encoder / masknet / decoder): an error of 0.5 % on a whole branch fails the 2.5e-3 bar.  The
-        # noise floor is activation sign flips, not arithmetic: MIOpen's solver for a shape depends on the workspace
-        # the caching allocator can hand it, so the 2-rank and the 1-process runs round differently and a ReLU / PReLU
-        # input within rounding of 0 can take the other branch (measured total 1.6e-3 on one box, < 5e-4 on another)
+        # nets, the Mamba encoder / masknet / decoder) the bar is 1e-2.  The noise floor is activation sign flips, not
+        # arithmetic: MIOpen's solver for a shape depends on the workspace the caching allocator can hand it, so the
+        # 2-rank and the 1-process runs round differently and a ReLU / PReLU input within rounding of 0 can take the
+        # other branch, which the lip trunk's BatchNorm backward amplifies (measured: total 1.2e-3 .. 1.6e-3, the lip
+        # branch alone up to 3.5e-3 on one box, < 5e-4 on another).  A race is far above that: with the test's 0.5 MB
+        # buckets, a bucket reduced before a side stream's gradients landed leaves whole parameters stale or zero, so
+        # a bucket holding even 1e-4 of the branch's squared gradient norm moves the branch error past 1e-2.
         branches = {}
         for name, (ei, ni) in zip(rec["names"], rec["errs"]):
             key = ".".join(name.split(".")[:2]) if workload == "mamba" else name.split(".")[0]
@@ -147,8 +150,8 @@ def test_two_ranks_one_gpu_side_stream_buckets(workload):
             branches[key] = (be + ei ** 2, bn + ni ** 2)
         for key, (be, bn) in branches.items():
             print(f"    branch {key}: rel err {(be / max(bn, 1e-60)) ** 0.5:.2e}")
-        assert e <= 2e-3 * n, (workload, r, e, n)
+        assert e <= 5e-3 * n, (workload, r, e, n)
         for key, (be, bn) in branches.items():
-            assert be ** 0.5 <= 2.5e-3 * bn ** 0.5 + 1e-6 * n, (workload, r, key, be ** 0.5, bn ** 0.5)
+            assert be ** 0.5 <= 1e-2 * bn ** 0.5 + 1e-6 * n, (workload, r, key, be ** 0.5, bn ** 0.5)
         for i, (ei, ni) in enumerate(rec["errs"]):
             assert ei <= 5e-2 * ni + 1e-4 * n, (workload, r, i, ei, ni)
