@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 : > gpurun_out/pg_abl.jsonl
-for v in base PRIO NOEPI; do
+for v in base LE LEB; do
   if [ $v = base ]; then lib=avse_challenge_amd/libavse_hip.so; else lib=expso/pg_$v.so; fi
   echo "== $v" >> gpurun_out/pg_abl.jsonl
   AVSE_HIP_LIB=$lib timeout -k 10 120 python -u tools/gemm_probe.py --reps 10 --no-lib >> gpurun_out/pg_abl.jsonl 2>&1 || exit 1
