@@ -53,8 +53,12 @@ constexpr int BK = AVSE_PG_BK;             // k per stage (32 or 64)
 constexpr int IMG = BT * BK * 2;           // one operand's image of one stage
 constexpr int STAGE = 2 * IMG;
 constexpr int NBUF = AVSE_PG_NBUF, AHEAD = NBUF - 1;   // LDS ring; stages in flight ahead of the one computed
-constexpr int PIECES = IMG / 1024 / WAVES; // LDS-DMA wave-instructions per operand, stage and wave
-constexpr int LOADS = 2 * PIECES;          // per stage and wave
+// Waves 0..LWAVES-1 issue every LDS-DMA, waves LWAVES.. every global store of the bf16 epilogue: a loader wave never
+// has a store outstanding, so its counted vmcnt waits for a stage are exact (vmcnt also counts stores, and loads and
+// stores may complete out of order), and a store wave never waits on vmcnt at all.
+constexpr int LWAVES = 4;
+constexpr int PIECES = IMG / 1024 / LWAVES; // LDS-DMA wave-instructions per operand, stage and loader wave
+constexpr int LOADS = 2 * PIECES;          // per stage and loader wave
 // K-contiguous image: rows of RB bytes (CPR 16-B chunks), RPL rows per 256-B bank line
 constexpr int RB = 2 * BK, CPR = BK / 8, RPL = 256 / RB;
 static_assert(NBUF * STAGE <= 160 * 1024, "LDS");
@@ -204,7 +208,7 @@ __device__ inline uint32_t pack_bf16x2(float a, float b) {
 }
 
 // Wave (wr, wc) = (wave >> 2, wave & 3) owns the p blocks 32 (2 i + wr), i = 0..3 (so an epilogue round i covers the
-// 64 contiguous p of 64 i .. 64 i + 63 over both wave rows) and the q columns 64 wc .. 64 wc + 63.
+// 64 contiguous p of 64 i .. 64 i + 63 over both wave rows) and the q columns 64 wc .. 64 wc + 63 (blocks j = 0, 1).
 struct Frags {
     bf16x8 a[4], b[2];
 };
@@ -258,11 +262,14 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
         piece_offsets<Q_KC>(vq, t.q0, a.q_sx, a.mq, wave, lane);
     };
     set_tile(base, 0);
+    const bool loader = wave < LWAVES;                          // wave-uniform
     auto issue = [&]() {
         if (ld_s >= total) return;
-        const uint32_t img = lds0 + (ld_s % NBUF) * STAGE;
-        stage_load<P_KC>(rp, img, vp, ld_kt * p_step, wave);
-        stage_load<Q_KC>(rq, img + IMG, vq, ld_kt * q_step, wave);
+        if (loader) {
+            const uint32_t img = lds0 + (ld_s % NBUF) * STAGE;
+            stage_load<P_KC>(rp, img, vp, ld_kt * p_step, wave);
+            stage_load<Q_KC>(rq, img + IMG, vq, ld_kt * q_step, wave);
+        }
         ++ld_s;
         if (++ld_kt == a.ntb) {
             ld_kt = 0;
@@ -276,6 +283,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
     // stage s's position in its tile: partial (masked) stage?  (k-stage index = s % ntb)
     auto masked = [&](int st) { return a.kv_last < BK && (st % a.ntb) == a.ntb - 1; };
     auto wait_landed = [&](int st) {   // stage st's DMAs done: only the stages issued after it may still fly
+        if (!loader) return;
         const int after = ld_s - st - 1;
         if (AHEAD >= 4 && after >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LOADS) : "memory");
         else if (AHEAD >= 3 && after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
@@ -368,14 +376,15 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
                     }
             }
         } else {
-            // bf16 out through stage s's buffer (free until iteration s + 1's barrier) in 4 rounds of 64 p x 256 q:
-            // each q row's 64 p leave as one 128-B line (8 lanes x 16 B), non-temporal (the output is not re-read
-            // here; it must not evict the operand tiles the next workgroups re-read from L2)
+            // bf16 out through stage s's buffer (free until iteration s + 1's barrier) in 4 rounds of 64 p x 256 q: all
+            // waves stage their accumulators, the store waves write each q row's 64 p as one 128-B line (8 lanes x
+            // 16 B), non-temporal (the output is not re-read here; it must not evict the operand tiles the next
+            // workgroups re-read from L2).  The loader waves go on as soon as the last round is staged.
             uint8_t* stg = lds + (s % NBUF) * STAGE;              // [256 q][128 B], 16-B chunk c of row q at c ^ (q & 7)
             uint16_t* cb = reinterpret_cast<uint16_t*>(a.c) + (int64_t)t.b * a.c_bs;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                barrier();                                      // all waves are done reading the buffer
+                barrier();                                      // the stage's / previous round's readers are done
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const int q = wq + 32 * j + (lane & 31);
@@ -390,28 +399,30 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 barrier();
+                if (!loader) {
 #pragma unroll
-                for (int r = 0; r < 256 / 64; ++r) {                // 8 rows per wave-instruction, 4 per wave
-                    const int ql = (r * WAVES + wave) * 8 + (lane >> 3), c = lane & 7;
-                    const uint4 v = *reinterpret_cast<const uint4*>(stg + ql * 128 + 16 * (c ^ (ql & 7)));
-                    const int q = t.q0 + ql, p = t.p0 + 64 * i + 8 * c;
-                    if (q < a.mq) {
-                        uint16_t* dst = cb + (int64_t)q * a.c_sq + p;
-                        if (p + 7 < a.mp && a.c_vec16) {
-                            typedef unsigned int u4v_t __attribute__((ext_vector_type(4)));
-                            __builtin_nontemporal_store(u4v_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u4v_t*>(dst));
-                        } else if (p + 7 < a.mp) {
-                            reinterpret_cast<uint2*>(dst)[0] = uint2{v.x, v.y};
-                            reinterpret_cast<uint2*>(dst)[1] = uint2{v.z, v.w};
-                        } else {
-                            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+                    for (int r = 0; r < 256 / 8 / (WAVES - LWAVES); ++r) {   // 8 rows per wave-instruction
+                        const int ql = (r * (WAVES - LWAVES) + (wave - LWAVES)) * 8 + (lane >> 3), c = lane & 7;
+                        const uint4 v = *reinterpret_cast<const uint4*>(stg + ql * 128 + 16 * (c ^ (ql & 7)));
+                        const int q = t.q0 + ql, p = t.p0 + 64 * i + 8 * c;
+                        if (q < a.mq) {
+                            uint16_t* dst = cb + (int64_t)q * a.c_sq + p;
+                            if (p + 7 < a.mp && a.c_vec16) {
+                                typedef unsigned int u4v_t __attribute__((ext_vector_type(4)));
+                                __builtin_nontemporal_store(u4v_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u4v_t*>(dst));
+                            } else if (p + 7 < a.mp) {
+                                reinterpret_cast<uint2*>(dst)[0] = uint2{v.x, v.y};
+                                reinterpret_cast<uint2*>(dst)[1] = uint2{v.z, v.w};
+                            } else {
+                                const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                            for (int e = 0; e < 8; ++e)
-                                if (p + e < a.mp) dst[e] = (uint16_t)(u[e >> 1] >> (16 * (e & 1)));
+                                for (int e = 0; e < 8; ++e)
+                                    if (p + e < a.mp) dst[e] = (uint16_t)(u[e >> 1] >> (16 * (e & 1)));
+                            }
                         }
                     }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
         }
 #pragma unroll
