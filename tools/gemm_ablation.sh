@@ -1,3 +1,5 @@
+# Ablation runner for the projection GEMM: tools/gemm_probe.py against libavse_hip.so and expso/pg_<V>.so variants built
+# by tools/build_exp.sh from tools/pg_exp.patch (e.g. -DPG_NOLOAD -DPG_NOEPI -DPG_NOBAR).  usage: bash tools/gemm_ablation.sh
 set -o pipefail
 mkdir -p gpurun_out
 : > gpurun_out/pg_abl.jsonl
