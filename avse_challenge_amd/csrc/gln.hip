@@ -460,7 +460,10 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int 
                                                                   const float2* __restrict__ ws_rows,
                                                                   const float* __restrict__ dy, float* __restrict__ dx,
                                                                   float* __restrict__ ws_dw, float* __restrict__ ws_alpha) {
-    constexpr int V = 4, UB = 2;                  // 4 consecutive elements per thread, 2 quadruples in flight
+#ifndef AVSE_GLN_BWD_UB
+#define AVSE_GLN_BWD_UB 2
+#endif
+    constexpr int V = 4, UB = AVSE_GLN_BWD_UB;    // 4 consecutive elements per thread, UB quadruples in flight
     constexpr int H = (P - 1) / 2, NX = 2 * P - 1;
     __shared__ float red[THREADS / 64][DW_MAXP + 1];
     __shared__ double dred[8];
