@@ -460,10 +460,10 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int 
                                                                   const float2* __restrict__ ws_rows,
                                                                   const float* __restrict__ dy, float* __restrict__ dx,
                                                                   float* __restrict__ ws_dw, float* __restrict__ ws_alpha) {
-#ifndef AVSE_GLN_BWD_UB
-#define AVSE_GLN_BWD_UB 2
-#endif
-    constexpr int V = 4, UB = AVSE_GLN_BWD_UB;    // 4 consecutive elements per thread, UB quadruples in flight
+    // 4 consecutive elements per thread, one quadruple per loop trip: its 2P - 1 + P tap loads are already 8 in flight
+    // (P = 3), and the smaller register footprint keeps more waves resident (2 quadruples per trip: 0.144 ms, 3: 0.175,
+    // 4: 0.169, 1: 0.132 at C4; tools/gln_ub_ab.sh)
+    constexpr int V = 4, UB = 1;
     constexpr int H = (P - 1) / 2, NX = 2 * P - 1;
     __shared__ float red[THREADS / 64][DW_MAXP + 1];
     __shared__ double dred[8];
