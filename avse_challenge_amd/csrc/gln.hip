@@ -39,7 +39,7 @@ __device__ inline void st4_row(__amdgpu_buffer_rsrc_t r, float* row, int t, int 
             if (t + e < K) row[t + e] = v[e];
     }
 }
-constexpr int V4 = 4, UB4 = 2;                  // elements per thread per access, accesses in flight
+constexpr int V4 = 4, UB4 = 2;                  // elements per thread per access, accesses in flight (1 / 4: +-2 %)
 
 template <typename T>
 __device__ inline T block_sum(T v, T* red) {
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(THREADS) void apply_fused_kernel(int row0, int C, i
 __global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int row0, int C, int K, const float* __restrict__ x,
                                                              const float* __restrict__ alpha, const float2* __restrict__ stats,
                                                              const float* __restrict__ dy, float2* __restrict__ ws) {
-    constexpr int V = 4, UB = 2;
+    constexpr int V = 4, UB = 2;                  // 1 / 4 in flight: within +-2 % (tools/gln_ub_ab.sh)
     __shared__ float red[4];
     const int row = row0 + (int)blockIdx.x, b = row / C;
     const float a = alpha[0];
