@@ -25,7 +25,7 @@ os.environ.setdefault("MIOPEN_USER_DB_PATH", MIOPEN_DB)     # read by MIOpen at 
 
 # HIP graphs: the runtime's graph packet capture (ROCm 7.x CLR; AQL packets and kernel arguments prepared at
 # instantiate time) replays some kernel nodes of the long single-stream avse1 train-step graph with the wrong
-# arguments: reduction results land in each other's buffers (tools/avse1_graph_diag4.py; loss -1.0 instead of
+# arguments: reduction results land in each other's buffers (tools/avse1_graph_diag4.py @ 8f1eec2; loss -1.0 instead of
 # 0.34).  With the capture off every replay matches the eager step.  Read at HIP runtime init, i.e. at the
 # first GPU call, which comes after this import in every entry point (bench.py, tests, smoke()).
 _PRESET = os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE")

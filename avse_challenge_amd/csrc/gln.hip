@@ -158,7 +158,7 @@ __global__ __launch_bounds__(THREADS) void apply_fused_kernel(int row0, int C, i
 __global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int row0, int C, int K, const float* __restrict__ x,
                                                              const float* __restrict__ alpha, const float2* __restrict__ stats,
                                                              const float* __restrict__ dy, float2* __restrict__ ws) {
-    constexpr int V = 4, UB = 2;                  // 1 / 4 in flight: within +-2 % (tools/gln_ub_ab.sh)
+    constexpr int V = 4, UB = 2;                  // 1 / 4 in flight: within +-2 % (tools/gln_ub_ab.sh @ 8f1eec2)
     __shared__ float red[4];
     const int row = row0 + (int)blockIdx.x, b = row / C;
     const float a = alpha[0];
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(THREADS) void dwconv_gln_bwd4_kernel(int row0, int 
                                                                   float* __restrict__ ws_dw, float* __restrict__ ws_alpha) {
     // 4 consecutive elements per thread, one quadruple per loop trip: its 2P - 1 + P tap loads are already 8 in flight
     // (P = 3), and the smaller register footprint keeps more waves resident (2 quadruples per trip: 0.144 ms, 3: 0.175,
-    // 4: 0.169, 1: 0.132 at C4; tools/gln_ub_ab.sh)
+    // 4: 0.169, 1: 0.132 at C4; tools/gln_ub_ab.sh @ 8f1eec2)
     constexpr int V = 4, UB = 1;
     constexpr int H = (P - 1) / 2, NX = 2 * P - 1;
     __shared__ float red[THREADS / 64][DW_MAXP + 1];

@@ -42,17 +42,11 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) s4_t lds_s4_t;
 
-#ifndef AVSE_PG_BK
-#define AVSE_PG_BK 32
-#endif
-#ifndef AVSE_PG_NBUF
-#define AVSE_PG_NBUF 4
-#endif
 constexpr int BT = 256, THREADS = 512, WAVES = THREADS / 64;
-constexpr int BK = AVSE_PG_BK;             // k per stage (32 or 64)
+constexpr int BK = 32;                     // k per stage
 constexpr int IMG = BT * BK * 2;           // one operand's image of one stage
 constexpr int STAGE = 2 * IMG;
-constexpr int NBUF = AVSE_PG_NBUF, AHEAD = NBUF - 1;   // LDS ring; stages in flight ahead of the one computed
+constexpr int NBUF = 4, AHEAD = NBUF - 1;   // LDS ring; stages in flight ahead of the one computed
 // Waves 0..LWAVES-1 issue every LDS-DMA, waves LWAVES.. every global store of the bf16 epilogue: a loader wave never
 // has a store outstanding, so its counted vmcnt waits for a stage are exact (vmcnt also counts stores, and loads and
 // stores may complete out of order), and a store wave never waits on vmcnt at all.

@@ -23,9 +23,13 @@ With ``use_graph`` (single GPU) the forward/backward and the optimizer step are 
 HIP graph; with world > 1 the forward/backward stays eager (the collectives are launched from autograd hooks)
 and only the optimizer step is captured.
 Kernel errors: the grouped LSTM recurrence (csrc/lstm_group.hip) writes a sticky device flag when its workgroups
-were not co-resident (its outputs are then invalid).  Every step enqueues a 4-byte copy of that flag into pinned
-memory and checks the previous copy once it has landed (no synchronisation); ``check_kernel_errors()`` is the
-blocking form.  Either raises ``kernels.HipKernelError``.
+were not co-resident (its outputs are then invalid).  The optimizer update is gated on that flag ON THE DEVICE: the
+step's ``found`` scalar (the flag, with world > 1 max-all-reduced together with the gradient buckets so every rank
+sees the same value) is fused Adam's ``found_inf``, so a step whose gradients are invalid updates no parameter and
+no Adam moment on any rank — nor does any later step while the flag stays set.  Every step enqueues a 4-byte copy
+of ``found`` into pinned memory and checks the previous copy once it has landed (no synchronisation); when it is
+set, every rank raises ``kernels.HipKernelError`` in the same step and the flag is cleared.
+``check_kernel_errors()`` is the blocking form.  The parameters are those from before the failed step.
 """
 import functools
 
@@ -66,33 +70,50 @@ class Trainer:
             for i, p in enumerate(self.params):
                 p.register_post_accumulate_grad_hook(functools.partial(self._grad_ready, i))
         self._armed = False
-        self.opt = torch.optim.Adam(self.params, lr=step.lr, capturable=self.use_graph, foreach=True)
+        self._flag = self._found = None
+        if dev.type == "cuda":
+            from . import kernels
+            # created here, outside any graph pool: captured launches and the captured optimizer keep its pointer
+            self._flag = kernels._kernel_error_flag(dev)
+            self._found = torch.zeros(1, device=dev, dtype=torch.float32)
+            self.opt = torch.optim.Adam(self.params, lr=step.lr, capturable=self.use_graph, fused=True)
+            self.opt.found_inf = self._found          # read by Adam.step (fused): skip the update when nonzero
+        else:
+            self.opt = torch.optim.Adam(self.params, lr=step.lr, foreach=True)
         self.g_fb = self.g_opt = None
         self.loss = None
         self._err_host = self._err_ev = None
 
     # ------------------------------------------------------------------ kernel error flag
     def _poll_kernel_errors(self):
-        """Lagged, non-blocking check of the device's sticky kernel-error flag (ddp module docstring)."""
-        if self.dev.type != "cuda":
-            return
-        from . import kernels
-        flag = kernels._ERROR_FLAGS.get(self.dev.index if self.dev.index is not None else torch.cuda.current_device())
-        if flag is None:
+        """Lagged, non-blocking check of the step's ``found`` scalar (ddp module docstring)."""
+        if self._found is None:
             return
         if self._err_host is None:
-            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._err_host = torch.zeros(1, dtype=torch.float32, pin_memory=True)
             self._err_ev = torch.cuda.Event()
-        elif self._err_ev.query() and int(self._err_host[0]) != 0:
-            kernels.raise_if_kernel_error(self.dev)
-        self._err_host.copy_(flag, non_blocking=True)      # the flag is sticky: a later copy misses nothing
+        elif self._err_ev.query() and float(self._err_host[0]) != 0.0:
+            self._raise_kernel_error()
+        self._err_host.copy_(self._found, non_blocking=True)   # the flag is sticky: a later copy misses nothing
         self._err_ev.record()
+
+    def _raise_kernel_error(self):
+        from . import kernels
+        code = int(self._flag.item()) & 0xFFFFFFFF           # this rank's own code (0: another rank's launch failed)
+        self._flag.zero_()
+        self._found.zero_()
+        if self._err_host is not None:
+            self._err_host.zero_()
+        raise kernels.HipKernelError(kernels.kernel_error_message(code) if code else
+                                     "a grouped LSTM launch on another rank timed out; this step's update was skipped "
+                                     "on every rank")
 
     def check_kernel_errors(self):
         """Blocking: raise kernels.HipKernelError if any kernel of the steps so far reported invalid outputs."""
-        if self.dev.type == "cuda":
-            from . import kernels
-            kernels.raise_if_kernel_error(self.dev)
+        if self._found is not None:
+            torch.cuda.synchronize(self.dev)
+            if float(self._found.item()) != 0.0 or int(self._flag.item()) != 0:
+                self._raise_kernel_error()
 
     # ------------------------------------------------------------------ buckets
     def _make_buckets(self, ranges, bucket_mb):
@@ -174,6 +195,10 @@ class Trainer:
         if self.sync_loss:
             self.loss = self.loss.clone()
             self.works.append(dist.all_reduce(self.loss, async_op=True))
+        if self._found is not None:
+            # every rank skips the update when any rank's kernels reported invalid outputs (found is Adam's found_inf)
+            self._found.copy_(self._flag.ne(0))          # Adam skips on found_inf == 1 exactly
+            self.works.append(dist.all_reduce(self._found, op=dist.ReduceOp.MAX, async_op=True))
         for w in self.works:
             w.wait()
         self.works = []
@@ -204,12 +229,19 @@ class Trainer:
         loss = self.step.loss()
         if out is not None:
             out.copy_(loss.detach())
-        loss.backward()
+        if self.world > 1:
+            from . import kernels
+            with kernels.no_grouped_lstm():         # bucket all-reduces may be in flight (kernels.NO_GROUPED_LSTM)
+                loss.backward()
+        else:
+            loss.backward()
         return loss.detach() if out is None else out
 
     def _opt(self):
         if self.world > 1:
             self.flat.mul_(1.0 / self.world)
+        elif self._found is not None:
+            self._found.copy_(self._flag.ne(0))       # world > 1: max over ranks, set in _finish_allreduce
         if self.step.clip is not None:
             torch.nn.utils.clip_grad_norm_(self.params, self.step.clip, foreach=True)
         self.opt.step()

@@ -23,13 +23,16 @@ def _tap_begin(name, device):
         return None
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(torch.cuda.current_stream(device))
-    taps.append((e0, e1))
-    return e1, device
+    return taps, e0, e1, device
 
 
 def _tap_end(tap):
+    """Called after the launch returned AVSE_OK: only then is the pair appended (a failed launch leaves no
+    half-recorded pair behind for bench.roofline's elapsed_time)."""
     if tap is not None:
-        tap[0].record(torch.cuda.current_stream(tap[1]))
+        taps, e0, e1, device = tap
+        e1.record(torch.cuda.current_stream(device))
+        taps.append((e0, e1))
 
 
 def _need_gpu(*ts):
@@ -753,11 +756,37 @@ _GROUP_CAPACITY = {}     # (device index, H, backward) -> workgroups of that gro
 _ERROR_FLAGS = {}        # device index -> int32 sticky error flag of the grouped LSTM launches (never freed)
 
 
+# While > 0 the grouped LSTM kernels are not launched (lstm.hip's single-workgroup kernels run instead).  ddp.Trainer
+# raises it around the backward at world > 1: bucket all-reduces launched from gradient hooks can be in flight then,
+# and RCCL's kernels hold CUs the grouped launch needs co-resident (its static capacity query cannot see them).  The
+# forward needs no such guard: every collective of the previous step was waited for by the compute stream before it.
+NO_GROUPED_LSTM = 0
+
+
+class no_grouped_lstm:
+    """Context manager: lstm.hip's kernels for every LSTM launch inside (process-wide: autograd's device threads run
+    the backward, so a thread-local switch would not reach them)."""
+
+    def __enter__(self):
+        global NO_GROUPED_LSTM
+        NO_GROUPED_LSTM += 1
+        return self
+
+    def __exit__(self, *exc):
+        global NO_GROUPED_LSTM
+        NO_GROUPED_LSTM -= 1
+        return False
+
+
+def lstm_group_allowed():
+    return NO_GROUPED_LSTM == 0 and os.environ.get("AVSE_LSTM_GROUP", "1") == "1"
+
+
 def _lstm_group_ws(L, Bn, H, device, backward):
-    """Workspace of the grouped LSTM kernels, or None when they do not apply: AVSE_LSTM_GROUP=0; B * G > 256 or
-    H > 384 (avse_lstm_group_size); or B * G workgroups cannot be co-resident on this device
-    (avse_lstm_group_capacity).  Those cases run lstm.hip's one-workgroup-per-sequence kernels."""
-    if os.environ.get("AVSE_LSTM_GROUP", "1") != "1":
+    """Workspace of the grouped LSTM kernels, or None when they do not apply: AVSE_LSTM_GROUP=0 or inside
+    no_grouped_lstm(); B * G > 256 or H > 384 (avse_lstm_group_size); or B * G workgroups cannot be co-resident on
+    this device (avse_lstm_group_capacity).  Those cases run lstm.hip's one-workgroup-per-sequence kernels."""
+    if not lstm_group_allowed():
         return None
     G = int(L.avse_lstm_group_size(Bn, H))
     if G == 0:
@@ -795,13 +824,15 @@ def lstm_group_status(device=None):
     """0 when every grouped LSTM launch on `device` (default: all used devices) since the last reset completed its
     hand-offs; else the timeout code one of them wrote (0x71000000 + step): a sequence's workgroups were not
     co-resident and that launch's outputs are invalid.  Synchronises with the flag's device."""
+    return max([int(f.item()) & 0xFFFFFFFF for f in _flags_of(device)] + [0])
+
+
+def _flags_of(device):
     if device is None:
-        flags = list(_ERROR_FLAGS.values())
-    else:
-        idx = torch.device(device).index
-        idx = torch.cuda.current_device() if idx is None else idx
-        flags = [f for i, f in _ERROR_FLAGS.items() if i == idx]
-    return max([int(f.item()) & 0xFFFFFFFF for f in flags] + [0])
+        return list(_ERROR_FLAGS.values())
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    return [f for i, f in _ERROR_FLAGS.items() if i == idx]
 
 
 def raise_if_kernel_error(device=None, reset=True):
@@ -809,11 +840,15 @@ def raise_if_kernel_error(device=None, reset=True):
     flag afterwards (a raised error is reported once)."""
     code = lstm_group_status(device)
     if code and reset:
-        for f in _ERROR_FLAGS.values():
+        for f in _flags_of(device):      # only the flags that were read: another device's error stays reported
             f.zero_()
     if code:
-        raise HipKernelError(f"grouped LSTM recurrence timed out waiting for its workgroups (code {code:#x}): the "
-                             "grid was not co-resident on the GPU; the step's outputs and gradients are invalid")
+        raise HipKernelError(kernel_error_message(code))
+
+
+def kernel_error_message(code):
+    return (f"grouped LSTM recurrence timed out waiting for its workgroups (code {code:#x}): the grid was not "
+            "co-resident on the GPU; the step's outputs and gradients are invalid")
 
 
 def lstm_bwd(dh, gates, c_all, w_hh, reverse=False):

@@ -144,7 +144,7 @@ def _conv3d_fwd_folded(x, w, padding):
     (x_unf[b*T + t, ci*KT + kt] = x_pad[b, ci, t + kt], plane copies), the weight (Cout, Cin, KT, KH, KW) is then
     (Cout, Cin*KT, KH, KW) as it lies, and the (B*T, Cout, Ho, Wo) result is permuted back to (B, Cout, T, Ho, Wo).
     MIOpen runs this 2-D shape (Winograd f3x2, find-db record) in 7.1 ms against 8.6 ms for its 3-D path at the avse1
-    C2 shape, copies included (tools/conv3d_fold_probe.py; AVSE_CONV3D_FOLD=0 restores F.conv3d)."""
+    C2 shape, copies included (tools/conv3d_fold_probe.py @ 8f1eec2; AVSE_CONV3D_FOLD=0 restores F.conv3d)."""
     B, Cin, T, H, W = x.shape
     Co, _, KT, KH, KW = w.shape
     PT, PH, PW = padding

@@ -4,7 +4,7 @@ Why: a ReLU / PReLU whose input sits within fp32 rounding of 0 takes one branch 
 in fp64.  One such flip moves one term of the activation's BatchNorm bias gradient, which is a sum of thousands of
 terms cancelling to ~1e-2 of their size in the avse1 ResNet trunk: measured 1.1e-2 of the gradient's max at
 net_visualfeat.trunk.layer3.0.bn1 from 2 flips with |z| < 8e-7, while the gradient reaching that site was within
-3.5e-6 of fp64 (tools/avse1_site_diag.py, profiles/r03_avse1_site_diag.txt).  No fp32 tolerance separates that from
+3.5e-6 of fp64 (tools/avse1_site_diag.py @ 8f1eec2, profiles/r03_avse1_site_diag.txt).  No fp32 tolerance separates that from
 a bug.  So the truth is the fp64 oracle evaluated with the activation patterns (and L1 signs) of the run under test:
 every ReLU / PReLU of baseline/avse1/model.py:29-34, 199-215, utils/resnet.py:26-67 and utils/tcn.py:144-243 and the
 L1 loss of model.py:164-168 are replaced by torch.where on our masks, and each disagreement with fp64's own sign must

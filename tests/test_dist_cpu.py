@@ -97,6 +97,54 @@ def test_trainer_gloo_world2_matches_single_process(clip):
     torch.testing.assert_close(torch.tensor(out[0][1]), torch.tensor(losses), atol=1e-6, rtol=1e-5)
 
 
+class _Probe(torch.autograd.Function):
+    """Identity whose backward records whether the grouped LSTM kernels may launch at that moment."""
+    seen = []
+
+    @staticmethod
+    def forward(ctx, x):
+        from avse_challenge_amd import kernels
+        _Probe.seen.append(("fwd", kernels.lstm_group_allowed()))
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        from avse_challenge_amd import kernels
+        _Probe.seen.append(("bwd", kernels.lstm_group_allowed()))
+        return g
+
+
+class _ProbeStep(_ToyStep):
+    def loss(self):
+        return torch.nn.functional.mse_loss(self.model(_Probe.apply(self.x.requires_grad_(True))), self.y)
+
+
+def _lstm_choice_worker(rank, world, port, q):
+    _init(rank, world, port)
+    import bench
+    tr = bench.Trainer(_ProbeStep(*_data(rank)), world, torch.device("cpu"), use_graph=False)
+    for _ in range(2):
+        tr()
+    q.put((rank, list(_Probe.seen)))
+    dist.destroy_process_group()
+
+
+def test_trainer_world2_backward_uses_single_workgroup_lstm():
+    """At world > 1 ddp.Trainer runs the backward inside kernels.no_grouped_lstm(): bucket all-reduces launched from
+    gradient hooks may be in flight then, and their RCCL kernels hold CUs that the grouped LSTM (csrc/lstm_group.hip)
+    needs co-resident, so the LSTM backward takes lstm.hip.  The forward (no collective in flight) and every pass of
+    a one-process run keep the grouped kernels."""
+    sys.path.insert(0, REPO)
+    import bench
+    out = _spawn(_lstm_choice_worker, ())
+    for r in (0, 1):
+        assert out[r] == [("fwd", True), ("bwd", False)] * 2, out[r]
+    _Probe.seen.clear()
+    tr = bench.Trainer(_ProbeStep(*_data(0)), 1, torch.device("cpu"), use_graph=False)
+    tr()
+    assert _Probe.seen == [("fwd", True), ("bwd", True)]
+
+
 # ------------------------------------------------------------------ BatchNorm model (avse1 AudioFeatNet)
 
 STEPS = 3

@@ -809,7 +809,7 @@ def test_lstm_group_error_flag_raises():
     0x71000000 + step into the device's sticky error flag (the launch's outputs are then invalid).  With that value in
     the flag — written here directly, as the kernel would — kernels.raise_if_kernel_error and ddp.Trainer's lagged
     per-step check both raise HipKernelError, and a reported error is cleared.  (Forcing a real non-resident grid was
-    tried with a bounded CU-occupying kernel from the same and from another process, tools/lstm_hog_probe.py: this
+    tried with a bounded CU-occupying kernel from the same and from another process, tools/lstm_hog_probe.py @ 8f1eec2: this
     pool's GPU never dispatched the LSTM beside it, so the launch only ever ran after the occupier — no timeout.)"""
     import bench
     from avse_challenge_amd import layers
@@ -833,17 +833,26 @@ def test_lstm_group_error_flag_raises():
         def loss(self):
             return self.model(self.x)[0].square().mean()
 
-    tr = bench.Trainer(Step(), 1, dev, use_graph=False)
-    tr()
-    torch.cuda.synchronize()
-    tr()                                          # enqueues the flag copy it checks on the next step
-    flag.fill_(0x71000000 + 5)
-    torch.cuda.synchronize()
-    tr()                                          # sees the previous (clean) copy, enqueues one of the set flag
-    torch.cuda.synchronize()
-    with pytest.raises(K().HipKernelError):
+    for graph in (False, True):
+        st = Step()
+        tr = bench.Trainer(st, 1, dev, use_graph=graph)
         tr()
-    K().raise_if_kernel_error()
+        tr.capture()
+        torch.cuda.synchronize()
+        tr()                                      # enqueues the found copy it checks on the next step
+        torch.cuda.synchronize()
+        before = [p.detach().clone() for p in st.model.parameters()]
+        flag.fill_(0x71000000 + 5)
+        torch.cuda.synchronize()
+        tr()                                      # sees the previous (clean) copy; its own update is skipped on device
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, p) for a, p in zip(before, st.model.parameters())), "update not gated on the flag"
+        with pytest.raises(K().HipKernelError, match="timed out"):
+            tr()
+        K().raise_if_kernel_error()               # cleared by the trainer's report
+        tr()
+        torch.cuda.synchronize()
+        assert not all(torch.equal(a, p) for a, p in zip(before, st.model.parameters())), "update after the report"
 
 
 # ------------------------------------------------------------------ fused dwconv <-> PReLU -> gLN (avse4 TCN)

@@ -347,11 +347,11 @@ def test_avse4_full_train_step_vs_oracle():
         cos = torch.nn.functional.cosine_similarity(p.grad.double().cpu().reshape(-1), q.grad.reshape(-1), 0)
         # a scalar PReLU slope's gradient is one sum over B*C*K terms of both signs (cancellation), so its
         # relative error swings with the upstream MIOpen error from process to process (measured 3e-3 ..
-        # 5e-2, tools/avse4_grad_diag.py); such 1-element parameters get a 1e-1 floor
+        # 5e-2, tools/avse4_grad_diag.py @ 8f1eec2); such 1-element parameters get a 1e-1 floor
         # a lip front-end ReLU whose input sits within rounding of 0 flips in one fp32 run and not in another
         # (MIOpen's solver choice and the BN reduction order both move it): the channel's BN bias / weight
         # gradient then moves by one term, 1e-2 .. 3e-2 of the gradient's max in every fp32 run alike
-        # (profiles/r02c_avse4_grad_diag.txt, tools/avse4_bn_diag.py: layer4.outbna.bias 2.7e-2 in ours, torch
+        # (profiles/r02c_avse4_grad_diag.txt, tools/avse4_bn_diag.py @ 8f1eec2: layer4.outbna.bias 2.7e-2 in ours, torch
         # GPU and torch CPU), so whether ours and torch's flips coincide varies from box to box; the
         # cosine bar stays 1e-4
         if p.numel() == 1:
@@ -616,5 +616,5 @@ def test_avse1_audio_only_c1_golden():
         cosf = lambda a: float((a * truth).sum() / (np.linalg.norm(a) * np.linalg.norm(truth) + 1e-300))  # noqa: E731
         cos, cos_ref = cosf(got), cosf(gold)
         # floors: a single activation-mask flip (|z| ~ 1e-6 at a ReLU, rounding-order dependent: 0-3 per BN site
-        # in either fp32 run, tools/bnact_fwd_chain_diag.py) moves one gradient term, ~1e-3 relative / 1e-6 cosine
+        # in either fp32 run, tools/bnact_fwd_chain_diag.py @ 8f1eec2) moves one gradient term, ~1e-3 relative / 1e-6 cosine
         assert e_gpu <= max(3 * e_ref, 1e-2) and 1 - cos <= max(3 * (1 - cos_ref), 1e-5), (k, e_gpu, e_ref, cos, cos_ref)
