@@ -80,6 +80,8 @@ SIGNATURES = {
     "avse_scan_bwd_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "avse_scan_fwd": (c_i32, [ctypes.POINTER(ScanFwdArgs), c_vp]),
     "avse_scan_bwd": (c_i32, [ctypes.POINTER(ScanBwdArgs), c_vp]),
+    "avse_dtproj": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64,
+                            c_i64, c_vp]),
     "avse_cconv_bwd_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "avse_cconv_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                                c_i32, c_i32, c_vp]),
@@ -139,6 +141,10 @@ SIGNATURES = {
     "avse_lstm_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "avse_lstm_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_gemm_bf16": (c_i32, [ctypes.POINTER(GemmBf16Args), c_vp]),
+    "avse_dconv_wprep_bytes": (c_i64, []),
+    "avse_split16": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "avse_dconv_wprep": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp]),
+    "avse_dconv_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

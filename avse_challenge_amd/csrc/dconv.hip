@@ -1,0 +1,386 @@
+// Forward and input gradient of the avse1 AudioFeatNet dilated convolutions for gfx950, as an implicit GEMM on the
+// fp16 MFMA with fp32-accurate split operands ("fp16x3").
+//
+// Replaces the forward and the data-gradient halves of nn.Conv2d(64, 64, 5, padding=2d, dilation=d), d = 2, 4, 8, 16 —
+// conv2..conv5 of /root/reference/baseline/avse1/model.py:199-215 (AudioFeatNet, built in the loop at :202-209).  MIOpen
+// ran them at 0.6-0.8 of the fp32 MFMA peak (29 + 27 ms of the 145 ms avse1 C2 step, profiles/r04p_*).
+//
+//   Y[n][h][w][o] = sum_{i,kh,kw} X[n][h + d (kh - 2)][w + d (kw - 2)][i] * W[o][i][kh][kw]      (0 outside the image)
+//   input gradient: the same with X = dY and W'[o = ci][i = co][kh][kw] = W[co][ci][4 - kh][4 - kw]
+//
+// Precision: the fp32 MFMA (v_mfma_f32_32x32x2_f32) runs at 1/16 of the f16 rate.  Each fp32 operand is split into
+// two fp16 values after a power-of-two scale 2^e that puts the tensor's max |x| in [2^14, 2^15):
+//   hi = fp16(x 2^e), lo = fp16(x 2^e - hi)        (22 significant bits; hi <= 2^15 cannot overflow)
+// and each product is formed as hi*hi + hi*lo + lo*hi: three v_mfma_f32_32x32x16_f16 (exact 22-bit products, fp32
+// accumulation), dropping lo*lo (2^-22 of the product).  The representation error (2^-22 relative per operand) is below
+// the fp32 accumulation error of a K = 1600 dot product, so the result has fp32 accuracy at 16/3 = 5.3x the fp32 MFMA
+// rate.  Elements far below the tensor's max keep an absolute error of 2^-25 of the scaled unit (fp16 subnormals).
+//
+// Operands: X (and dY) are split once into the "Q4" layout: per pixel 4 channel quarters of 64 B = [hi 16 ci][lo 16 ci]
+// (avse_split16: absmax pass, then the split; the same 256 B per pixel as fp32).  W is split into
+// [stage = kh * 4 + quarter][kw][o][hi 16 | lo 16] (avse_dconv_wprep), 20 KB per stage.
+//
+// Work decomposition: workgroup = 256 consecutive output pixels of one image in raster order (they span one row or
+// the end of one and the start of the next, W = 257 > 256) x all 64 output channels; 4 waves, wave w = pixels
+// 64 w .. 64 w + 63 (2 MFMA blocks) x 64 channels (2 blocks): 64 accumulators per lane.  The reduction runs in 20
+// stages (kernel row kh x channel quarter q); per stage the input segment is staged once for all 5 kw taps: the tile's
+// pixels of row h, shifted by d (kh - 2), with the 2d halo on both sides, at LDS positions 0 .. nA + 4d, and for a
+// two-row tile the next row's pixels behind a 4d gap, so that output pixel j reads position pos(j) + d kw for tap kw
+// (pos(j) = j, or j + 4d in the second row) and the halo columns outside the image stage as zeros.  Per stage and
+// wave: 5 taps x 2 x 2 blocks x 3 products = 60 MFMAs on 8 fragment reads per tap.  Stages are staged HBM/L2 -> LDS
+// by LDS-DMA (buffer_load_dwordx4 ... lds, out-of-image pixels read past the buffer range and land as 0) into a ring
+// of 3 buffers, issued 2 stages ahead; one barrier per stage.  LDS rows are 64 B with the 16-B chunk c of row r at
+// c ^ ((r >> 2) & 3), so the 16 lanes of a ds_read_b128 group read 16 distinct bank slots.
+#include <algorithm>
+
+#include "common.h"
+
+namespace avse {
+namespace dcf {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef int i4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int C = 64, KS = 5, NQ = 4, TP = 256, THREADS = 256, WAVES = THREADS / 64;
+constexpr int ROWB = 64;                       // LDS bytes per staged row (position or W row): hi 16 | lo 16 channels
+constexpr int WIMG = KS * C * ROWB;            // one stage's W image: 5 taps x 64 output channels (20 KB)
+constexpr int NSTG = KS * NQ;                  // stages per tile
+constexpr int MAXD = 16;
+constexpr int XIMG_MAX = (TP + 8 * MAXD) * ROWB;
+constexpr int STAGE = XIMG_MAX + WIMG;         // ring slot (44 KB)
+constexpr int NBUF = 3;
+constexpr int MAXP = (XIMG_MAX + WIMG) / 1024 / WAVES + 1;   // LDS-DMA pieces per wave and stage (<= 11)
+static_assert(NBUF * STAGE <= 160 * 1024, "LDS");
+
+__device__ inline int swz(int r) { return (r >> 2) & 3; }
+
+// power-of-two scale exponent e for a tensor whose max |x| has the float bits mb: max 2^e in [2^14, 2^15)
+__device__ inline int split_exp(uint32_t mb) {
+    const int ef = (int)((mb >> 23) & 0xff);
+    if (mb == 0) return 0;
+    const int k = ef == 0 ? -127 : ef - 127;
+    return min(100, max(-100, 14 - k));
+}
+
+__device__ inline i4_t rsrc_of(const void* base, int64_t bytes) {
+    if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+    const uint64_t a = (uint64_t)base;
+    return i4_t{__builtin_amdgcn_readfirstlane((int)(uint32_t)a), __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff)),
+                __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
+
+// one 16-B-per-lane LDS-DMA wave-instruction: LDS[lds_addr + 16 lane] = buffer[voff] (0 past the range).  Inline asm:
+// the compiler's LDS-DMA builtin makes it wait vmcnt(0) before every ds_read of the array.  Nothing else uses M0.
+__device__ inline void dma16(i4_t r, uint32_t lds_addr, uint32_t voff) {
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds_addr)
+                 : "memory");
+}
+
+__device__ inline uint32_t lds_u32(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_void_t*)p);
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in 0 .. 12 (the immediate must be a constant)
+__device__ inline void wait_all_but(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    }
+}
+
+__device__ inline half8 frag(const uint8_t* img, int row, int c) {
+    return *reinterpret_cast<const half8*>(img + row * ROWB + 16 * (c ^ swz(row)));
+}
+
+struct Args {
+    const void* xq;              // Q4 split input (n_pix x 256 B)
+    const void* wq;              // prepped weights (NSTG x WIMG)
+    const uint32_t* maxbits;     // [0] = max |x| bits, [1] = max |w| bits
+    const float* bias;           // (64) or NULL
+    float* y;                    // NHWC fp32
+    int N, H, W, tiles;          // tiles per image
+};
+
+template <int D>
+__global__ __launch_bounds__(THREADS, 1) void fwd_kernel(Args a) {
+    constexpr int NP = TP + 8 * D;             // staged positions
+    constexpr int XIMG = NP * ROWB;
+    constexpr int PX = XIMG / 1024, PT = PX + WIMG / 1024;      // X pieces, all pieces of a stage
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[NBUF * STAGE];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int n = bid / a.tiles, t = bid % a.tiles;
+    const int HW = a.H * a.W;
+    const int p0 = t * TP;
+    const int hA = p0 / a.W, wA0 = p0 - hA * a.W;
+    const int nA = min(TP, a.W - wA0);          // tile pixels in row hA (the rest continue in row hA + 1)
+    const bool two = nA < TP;
+    const i4_t rx = rsrc_of(a.xq, (int64_t)a.N * HW * 256);
+    const i4_t rw = rsrc_of(a.wq, (int64_t)NSTG * WIMG);
+    const uint32_t lds0 = lds_u32(lds);
+
+    // this wave's LDS-DMA pieces of a stage: k = wave + 4 m; X pieces (k < PX) carry the lane's position column (or -1
+    // outside the image / the segment) and segment row offset; W pieces the lane's byte offset in the stage's W image
+    int pcol[MAXP], prow[MAXP];
+    uint32_t pchunk[MAXP];
+    const int npieces = (PT - wave + WAVES - 1) / WAVES;
+#pragma unroll
+    for (int m = 0; m < MAXP; ++m) {
+        const int k = wave + WAVES * m;
+        if (k < PX) {
+            const int r = 16 * k + (lane >> 2), c = (lane & 3) ^ swz(r);
+            int col, row;
+            if (r < nA + 4 * D) {
+                col = wA0 - 2 * D + r;
+                row = hA;
+            } else {
+                col = -2 * D + (r - nA - 4 * D);
+                row = two ? hA + 1 : -1000000;
+            }
+            pcol[m] = (col >= 0 && col < a.W) ? col : -1;
+            prow[m] = row;
+            pchunk[m] = 16u * c;
+        } else {
+            const int r = 16 * (k - PX) + (lane >> 2), c = (lane & 3) ^ swz(r);
+            pcol[m] = 0;
+            prow[m] = 0;
+            pchunk[m] = (uint32_t)(r * ROWB + 16 * c);
+        }
+    }
+    auto issue = [&](int s) {
+        const int kh = s / NQ, q = s % NQ;
+        const uint32_t img = lds0 + (s % NBUF) * STAGE;
+#pragma unroll
+        for (int m = 0; m < MAXP; ++m) {
+            if (m >= npieces) break;
+            const int k = wave + WAVES * m;
+            if (k < PX) {
+                const int row = prow[m] + D * (kh - 2);
+                const bool ok = pcol[m] >= 0 && row >= 0 && row < a.H;
+                const uint32_t pix = ((uint32_t)n * (uint32_t)a.H + (uint32_t)row) * (uint32_t)a.W + (uint32_t)pcol[m];
+                const uint32_t off = ok ? pix * 256u + (uint32_t)(q * 64) + pchunk[m] : 0x7FFFFFF0u;
+                dma16(rx, img + k * 1024, off);
+            } else {
+                dma16(rw, img + XIMG + (k - PX) * 1024, (uint32_t)(s * WIMG) + pchunk[m]);
+            }
+        }
+    };
+
+    // the lane's fragment rows: output pixel j = 64 wave + 32 i + (lane & 31) reads position pos(j) + D kw
+    int posA[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int j = 64 * wave + 32 * i + (lane & 31);
+        posA[i] = j < nA ? j : j + 4 * D;
+    }
+    const int hc = lane >> 5;                   // fragment chunk: hi = hc, lo = 2 + hc
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    issue(0);
+    issue(1);
+    for (int s = 0; s < NSTG; ++s) {
+        // stage s + 1 issued last iteration (or in the prologue) has landed, stage s long before; the barrier also
+        // releases stage s - 1's buffer, which stage s + 2 then refills
+        if (s + 1 < NSTG) wait_all_but(npieces);      // this wave's stage-s pieces landed (stage s + 1 may fly)
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + 2 < NSTG) issue(s + 2);
+        const uint8_t* ximg = lds + (s % NBUF) * STAGE;
+        const uint8_t* wimg = ximg + XIMG;
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+            half8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int r = posA[i] + D * kw;
+                ah[i] = frag(ximg, r, hc);
+                al[i] = frag(ximg, r, 2 + hc);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = kw * C + 32 * j + (lane & 31);
+                bh[j] = frag(wimg, r, hc);
+                bl[j] = frag(wimg, r, 2 + hc);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+    }
+
+    // epilogue: acc[i][j] register 4 g + e = pixel 64 wave + 32 i + 8 g + 4 (lane >> 5) + e, channel 32 j + (lane & 31)
+    const float scale = __builtin_ldexpf(1.f, -(split_exp(a.maxbits[0]) + split_exp(a.maxbits[1])));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int o = 32 * j + (lane & 31);
+        const float bv = a.bias ? a.bias[o] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int p = p0 + 64 * wave + 32 * i + 8 * g + 4 * (lane >> 5) + e;
+                    if (p < HW) a.y[((int64_t)n * HW + p) * C + o] = acc[i][j][4 * g + e] * scale + bv;
+                }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ operand preparation
+// max |x| over n floats -> atomicMax on the float bits (non-negative floats order like their bits; NaN wins)
+__global__ void absmax_kernel(const float4* x, int64_t n4, uint32_t* out) {
+    float m = 0.f;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 v = x[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    uint32_t b = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
+    if ((threadIdx.x & 63) == 0 && b) atomicMax(out, b);
+}
+
+__device__ inline uint32_t split2(float x0, float x1, float sc, uint32_t& lo) {
+    const float s0 = x0 * sc, s1 = x1 * sc;
+    const _Float16 h0 = (_Float16)s0, h1 = (_Float16)s1;
+    const _Float16 l0 = (_Float16)(s0 - (float)h0), l1 = (_Float16)(s1 - (float)h1);
+    lo = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+    return (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+}
+
+// NHWC fp32 (n_pix x 64) -> Q4 (n_pix x 4 quarters x [hi 16 | lo 16] fp16); thread = one (pixel, quarter)
+__global__ void split_kernel(const float* x, int64_t nq, const uint32_t* maxbits, uint4* xq) {
+    const float sc = __builtin_ldexpf(1.f, split_exp(maxbits[0]));
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4* s = reinterpret_cast<const float4*>(x + i * 16);
+        uint32_t hi[8], lo[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 v = s[k];
+            hi[2 * k] = split2(v.x, v.y, sc, lo[2 * k]);
+            hi[2 * k + 1] = split2(v.z, v.w, sc, lo[2 * k + 1]);
+        }
+        uint4* d = xq + i * 4;
+        d[0] = uint4{hi[0], hi[1], hi[2], hi[3]};
+        d[1] = uint4{hi[4], hi[5], hi[6], hi[7]};
+        d[2] = uint4{lo[0], lo[1], lo[2], lo[3]};
+        d[3] = uint4{lo[4], lo[5], lo[6], lo[7]};
+    }
+}
+
+// W (64 o, 64 i, 5, 5) fp32 -> [kh * 4 + q][kw][o][hi 16 | lo 16]; transposed = the input gradient's W'[o][i][kh][kw] =
+// W[i][o][4 - kh][4 - kw].  One workgroup: max |w| first, then the split with that scale.
+__global__ __launch_bounds__(1024) void wprep_kernel(const float* w, int transposed, uint32_t* maxbits, uint16_t* wq) {
+    __shared__ uint32_t red[16];
+    constexpr int TOT = C * C * KS * KS;
+    float m = 0.f;
+    for (int i = threadIdx.x; i < TOT; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
+    uint32_t b = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    b = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) b = max(b, red[k]);
+    if (threadIdx.x == 0) maxbits[1] = b;
+    const float sc = __builtin_ldexpf(1.f, split_exp(b));
+    // destination element e: stage s = kh * 4 + q, kw, o, plane, c (16)
+    for (int e = threadIdx.x; e < TOT; e += blockDim.x) {
+        const int c = e % 16, o = (e / 16) % C, kw = (e / (16 * C)) % KS, s = e / (16 * C * KS);
+        const int kh = s / NQ, q = s % NQ, i = q * 16 + c;
+        const float v = transposed ? w[((i * C + o) * KS + (KS - 1 - kh)) * KS + (KS - 1 - kw)]
+                                   : w[((o * C + i) * KS + kh) * KS + kw];
+        const float sv = v * sc;
+        const _Float16 h = (_Float16)sv, l = (_Float16)(sv - (float)h);
+        const int64_t row = ((int64_t)s * KS + kw) * C + o;
+        wq[row * 32 + c] = __builtin_bit_cast(uint16_t, h);
+        wq[row * 32 + 16 + c] = __builtin_bit_cast(uint16_t, l);
+    }
+}
+
+}  // namespace dcf
+}  // namespace avse
+
+using namespace avse::dcf;
+
+extern "C" {
+
+int64_t avse_dconv_wprep_bytes(void) { return (int64_t)NSTG * WIMG; }
+
+int avse_split16(int64_t n_pix, const float* x, void* xq, uint32_t* maxbits, avse_stream_t stream) {
+    if (!x || !xq || !maxbits) return AVSE_EINVAL;
+    if (n_pix <= 0) return AVSE_ESHAPE;
+    if (((uintptr_t)x & 15) || ((uintptr_t)xq & 15)) return AVSE_EALIGN;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
+    const int64_t n4 = n_pix * C / 4;
+    hipLaunchKernelGGL(absmax_kernel, dim3(2048), dim3(256), 0, st, reinterpret_cast<const float4*>(x), n4, maxbits);
+    AVSE_CHECK_LAUNCH();
+    const int64_t nq = n_pix * NQ;
+    const int blocks = (int)std::min<int64_t>((nq + 255) / 256, 8192);
+    hipLaunchKernelGGL(split_kernel, dim3(blocks), dim3(256), 0, st, x, nq, maxbits, reinterpret_cast<uint4*>(xq));
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* maxbits, avse_stream_t stream) {
+    if (!w || !wq || !maxbits) return AVSE_EINVAL;
+    hipLaunchKernelGGL(wprep_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, w, transposed, maxbits,
+                       reinterpret_cast<uint16_t*>(wq));
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_dconv_fwd(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq, const void* wq,
+                   const uint32_t* maxbits, const float* bias, float* y, avse_stream_t stream) {
+    if (!xq || !wq || !maxbits || !y) return AVSE_EINVAL;
+    if (N <= 0 || H <= 0 || W < TP || (dil != 2 && dil != 4 && dil != 8 && dil != 16)) return AVSE_ESHAPE;
+    if (N * H * W * 256 >= (1LL << 31) - 1024) return AVSE_ESHAPE;       // 32-bit byte offsets into the split input
+    Args a;
+    a.xq = xq;
+    a.wq = wq;
+    a.maxbits = maxbits;
+    a.bias = bias;
+    a.y = y;
+    a.N = (int)N;
+    a.H = (int)H;
+    a.W = (int)W;
+    a.tiles = (int)((H * W + TP - 1) / TP);
+    const dim3 grid((unsigned)(N * a.tiles)), block(THREADS);
+    hipStream_t st = (hipStream_t)stream;
+    switch (dil) {
+        case 2: hipLaunchKernelGGL(fwd_kernel<2>, grid, block, 0, st, a); break;
+        case 4: hipLaunchKernelGGL(fwd_kernel<4>, grid, block, 0, st, a); break;
+        case 8: hipLaunchKernelGGL(fwd_kernel<8>, grid, block, 0, st, a); break;
+        default: hipLaunchKernelGGL(fwd_kernel<16>, grid, block, 0, st, a); break;
+    }
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+}  // extern "C"

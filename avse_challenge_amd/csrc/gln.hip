@@ -634,6 +634,16 @@ __global__ void dw_tail_kernel(const float* __restrict__ ws_dw, const float2* __
 
 using namespace avse::gln;
 
+// Samples per launch pair of a two-pass kernel: the group's inputs of the first pass (bytes_per_sample) stay within
+// 64 MiB, so the second pass re-reads them from the 256 MiB Infinity Cache instead of HBM (with every sample in one
+// launch, C4's 262 MB of (x, dy) had left the cache by the time the second pass reached it: PMC 1.67x the algorithmic
+// bytes, profiles/r04_traffic.json).  The passes' own bytes in between (the first pass's reads, the second's writes)
+// stay inside the cache's reuse window (MI355X_MICROARCH.md 'Infinity Cache').
+static int64_t group_samples(int64_t B, int64_t bytes_per_sample) {
+    const int64_t cap = (64LL << 20) / (bytes_per_sample > 0 ? bytes_per_sample : 1);
+    return cap < 1 ? 1 : (cap > B ? B : cap);
+}
+
 extern "C" {
 
 int64_t avse_prelu_gln_workspace_bytes(int64_t B, int64_t C) { return 8 * B * C + 4 * B * C + 16 * B; }
@@ -644,14 +654,17 @@ int avse_prelu_gln_fwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     if (B <= 0 || C <= 0 || K <= 0 || B * C > (1LL << 31) - 1) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     float2* ws = (float2*)workspace;
-    // row statistics, then the apply pass with the finalize folded in (no finalize launch between them)
-    const int row0 = 0;
-    const unsigned rows = (unsigned)(B * C);
-    hipLaunchKernelGGL(stats_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, ws);
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
-                       beta, (const float2*)ws, eps, (float2*)stats, y);
-    AVSE_CHECK_LAUNCH();
+    // row statistics, then the apply pass, per group of samples (group_samples: x re-read from the Infinity Cache)
+    const int64_t S = group_samples(B, 4 * C * K);
+    for (int64_t b0 = 0; b0 < B; b0 += S) {
+        const int row0 = (int)(b0 * C);
+        const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
+        hipLaunchKernelGGL(stats_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, ws);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
+                           beta, (const float2*)ws, eps, (float2*)stats, y);
+        AVSE_CHECK_LAUNCH();
+    }
     return AVSE_OK;
 }
 
@@ -665,14 +678,18 @@ int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     float2* ws = (float2*)workspace;
     float* ws_a = (float*)(ws + B * C);
     float2* smeans = (float2*)(ws_a + B * C);
-    const int row0 = 0;
-    const unsigned rows = (unsigned)(B * C);
-    hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha,
-                       (const float2*)stats, dy, ws);
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(bwd_apply_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
-                       (const float2*)stats, (const float2*)ws, dy, dx, ws_a);
-    AVSE_CHECK_LAUNCH();
+    // (x, dy) row reduction, then the apply pass, per group of samples (its (x, dy) re-read from the Infinity Cache)
+    const int64_t S = group_samples(B, 8 * C * K);
+    for (int64_t b0 = 0; b0 < B; b0 += S) {
+        const int row0 = (int)(b0 * C);
+        const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
+        hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha,
+                           (const float2*)stats, dy, ws);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(bwd_apply_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
+                           (const float2*)stats, (const float2*)ws, dy, dx, ws_a);
+        AVSE_CHECK_LAUNCH();
+    }
     // dgamma / dbeta (sum over samples of the row partials) and the PReLU slope
     const unsigned cblocks = (unsigned)((C + 255) / 256);
     hipLaunchKernelGGL(bwd_finalize, dim3((unsigned)B + cblocks), dim3(256), 0, st, (int)B, (int)C, (int)K, ws, gamma,
@@ -711,16 +728,20 @@ int avse_dwconv_gln_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     if (int rc = dw_check(B, C, K, P, dil)) return rc;
     hipStream_t st = (hipStream_t)stream;
     float2* ws = (float2*)workspace;
-    const int row0 = 0;
-    const unsigned rows = (unsigned)(B * C);
+    // per group of samples: y1 (written by the first pass) re-read from the Infinity Cache by the apply pass
+    const int64_t S = group_samples(B, 8 * C * K);
+    for (int64_t b0 = 0; b0 < B; b0 += S) {
+        const int row0 = (int)(b0 * C);
+        const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
 #define L_(PP) hipLaunchKernelGGL(dwconv_stats_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, \
                               (int)dil, x, w, alpha, y1, ws)
-    AVSE_DW_P_SWITCH(P, L_)
+        AVSE_DW_P_SWITCH(P, L_)
 #undef L_
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha, gamma,
-                       beta, (const float2*)ws, eps, (float2*)stats, y);
-    AVSE_CHECK_LAUNCH();
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha, gamma,
+                           beta, (const float2*)ws, eps, (float2*)stats, y);
+        AVSE_CHECK_LAUNCH();
+    }
     return AVSE_OK;
 }
 
@@ -732,11 +753,14 @@ int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
         return AVSE_EINVAL;
     if (int rc = dw_check(B, C, K, P, dil)) return rc;
     hipStream_t st = (hipStream_t)stream;
-    const unsigned rows = (unsigned)(B * C);
     float2* ws = (float2*)workspace;
     float* ws_a = (float*)(ws + B * C);
     float* ws_dw = (float*)((float2*)(ws_a + B * C) + B);
-    const int row0 = 0;
+    // per group of samples: dy (read by the reduction) re-read from the Infinity Cache by the main pass
+    const int64_t S = group_samples(B, 8 * C * K);
+    for (int64_t b0 = 0; b0 < B; b0 += S) {
+    const int row0 = (int)(b0 * C);
+    const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
     hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha,
                        (const float2*)stats, dy, ws);
     AVSE_CHECK_LAUNCH();
@@ -753,6 +777,7 @@ int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
 #undef L_
 #undef L4_
     AVSE_CHECK_LAUNCH();
+    }
     const int n = (int)(C * P + C);
     hipLaunchKernelGGL(dw_tail_kernel, dim3(1 + (n + 255) / 256), dim3(256), 0, st, ws_dw, (const float2*)ws, ws_a,
                        (int)B, (int)C, (int)P, dw, dgamma, dbeta, dalpha);

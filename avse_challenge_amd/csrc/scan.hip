@@ -378,7 +378,9 @@ constexpr int RED = 8;   // adjoint steps buffered per cross-wave dB/dC flush
 // C3 and C5 backward by -0.7 .. +1.8 %: the kernel is VALU-throughput bound, not latency bound)
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
-template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS, bool FOLD>
+// PRE (delta_softplus == 2): delta already holds softplus(delta_raw + bias) (avse_dtproj's epilogue), so staging applies
+// neither; the epilogue still returns ddelta w.r.t. delta_raw (x sigma = 1 - exp(-dt)) and accumulates ddelta_bias.
+template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS, bool FOLD, bool PRE = false>
 __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, int nblk_d) {
     __shared__ __attribute__((aligned(16))) float s_ud[CPB * UD_STRIDE];   // (u, dt) -> (du, ddelta)
     __shared__ __attribute__((aligned(16))) float s_zg[CPB * Z_STRIDE];    // (F, g) -> (dz, g)  [(z, dout) unfolded]
@@ -631,7 +633,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                     const float gv = s_zg[id.c * Z_STRIDE + 2 * tg + 1];
                     const float ddt = ddt_s * AVSE_LN2 + ud.x * dus;
                     const float du = dus * ud.y + gv * Dv;
-                    const float sig = SOFTPLUS ? (1.f - fast_exp(-ud.y)) : 1.f;
+                    const float sig = (SOFTPLUS || PRE) ? (1.f - fast_exp(-ud.y)) : 1.f;
                     const float ddr = ddt * sig;
                     dD_acc += gv * ud.x;
                     dbias_acc += ddr;
@@ -755,7 +757,7 @@ __global__ __launch_bounds__(THREADS) void reduce_d_kernel(const float* ws_d, in
 
 template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS>
 static void launch_fwd(const avse_scan_fwd_args& a, int nblk_d, int nblocks, hipStream_t st) {
-    if (a.delta_softplus)
+    if (a.delta_softplus == 1)          // 2: delta holds the final step sizes (avse_dtproj), nothing to apply
         hipLaunchKernelGGL((fwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, true>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
     else
         hipLaunchKernelGGL((fwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, false>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
@@ -764,6 +766,17 @@ static void launch_fwd(const avse_scan_fwd_args& a, int nblk_d, int nblocks, hip
 template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS>
 static void launch_bwd(const avse_scan_bwd_args& a, int nblk_d, int nblocks, hipStream_t st) {
     const bool fold = !(HAS_Z && a.recompute_out_z);
+    if constexpr (!HAS_BIAS) {
+        if (a.delta_softplus == 2) {
+            if (fold)
+                hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, false, false, true, true>), dim3(nblocks), dim3(THREADS), 0,
+                                   st, a, nblk_d);
+            else
+                hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, false, false, false, true>), dim3(nblocks), dim3(THREADS),
+                                   0, st, a, nblk_d);
+            return;
+        }
+    }
     if (a.delta_softplus && fold)
         hipLaunchKernelGGL((bwd_kernel<Tin, HAS_Z, HAS_D, HAS_BIAS, true, true>), dim3(nblocks), dim3(THREADS), 0, st, a, nblk_d);
     else if (a.delta_softplus)
@@ -803,6 +816,12 @@ int64_t avse_scan_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t seqlen
     return 4 * (batch * nblk_d * 2 * NSTATE * seqlen + batch * dim * (NSTATE + 2));
 }
 
+static int check_mode(int32_t delta_softplus, const float* delta_bias) {
+    if (delta_softplus < 0 || delta_softplus > 2) return AVSE_EINVAL;
+    if (delta_softplus == 2 && delta_bias) return AVSE_EINVAL;     // the bias is already inside delta
+    return AVSE_OK;
+}
+
 static int check_common(int64_t batch, int64_t dim, int64_t seqlen, int64_t dstate, int32_t dtype) {
     if (batch <= 0 || dim <= 0 || seqlen <= 0) return AVSE_ESHAPE;
     if (dstate != NSTATE) return AVSE_ESHAPE;
@@ -814,7 +833,9 @@ static int check_common(int64_t batch, int64_t dim, int64_t seqlen, int64_t dsta
 int avse_scan_fwd(const avse_scan_fwd_args* a, avse_stream_t stream) {
     if (!a || !a->u || !a->delta || !a->A || !a->B || !a->C || !a->x) return AVSE_EINVAL;
     if (a->z ? !a->out_z : !a->out) return AVSE_EINVAL;
-    int rc = check_common(a->batch, a->dim, a->seqlen, a->dstate, a->in_dtype);
+    int rc = check_mode(a->delta_softplus, a->delta_bias);
+    if (rc) return rc;
+    rc = check_common(a->batch, a->dim, a->seqlen, a->dstate, a->in_dtype);
     if (rc) return rc;
     const int nblk_d = (int)((a->dim + CPB - 1) / CPB);
     const int nblocks = (int)(a->batch * nblk_d);
@@ -833,7 +854,9 @@ int avse_scan_bwd(const avse_scan_bwd_args* a, avse_stream_t stream) {
     if (a->recompute_out_z && (!a->z || !a->out_z)) return AVSE_EINVAL;
     if (a->D && !a->dD) return AVSE_EINVAL;
     if (a->delta_bias && !a->ddelta_bias) return AVSE_EINVAL;
-    int rc = check_common(a->batch, a->dim, a->seqlen, a->dstate, a->in_dtype);
+    int rc = check_mode(a->delta_softplus, a->delta_bias);
+    if (rc) return rc;
+    rc = check_common(a->batch, a->dim, a->seqlen, a->dstate, a->in_dtype);
     if (rc) return rc;
     const int nblk_d = (int)((a->dim + CPB - 1) / CPB);
     const int nblocks = (int)(a->batch * nblk_d);

@@ -90,6 +90,42 @@ def _bc4(M, dtype):
 
 # ------------------------------------------------------------------------ selective scan
 
+def _sp_mode(delta_softplus, delta_bias):
+    """The C ABI's delta_softplus: 0 / 1 (False / True, selective_scan_cuda's flag) or 2 = delta already holds
+    softplus(delta_raw + bias) from dtproj(); the backward then returns ddelta and ddelta_bias for delta_raw and the
+    bias (so a ddelta_bias is produced although delta_bias is None)."""
+    if delta_softplus is not True and delta_softplus == 2:
+        if delta_bias is not None:
+            raise RuntimeError("delta_softplus=2: the bias is already inside delta (pass delta_bias=None)")
+        return 2
+    return int(bool(delta_softplus))
+
+
+def dtproj(w, x, bias=None, softplus=True):
+    """delta = softplus(w @ x + bias[:, None]) per batch: w (D, R), x (b, R, l) with unit last stride (e.g. the first R
+    rows of x_proj's (b, R + 2n, l) output), bias (D) fp32 or None -> (b, D, l) in x's dtype with the scan layout's
+    padded time stride (csrc/dtproj.hip; fp32 accumulation).  The scan takes the result with delta_softplus=2."""
+    _need_gpu(w, x, bias)
+    dt = x.dtype
+    code = _dtype_code(dt)
+    if x.dim() != 3 or x.stride(2) != 1 or w.dim() != 2 or w.shape[1] != x.shape[1]:
+        raise RuntimeError(f"dtproj: w (D, R) and x (b, R, l) with unit last stride, got {tuple(w.shape)}, "
+                           f"{tuple(x.shape)}/{x.stride()}")
+    w = w.to(dt)
+    if w.stride(1) != 1:
+        w = w.contiguous()
+    b, R, l = x.shape
+    D = w.shape[0]
+    bias = None if bias is None else bias.float().contiguous()
+    out = _bdl_empty(b, D, l, dt, x.device)
+    tap = _tap_begin("avse_dtproj", x.device)
+    check(_lib.lib().avse_dtproj(b, D, R, l, code, ptr(w), w.stride(0), ptr(x), x.stride(0) if b > 1 else (R - 1) *
+                                 x.stride(1) + l, x.stride(1), ptr(bias), int(bool(softplus)), ptr(out), out.stride(0),
+                                 out.stride(1), stream_ptr(x.device)), "avse_dtproj")
+    _tap_end(tap)
+    return out
+
+
 def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False, reverse=False,
                        return_out=True):
     """Returns (out, x, out_z|None) — the selective_scan_cuda.fwd contract.
@@ -117,7 +153,7 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
     out_z = _bdl_empty(b, d, l, dt, u.device) if z is not None else None
     a = ScanFwdArgs()
     a.batch, a.dim, a.seqlen, a.dstate = b, d, l, NSTATE
-    a.in_dtype, a.delta_softplus, a.reverse = _dtype_code(dt), int(bool(delta_softplus)), int(bool(reverse))
+    a.in_dtype, a.delta_softplus, a.reverse = _dtype_code(dt), _sp_mode(delta_softplus, delta_bias), int(bool(reverse))
     a.u, a.u_bs, a.u_ds = u.data_ptr(), u.stride(0), u.stride(1)
     a.delta, a.delta_bs, a.delta_ds = delta.data_ptr(), delta.stride(0), delta.stride(1)
     a.A = A.data_ptr()
@@ -131,7 +167,9 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
     if out is not None:
         a.out, a.out_bs, a.out_ds = out.data_ptr(), out.stride(0), out.stride(1)
     a.x = x.data_ptr()
+    tap = _tap_begin("avse_scan_fwd", u.device)
     check(L.avse_scan_fwd(a, stream_ptr(u.device)), "avse_scan_fwd")
+    _tap_end(tap)
     return out, x, out_z
 
 
@@ -169,7 +207,8 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
         return o
     dB, dC = _grad_bc(dB_out), _grad_bc(dC_out)
     dD = torch.empty((d,), device=dev, dtype=torch.float32) if D is not None else None
-    dbias = torch.empty((d,), device=dev, dtype=torch.float32) if delta_bias is not None else None
+    mode = _sp_mode(delta_softplus, delta_bias)
+    dbias = torch.empty((d,), device=dev, dtype=torch.float32) if (delta_bias is not None or mode == 2) else None
     if z is not None:
         if dz is None:
             dz = _bdl_empty(b, d, l, dt, dev)
@@ -181,7 +220,7 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
     ws = torch.empty((L.avse_scan_bwd_workspace_bytes(b, d, l, NSTATE) + 3) // 4, device=dev, dtype=torch.float32)
     a = ScanBwdArgs()
     a.batch, a.dim, a.seqlen, a.dstate = b, d, l, NSTATE
-    a.in_dtype, a.delta_softplus = _dtype_code(dt), int(bool(delta_softplus))
+    a.in_dtype, a.delta_softplus = _dtype_code(dt), mode
     a.recompute_out_z = int(out_z is not None)
     a.reverse = int(bool(reverse))
     a.u, a.u_bs, a.u_ds = u.data_ptr(), u.stride(0), u.stride(1)
@@ -206,7 +245,9 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
     a.dD = dD.data_ptr() if dD is not None else None
     a.ddelta_bias = dbias.data_ptr() if dbias is not None else None
     a.workspace = ws.data_ptr()
+    tap = _tap_begin("avse_scan_bwd", dev)
     check(L.avse_scan_bwd(a, stream_ptr(dev)), "avse_scan_bwd")
+    _tap_end(tap)
     return [du, ddelta, dA, dB, dC, dD, dbias, dz, out_z]
 
 
@@ -417,6 +458,59 @@ def dconv_wgrad(x, dy, dilation, bias_grad=False):
                              stream_ptr(x.device)), "avse_dconv_wgrad")
     _tap_end(tap)
     return (out, db) if bias_grad else out
+
+
+# ------------------------------------------------------------------------ dilated Conv2d fwd / dX (split fp16 MFMA)
+
+DCONV_DILATIONS = (2, 4, 8, 16)     # dconv.hip instantiations
+
+
+def dconv_split_ok(x, dilation):
+    """True when csrc/dconv.hip takes conv(x) / its input gradient: (N, 64, H, W >= 256) fp32 GPU tensor, d in 2..16."""
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] == 64 and x.shape[3] >= 256
+            and dilation in DCONV_DILATIONS and x.shape[0] * x.shape[2] * x.shape[3] * 256 < (1 << 31) - 1024)
+
+
+def split16(x, maxbits):
+    """x (N, 64, H, W) fp32 (channels-last memory is read as it lies, anything else made so) -> its fp16 hi / lo split
+    in dconv.hip's Q4 layout (uint8 (N*H*W, 256)); writes max |x| (float bits) into maxbits[0]."""
+    _need_gpu(x)
+    x = x.contiguous(memory_format=torch.channels_last)
+    npix = x.shape[0] * x.shape[2] * x.shape[3]
+    xq = torch.empty((npix, 256), device=x.device, dtype=torch.uint8)
+    check(_lib.lib().avse_split16(npix, ptr(x), ptr(xq), ptr(maxbits), stream_ptr(x.device)), "avse_split16")
+    return xq
+
+
+def dconv_wprep(w, transposed, maxbits):
+    """W (64, 64, 5, 5) fp32 -> dconv.hip's split weight image (transposed: the input gradient's flipped W'); writes
+    max |w| into maxbits[1]."""
+    _need_gpu(w)
+    L = _lib.lib()
+    wq = torch.empty(int(L.avse_dconv_wprep_bytes()), device=w.device, dtype=torch.uint8)
+    check(L.avse_dconv_wprep(ptr(w.float().contiguous()), int(bool(transposed)), ptr(wq), ptr(maxbits),
+                             stream_ptr(w.device)), "avse_dconv_wprep")
+    return wq
+
+
+def dconv_fwd(x, w, dilation, bias=None, transposed=False):
+    """conv2d(x, w, bias, padding=2d, dilation=d) for the 64 -> 64 5x5 AudioFeatNet convs on csrc/dconv.hip (fp16x3
+    split MFMA, fp32-accurate); transposed=True: the input gradient conv_transpose(x = dY, w).  x (N, 64, H, W) fp32;
+    returns (N, 64, H, W) in channels-last memory."""
+    _need_gpu(x, w, bias)
+    if not dconv_split_ok(x, dilation) or tuple(w.shape) != (64, 64, 5, 5):
+        raise RuntimeError(f"dconv_fwd: unsupported shape {tuple(x.shape)} / {tuple(w.shape)} dilation {dilation}")
+    N, _, H, W = x.shape
+    maxbits = torch.empty(2, device=x.device, dtype=torch.int32)
+    xq = split16(x, maxbits)
+    wq = dconv_wprep(w, transposed, maxbits)
+    y = torch.empty((N, 64, H, W), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+    tap = _tap_begin("avse_dconv_fwd", x.device)
+    check(_lib.lib().avse_dconv_fwd(N, H, W, dilation, ptr(xq), ptr(wq), ptr(maxbits),
+                                    ptr(None if bias is None else bias.float().contiguous()), ptr(y),
+                                    stream_ptr(x.device)), "avse_dconv_fwd")
+    _tap_end(tap)
+    return y
 
 
 # ------------------------------------------------------------------------ ResNet trunk 3x3 Conv2d dW
@@ -634,9 +728,11 @@ def prelu_gln_fwd(x, alpha, gamma, beta, eps=1e-8):
     stats = torch.empty((Bn, 2), device=x.device, dtype=torch.float32)
     L = _lib.lib()
     ws = torch.empty((L.avse_prelu_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    tap = _tap_begin("avse_prelu_gln_fwd", x.device)
     check(L.avse_prelu_gln_fwd(Bn, C, Kn, ptr(x), ptr(alpha.float().contiguous()), ptr(gamma.float().contiguous()),
                                ptr(beta.float().contiguous()), float(eps), ptr(y), ptr(stats), ptr(ws),
                                stream_ptr(x.device)), "avse_prelu_gln_fwd")
+    _tap_end(tap)
     return y, stats
 
 
@@ -650,9 +746,11 @@ def prelu_gln_bwd(x, alpha, gamma, stats, dy):
     dbeta = torch.empty((C,), device=x.device, dtype=torch.float32)
     L = _lib.lib()
     ws = torch.empty((L.avse_prelu_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    tap = _tap_begin("avse_prelu_gln_bwd", x.device)
     check(L.avse_prelu_gln_bwd(Bn, C, Kn, ptr(x), ptr(alpha.float().contiguous()), ptr(gamma.float().contiguous()),
                                ptr(stats), ptr(dy), ptr(dx), ptr(dalpha), ptr(dgamma), ptr(dbeta), ptr(ws),
                                stream_ptr(x.device)), "avse_prelu_gln_bwd")
+    _tap_end(tap)
     return dx, dalpha, dgamma, dbeta
 
 
@@ -696,9 +794,11 @@ def dwconv_gln_fwd(x, w, dilation, alpha, gamma, beta, eps=1e-8):
     stats = torch.empty((Bn, 2), device=x.device, dtype=torch.float32)
     L = _lib.lib()
     ws = torch.empty((L.avse_dwconv_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    tap = _tap_begin("avse_dwconv_gln_fwd", x.device)
     check(L.avse_dwconv_gln_fwd(Bn, C, Kn, w2.shape[1], int(dilation), ptr(x), ptr(w2), ptr(alpha.float().contiguous()),
                                 ptr(gamma.float().contiguous()), ptr(beta.float().contiguous()), float(eps), ptr(y1),
                                 ptr(y), ptr(stats), ptr(ws), stream_ptr(x.device)), "avse_dwconv_gln_fwd")
+    _tap_end(tap)
     return y, y1, stats
 
 
@@ -715,10 +815,12 @@ def dwconv_gln_bwd(x, w, dilation, y1, alpha, gamma, stats, dy):
     dbeta = torch.empty((C,), device=x.device, dtype=torch.float32)
     L = _lib.lib()
     ws = torch.empty((L.avse_dwconv_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    tap = _tap_begin("avse_dwconv_gln_bwd", x.device)
     check(L.avse_dwconv_gln_bwd(Bn, C, Kn, w2.shape[1], int(dilation), ptr(x), ptr(w2), ptr(y1.contiguous()),
                                 ptr(alpha.float().contiguous()), ptr(gamma.float().contiguous()), ptr(stats), ptr(dy),
                                 ptr(dx), ptr(dw), ptr(dalpha), ptr(dgamma), ptr(dbeta), ptr(ws), stream_ptr(x.device)),
           "avse_dwconv_gln_bwd")
+    _tap_end(tap)
     return dx, dw.view_as(w), dalpha, dgamma, dbeta
 
 

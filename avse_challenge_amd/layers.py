@@ -210,15 +210,24 @@ def _conv2d_dgrad(x, w, dy, stride, padding, dilation):
                                                [0, 0], 1, [True, False, False])[0]
 
 
+# forward and input gradient of the 64 -> 64 dilated convs on csrc/dconv.hip (fp16x3 split-operand MFMA, fp32-accurate);
+# "0": MIOpen's fp32 convolutions
+_DCONV_SPLIT = os.environ.get("AVSE_DCONV_SPLIT", "1") == "1"
+
+
 class _DilatedConvFn(torch.autograd.Function):
-    """Conv2d(64, 64, 5, padding=2d, dilation=d) with the weight (and bias) gradient on the MFMA implicit-GEMM kernel
-    (csrc/dconv_wgrad.hip); forward and input gradient on MIOpen.  add_bias=False leaves the bias out of the output
+    """Conv2d(64, 64, 5, padding=2d, dilation=d): forward and input gradient on the split-fp16 MFMA implicit GEMM
+    (csrc/dconv.hip) where it applies (W >= 256: the avse1 spectrogram's 257 bins), else MIOpen; the weight (and bias)
+    gradient on the fp32 MFMA implicit GEMM (csrc/dconv_wgrad.hip).  add_bias=False leaves the bias out of the output
     (for a training-mode BatchNorm consumer, which removes it: see DilatedConv2d) but still returns its gradient."""
 
     @staticmethod
     def forward(ctx, x, w, b, dilation, add_bias):
         ctx.save_for_backward(x, w)
         ctx.dilation = dilation
+        ctx.split = _DCONV_SPLIT and K.dconv_split_ok(x, dilation)
+        if ctx.split:
+            return K.dconv_fwd(x, w, dilation, b if add_bias else None)
         pad = 2 * dilation
         return F.conv2d(x, w, b if add_bias else None, 1, pad, dilation)
 
@@ -228,7 +237,7 @@ class _DilatedConvFn(torch.autograd.Function):
         d = ctx.dilation
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = _conv2d_dgrad(x, w, dy, 1, 2 * d, d)
+            dx = K.dconv_fwd(dy, w, d, transposed=True) if ctx.split else _conv2d_dgrad(x, w, dy, 1, 2 * d, d)
         if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
             dw, db = K.dconv_wgrad(x, dy, d, bias_grad=True)
         elif ctx.needs_input_grad[1]:

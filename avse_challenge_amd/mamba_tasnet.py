@@ -10,8 +10,8 @@ Mirrors, with identical parameter names / state_dict keys (checkpoints load unch
   MambaTasNet.forward  train_wsj0mix.py:86-111 compute_forward
 The scan, the causal conv and the add+RMSNorm run in libavse_hip.so; the dense projections
 are GEMMs: bf16 (autocast) in_proj / out_proj / x_proj and their input gradients on the HIP MFMA GEMM
-(csrc/projgemm.hip), the fp32 ones, dt_proj (K = dt_rank) and the weight gradients on hipBLASLt
-(torch.matmul).  No CPU fallback: CPU tensors raise.
+(csrc/projgemm.hip), the fp32 ones and the weight gradients on hipBLASLt (torch.matmul); dt_proj (K = dt_rank) is
+csrc/dtproj.hip with the scan's softplus in its epilogue.  No CPU fallback: CPU tensors raise.
 """
 import math
 import os
@@ -46,8 +46,9 @@ def _autocast_dtype():
 
 def _hip_gemm(P, Q, out, alpha=1.0, fold=1):
     """out[g, q, p] = alpha sum_{b in group g} sum_k P[b, p, k] Q[b, q, k] on the HIP bf16 GEMM; None when it does not
-    take them."""
-    if _HIP_GEMM and min(P.shape[1], Q.shape[1]) >= 128 and K.gemm_bf16_supported(P, Q, out, fold):
+    take them.  Reductions shorter than 64 (dt_proj's K = dt_rank with AVSE_DTPROJ=0) stay on the library: their
+    single-stage tiles are all epilogue."""
+    if _HIP_GEMM and min(P.shape[1], Q.shape[1]) >= 128 and P.shape[2] >= 64 and K.gemm_bf16_supported(P, Q, out, fold):
         return K.gemm_bf16(P, Q, out, alpha, fold)
     return None
 
@@ -134,6 +135,20 @@ def _bsum_mm(a, bt, alpha=1.0):
     return r if alpha == 1.0 else alpha * r
 
 
+# dt_proj with the softplus in its epilogue (csrc/dtproj.hip) feeding the scan in delta_softplus mode 2 (default); "0": the
+# GEMM (hipBLASLt / the bf16 HIP GEMM) and the scan's own per-element softplus (mode 1), as the reference calls it.
+_DTPROJ = os.environ.get("AVSE_DTPROJ", "1") == "1"
+
+
+def _delta(dt_proj_w, x_rows, dt_bias):
+    """(delta, delta_bias, delta_softplus) for the scan: softplus(W x + b) from the fused kernel (bias None, mode 2), or
+    the raw GEMM output with the bias and mode 1 (rank > 64, or AVSE_DTPROJ=0)."""
+    if _DTPROJ and dt_proj_w.shape[1] <= 64:
+        dt = _autocast_dtype() or torch.result_type(dt_proj_w, x_rows)
+        return K.dtproj(dt_proj_w.to(dt), x_rows.to(dt), dt_bias, True), None, 2
+    return _wbmm(dt_proj_w, x_rows), dt_bias, True
+
+
 class MambaInnerNoOutProj(torch.autograd.Function):
     """Conv1d(k4)+SiLU -> x_proj -> dt_proj -> selective scan (z-gated); checkpoint_lvl 1.
 
@@ -153,11 +168,11 @@ class MambaInnerNoOutProj(torch.autograd.Function):
         x, z = xz.chunk(2, dim=1)
         conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=reverse)     # (b, d, l)
         x_dblT = _wbmm(x_proj_w, conv_out)                                       # (b, R + 2n, l)
-        delta = _wbmm(dt_proj_w, x_dblT[:, :R])                                  # (b, d, l)
+        delta, bias, mode = _delta(dt_proj_w, x_dblT[:, :R], dt_bias)             # (b, d, l)
         Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]                 # (b, n, l) views
         # the pre-gate `out` is neither written nor saved (the reference saves it, :212): the scan
         # backward recomputes y + D u per step anyway, so it only cost HBM traffic and memory
-        _, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, dt_bias, True, reverse=reverse,
+        _, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, bias, mode, reverse=reverse,
                                              return_out=False)
         ctx.save_for_backward(xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck)
         ctx.reverse = reverse
@@ -171,13 +186,14 @@ class MambaInnerNoOutProj(torch.autograd.Function):
         R = dt_proj_w.shape[1]
         x, z = xz.chunk(2, dim=1)
         conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=rev)
-        delta = _wbmm(dt_proj_w, x_dblT[:, :R])
+        delta, bias, mode = _delta(dt_proj_w, x_dblT[:, :R], dt_bias)             # the forward's values bit for bit
         Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]
         dxz = K.bdl_empty(xz.shape[0], xz.shape[1], xz.shape[2], xz.dtype, xz.device)
         dx, dz = dxz.chunk(2, dim=1)
         dx_dblT = K.bdl_empty(*x_dblT.shape, torch.float32, x_dblT.device)         # scan writes fp32 dB/dC
+        # ddelta / ddt_bias: gradients w.r.t. the pre-softplus dt_proj output and the bias in either mode
         dconv, ddelta, dA, _, _, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
-            conv_out, delta, A, Bm, Cm, D, z, dt_bias, dout, xck, None, dz, True, False, reverse=rev,
+            conv_out, delta, A, Bm, Cm, D, z, bias, dout, xck, None, dz, mode, False, reverse=rev,
             dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:])
         dx_dblT[:, :R] = _wbmm(dt_proj_w.t(), ddelta)
         ddt_proj_w = _bsum_mm(ddelta, x_dblT[:, :R].transpose(1, 2))               # (d, R)

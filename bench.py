@@ -186,7 +186,7 @@ class Avse1Step:
         from avse_challenge_amd import kernels as K
         cl = torch.channels_last
         flops = 2.0 * self.B * 64 * 64 * 25 * 376 * 257
-        mark = bool(int(os.environ.get("AVSE_PROFILE_MARK", "0")))    # tools/ktrace_window.py OUT_ROOF.csv
+        mark = os.environ.get("AVSE_PROFILE_MARK", "0") == "1"        # tools/ktrace_window.py OUT_ROOF.csv
         K.LAUNCH_TAPS["avse_dconv_wgrad"] = taps = []
         try:
             if mark:
@@ -269,32 +269,27 @@ class MambaStep:
                 "per_gpu_batch": self.B, "seq_len": 32000, "frames": 3999, "parallelism": f"dp{world}",
                 "direction_streams": self.direction_streams}
 
+    # the step's dominant hand-written kernels (rocprofv3 window: the scan backward, then the forward)
+    tap_kernels = ("avse_scan_bwd", "avse_scan_fwd")
+    scan_dtype, scan_len = torch.float32, 3999
+
     def roofline(self, dev):
-        from avse_challenge_amd import kernels as K
+        """In-step figure of the step's dominant kernel, the selective-scan backward (main._in_step_hbm): bytes as
+        MambaInnerNoOutProj calls it (u, delta, z, dout, B, C read; du, ddelta, dz and fp32 dB, dC written); the
+        forward's in-step figure and each kernel's isolated launch at the step's shape beside it."""
         d = 2 * self.model.masknet.mamba_net.layers[0].mixer.d_model
-        b, l = self.B, 3999
-        al = lambda *sh, scale=1.0: K.bdl_empty(*sh, torch.float32, dev).copy_(scale * torch.randn(sh, device=dev))  # noqa: E731
-        u, dl, z = al(b, d, l), al(b, d, l, scale=0.1), al(b, d, l)           # the model's aligned layout
-        A = -torch.rand(d, 16, device=dev) - 0.5
-        Bm, Cm = al(b, 16, l), al(b, 16, l)
-        D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
-        for _ in range(2):
-            K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        n = 5
-        e0.record()
-        for _ in range(n):
-            K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False)
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / n
-        byts = 4.0 * b * l * (4 * d + 2 * 16)     # u, delta, z, B, C read; out_z written
-        ach = byts / (ms * 1e-3) / 1e9
-        roof = {"kernel": "avse_scan_fwd (selective scan, fp32, training fwd: out_z + chunk states)", "bound": "hbm",
-                "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": None, "avg_ms": round(ms, 4), "algorithmic_bytes_per_launch": byts}
-        return _with_traffic(roof, "scan") if b == 64 else roof
+        b, l = self.B, self.scan_len
+        s = 2 if self.scan_dtype == torch.bfloat16 else 4
+        bwd = b * l * (7 * s * d + 2 * s * 16 + 2 * 4 * 16)
+        fwd = s * b * l * (4 * d + 2 * 16)
+        tag = "bf16" if s == 2 else "fp32"
+        roof = _in_step_hbm(self, "avse_scan_bwd", bwd, f"avse_scan_bwd (selective scan backward, {tag}, "
+                            f"{b} x {d} x {l}; entry point: main kernel + dB/dC and dA/dD/dbias reductions)")
+        f = _in_step_hbm(self, "avse_scan_fwd", fwd, f"avse_scan_fwd (training fwd, {tag}, out_z + checkpoints)")
+        if roof is None:
+            return None
+        roof["in_step_fwd"] = {k: f[k] for k in ("avg_ms", "achieved", "frac", "launches")} if f else None
+        return roof
 
     def cpu_baseline(self):
         """The oracle's full train step (every BiMamba layer, PIT SI-SNR, bwd, Adam), 1 warm-up + median of 3 — on
@@ -401,18 +396,9 @@ class AVMambaStep:
                 "global_batch": self.B * world, "per_gpu_batch": self.B, "seq_len": 48000, "frames": 5999,
                 "lip_frames": 75, "lip_hw": 112, "parallelism": f"dp{world}"}
 
-    def roofline(self, dev):
-        """Selective scan fwd at the step's shape, bf16 u/delta/z/B/C/out_z: (B, 1024, 5999)."""
-        from avse_challenge_amd import kernels as K
-        d = 2 * self.model.masknet.mamba_net.layers[0].mixer.d_model
-        b, l, bf = self.B, 5999, torch.bfloat16
-        al = lambda *sh, scale=1.0: K.bdl_empty(*sh, bf, dev).copy_(scale * torch.randn(sh, device=dev))  # noqa: E731
-        u, z, dl = al(b, d, l), al(b, d, l), al(b, d, l, scale=0.1)           # the model's aligned layout
-        A = -torch.rand(d, 16, device=dev) - 0.5
-        Bm, Cm = al(b, 16, l), al(b, 16, l)
-        D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
-        return _time_hbm(lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False),
-                         2.0 * b * l * (4 * d + 2 * 16), f"avse_scan_fwd (bf16, {b} x {d} x {l}, training fwd)")
+    tap_kernels = ("avse_scan_bwd", "avse_scan_fwd")
+    scan_dtype, scan_len = torch.bfloat16, 5999
+    roofline = MambaStep.roofline
 
     def cpu_baseline(self):
         """The oracle's full fp32 train step (lip encoder + all BiMamba layers, SI-SNR, bwd, Adam), 1 warm-up + median
@@ -487,15 +473,28 @@ class Avse4Step:
                 "global_batch": self.B * world, "per_gpu_batch": self.B, "seq_len": 80000, "channels": 2,
                 "frames": 3999, "lip_frames": 125, "lip_hw": 112, "parallelism": f"dp{world}"}
 
+    # the TCN's hand-written kernels (32 TemporalBlocks: fused dwconv -> PReLU -> gLN and PReLU -> gLN, each way)
+    tap_kernels = ("avse_dwconv_gln_bwd", "avse_dwconv_gln_fwd", "avse_prelu_gln_bwd", "avse_prelu_gln_fwd")
+
     def roofline(self, dev):
-        """HBM-bound TCN kernel at the step's shape: depthwise dilated conv1d fwd on (B, 512, 3999), dil 128.
-        Algorithmic bytes = read x + write y = 8 B per element."""
-        from avse_challenge_amd import kernels as K
-        x = torch.randn(self.B, 512, 3999, device=dev)
-        w = torch.randn(512, 1, 3, device=dev)
-        roof = _time_hbm(lambda: K.dwconv_fwd(x, w, 128), 8.0 * x.numel(),
-                         "avse_dwconv_fwd (depthwise dilated conv1d, H=512, K=3999, dil 128)")
-        return _with_traffic(roof, "dwconv") if self.B == 16 else roof
+        """In-step figures of the TCN's hand-written kernels (main._in_step_hbm) on (B, 512, 3999): algorithmic bytes
+        per element dwconv_gln fwd 12 (x read, y1 + y written), bwd 16 (x, y1, dy read, dx written), prelu_gln fwd 8,
+        bwd 12.  ``roofline`` is the one with the most kernel time in the step; all four are listed."""
+        ne = self.B * 512 * 3999
+        recs = []
+        for name, bpe, desc in (("avse_dwconv_gln_bwd", 16, "fused dwconv <- PReLU <- gLN backward"),
+                                ("avse_dwconv_gln_fwd", 12, "fused dwconv -> PReLU -> gLN forward"),
+                                ("avse_prelu_gln_bwd", 12, "PReLU <- gLN backward (after the 1x1 conv)"),
+                                ("avse_prelu_gln_fwd", 8, "PReLU -> gLN forward (after the 1x1 conv)")):
+            r = _in_step_hbm(self, name, bpe * ne, f"{name} ({desc}, {self.B} x 512 x 3999)")
+            if r is not None:
+                recs.append(r)
+        if not recs:
+            return None
+        roof = dict(max(recs, key=lambda r: r["step_ms"]))
+        roof["tcn_kernels"] = [{k: r[k] for k in ("kernel", "avg_ms", "achieved", "frac", "launches", "step_ms")}
+                               for r in recs]
+        return roof
 
     def cpu_baseline(self):
         """the oracle's train step (fwd + SI-SNR + bwd + Adam) on the same synthetic inputs,
@@ -650,6 +649,28 @@ def _with_traffic(roof, phase):
     return roof
 
 
+def _in_step_hbm(work, name, byts, desc, isolated=None, traffic_phase=None):
+    """roofline record of one tapped entry point from the last eager warm-up step (main: ``tap_kernels``): algorithmic
+    bytes per launch over the mean HIP-event duration of its launches in the step."""
+    per = getattr(work, "step_taps", {}).get(name) or []
+    if not per:
+        return None
+    ms = sum(per) / len(per)
+    ach = byts / (ms * 1e-3) / 1e9
+    rec = {"kernel": desc, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_ms": round(ms, 4),
+           "launches": len(per), "step_ms": round(sum(per), 3), "per_launch_ms": [round(v, 3) for v in per[:4]],
+           "measured": f"in-step: all {len(per)} launches of {name} in the last eager warm-up train step of the "
+                       "benchmarked model (same kernels, streams and concurrency as the captured timed step), HIP "
+                       "events on each launch's stream",
+           "algorithmic_bytes_per_launch": byts}
+    if traffic_phase:
+        _with_traffic(rec, traffic_phase)
+    if isolated is not None:
+        rec["isolated"] = isolated
+    return rec
+
+
 def _time_hbm(fn, byts, name, n=10):
     for _ in range(3):
         fn()
@@ -733,20 +754,28 @@ def roofline_hip(dev):
         pmcf = "r03b_scan_pmc_c3_fp32.txt" if tag == "C3" else "r03e_scan_pmc_c5_bf16.txt"
         ktype = "float" if s == 4 else "avse::bf16_t"
         u, z, dout = rnd(b, d, l, dtype=dt), rnd(b, d, l, dtype=dt), rnd(b, d, l, dtype=dt)
-        delta = rnd(b, d, l, dtype=dt, scale=0.1)
         A = -torch.rand(d, n, device=dev, generator=g) - 0.5
         Bm, Cm = rnd(b, n, l, dtype=dt), rnd(b, n, l, dtype=dt)
-        D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
-        _, x, _ = K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, return_out=False)
+        D = torch.ones(d, device=dev)
+        # the step sizes as the model makes them (mamba_tasnet._delta): dt_proj with the softplus in its epilogue
+        # (csrc/dtproj.hip, K = dt_rank = 32, the first 32 rows of x_proj's (b, 64, l) output), scanned in mode 2
+        xdbl = rnd(b, 64, l, dtype=dt)
+        wdt = ((32 ** -0.5) * torch.randn(d, 32, device=dev, generator=g)).to(dt)
+        bdt = torch.log(torch.expm1(0.001 + 0.099 * torch.rand(d, device=dev, generator=g)))   # dt init 1e-3 .. 0.1
+        add_hbm(f"avse_dtproj ({tag}, dt_proj + bias + softplus: 32 rows of x read, delta written)", [b, d, l], name,
+                s * b * l * (d + 32), lambda: K.dtproj(wdt, xdbl[:, :32], bdt))
+        delta = K.dtproj(wdt, xdbl[:, :32], bdt)
+        _, x, _ = K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, None, 2, return_out=False)
         # training fwd: reads u, delta, z, B, C; writes out_z
-        add_hbm(f"avse_scan_fwd ({tag}, training fwd, out_z only)", [b, d, l], name, s * b * l * (4 * d + 2 * n),
-                lambda: K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, bias, True, return_out=False),
+        add_hbm(f"avse_scan_fwd ({tag}, training fwd, out_z only; delta from avse_dtproj)", [b, d, l], name,
+                s * b * l * (4 * d + 2 * n),
+                lambda: K.selective_scan_fwd(u, delta, A, Bm, Cm, D, z, None, 2, return_out=False),
                 "scan" if tag == "C3" else "scan_c5", (pmcf, f"void avse::scan::fwd_kernel<{ktype},"))
         # bwd as the model calls it (out=None, no out_z recompute): reads u, delta, z, dout, B, C; writes du,
         # ddelta, dz (input dtype) and fp32 dB, dC
         add_hbm(f"avse_scan_bwd ({tag}, as MambaInnerNoOutProj calls it)", [b, d, l], name,
                 b * l * (7 * s * d + 2 * s * n + 2 * 4 * n),
-                lambda: K.selective_scan_bwd(u, delta, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False),
+                lambda: K.selective_scan_bwd(u, delta, A, Bm, Cm, D, z, None, dout, x, None, None, 2, False),
                 "scan_bwd" if tag == "C3" else "scan_bwd_c5",
                 (pmcf, f"void avse::scan::bwd_kernel<{ktype},"))
         if tag == "C3":
@@ -755,7 +784,7 @@ def roofline_hip(dev):
                     lambda: K.causal_conv1d_fwd(u, w, cb, True), "cconv")
             add_hbm("avse_cconv_bwd (C3, k4 + SiLU)", [b, d, l], name, 3 * s * b * d * l,
                     lambda: K.causal_conv1d_bwd(u, w, cb, dout, silu=True))
-        del u, z, dout, delta, Bm, Cm, x
+        del u, z, dout, delta, Bm, Cm, x, xdbl
         torch.cuda.empty_cache()
     xd = torch.randn(16, 512, 3999, device=dev, generator=g)          # the TCN kernels take contiguous (B, C, K)
     wd, gy = rnd(512, 1, 3), torch.randn(16, 512, 3999, device=dev, generator=g)
@@ -869,10 +898,33 @@ def main():
 
     use_graph = work.graph_ok and not args.no_graph and dev.type == "cuda"
     step = Trainer(work, world, dev, use_graph=use_graph, bucket_mb=args.bucket_mb)
-    for i in range(max(args.warmup, 1 if use_graph else 0)):
+    # in-step roofline of C3 / C4 / C5: every launch of the workload's dominant hand-written kernels inside the last
+    # eager warm-up step (the same kernels, streams and concurrency the captured step replays), HIP events on each
+    # launch's stream (kernels.LAUNCH_TAPS).  AVSE_PROFILE_MARK=roof brackets that step with marker kernels instead of
+    # the timed region (tools/profile_bench.sh: the window's kernel averages are the line's in-step avg_ms).
+    taps = getattr(work, "tap_kernels", ()) if (dev.type == "cuda" and rank == 0 and not args.no_roofline) else ()
+    roof_mark = os.environ.get("AVSE_PROFILE_MARK", "0") == "roof"
+    nwarm = max(args.warmup, 1 if use_graph else 0)
+    for i in range(nwarm):
         t = time.perf_counter()
-        step()
-        sync(dev)
+        tapping = bool(taps) and i == nwarm - 1
+        if tapping:
+            from avse_challenge_amd import kernels as K
+            for n in taps:
+                K.LAUNCH_TAPS[n] = []
+            if roof_mark:
+                torch.cuda._sleep(1000)
+        try:
+            step()
+            if tapping and roof_mark:
+                torch.cuda._sleep(1000)
+            sync(dev)
+            if tapping:
+                work.step_taps = {n: [a.elapsed_time(b) for a, b in K.LAUNCH_TAPS[n]] for n in taps}
+        finally:
+            if tapping:
+                for n in taps:
+                    K.LAUNCH_TAPS.pop(n, None)
         if rank == 0:
             print(f"[bench] warmup {i + 1}/{args.warmup}: {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
     graph = False
@@ -893,7 +945,7 @@ def main():
     sync(dev)
     barrier(world)
     sync(dev)
-    mark = bool(int(os.environ.get("AVSE_PROFILE_MARK", "0")))   # tools/ktrace_window.py brackets the timed steps
+    mark = os.environ.get("AVSE_PROFILE_MARK", "0") == "1"   # tools/ktrace_window.py brackets the timed steps
     if mark:
         torch.cuda._sleep(1000)
     t0 = time.perf_counter()

@@ -47,7 +47,10 @@ int avse_abi_version(void);
 typedef struct {
     int64_t batch, dim, seqlen, dstate;
     int32_t in_dtype;          /* AVSE_F32 or AVSE_BF16: dtype of u, delta, z, B, C, out, out_z */
-    int32_t delta_softplus;
+    int32_t delta_softplus;    /* 0: delta used as given (+ delta_bias); 1: softplus(delta + delta_bias) per element, as
+                                  selective_scan_cuda; 2: delta already holds softplus(delta_raw + bias) (avse_dtproj's
+                                  epilogue; delta_bias must be NULL) -- the backward then returns ddelta and
+                                  ddelta_bias w.r.t. delta_raw and the bias (x sigmoid = 1 - exp(-delta)) */
     int32_t reverse;           /* 1: scan over time backwards, i.e. flip(scan(flip(.))) without copies
                                   (the BiMamba v2 backward direction, bimamba.py:236-253) */
     const void* u;      int64_t u_bs, u_ds;          /* batch / dim strides */
@@ -95,6 +98,19 @@ int64_t avse_scan_n_chunks(int64_t seqlen);
 int64_t avse_scan_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t seqlen, int64_t dstate);
 int avse_scan_fwd(const avse_scan_fwd_args* a, avse_stream_t stream);
 int avse_scan_bwd(const avse_scan_bwd_args* a, avse_stream_t stream);
+
+/* dt_proj with the scan's softplus in the epilogue.  Replaces
+ *   delta = delta_proj_weight @ x_dbl[:, :delta_rank].t()      selective_scan_interface.py:187
+ * followed by selective_scan_cuda's per-element softplus(delta + delta_bias) (selective_scan_ref :110-112):
+ *   delta[b][d][t] = softplus(sum_r W[d][r] x[b][r][t] + bias[d])   (softplus = 0: the affine value only).
+ * x (b, rank, l) with t contiguous (rows x_rs apart, batches x_bs apart; the first rank rows of x_proj's
+ * transposed output), W (dim, rank) rows w_ds apart, bias (dim) fp32 or NULL, delta (b, dim, l) rows delta_ds
+ * apart.  dtype AVSE_F32 or AVSE_BF16 for x, W and delta; fp32 accumulation; rank <= 64.  Feeds avse_scan_* with
+ * delta_softplus = 2. */
+int avse_dtproj(int64_t batch, int64_t dim, int64_t rank, int64_t seqlen, int32_t dtype,
+                const void* w, int64_t w_ds, const void* x, int64_t x_bs, int64_t x_rs,
+                const float* bias, int32_t softplus, void* delta, int64_t delta_bs, int64_t delta_ds,
+                avse_stream_t stream);
 
 /* ---------------------------------------------------------------- causal conv1d -------
  * Replaces causal_conv1d_cuda.causal_conv1d_fwd / causal_conv1d_bwd (causal-conv1d
@@ -354,6 +370,25 @@ typedef struct {
     int32_t c_dtype;                 /* AVSE_BF16 */
 } avse_gemm_bf16_args;
 int avse_gemm_bf16(const avse_gemm_bf16_args* a, avse_stream_t stream);
+
+/* ---------------------------------------------------------------- dilated Conv2d fwd / input gradient ----
+ * Replaces the forward and the data gradient of nn.Conv2d(64, 64, 5, padding=2d, dilation=d), d = 2, 4, 8, 16
+ * (AudioFeatNet conv2..conv5, baseline/avse1/model.py:199-215), channels-last activations, as an implicit GEMM on the
+ * fp16 MFMA with fp32-accurate split operands: every operand x is scaled by 2^e (the tensor's max |x| into
+ * [2^14, 2^15)) and split into hi = fp16(x 2^e) and lo = fp16(x 2^e - hi); each product is hi*hi + hi*lo + lo*hi with
+ * fp32 accumulation.
+ *   avse_split16: x NHWC fp32 (n_pix, 64) -> xq (n_pix, 256 B): 4 channel quarters of [hi 16][lo 16] fp16, and
+ *                 maxbits[0] = bits of max |x| (maxbits is a 2-entry device buffer: [0] input, [1] weight).
+ *   avse_dconv_wprep: W (64, 64, 5, 5) fp32 -> wq (avse_dconv_wprep_bytes()), maxbits[1]; transposed = 1 prepares
+ *                 the input gradient's W'[o][i][kh][kw] = W[i][o][4 - kh][4 - kw].
+ *   avse_dconv_fwd: y[n][h][w][o] = sum x[n][h + d (kh - 2)][w + d (kw - 2)][i] W[o][i][kh][kw] (+ bias[o]); with
+ *                 x = dY and a transposed wq it is the input gradient.  W >= 256 (tiles of 256 raster pixels span at
+ *                 most two rows), n_pix * 256 < 2^31. */
+int64_t avse_dconv_wprep_bytes(void);
+int avse_split16(int64_t n_pix, const float* x, void* xq, uint32_t* maxbits, avse_stream_t stream);
+int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* maxbits, avse_stream_t stream);
+int avse_dconv_fwd(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq, const void* wq,
+                   const uint32_t* maxbits, const float* bias, float* y, avse_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -107,6 +107,94 @@ def test_scan_bwd_bf16_vs_oracle(reverse):
         close(v.float(), ref, 5e-5 * scale, tol, name)
 
 
+# ------------------------------------------------------------------ dt_proj + softplus (csrc/dtproj.hip)
+
+def _softplus64(v):
+    return torch.where(v > 20, v, torch.log1p(torch.exp(v)))
+
+
+@pytest.mark.parametrize("b,D,R,l,dtype", [(2, 1024, 32, 3999, torch.float32), (2, 1024, 32, 5999, torch.bfloat16),
+                                           (3, 100, 7, 301, torch.float32), (1, 64, 1, 5, torch.float32),
+                                           (2, 130, 64, 257, torch.bfloat16), (4, 512, 16, 36, torch.float32)])
+def test_dtproj_vs_fp64(b, D, R, l, dtype):
+    """delta = softplus(W x + bias) (selective_scan_interface.py:187 + the scan's softplus, :110-112) from the fused
+    kernel vs fp64 on the same (dtype-rounded) operands.  x is a row slice of a wider padded-stride tensor, as the model
+    passes x_proj's output; fp32 within 1e-5 of the output's scale; bf16 within one bf16 rounding (2^-8) + 1e-5."""
+    seed = b + D + R + l
+    xfull = K().bdl_empty(b, R + 32, l, dtype, torch.device(DEV))
+    xfull.copy_(det_input((b, R + 32, l), seed).to(DEV, dtype))
+    x = xfull[:, :R]
+    w = ((R ** -0.5) * det_input((D, R), seed + 1)).to(DEV, dtype)
+    bias = (-4.0 + det_input((D,), seed + 2)).to(DEV)
+    y = K().dtproj(w, x, bias)
+    assert y.dtype == dtype and y.shape == (b, D, l) and y.stride(2) == 1
+    ref = _softplus64(torch.einsum("dr,brl->bdl", w.double().cpu(), x.double().cpu()) + bias.double().cpu()[None, :, None])
+    tol = 1e-5 if dtype == torch.float32 else 2 ** -8
+    close(y.float(), ref, 1e-5 * float(ref.abs().max()), tol, "delta")
+    y0 = K().dtproj(w, x, None, softplus=False)
+    ref0 = torch.einsum("dr,brl->bdl", w.double().cpu(), x.double().cpu())
+    close(y0.float(), ref0, 1e-5 * float(ref0.abs().max()), tol, "affine, no bias")
+
+
+@pytest.mark.parametrize("reverse", [False, True])
+@pytest.mark.parametrize("b,d,l", [(2, 128, 300), (1, 64, 65)])
+def test_scan_mode2_bitwise_equals_mode1_fp32(b, d, l, reverse):
+    """delta_softplus = 2 (delta already softplus(W x + bias), the model's path) against the reference's call (mode 1:
+    raw W x + delta_bias, softplus inside the scan): both stage the same fp32 step sizes (the same softplus of the same
+    sum), so out_z, the checkpoints and every gradient (ddelta and ddelta_bias w.r.t. the raw value and the bias) are
+    bit-identical."""
+    seed = 7 * b + d + l
+    xr = det_input((b, 8, l), seed).to(DEV)
+    w = (0.3 * det_input((d, 8), seed + 1)).to(DEV)
+    bias = (-3.0 + det_input((d,), seed + 2)).to(DEV)
+    raw = K().dtproj(w, xr, None, softplus=False)
+    dt = K().dtproj(w, xr, bias)
+    u, z, dout = (det_input((b, d, l), seed + i).to(DEV) for i in (3, 4, 5))
+    A = -torch.exp(0.5 * det_input((d, 16), seed + 6)).to(DEV)
+    Bm, Cm = (det_input((b, 16, l), seed + i).to(DEV) for i in (7, 8))
+    D = det_input((d,), seed + 9).to(DEV)
+    _, x1, o1 = K().selective_scan_fwd(u, raw, A, Bm, Cm, D, z, bias, True, reverse=reverse, return_out=False)
+    _, x2, o2 = K().selective_scan_fwd(u, dt, A, Bm, Cm, D, z, None, 2, reverse=reverse, return_out=False)
+    assert torch.equal(o1, o2) and torch.equal(x1, x2)
+    g1 = K().selective_scan_bwd(u, raw, A, Bm, Cm, D, z, bias, dout, x1, None, None, True, False, reverse=reverse)
+    g2 = K().selective_scan_bwd(u, dt, A, Bm, Cm, D, z, None, dout, x2, None, None, 2, False, reverse=reverse)
+    for name, a_, b_ in zip(("du", "ddelta", "dA", "dB", "dC", "dD", "ddelta_bias", "dz"), g1[:8], g2[:8]):
+        assert torch.equal(a_, b_), name
+    with pytest.raises(RuntimeError):
+        K().selective_scan_fwd(u, dt, A, Bm, Cm, D, z, bias, 2)            # mode 2 takes no bias
+
+
+def test_scan_mode2_bf16_vs_oracle():
+    """C5 dtype: dt = softplus(W x + bias) rounded to bf16 once (the fused kernel), scanned in mode 2; out_z and the
+    gradients of the raw pre-bias value and the bias vs fp64 autograd through the oracle (softplus applied by the
+    oracle to the same raw value): bf16 outputs within one bf16 rounding plus the rounding of dt itself (2 x 2^-8)."""
+    b, d, l = 2, 128, 400
+    xr = det_input((b, 8, l), 5150).to(DEV, torch.bfloat16)
+    w = (0.3 * det_input((d, 8), 5151)).to(DEV, torch.bfloat16)
+    bias = (-3.0 + det_input((d,), 5152)).to(DEV)
+    dt = K().dtproj(w, xr, bias)
+    u, z, dout = (det_input((b, d, l), 5153 + i).to(DEV, torch.bfloat16) for i in range(3))
+    A = -torch.exp(0.5 * det_input((d, 16), 5156)).to(DEV)
+    Bm, Cm = (det_input((b, 16, l), 5157 + i).to(DEV, torch.bfloat16) for i in range(2))
+    D = det_input((d,), 5159).to(DEV)
+    _, x, out_z = K().selective_scan_fwd(u, dt, A, Bm, Cm, D, z, None, 2, return_out=False)
+    du, ddelta, dA, dB, dC, dD, dbias, dz, _ = K().selective_scan_bwd(u, dt, A, Bm, Cm, D, z, None, dout, x, None, None,
+                                                                      2, False)
+    raw = torch.einsum("dr,brl->bdl", w.double().cpu(), xr.double().cpu()).requires_grad_(True)
+    rb = bias.double().cpu().requires_grad_(True)
+    leaves = {k: v.double().cpu().requires_grad_(True) for k, v in (("u", u), ("B", Bm), ("C", Cm), ("z", z))}
+    rA, rD = A.double().cpu().requires_grad_(True), D.double().cpu().requires_grad_(True)
+    ref = mamba_ref.selective_scan(leaves["u"], raw, rA, leaves["B"], leaves["C"], rD, leaves["z"], rb, True,
+                                   acc_dtype=torch.float64)
+    ref.backward(dout.double().cpu())
+    close(out_z.float(), ref.detach(), 5e-5 * float(ref.abs().max()), 2 * 2 ** -8, "out_z")
+    for name, v, r_ in (("du", du, leaves["u"].grad), ("ddelta", ddelta, raw.grad), ("dz", dz, leaves["z"].grad),
+                        ("dA", dA, rA.grad), ("dB", dB.reshape(b, 16, l), leaves["B"].grad),
+                        ("dC", dC.reshape(b, 16, l), leaves["C"].grad), ("dD", dD, rD.grad), ("ddelta_bias", dbias, rb.grad)):
+        r_ = r_.detach()
+        close(v.float(), r_, 2e-3 * float(r_.abs().max()), 2 * 2 ** -8, name)
+
+
 # ------------------------------------------------------------------ selective scan: edge shapes vs oracle
 
 @pytest.mark.parametrize("b,d,l", [(1, 64, 1), (2, 64, 63), (1, 96, 65), (3, 130, 129), (1, 64, 200)])
@@ -916,6 +1004,39 @@ def test_dconv_wgrad_vs_fp64(N, H, W, dil):
     assert torch.equal(got3, got)
     dbt, dbb = dyd.sum((0, 2, 3)), dyd.abs().sum((0, 2, 3))
     assert float(((db.double().cpu() - dbt).abs() / dbb).max()) <= 1e-6
+
+
+@pytest.mark.parametrize("N,H,W,dil", [(2, 37, 257, 2), (2, 37, 257, 4), (1, 40, 257, 8), (2, 33, 257, 16),
+                                       (1, 5, 300, 16), (3, 9, 256, 2), (1, 3, 513, 8), (2, 2, 257, 16)])
+@pytest.mark.parametrize("transposed", [False, True])
+def test_dconv_split_fwd_vs_fp64(N, H, W, dil, transposed):
+    """K.dconv_fwd (csrc/dconv.hip: fp16x3 split-operand MFMA) vs fp64: the forward conv2d(x, W, padding=2d, dilation=d)
+    and the input gradient conv_transpose2d(dy, W, ...) (baseline/avse1/model.py:199-215).  Every element within 2e-6 of
+    its sum of |terms| (22-bit operands: ~5e-7 measured is the design bound; fp32 accumulation on top), 256-pixel tiles
+    spanning one or two rows, images shorter than the kernel, rows wider than two tiles.  The input mixes scales over 9
+    decades (the power-of-two scale follows the tensor's max) and the result is bit-identical on rerun."""
+    import torch.nn.functional as F
+    x = det_input((N, 64, H, W), 1900 + dil + W + H)
+    x = x * torch.exp(4.0 * det_input((N, 64, H, W), 1901 + dil))          # |x| from ~1e-7 to ~1e2
+    w = 0.03 * det_input((64, 64, 5, 5), 1902 + dil)
+    b = det_input((64,), 1903)
+    xd, wd = x.double(), w.double()
+    op = F.conv_transpose2d if transposed else F.conv2d
+    truth = op(xd, wd, None, 1, 2 * dil, dilation=dil)
+    bound = op(xd.abs(), wd.abs(), None, 1, 2 * dil, dilation=dil)
+    cl = torch.channels_last
+    xg = x.to(DEV).contiguous(memory_format=cl)
+    got = K().dconv_fwd(xg, w.to(DEV), dil, transposed=transposed)
+    assert got.is_contiguous(memory_format=cl) and got.shape == truth.shape
+    worst = float(((got.double().cpu() - truth).abs() / (bound + 1e-30)).max())
+    lib = op(xg, w.to(DEV), None, 1, 2 * dil, dilation=dil)
+    worst_lib = float(((lib.double().cpu() - truth).abs() / (bound + 1e-30)).max())
+    print(f"dconv split vs fp64: {worst:.2e} of sum|terms| (MIOpen fp32: {worst_lib:.2e})")
+    assert worst <= 2e-6, (worst, worst_lib)
+    assert torch.equal(K().dconv_fwd(xg, w.to(DEV), dil, transposed=transposed), got)
+    if not transposed:
+        gb = K().dconv_fwd(xg, w.to(DEV), dil, bias=b.to(DEV))
+        close(gb - got, b.to(DEV)[None, :, None, None].expand_as(got), 1e-5 * float(got.abs().max()), 0, "bias")
 
 
 def test_audiofeat_bias_folded_into_batchnorm():
