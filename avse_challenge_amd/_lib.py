@@ -72,6 +72,18 @@ class GemmBf16Args(ctypes.Structure):
     ]
 
 
+class GemmF32sArgs(ctypes.Structure):
+    _fields_ = [
+        ("batch", c_i64), ("mp", c_i64), ("mq", c_i64), ("k", c_i64), ("fold", c_i64),
+        ("p_hi", c_vp), ("p_lo", c_vp), ("p_bs", c_i64), ("p_sx", c_i64), ("p_sk", c_i64), ("p_extent", c_i64),
+        ("p_max", c_vp),
+        ("q_hi", c_vp), ("q_lo", c_vp), ("q_bs", c_i64), ("q_sx", c_i64), ("q_sk", c_i64), ("q_extent", c_i64),
+        ("q_max", c_vp),
+        ("c", c_vp), ("c_bs", c_i64), ("c_sq", c_i64),
+        ("alpha", c_f32),
+    ]
+
+
 # name -> (restype, argtypes); every symbol include/avse_hip.h declares
 SIGNATURES = {
     "avse_strerror": (ctypes.c_char_p, [c_i32]),
@@ -141,10 +153,14 @@ SIGNATURES = {
     "avse_lstm_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "avse_lstm_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_gemm_bf16": (c_i32, [ctypes.POINTER(GemmBf16Args), c_vp]),
+    "avse_gemm_f32s": (c_i32, [ctypes.POINTER(GemmF32sArgs), c_vp]),
+    "avse_split16_planes": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_dconv_wprep_bytes": (c_i64, []),
     "avse_split16": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_dconv_wprep": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp]),
     "avse_dconv_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_dconv_wgrad16_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
+    "avse_dconv_wgrad16": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

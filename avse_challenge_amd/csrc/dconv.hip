@@ -253,6 +253,195 @@ __global__ __launch_bounds__(THREADS, 1) void fwd_kernel(Args a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------ weight gradient
+// dW[o][i][kh][kw] = sum_{n,h,w} dY[n][h][w][o] X[n][h + d (kh - 2)][w + d (kw - 2)][i] from the two Q4-split operands
+// (X split in the forward, dY for the input gradient), scaled back by 2^-(e_dy + e_x).  Per-tap GEMM with M = o, N = i
+// and the reduction over pixels: workgroup (chunk range r, kernel row kh) runs over a contiguous range of 64-pixel raster
+// chunks; per chunk the dY rows and the input segment of row kh (positions as in the forward: the chunk's pixels of one
+// or two rows, 2d halo, 4d gap) are staged by LDS-DMA; wave (o block, i block) accumulates the 5 kw tiles (80
+// accumulators per lane).  Both operands are contiguous along the GEMM's M / N (channels), so the fragments are read with
+// ds_read_b64_tr_b16 (4 pixels x 16 channels per 16-lane group, delivered transposed) from 256-B pixel rows whose 16-B
+// chunk c sits at c ^ ((r & 3) << 2).  The kh = 0 workgroups add one more MFMA pair per k-step against a ones fragment:
+// the bias gradient db[o] = sum dY[.][o].  Per-workgroup partial slabs, summed by a second kernel (deterministic).
+constexpr int WG_CHUNK = 64;                     // pixels per chunk (4 k-steps of 16)
+constexpr int PIXB = 256;                        // LDS / Q4 bytes per pixel
+
+typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+
+__device__ inline int tswz(int r, int c) { return c ^ ((r & 3) << 2); }
+
+// MFMA operand fragment (32 channels x 16 pixels) of the channel block cb (quarters 2 cb, 2 cb + 1), plane pl (0 hi,
+// 1 lo), k-step rows rows[0..15] given per lane: lane l (group g = l >> 4, i = l & 15) reads pixel rows
+// row(8 (g >> 1) + (i >> 2) + 4 u), channels 16 (g & 1) + 4 (i & 3) .. + 3 of the block
+__device__ inline half8 tfrag(const uint8_t* img, const int (&row)[2], int cb, int pl, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    const int q = 2 * cb + (g & 1);
+    s4_t v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int r = row[u];
+        const int byte = q * 64 + pl * 32 + 8 * (i & 3);                 // within the pixel's 256 B
+        const int off = r * PIXB + 16 * tswz(r, byte >> 4) + (byte & 15);
+        v[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(img + off));
+    }
+    const s4_t w0 = v[0], w1 = v[1];
+    const short __attribute__((ext_vector_type(8))) w = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+    return __builtin_bit_cast(half8, w);
+}
+
+struct WArgs {
+    const void* xq;
+    const void* dyq;
+    const uint32_t* xmax;
+    const uint32_t* dymax;
+    float* part;                 // [ranges][kh][kw][o][i]
+    float* dbpart;               // [ranges][o] (kh = 0 workgroups) or NULL
+    int N, H, W, cpi, chunks, ranges;
+};
+
+template <int D>
+__global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(WArgs a) {
+    constexpr int NP = WG_CHUNK + 8 * D;           // staged input positions per chunk
+    constexpr int YIMG = WG_CHUNK * PIXB, XIMG = NP * PIXB, STG = YIMG + XIMG;
+    constexpr int NB = (3 * STG <= 160 * 1024) ? 3 : 2;
+    constexpr int PY = YIMG / 1024, PT = PY + XIMG / 1024;       // pieces per chunk (4 pixels per 1-KB piece)
+    constexpr int MAXPW = PT / WAVES + 1;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[NB * STG];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);       // the 5 kh workgroups of a range share an XCD's L2
+    const int r = bid / KS, kh = bid % KS;
+    const int c_lo = (int)((int64_t)r * a.chunks / a.ranges), c_hi = (int)((int64_t)(r + 1) * a.chunks / a.ranges);
+    const int HW = a.H * a.W;
+    const i4_t rx = rsrc_of(a.xq, (int64_t)a.N * HW * PIXB);
+    const i4_t ry = rsrc_of(a.dyq, (int64_t)a.N * HW * PIXB);
+    const uint32_t lds0 = lds_u32(lds);
+    const int npieces = (PT - wave + WAVES - 1) / WAVES;
+    const int pr = lane >> 4, pc = lane & 15;                    // a piece's lane: row (of 4), physical chunk
+
+    auto issue = [&](int c, int buf) {
+        const int n = c / a.cpi, p0 = (c % a.cpi) * WG_CHUNK;
+        const int hA = p0 / a.W, wA0 = p0 - hA * a.W, nA = min(WG_CHUNK, a.W - wA0);
+        const uint32_t img = lds0 + buf * STG;
+#pragma unroll
+        for (int m = 0; m < MAXPW; ++m) {
+            if (m >= npieces) break;
+            const int k = wave + WAVES * m;
+            if (k < PY) {                                        // dY rows: chunk pixel j = 4 k + pr
+                const int j = 4 * k + pr, p = p0 + j;
+                const uint32_t off = p < HW ? ((uint32_t)(n * HW + p) * PIXB + 16u * tswz(j, pc)) : 0x7FFFFFF0u;
+                dma16(ry, img + k * 1024, off);
+            } else {
+                const int q = 4 * (k - PY) + pr;                 // input position
+                int col, row;
+                if (q < nA + 4 * D) {
+                    col = wA0 - 2 * D + q;
+                    row = hA + D * (kh - 2);
+                } else {
+                    col = -2 * D + (q - nA - 4 * D);
+                    row = nA < WG_CHUNK ? hA + 1 + D * (kh - 2) : -1000000;
+                }
+                const bool ok = col >= 0 && col < a.W && row >= 0 && row < a.H;
+                const uint32_t pix = ((uint32_t)n * (uint32_t)a.H + (uint32_t)row) * (uint32_t)a.W + (uint32_t)col;
+                dma16(rx, img + YIMG + (k - PY) * 1024, ok ? pix * PIXB + 16u * tswz(q, pc) : 0x7FFFFFF0u);
+            }
+        }
+    };
+
+    const int ob = wave >> 1, ib = wave & 1;                    // this wave's (o, i) 32 x 32 block
+    const bool want_db = a.dbpart != nullptr && kh == 0 && ib == 0;      // wave-uniform
+    floatx16 acc[KS], accb;
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[k][e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) accb[e] = 0.f;
+    half8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (_Float16)1.0f;
+
+    const int g = lane >> 4, li = lane & 15;
+    if (c_lo < c_hi) issue(c_lo, 0);
+    if (NB == 3 && c_lo + 1 < c_hi) issue(c_lo + 1, 1);
+    for (int c = c_lo; c < c_hi; ++c) {
+        const int it = c - c_lo;
+        const bool ahead = NB == 3 && c + 1 < c_hi;              // the next chunk's pieces may still fly
+        if (ahead) wait_all_but(npieces);
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (c + NB - 1 < c_hi) issue(c + NB - 1, (it + NB - 1) % NB);
+        const uint8_t* yimg = lds + (it % NB) * STG;
+        const uint8_t* ximg = yimg + YIMG;
+        const int p0 = (c % a.cpi) * WG_CHUNK, hA = p0 / a.W, nA = min(WG_CHUNK, a.W - (p0 - hA * a.W));
+#pragma unroll
+        for (int s = 0; s < WG_CHUNK / 16; ++s) {
+            int ry_[2], rx_[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int j = 16 * s + 8 * (g >> 1) + (li >> 2) + 4 * u;       // the lane's pixel of the k-step
+                ry_[u] = j;
+                rx_[u] = j < nA ? j : j + 4 * D;
+            }
+            const half8 ah = tfrag(yimg, ry_, ob, 0, lane), al = tfrag(yimg, ry_, ob, 1, lane);
+#pragma unroll
+            for (int kw = 0; kw < KS; ++kw) {
+                const int rk[2] = {rx_[0] + D * kw, rx_[1] + D * kw};
+                const half8 bh = tfrag(ximg, rk, ib, 0, lane), bl = tfrag(ximg, rk, ib, 1, lane);
+                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[kw], 0, 0, 0);
+                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[kw], 0, 0, 0);
+                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[kw], 0, 0, 0);
+            }
+            if (want_db) {
+                accb = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ones, accb, 0, 0, 0);
+                accb = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ones, accb, 0, 0, 0);
+            }
+        }
+    }
+    // partial tiles: acc[kw] register 4 q + e = row o = 32 ob + 8 q + 4 (lane >> 5) + e, column i = 32 ib + (lane & 31)
+    const float sc = __builtin_ldexpf(1.f, -(split_exp(*a.xmax) + split_exp(*a.dymax)));
+    float* pp = a.part + ((int64_t)r * KS + kh) * KS * C * C;
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = 32 * ob + 8 * q + 4 * (lane >> 5) + e, i = 32 * ib + (lane & 31);
+                pp[((int64_t)kw * C + o) * C + i] = acc[kw][4 * q + e] * sc;
+            }
+    if (want_db && (lane & 31) == 0) {
+        const float sd = __builtin_ldexpf(1.f, -split_exp(*a.dymax));
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a.dbpart[(int64_t)r * C + 32 * ob + 8 * q + 4 * (lane >> 5) + e] = accb[4 * q + e] * sd;
+    }
+}
+
+// dW[o][i][kh][kw] = sum over ranges of part[range][kh][kw][o][i]; db[o] = sum over ranges of dbpart[range][o]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ dbpart, int ranges,
+                                    float* __restrict__ dw, float* __restrict__ db) {
+    constexpr int TOTAL = KS * KS * C * C;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= TOTAL) {
+        if (db != nullptr && idx < TOTAL + C) {
+            float v = 0.f;
+            for (int g = 0; g < ranges; ++g) v += dbpart[(int64_t)g * C + idx - TOTAL];
+            db[idx - TOTAL] = v;
+        }
+        return;
+    }
+    float v = 0.f;
+    for (int g = 0; g < ranges; ++g) v += part[(int64_t)g * TOTAL + idx];
+    const int i = idx % C, o = (idx / C) % C, kw = (idx / (C * C)) % KS, kh = idx / (KS * C * C);
+    dw[((o * C + i) * KS + kh) * KS + kw] = v;
+}
+
+inline int wgrad_ranges(int chunks) { return std::max(1, std::min(chunks, 256 / KS * 1)); }
+
 // ------------------------------------------------------------------------------------------------ operand preparation
 // max |x| over n floats -> atomicMax on the float bits (non-negative floats order like their bits; NaN wins)
 __global__ void absmax_kernel(const float4* x, int64_t n4, uint32_t* out) {
@@ -352,6 +541,46 @@ int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* max
     if (!w || !wq || !maxbits) return AVSE_EINVAL;
     hipLaunchKernelGGL(wprep_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, w, transposed, maxbits,
                        reinterpret_cast<uint16_t*>(wq));
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int64_t avse_dconv_wgrad16_workspace_bytes(int64_t N, int64_t H, int64_t W) {
+    const int64_t chunks = N * ((H * W + WG_CHUNK - 1) / WG_CHUNK);
+    return 4 * (int64_t)wgrad_ranges((int)std::min<int64_t>(chunks, 1 << 30)) * (KS * KS * C * C + C);
+}
+
+int avse_dconv_wgrad16(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq, const uint32_t* xmax,
+                       const void* dyq, const uint32_t* dymax, float* dw, float* db, float* workspace,
+                       avse_stream_t stream) {
+    if (!xq || !xmax || !dyq || !dymax || !dw || !workspace) return AVSE_EINVAL;
+    if (N <= 0 || H <= 0 || W < WG_CHUNK || (dil != 2 && dil != 4 && dil != 8 && dil != 16)) return AVSE_ESHAPE;
+    if (N * H * W * 256 >= (1LL << 31) - 1024) return AVSE_ESHAPE;
+    WArgs a;
+    a.xq = xq;
+    a.dyq = dyq;
+    a.xmax = xmax;
+    a.dymax = dymax;
+    a.N = (int)N;
+    a.H = (int)H;
+    a.W = (int)W;
+    a.cpi = (int)((H * W + WG_CHUNK - 1) / WG_CHUNK);
+    a.chunks = (int)(N * a.cpi);
+    a.ranges = wgrad_ranges(a.chunks);
+    a.part = workspace;
+    a.dbpart = db ? workspace + (int64_t)a.ranges * KS * KS * C * C : nullptr;
+    const dim3 grid((unsigned)(a.ranges * KS)), block(THREADS);
+    hipStream_t st = (hipStream_t)stream;
+    switch (dil) {
+        case 2: hipLaunchKernelGGL(wgrad_kernel<2>, grid, block, 0, st, a); break;
+        case 4: hipLaunchKernelGGL(wgrad_kernel<4>, grid, block, 0, st, a); break;
+        case 8: hipLaunchKernelGGL(wgrad_kernel<8>, grid, block, 0, st, a); break;
+        default: hipLaunchKernelGGL(wgrad_kernel<16>, grid, block, 0, st, a); break;
+    }
+    AVSE_CHECK_LAUNCH();
+    constexpr int TOTAL = KS * KS * C * C;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((TOTAL + C + 255) / 256), dim3(256), 0, st, a.part, a.dbpart, a.ranges,
+                       dw, db);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

@@ -76,7 +76,21 @@ struct Args {
     int32_t q_fast;                        // q tile index runs fastest in the tile order
     int32_t c_vec16;                       // bf16 out: rows 16-B aligned (c and c_sq * 2 multiples of 16)
     float alpha;
+    // split mode (fp32 GEMM on fp16 hi / lo planes): the lo planes (same strides as p / q) and the device max-|x| bits
+    // the planes were scaled by (dconv.hip split_exp)
+    const uint16_t* p_lo;
+    const uint16_t* q_lo;
+    const uint32_t* p_max;
+    const uint32_t* q_max;
 };
+
+// power-of-two split scale of a tensor with max |x| bits mb (the same function as dconv.hip's / gemmsplit's)
+__device__ inline int split_exp_pg(uint32_t mb) {
+    const int ef = (int)((mb >> 23) & 0xff);
+    if (mb == 0) return 0;
+    const int k = ef == 0 ? -127 : ef - 127;
+    return min(100, max(-100, 14 - k));
+}
 
 typedef int i4_t __attribute__((ext_vector_type(4)));
 
@@ -213,11 +227,19 @@ __device__ inline void read_frags(Frags& f, const uint8_t* img, int ks, int wr, 
 #pragma unroll
     for (int j = 0; j < 2; ++j) f.b[j] = frag_raw<Q_KC>(img + IMG, wq + 32 * j, ks, lane);
 }
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+template <bool F16>
 __device__ inline void mma(floatx16 (&acc)[4][2], const Frags& f) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+            if constexpr (F16)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, f.a[i]),
+                                                                   __builtin_bit_cast(half8, f.b[j]), acc[i][j], 0, 0, 0);
+            else
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+        }
 }
 
 // Pipeline (one barrier per stage).  Stage s is certified readable by the barrier of iteration s - 1 (its DMAs'
@@ -226,8 +248,14 @@ __device__ inline void mma(floatx16 (&acc)[4][2], const Frags& f) {
 // wave has finished reading stage s - 1) -> DMA stage s + AHEAD into stage s - 1's buffer -> MFMAs of stage s with the
 // next substep's / stage's fragment reads interleaved.  Before the barrier each wave's reads of the stage leaving the
 // ring have completed: an lgkmcnt(0) sits between the last read of stage s and the first prefetch read of stage s + 1.
-template <bool P_KC, bool Q_KC, bool OUT_F32>
+// EPI: 0 = bf16 out, LDS-staged 128-B lines; 1 = fp32 out straight from the accumulators (weight gradients: small
+// outputs); 2 = fp32 out, LDS-staged 128-B lines (large outputs).  SPLIT: the fp32 GEMM on fp16 hi / lo planes of both
+// operands (gemmsplit.hip): the k-stage sequence of a tile runs three segments, P_hi Q_hi, P_hi Q_lo, P_lo Q_hi, on the
+// f16 MFMA, and the epilogue scales by 2^-(e_p + e_q).
+template <bool P_KC, bool Q_KC, int EPI, bool SPLIT = false>
 __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
+    constexpr bool OUT_F32 = EPI != 0;
+    constexpr int NSEG = SPLIT ? 3 : 1;
     __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * STAGE];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -236,7 +264,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
     const int G = gridDim.x;
     const int base = (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8;
     const int my_tiles = base < a.ntiles ? (a.ntiles - base + G - 1) / G : 0;
-    const int per_tile = a.ntb * a.fold;
+    const int per_tile = NSEG * a.ntb * a.fold;
     const int total = my_tiles * per_tile;
     if (total == 0) return;                                    // workgroup-uniform: no barrier is skipped by part
     const int wr = wave >> 2, wc = wave & 3, wq = wc * 64;
@@ -246,12 +274,16 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
     // load cursor: the stage issued next = (tile ld_T, batch ld_f of its group, k-stage ld_kt)
     int ld_s = 0, ld_kt = 0, ld_f = 0, ld_T = base;
     uint32_t vp[PIECES], vq[PIECES];
-    i4_t rp, rq;
+    i4_t rp, rq, rp_lo, rq_lo;
     auto set_tile = [&](int T, int f) {
         const Tile t = tile_of(a, T);
         const int b = t.b * a.fold + f;
         rp = rsrc_from(a.p + (int64_t)b * a.p_bs, a.p_ext - (int64_t)b * a.p_bs);
         rq = rsrc_from(a.q + (int64_t)b * a.q_bs, a.q_ext - (int64_t)b * a.q_bs);
+        if constexpr (SPLIT) {
+            rp_lo = rsrc_from(a.p_lo + (int64_t)b * a.p_bs, a.p_ext - (int64_t)b * a.p_bs);
+            rq_lo = rsrc_from(a.q_lo + (int64_t)b * a.q_bs, a.q_ext - (int64_t)b * a.q_bs);
+        }
         piece_offsets<P_KC>(vp, t.p0, a.p_sx, a.mp, wave, lane);
         piece_offsets<Q_KC>(vq, t.q0, a.q_sx, a.mq, wave, lane);
     };
@@ -261,11 +293,17 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
         if (ld_s >= total) return;
         if (loader) {
             const uint32_t img = lds0 + (ld_s % NBUF) * STAGE;
-            stage_load<P_KC>(rp, img, vp, ld_kt * p_step, wave);
-            stage_load<Q_KC>(rq, img + IMG, vq, ld_kt * q_step, wave);
+            if constexpr (SPLIT) {
+                const int seg = ld_kt / a.ntb, kin = ld_kt - seg * a.ntb;     // segments: hi hi, hi lo, lo hi
+                stage_load<P_KC>(seg == 2 ? rp_lo : rp, img, vp, kin * p_step, wave);
+                stage_load<Q_KC>(seg == 1 ? rq_lo : rq, img + IMG, vq, kin * q_step, wave);
+            } else {
+                stage_load<P_KC>(rp, img, vp, ld_kt * p_step, wave);
+                stage_load<Q_KC>(rq, img + IMG, vq, ld_kt * q_step, wave);
+            }
         }
         ++ld_s;
-        if (++ld_kt == a.ntb) {
+        if (++ld_kt == NSEG * a.ntb) {
             ld_kt = 0;
             if (++ld_f == a.fold) {
                 ld_f = 0;
@@ -310,6 +348,9 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
+    float alpha_eff = a.alpha;
+    if constexpr (SPLIT) alpha_eff = __builtin_ldexpf(a.alpha, -(split_exp_pg(*a.p_max) + split_exp_pg(*a.q_max)));
+
     Frags f0, f1;
     read_frags<P_KC, Q_KC>(f0, lds, 0, wr, wq, lane);
 
@@ -326,7 +367,7 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
             Frags& cur = (ks & 1) ? f0 : f1;
             Frags& nxt = (ks & 1) ? f1 : f0;
             read_frags<P_KC, Q_KC>(nxt, img, ks, wr, wq, lane);
-            mma(acc, cur);
+            mma<SPLIT>(acc, cur);
             // keep these MFMAs ahead of the wait below: the compiler would otherwise sink them past it (they touch
             // no memory) and the wave would stall on the reads with the MFMA pipe idle
             __builtin_amdgcn_sched_barrier(0);
@@ -335,8 +376,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
         Frags& last = ((BK / 16) & 1) ? f0 : f1;                // the final substep's fragments
         Frags& pre = ((BK / 16) & 1) ? f1 : f0;                 // BK / 16 even: f0 again holds substep 0
         if (more) read_frags<P_KC, Q_KC>(pre, lds + ((s + 1) % NBUF) * STAGE, 0, wr, wq, lane);
-        mma(acc, last);
-        if (++kt < a.ntb) continue;
+        mma<SPLIT>(acc, last);
+        if (++kt < NSEG * a.ntb) continue;
         kt = 0;
         if (++f < a.fold) continue;
         f = 0;
@@ -344,7 +385,54 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
         // column q = q0 + wq + 32 j + (lane & 31)
         const Tile t = tile_of(a, T);
         T += G;
-        if constexpr (OUT_F32) {
+        if constexpr (EPI == 2) {
+            // fp32 out through stage s's buffer in 8 rounds of 32 p x 256 q (32 KB): the waves of wave row wr stage the
+            // accumulator block i, the store waves write each q row's 32 p as one 128-B line, non-temporal
+            uint8_t* stg = lds + (s % NBUF) * STAGE;               // [256 q][128 B], 16-B chunk c of row q at c ^ (q & 7)
+            float* cf = reinterpret_cast<float*>(a.c) + (int64_t)t.b * a.c_bs;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    barrier();                                  // the stage's / previous round's readers are done
+                    if (wr == h) {
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const int q = wq + 32 * j + (lane & 31);
+#pragma unroll
+                            for (int g = 0; g < 4; ++g) {
+                                const int pl = 8 * g + 4 * (lane >> 5);        // p within the round's 32
+                                const float4 v = {alpha_eff * acc[i][j][4 * g], alpha_eff * acc[i][j][4 * g + 1],
+                                                  alpha_eff * acc[i][j][4 * g + 2], alpha_eff * acc[i][j][4 * g + 3]};
+                                *reinterpret_cast<float4*>(stg + q * 128 + 16 * ((pl >> 2) ^ (q & 7))) = v;
+                            }
+                        }
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    barrier();
+                    if (!loader) {
+#pragma unroll
+                        for (int r = 0; r < 256 / 8 / (WAVES - LWAVES); ++r) {   // 8 rows per wave-instruction
+                            const int ql = (r * (WAVES - LWAVES) + (wave - LWAVES)) * 8 + (lane >> 3), c = lane & 7;
+                            const float4 v = *reinterpret_cast<const float4*>(stg + ql * 128 + 16 * (c ^ (ql & 7)));
+                            const int q = t.q0 + ql, p = t.p0 + 32 * (2 * i + h) + 4 * c;
+                            if (q < a.mq) {
+                                float* dst = cf + (int64_t)q * a.c_sq + p;
+                                if (p + 3 < a.mp && a.c_vec16) {
+                                    typedef float f4v_t __attribute__((ext_vector_type(4)));
+                                    __builtin_nontemporal_store(f4v_t{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v_t*>(dst));
+                                } else {
+                                    const float w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                                    for (int e = 0; e < 4; ++e)
+                                        if (p + e < a.mp) dst[e] = w[e];
+                                }
+                            }
+                        }
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    }
+                }
+        } else if constexpr (OUT_F32) {
             // the weight gradients: small outputs, written straight from the accumulators (16 B per lane)
             float* cf = reinterpret_cast<float*>(a.c) + (int64_t)t.b * a.c_bs;
 #pragma unroll
@@ -357,8 +445,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
                         const int p = t.p0 + 32 * (2 * i + wr) + 8 * g + 4 * (lane >> 5);
-                        const float4 v = {a.alpha * acc[i][j][4 * g], a.alpha * acc[i][j][4 * g + 1],
-                                          a.alpha * acc[i][j][4 * g + 2], a.alpha * acc[i][j][4 * g + 3]};
+                        const float4 v = {alpha_eff * acc[i][j][4 * g], alpha_eff * acc[i][j][4 * g + 1],
+                                          alpha_eff * acc[i][j][4 * g + 2], alpha_eff * acc[i][j][4 * g + 3]};
                         if (qok && p + 3 < a.mp) {
                             *reinterpret_cast<float4*>(crow + p) = v;
                         } else if (qok) {
@@ -386,8 +474,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
                     for (int g = 0; g < 4; ++g) {
                         const int pl = 32 * wr + 8 * g + 4 * (lane >> 5);       // p within the round's 64
                         uint2 w;
-                        w.x = pack_bf16x2(a.alpha * acc[i][j][4 * g], a.alpha * acc[i][j][4 * g + 1]);
-                        w.y = pack_bf16x2(a.alpha * acc[i][j][4 * g + 2], a.alpha * acc[i][j][4 * g + 3]);
+                        w.x = pack_bf16x2(alpha_eff * acc[i][j][4 * g], alpha_eff * acc[i][j][4 * g + 1]);
+                        w.y = pack_bf16x2(alpha_eff * acc[i][j][4 * g + 2], alpha_eff * acc[i][j][4 * g + 3]);
                         *reinterpret_cast<uint2*>(stg + q * 128 + 16 * ((pl >> 3) ^ (q & 7)) + (pl & 7) * 2) = w;
                     }
                 }
@@ -433,55 +521,38 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
 
 using namespace avse::pg;
 
-extern "C" {
+// ------------------------------------------------------------------------------------------------ split planes
+// x (b, r, c) fp32, c contiguous -> hi / lo fp16 planes with x's strides: hi = fp16(x 2^e), lo = fp16(x 2^e - hi) with
+// max |x| 2^e in [2^14, 2^15) (dconv.hip's split, the same 22 significant bits); the planes' padding is not written.
+__global__ void planes_absmax_kernel(const float* x, int64_t b, int64_t r, int64_t c, int64_t bs, int64_t rs,
+                                     uint32_t* out) {
+    float m = 0.f;
+    const int64_t rows = b * r;
+    for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+        const float* xr = x + (row / r) * bs + (row % r) * rs;
+        for (int64_t i = threadIdx.x; i < c; i += blockDim.x) m = fmaxf(m, fabsf(xr[i]));
+    }
+    uint32_t v = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    if ((threadIdx.x & 63) == 0 && v) atomicMax(out, v);
+}
 
-int avse_gemm_bf16(const avse_gemm_bf16_args* g, avse_stream_t stream) {
-    if (!g || !g->p || !g->q || !g->c) return AVSE_EINVAL;
-    if (g->c_dtype != AVSE_BF16 && g->c_dtype != AVSE_F32) return AVSE_EDTYPE;
-    const int64_t fold = g->fold > 0 ? g->fold : 1;
-    if (g->batch <= 0 || g->mp <= 0 || g->mq <= 0 || g->k <= 0 || g->batch % fold) return AVSE_ESHAPE;
-    const bool p_kc = g->p_sk == 1, q_kc = g->q_sk == 1;
-    if (!p_kc && g->p_sx != 1) return AVSE_ESHAPE;
-    if (!q_kc && g->q_sx != 1) return AVSE_ESHAPE;
-    const int64_t p_s = p_kc ? g->p_sx : g->p_sk, q_s = q_kc ? g->q_sx : g->q_sk;
-    const int c_align = g->c_dtype == AVSE_F32 ? 15 : 7;
-    if (p_s % 8 || q_s % 8 || ((uintptr_t)g->p & 15) || ((uintptr_t)g->q & 15) || ((uintptr_t)g->c & c_align) ||
-        g->c_sq % 4)
-        return AVSE_EALIGN;
-    const int64_t tp = (g->mp + BT - 1) / BT, tq = (g->mq + BT - 1) / BT, ntb = (g->k + BK - 1) / BK;
-    // 32-bit per-batch byte offsets: the farthest element a stage reads
-    const int64_t p_far = p_kc ? (tp * BT) * p_s + ntb * BK : ntb * BK * p_s + tp * BT;
-    const int64_t q_far = q_kc ? (tq * BT) * q_s + ntb * BK : ntb * BK * q_s + tq * BT;
-    if (p_far * 2 >= (1LL << 31) || q_far * 2 >= (1LL << 31)) return AVSE_ESHAPE;
-    const int64_t ntiles = g->batch / fold * tp * tq;
-    if (g->mp >= (1 << 30) || g->mq >= (1 << 30) || ntiles * ntb * fold >= (1LL << 31)) return AVSE_ESHAPE;
-    Args a;
-    a.p = (const uint16_t*)g->p;
-    a.q = (const uint16_t*)g->q;
-    a.c = g->c;
-    a.p_bs = g->p_bs;
-    a.q_bs = g->q_bs;
-    a.c_bs = g->c_bs;
-    a.p_ext = g->p_extent;
-    a.q_ext = g->q_extent;
-    a.p_sx = (int32_t)p_s;
-    a.q_sx = (int32_t)q_s;
-    a.c_sq = (int32_t)g->c_sq;
-    a.mp = (int32_t)g->mp;
-    a.mq = (int32_t)g->mq;
-    a.k = (int32_t)g->k;
-    a.batch = (int32_t)g->batch;
-    a.tp = (int32_t)tp;
-    a.tq = (int32_t)tq;
-    a.ntiles = (int32_t)ntiles;
-    a.ntb = (int32_t)ntb;
-    a.fold = (int32_t)fold;
-    a.kv_last = (int32_t)(g->k - (ntb - 1) * BK);
-    // the shared weight's tiles vary fastest; otherwise the operand with fewer tiles
-    a.q_fast = (g->q_bs == 0) ? 1 : (g->p_bs == 0) ? 0 : (tq <= tp);
-    a.alpha = g->alpha;
-    a.c_vec16 = ((uintptr_t)g->c % 16 == 0) && (g->c_sq % 8 == 0);
-    // persistent: one workgroup per CU (128 KB of LDS each), a multiple of 8 (the XCD tile split)
+__global__ void planes_split_kernel(const float* x, int64_t b, int64_t r, int64_t c, int64_t bs, int64_t rs,
+                                    const uint32_t* maxbits, _Float16* hi, _Float16* lo) {
+    const float sc = __builtin_ldexpf(1.f, split_exp_pg(*maxbits));
+    const int64_t rows = b * r;
+    for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+        const int64_t off = (row / r) * bs + (row % r) * rs;
+        for (int64_t i = threadIdx.x; i < c; i += blockDim.x) {
+            const float v = x[off + i] * sc;
+            const _Float16 h = (_Float16)v;
+            hi[off + i] = h;
+            lo[off + i] = (_Float16)(v - (float)h);
+        }
+    }
+}
+
+static int cu_count_cached() {
     static int cu_count[64];
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
@@ -490,22 +561,119 @@ int avse_gemm_bf16(const avse_gemm_bf16_args* g, avse_stream_t stream) {
             cu_count[dev] = 256;
         cus = cu_count[dev];
     }
-    int64_t G = ((int64_t)cus + 7) / 8 * 8;
+    return cus;
+}
+
+// shared host path of avse_gemm_bf16 / avse_gemm_f32s: operand checks, Args, persistent grid, instantiation
+template <bool SPLIT>
+static int launch_gemm(int64_t batch, int64_t mp, int64_t mq, int64_t k, int64_t fold_in, const void* p, const void* p_lo,
+                       int64_t p_bs, int64_t p_sx, int64_t p_sk, int64_t p_extent, const uint32_t* p_max, const void* q,
+                       const void* q_lo, int64_t q_bs, int64_t q_sx, int64_t q_sk, int64_t q_extent,
+                       const uint32_t* q_max, void* c, int64_t c_bs, int64_t c_sq, float alpha, int32_t c_dtype,
+                       avse_stream_t stream) {
+    if (!p || !q || !c || (SPLIT && (!p_lo || !q_lo || !p_max || !q_max))) return AVSE_EINVAL;
+    if (c_dtype != AVSE_BF16 && c_dtype != AVSE_F32) return AVSE_EDTYPE;
+    if (SPLIT && c_dtype != AVSE_F32) return AVSE_EDTYPE;
+    const int64_t fold = fold_in > 0 ? fold_in : 1;
+    if (batch <= 0 || mp <= 0 || mq <= 0 || k <= 0 || batch % fold) return AVSE_ESHAPE;
+    const bool p_kc = p_sk == 1, q_kc = q_sk == 1;
+    if (!p_kc && p_sx != 1) return AVSE_ESHAPE;
+    if (!q_kc && q_sx != 1) return AVSE_ESHAPE;
+    const int64_t p_s = p_kc ? p_sx : p_sk, q_s = q_kc ? q_sx : q_sk;
+    const int c_align = c_dtype == AVSE_F32 ? 15 : 7;
+    if (p_s % 8 || q_s % 8 || ((uintptr_t)p & 15) || ((uintptr_t)q & 15) || ((uintptr_t)c & c_align) || c_sq % 4 ||
+        (SPLIT && (((uintptr_t)p_lo & 15) || ((uintptr_t)q_lo & 15))))
+        return AVSE_EALIGN;
+    const int64_t tp = (mp + BT - 1) / BT, tq = (mq + BT - 1) / BT, ntb = (k + BK - 1) / BK;
+    // 32-bit per-batch byte offsets: the farthest element a stage reads
+    const int64_t p_far = p_kc ? (tp * BT) * p_s + ntb * BK : ntb * BK * p_s + tp * BT;
+    const int64_t q_far = q_kc ? (tq * BT) * q_s + ntb * BK : ntb * BK * q_s + tq * BT;
+    if (p_far * 2 >= (1LL << 31) || q_far * 2 >= (1LL << 31)) return AVSE_ESHAPE;
+    const int64_t ntiles = batch / fold * tp * tq;
+    if (mp >= (1 << 30) || mq >= (1 << 30) || ntiles * ntb * fold * (SPLIT ? 3 : 1) >= (1LL << 31)) return AVSE_ESHAPE;
+    Args a;
+    a.p = (const uint16_t*)p;
+    a.q = (const uint16_t*)q;
+    a.p_lo = (const uint16_t*)p_lo;
+    a.q_lo = (const uint16_t*)q_lo;
+    a.p_max = p_max;
+    a.q_max = q_max;
+    a.c = c;
+    a.p_bs = p_bs;
+    a.q_bs = q_bs;
+    a.c_bs = c_bs;
+    a.p_ext = p_extent;
+    a.q_ext = q_extent;
+    a.p_sx = (int32_t)p_s;
+    a.q_sx = (int32_t)q_s;
+    a.c_sq = (int32_t)c_sq;
+    a.mp = (int32_t)mp;
+    a.mq = (int32_t)mq;
+    a.k = (int32_t)k;
+    a.batch = (int32_t)batch;
+    a.tp = (int32_t)tp;
+    a.tq = (int32_t)tq;
+    a.ntiles = (int32_t)ntiles;
+    a.ntb = (int32_t)ntb;
+    a.fold = (int32_t)fold;
+    a.kv_last = (int32_t)(k - (ntb - 1) * BK);
+    // the shared weight's tiles vary fastest; otherwise the operand with fewer tiles
+    a.q_fast = (q_bs == 0) ? 1 : (p_bs == 0) ? 0 : (tq <= tp);
+    a.alpha = alpha;
+    a.c_vec16 = ((uintptr_t)c % 16 == 0) && (c_sq % 8 == 0);
+    // persistent: one workgroup per CU (128 KB of LDS each), a multiple of 8 (the XCD tile split)
+    int64_t G = ((int64_t)cu_count_cached() + 7) / 8 * 8;
     const int64_t need = (ntiles + 7) / 8 * 8;
     if (G > need) G = need;
     const dim3 grid((unsigned)G), block(THREADS);
     hipStream_t st = (hipStream_t)stream;
-    if (g->c_dtype == AVSE_BF16) {
-        if (p_kc && q_kc) hipLaunchKernelGGL((gemm_kernel<true, true, false>), grid, block, 0, st, a);
-        else if (p_kc) hipLaunchKernelGGL((gemm_kernel<true, false, false>), grid, block, 0, st, a);
-        else if (q_kc) hipLaunchKernelGGL((gemm_kernel<false, true, false>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((gemm_kernel<false, false, false>), grid, block, 0, st, a);
-    } else {
-        if (p_kc && q_kc) hipLaunchKernelGGL((gemm_kernel<true, true, true>), grid, block, 0, st, a);
-        else if (p_kc) hipLaunchKernelGGL((gemm_kernel<true, false, true>), grid, block, 0, st, a);
-        else if (q_kc) hipLaunchKernelGGL((gemm_kernel<false, true, true>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((gemm_kernel<false, false, true>), grid, block, 0, st, a);
-    }
+    // fp32 out: straight from the accumulators for the folded weight gradients (small), LDS-staged lines otherwise
+    const int epi = c_dtype == AVSE_BF16 ? 0 : (fold > 1 || !SPLIT) ? 1 : 2;
+#define AVSE_PG_LAUNCH(PK, QK, E) hipLaunchKernelGGL((gemm_kernel<PK, QK, E, SPLIT>), grid, block, 0, st, a)
+#define AVSE_PG_EPI(PK, QK)                                \
+    do {                                                   \
+        if (epi == 0) AVSE_PG_LAUNCH(PK, QK, 0);           \
+        else if (epi == 1) AVSE_PG_LAUNCH(PK, QK, 1);      \
+        else AVSE_PG_LAUNCH(PK, QK, 2);                    \
+    } while (0)
+    if (p_kc && q_kc) AVSE_PG_EPI(true, true);
+    else if (p_kc) AVSE_PG_EPI(true, false);
+    else if (q_kc) AVSE_PG_EPI(false, true);
+    else AVSE_PG_EPI(false, false);
+#undef AVSE_PG_EPI
+#undef AVSE_PG_LAUNCH
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+extern "C" {
+
+int avse_gemm_bf16(const avse_gemm_bf16_args* g, avse_stream_t stream) {
+    if (!g) return AVSE_EINVAL;
+    return launch_gemm<false>(g->batch, g->mp, g->mq, g->k, g->fold, g->p, nullptr, g->p_bs, g->p_sx, g->p_sk,
+                              g->p_extent, nullptr, g->q, nullptr, g->q_bs, g->q_sx, g->q_sk, g->q_extent, nullptr, g->c,
+                              g->c_bs, g->c_sq, g->alpha, g->c_dtype, stream);
+}
+
+int avse_gemm_f32s(const avse_gemm_f32s_args* g, avse_stream_t stream) {
+    if (!g) return AVSE_EINVAL;
+    return launch_gemm<true>(g->batch, g->mp, g->mq, g->k, g->fold, g->p_hi, g->p_lo, g->p_bs, g->p_sx, g->p_sk,
+                             g->p_extent, g->p_max, g->q_hi, g->q_lo, g->q_bs, g->q_sx, g->q_sk, g->q_extent, g->q_max,
+                             g->c, g->c_bs, g->c_sq, g->alpha, AVSE_F32, stream);
+}
+
+int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi, void* lo,
+                        uint32_t* maxbits, avse_stream_t stream) {
+    if (!x || !hi || !lo || !maxbits) return AVSE_EINVAL;
+    if (b <= 0 || r <= 0 || c <= 0 || x_rs < c || (b > 1 && x_bs < (r - 1) * x_rs + c)) return AVSE_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
+    const int64_t rows = b * r;
+    const unsigned blocks = (unsigned)(rows < 8192 ? rows : 8192);
+    hipLaunchKernelGGL(planes_absmax_kernel, dim3(blocks), dim3(256), 0, st, x, b, r, c, x_bs, x_rs, maxbits);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(planes_split_kernel, dim3(blocks), dim3(256), 0, st, x, b, r, c, x_bs, x_rs, maxbits,
+                       (_Float16*)hi, (_Float16*)lo);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

@@ -493,16 +493,20 @@ def dconv_wprep(w, transposed, maxbits):
     return wq
 
 
-def dconv_fwd(x, w, dilation, bias=None, transposed=False):
+def dconv_fwd(x, w, dilation, bias=None, transposed=False, split=None):
     """conv2d(x, w, bias, padding=2d, dilation=d) for the 64 -> 64 5x5 AudioFeatNet convs on csrc/dconv.hip (fp16x3
-    split MFMA, fp32-accurate); transposed=True: the input gradient conv_transpose(x = dY, w).  x (N, 64, H, W) fp32;
+    split MFMA, fp32-accurate); transposed=True: the input gradient conv_transpose(x = dY, w).  x (N, 64, H, W) fp32
+    (its shape only, when ``split`` = (xq, maxbits) from split16 is given: maxbits[1] is then overwritten with W's);
     returns (N, 64, H, W) in channels-last memory."""
     _need_gpu(x, w, bias)
     if not dconv_split_ok(x, dilation) or tuple(w.shape) != (64, 64, 5, 5):
         raise RuntimeError(f"dconv_fwd: unsupported shape {tuple(x.shape)} / {tuple(w.shape)} dilation {dilation}")
     N, _, H, W = x.shape
-    maxbits = torch.empty(2, device=x.device, dtype=torch.int32)
-    xq = split16(x, maxbits)
+    if split is None:
+        maxbits = torch.empty(2, device=x.device, dtype=torch.int32)
+        xq = split16(x, maxbits)
+    else:
+        xq, maxbits = split
     wq = dconv_wprep(w, transposed, maxbits)
     y = torch.empty((N, 64, H, W), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
     tap = _tap_begin("avse_dconv_fwd", x.device)
@@ -511,6 +515,24 @@ def dconv_fwd(x, w, dilation, bias=None, transposed=False):
                                     stream_ptr(x.device)), "avse_dconv_fwd")
     _tap_end(tap)
     return y
+
+
+def dconv_wgrad16(xs, dys, shape, dilation, bias_grad=False):
+    """dW (64, 64, 5, 5) [and db (64)] of Conv2d(64, 64, 5, padding=2d, dilation=d) from the split input and output
+    gradient: xs = (xq, x_maxbits), dys = (dyq, dy_maxbits) from split16 (csrc/dconv.hip, fp16x3 split MFMA);
+    shape = (N, 64, H, W)."""
+    (xq, xm), (dyq, dym) = xs, dys
+    _need_gpu(xq, dyq)
+    N, _, H, W = shape
+    L = _lib.lib()
+    dw = torch.empty((64, 64, 5, 5), device=xq.device, dtype=torch.float32)
+    db = torch.empty(64, device=xq.device, dtype=torch.float32) if bias_grad else None
+    ws = torch.empty((L.avse_dconv_wgrad16_workspace_bytes(N, H, W) + 3) // 4, device=xq.device, dtype=torch.float32)
+    tap = _tap_begin("avse_dconv_wgrad16", xq.device)
+    check(L.avse_dconv_wgrad16(N, H, W, dilation, ptr(xq), ptr(xm), ptr(dyq), ptr(dym), ptr(dw), ptr(db), ptr(ws),
+                               stream_ptr(xq.device)), "avse_dconv_wgrad16")
+    _tap_end(tap)
+    return (dw, db) if bias_grad else dw
 
 
 # ------------------------------------------------------------------------ ResNet trunk 3x3 Conv2d dW
@@ -1036,5 +1058,66 @@ def gemm_bf16(P, Q, out, alpha=1.0, fold=1):
     a.alpha, a.c_dtype = float(alpha), _dtype_code(out.dtype)
     tap = _tap_begin("avse_gemm_bf16", out.device)
     check(_lib.lib().avse_gemm_bf16(a, stream_ptr(out.device)), "avse_gemm_bf16")
+    _tap_end(tap)
+    return out
+
+
+# ------------------------------------------------------------------------ fp32 GEMM on split fp16 planes (C3 projections)
+
+def split_planes(t):
+    """t (b, r, c) fp32 view with stride(2) == 1 or stride(1) == 1 -> (hi, lo, maxbits): fp16 planes of t's shape and
+    strides holding fp16(t 2^e) and the remainder (csrc/projgemm.hip avse_split16_planes), and max |t|'s bits."""
+    _need_gpu(t)
+    if t.dtype != torch.float32 or t.dim() != 3:
+        raise RuntimeError("split_planes: (b, r, c) fp32 views only")
+    hi = torch.empty_strided(t.size(), t.stride(), device=t.device, dtype=torch.float16)
+    lo = torch.empty_strided(t.size(), t.stride(), device=t.device, dtype=torch.float16)
+    mb = torch.empty(1, device=t.device, dtype=torch.int32)
+    v = t if t.stride(2) == 1 else t.transpose(1, 2)
+    if v.stride(2) != 1:
+        raise RuntimeError(f"split_planes: no unit stride in {t.stride()}")
+    b, r, c = v.shape
+    check(_lib.lib().avse_split16_planes(b, r, c, ptr(v), v.stride(0) if b > 1 else (r - 1) * v.stride(1) + c,
+                                         v.stride(1), ptr(hi), ptr(lo), ptr(mb), stream_ptr(t.device)),
+          "avse_split16_planes")
+    return hi, lo, mb
+
+
+def gemm_f32s_supported(P, Q, out, fold=1):
+    """True when avse_gemm_f32s takes out[g, q, p] = sum_{b in g} sum_k P[b, p, k] Q[b, q, k] for these fp32 views."""
+    if not (P.is_cuda and P.dtype == Q.dtype == out.dtype == torch.float32):
+        return False
+    if P.dim() != 3 or Q.dim() != 3 or out.dim() != 3 or P.shape[2] != Q.shape[2] or P.shape[2] < 1:
+        return False
+    b = out.shape[0] * fold
+    if out.shape[1:] != (Q.shape[1], P.shape[1]) or P.shape[0] not in (1, b) or Q.shape[0] not in (1, b):
+        return False
+    if max(P.shape[0], Q.shape[0]) != b and fold != 1:
+        return False
+    if out.stride(2) != 1 or out.stride(1) % 4 or out.data_ptr() % 16:
+        return False
+    return _gemm_operand(P) is not None and _gemm_operand(Q) is not None
+
+
+def gemm_f32s(P, Q, out, alpha=1.0, fold=1):
+    """out[g, q, p] = alpha * sum_{b in group g} sum_k P[b, p, k] * Q[b, q, k] in fp32 on the split-fp16 MFMA GEMM
+    (csrc/projgemm.hip avse_gemm_f32s: both operands split into hi / lo fp16 planes, three MFMAs per product, fp32
+    accumulation, fp32-accurate).  Same operand rules as gemm_bf16; out fp32.  Returns out."""
+    _need_gpu(P, Q, out)
+    if not gemm_f32s_supported(P, Q, out, fold):
+        raise RuntimeError(f"avse_gemm_f32s: unsupported operands P {tuple(P.shape)}/{P.stride()} "
+                           f"Q {tuple(Q.shape)}/{Q.stride()} out {tuple(out.shape)}/{out.stride()} (fold {fold})")
+    ph, pl, pm = split_planes(P)
+    qh, ql, qm = split_planes(Q)
+    a = _lib.GemmF32sArgs()
+    a.batch, a.mp, a.mq, a.k, a.fold = out.shape[0] * fold, P.shape[1], Q.shape[1], P.shape[2], fold
+    a.p_hi, a.p_lo, (a.p_bs, a.p_sx, a.p_sk), a.p_extent, a.p_max = ph.data_ptr(), pl.data_ptr(), _gemm_operand(ph), \
+        _extent(ph), pm.data_ptr()
+    a.q_hi, a.q_lo, (a.q_bs, a.q_sx, a.q_sk), a.q_extent, a.q_max = qh.data_ptr(), ql.data_ptr(), _gemm_operand(qh), \
+        _extent(qh), qm.data_ptr()
+    a.c, a.c_bs, a.c_sq = out.data_ptr(), out.stride(0), out.stride(1)
+    a.alpha = float(alpha)
+    tap = _tap_begin("avse_gemm_f32s", out.device)
+    check(_lib.lib().avse_gemm_f32s(a, stream_ptr(out.device)), "avse_gemm_f32s")
     _tap_end(tap)
     return out

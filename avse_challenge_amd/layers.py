@@ -223,21 +223,38 @@ class _DilatedConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, dilation, add_bias):
-        ctx.save_for_backward(x, w)
         ctx.dilation = dilation
         ctx.split = _DCONV_SPLIT and K.dconv_split_ok(x, dilation)
         if ctx.split:
-            return K.dconv_fwd(x, w, dilation, b if add_bias else None)
+            # the fp16 hi / lo split of x is made once and kept for the weight gradient in place of x (same bytes)
+            mb = torch.empty(2, device=x.device, dtype=torch.int32)
+            xq = K.split16(x, mb)
+            y = K.dconv_fwd(x, w, dilation, b if add_bias else None, split=(xq, mb))
+            ctx.save_for_backward(xq, mb, w)
+            ctx.shape = tuple(x.shape)
+            return y
+        ctx.save_for_backward(x, w)
         pad = 2 * dilation
         return F.conv2d(x, w, b if add_bias else None, 1, pad, dilation)
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
         d = ctx.dilation
         dx = dw = db = None
+        if ctx.split:
+            xq, mb, w = ctx.saved_tensors
+            mbd = torch.empty(2, device=dy.device, dtype=torch.int32)
+            dyq = K.split16(dy, mbd)                   # shared by the input and the weight gradient
+            if ctx.needs_input_grad[0]:
+                dx = K.dconv_fwd(dy, w, d, transposed=True, split=(dyq, mbd))
+            if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+                dw, db = K.dconv_wgrad16((xq, mb[:1]), (dyq, mbd[:1]), ctx.shape, d, bias_grad=True)
+                dw = dw if ctx.needs_input_grad[1] else None
+                db = db if ctx.needs_input_grad[2] else None
+            return dx, dw, db, None, None
+        x, w = ctx.saved_tensors
         if ctx.needs_input_grad[0]:
-            dx = K.dconv_fwd(dy, w, d, transposed=True) if ctx.split else _conv2d_dgrad(x, w, dy, 1, 2 * d, d)
+            dx = _conv2d_dgrad(x, w, dy, 1, 2 * d, d)
         if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
             dw, db = K.dconv_wgrad(x, dy, d, bias_grad=True)
         elif ctx.needs_input_grad[1]:

@@ -10,8 +10,10 @@ Mirrors, with identical parameter names / state_dict keys (checkpoints load unch
   MambaTasNet.forward  train_wsj0mix.py:86-111 compute_forward
 The scan, the causal conv and the add+RMSNorm run in libavse_hip.so; the dense projections
 are GEMMs: bf16 (autocast) in_proj / out_proj / x_proj and their input gradients on the HIP MFMA GEMM
-(csrc/projgemm.hip), the fp32 ones and the weight gradients on hipBLASLt (torch.matmul); dt_proj (K = dt_rank) is
-csrc/dtproj.hip with the scan's softplus in its epilogue.  No CPU fallback: CPU tensors raise.
+(csrc/projgemm.hip); the fp32 in_proj / out_proj, their input and weight gradients on the same kernel's split-fp16 mode
+(avse_gemm_f32s, fp32-accurate); the rank-sized x_proj GEMMs and the bf16 weight gradients on hipBLASLt
+(torch.matmul); dt_proj (K = dt_rank) is csrc/dtproj.hip with the scan's softplus in its epilogue.  No CPU fallback:
+CPU tensors raise.
 """
 import math
 import os
@@ -53,6 +55,20 @@ def _hip_gemm(P, Q, out, alpha=1.0, fold=1):
     return None
 
 
+# fp32 projections (Mamba-TasNet C3) on the split-fp16 MFMA GEMM (avse_gemm_f32s: both operands split into hi / lo fp16
+# planes, three MFMAs per product, fp32 accumulation; fp32-accurate) where the tiles fill ("0": hipBLASLt fp32).
+_F32_SPLIT = os.environ.get("AVSE_F32_SPLIT", "1") == "1"
+
+
+def _f32_gemm(P, Q, out, alpha=1.0, fold=1):
+    """out[g, q, p] = alpha sum_{b in group g} sum_k P[b, p, k] Q[b, q, k] in fp32 on avse_gemm_f32s; None when it does
+    not take them (the x_proj / dt_proj rank-sized projections stay on the library)."""
+    if _F32_SPLIT and min(P.shape[1], Q.shape[1]) >= 128 and P.shape[2] >= 64 and \
+            K.gemm_f32s_supported(P, Q, out, fold):
+        return K.gemm_f32s(P, Q, out, alpha, fold)
+    return None
+
+
 def _wbmm(w, x, alpha=1.0):
     """alpha (m, k) weight @ (b, k, n) -> (b, m, n) as one strided-batched GEMM (weight batch stride 0).
     Keeping every projection in the scan's (b, channels, l) layout means no layout copies.  The output rows get
@@ -65,6 +81,8 @@ def _wbmm(w, x, alpha=1.0):
         dt = torch.result_type(w, x)
     out = K.bdl_empty(x.shape[0], w.shape[0], x.shape[2], dt, x.device)
     if _hip_gemm(x.transpose(1, 2), w[None], out, alpha) is not None:
+        return out
+    if dt == torch.float32 and _f32_gemm(x.transpose(1, 2), w[None], out, alpha) is not None:
         return out
     if alpha != 1.0:
         w = alpha * w
@@ -120,13 +138,16 @@ def _bsum_mm(a, bt, alpha=1.0):
     nb, m, l = a.shape
     n = bt.shape[2]
     dt = _autocast_dtype()
-    if dt == torch.bfloat16 and _HIP_GEMM_ALL:
+    if (dt == torch.bfloat16 and _HIP_GEMM_ALL) or (dt is None and _F32_SPLIT and a.dtype == bt.dtype == torch.float32):
         # batches folded into groups so that the launch has about one 256 x 256 tile per CU; groups summed after
         fold = max(1, nb * (-(-m // 256)) * (-(-n // 256)) // 256)
         while nb % fold:
             fold -= 1
         out = torch.empty(nb // fold, m, n, device=a.device, dtype=torch.float32)
-        if _hip_gemm(bt.to(dt).transpose(1, 2), a.to(dt), out, alpha, fold=fold) is not None:
+        if dt is None:
+            if _f32_gemm(bt.transpose(1, 2), a, out, alpha, fold=fold) is not None:
+                return out.sum(0)
+        elif _hip_gemm(bt.to(dt).transpose(1, 2), a.to(dt), out, alpha, fold=fold) is not None:
             return out.sum(0)
     if nb * m * n <= (1 << 27):
         r = torch.bmm(a, bt).float().sum(0)
@@ -224,6 +245,9 @@ class _InProj(torch.autograd.Function):
             wc, dxc = w.to(dt), dxz.to(dt)
             dh = _hip_gemm(wc.t()[None], dxc.transpose(1, 2),
                            torch.empty(dxz.shape[0], dxz.shape[2], w.shape[1], device=dxz.device, dtype=dt))
+        elif dxz.dtype == torch.float32:
+            dh = _f32_gemm(w.t()[None], dxz.transpose(1, 2),
+                           torch.empty(dxz.shape[0], dxz.shape[2], w.shape[1], device=dxz.device, dtype=torch.float32))
         if dh is None:
             dh = torch.bmm(dxz.transpose(1, 2), w.expand(dxz.shape[0], *w.shape))
         dw = _bsum_mm(dxz, h)
@@ -245,6 +269,11 @@ class _BiOutProj(torch.autograd.Function):
             wc, yc = w.to(dt), y.to(dt)
             out = _hip_gemm(wc[None], yc.transpose(1, 2),
                             torch.empty(y.shape[0], y.shape[2], w.shape[0], device=y.device, dtype=dt), 0.5)
+            if out is not None:
+                return out
+        if dt is None and y.dtype == torch.float32:
+            out = _f32_gemm(w[None], y.transpose(1, 2),
+                            torch.empty(y.shape[0], y.shape[2], w.shape[0], device=y.device, dtype=torch.float32), 0.5)
             if out is not None:
                 return out
         wt = 0.5 * w.t()

@@ -371,6 +371,24 @@ typedef struct {
 } avse_gemm_bf16_args;
 int avse_gemm_bf16(const avse_gemm_bf16_args* a, avse_stream_t stream);
 
+/* fp32 GEMMs of the fp32 models (Mamba-TasNet C3 projections) on the same kernel, fp32-accurate: each fp32 operand is
+ * given as two fp16 planes with the operand's strides, hi = fp16(x 2^e) and lo = fp16(x 2^e - hi), e from the operand's
+ * max |x| (bits in *p_max / *q_max, avse_split16_planes), and c = alpha 2^-(e_p + e_q) (P_hi Q_hi + P_hi Q_lo + P_lo Q_hi)
+ * on the f16 MFMA with fp32 accumulation: three MFMAs per product at 16/3 of the fp32 MFMA rate, 22-bit operands (the
+ * dropped lo*lo term is 2^-22 of a product).  Layout rules as avse_gemm_bf16; c fp32. */
+typedef struct {
+    int64_t batch, mp, mq, k, fold;
+    const void* p_hi; const void* p_lo;  int64_t p_bs, p_sx, p_sk, p_extent;  const uint32_t* p_max;
+    const void* q_hi; const void* q_lo;  int64_t q_bs, q_sx, q_sk, q_extent;  const uint32_t* q_max;
+    float* c;       int64_t c_bs, c_sq;
+    float alpha;
+} avse_gemm_f32s_args;
+int avse_gemm_f32s(const avse_gemm_f32s_args* a, avse_stream_t stream);
+/* x (b, r, c) fp32 with c contiguous (rows x_rs, batches x_bs apart) -> hi / lo fp16 planes at the same element
+ * offsets (their padding untouched) and *maxbits = bits of max |x|. */
+int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi, void* lo,
+                        uint32_t* maxbits, avse_stream_t stream);
+
 /* ---------------------------------------------------------------- dilated Conv2d fwd / input gradient ----
  * Replaces the forward and the data gradient of nn.Conv2d(64, 64, 5, padding=2d, dilation=d), d = 2, 4, 8, 16
  * (AudioFeatNet conv2..conv5, baseline/avse1/model.py:199-215), channels-last activations, as an implicit GEMM on the
@@ -389,6 +407,12 @@ int avse_split16(int64_t n_pix, const float* x, void* xq, uint32_t* maxbits, avs
 int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* maxbits, avse_stream_t stream);
 int avse_dconv_fwd(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq, const void* wq,
                    const uint32_t* maxbits, const float* bias, float* y, avse_stream_t stream);
+/* Weight (and bias) gradient of the same convolution from the split input xq (max bits *xmax) and the split output
+ * gradient dyq (*dymax): dw (64, 64, 5, 5), db (64) or NULL; workspace avse_dconv_wgrad16_workspace_bytes(). */
+int64_t avse_dconv_wgrad16_workspace_bytes(int64_t N, int64_t H, int64_t W);
+int avse_dconv_wgrad16(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq, const uint32_t* xmax,
+                       const void* dyq, const uint32_t* dymax, float* dw, float* db, float* workspace,
+                       avse_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1039,6 +1039,60 @@ def test_dconv_split_fwd_vs_fp64(N, H, W, dil, transposed):
         close(gb - got, b.to(DEV)[None, :, None, None].expand_as(got), 1e-5 * float(got.abs().max()), 0, "bias")
 
 
+@pytest.mark.parametrize("N,H,W,dil", [(2, 37, 257, 2), (2, 37, 257, 4), (1, 40, 257, 8), (2, 33, 257, 16),
+                                       (1, 5, 300, 16), (3, 9, 64, 2), (1, 3, 65, 8), (2, 2, 257, 16)])
+def test_dconv_wgrad16_vs_fp64(N, H, W, dil):
+    """K.dconv_wgrad16 (csrc/dconv.hip: fp16x3 split MFMA from the split input and output gradient) vs the fp64 weight
+    gradient of Conv2d(64, 64, 5, padding=2d, dilation=d) and dy's channel sums (the bias gradient from the same pass):
+    every element within 2e-6 of its sum of |terms| (the split operands carry 22 bits; fp32 accumulation over the
+    pixels on top); 64-pixel chunks spanning one or two rows and the images' partial last chunks; deterministic."""
+    x = det_input((N, 64, H, W), 1950 + dil + W) * torch.exp(3.0 * det_input((N, 64, H, W), 1951))
+    dy = det_input((N, 64, H, W), 1952 + dil + H)
+    xd, dyd = x.double(), dy.double()
+    truth = torch.nn.grad.conv2d_weight(xd, (64, 64, 5, 5), dyd, 1, 2 * dil, dil)
+    bound = torch.nn.grad.conv2d_weight(xd.abs(), (64, 64, 5, 5), dyd.abs(), 1, 2 * dil, dil)
+    cl = torch.channels_last
+    xm = torch.empty(2, device=DEV, dtype=torch.int32)
+    dm = torch.empty(2, device=DEV, dtype=torch.int32)
+    xq = K().split16(x.to(DEV).contiguous(memory_format=cl), xm)
+    dq = K().split16(dy.to(DEV).contiguous(memory_format=cl), dm)
+    dw, db = K().dconv_wgrad16((xq, xm[:1]), (dq, dm[:1]), (N, 64, H, W), dil, bias_grad=True)
+    worst = float(((dw.double().cpu() - truth).abs() / (bound + 1e-30)).max())
+    print(f"dconv wgrad16 vs fp64: {worst:.2e} of sum|terms|")
+    assert worst <= 2e-6, worst
+    dbt, dbb = dyd.sum((0, 2, 3)), dyd.abs().sum((0, 2, 3))
+    assert float(((db.double().cpu() - dbt).abs() / dbb).max()) <= 2e-6
+    dw2 = K().dconv_wgrad16((xq, xm[:1]), (dq, dm[:1]), (N, 64, H, W), dil)
+    assert torch.equal(dw2, dw)
+
+
+def test_dilated_conv2d_module_split_path_vs_torch():
+    """layers.DilatedConv2d at the avse1 spectrogram width (W = 257: the split-fp16 path of csrc/dconv.hip for the
+    output, the input gradient and the weight / bias gradients) vs nn.Conv2d in fp64 on the same parameters; the
+    bias-free form (bias_to_bn=True) returns the bias gradient all the same."""
+    from avse_challenge_amd.layers import DilatedConv2d
+    torch.manual_seed(4)
+    for dil in (2, 16):
+        ref = torch.nn.Conv2d(64, 64, 5, padding=2 * dil, dilation=dil).double()
+        ours = DilatedConv2d(64, 64, 5, padding=2 * dil, dilation=dil).to(DEV)
+        ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+        ours.to(memory_format=torch.channels_last)
+        x = det_input((2, 64, 20, 257), 1960 + dil)
+        gy = det_input((2, 64, 20, 257), 1961 + dil)
+        xr = x.double().requires_grad_(True)
+        yr = ref(xr)
+        (yr * gy.double()).sum().backward()
+        xg = x.to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        assert ours.hip_ok(xg)
+        y = ours(xg)
+        (y * gy.to(DEV)).sum().backward()
+        sc = lambda t: max(1e-6, float(t.abs().max()))                                             # noqa: E731
+        close(y, yr, 2e-5 * sc(yr), 0, f"y d={dil}")
+        close(xg.grad, xr.grad, 2e-5 * sc(xr.grad), 0, f"dx d={dil}")
+        close(ours.weight.grad, ref.weight.grad, 2e-5 * sc(ref.weight.grad), 0, f"dw d={dil}")
+        close(ours.bias.grad, ref.bias.grad, 2e-5 * sc(ref.bias.grad), 0, f"db d={dil}")
+
+
 def test_audiofeat_bias_folded_into_batchnorm():
     """AudioFeatNet (channels-last, training mode) with the conv2..conv5 biases folded into their BatchNorms
     (DilatedConv2d bias_to_bn + bn_act folded_bias) vs the same net with the biases added by the library convolution

@@ -119,3 +119,93 @@ def test_gemm_bf16_rejects_unsupported():
     assert not k.gemm_bf16_supported(a, a, out)
     with pytest.raises(RuntimeError):
         k.gemm_bf16(a, a, out)
+
+
+# ------------------------------------------------------------------ fp32 GEMM on split fp16 planes (avse_gemm_f32s)
+
+def _operand32(b, rows, k, kc, g, shared=False, spread=False):
+    """A (b or 1, rows, k) fp32 view, K-contiguous (kc) or contiguous along rows, with padded strides (NaN in the pads:
+    the split writes nothing there and the GEMM must not sum them); spread: magnitudes over ~7 decades."""
+    nb = 1 if shared else b
+    if kc:
+        base = torch.full((nb, rows, k + 8), float("nan"), device=DEV)
+        v = base[:, :, :k]
+    else:
+        base = torch.full((nb, k, -(-rows // 8) * 8 + 16), float("nan"), device=DEV)
+        v = base[:, :, :rows].transpose(1, 2)
+    x = torch.randn(v.shape, device=DEV, generator=g)
+    if spread:
+        x = x * torch.exp(4.0 * torch.randn(v.shape, device=DEV, generator=g))
+    v.copy_(x)
+    return v
+
+
+def _check32(out, P, Q, alpha, mp, fold=1):
+    prod = torch.matmul(Q.double(), P.double().transpose(1, 2))
+    mag = torch.matmul(Q.double().abs(), P.double().abs().transpose(1, 2))
+    if fold > 1:
+        prod = prod.reshape(-1, fold, *prod.shape[1:]).sum(1)
+        mag = mag.reshape(-1, fold, *mag.shape[1:]).sum(1)
+    ref, mag = alpha * prod, abs(alpha) * mag
+    err = ((out[..., :mp].double() - ref).abs() / (mag + 1e-300)).max()
+    return float(err)
+
+
+@pytest.mark.parametrize("p_kc", [True, False])
+@pytest.mark.parametrize("q_kc", [True, False])
+@pytest.mark.parametrize("shared", ["p", "q", None])
+def test_gemm_f32s_layouts_ragged_vs_fp64(p_kc, q_kc, shared):
+    """avse_gemm_f32s (fp32 GEMM as P_hi Q_hi + P_hi Q_lo + P_lo Q_hi on the f16 MFMA) vs fp64: every element within 2e-6
+    of its sum_k |P Q| (22-bit operands; fp32 accumulation), with operands spread over ~7 decades, ragged sizes, a K
+    tail, NaN in every padding column, and nothing written outside the logical output; compared with hipBLASLt's fp32
+    error on the same operands for the record."""
+    g = torch.Generator(device=DEV).manual_seed(70 + 2 * p_kc + q_kc)
+    b, mp, mq, k = 3, 300, 200, 200
+    P = _operand32(b, mp, k, p_kc, g, shared == "p", spread=True)
+    Q = _operand32(b, mq, k, q_kc, g, shared == "q")
+    out = torch.full((b, mq, mp + 20), float("nan"), device=DEV)[..., :mp]
+    assert K().gemm_f32s_supported(P, Q, out)
+    K().gemm_f32s(P, Q, out, 0.5)
+    err = _check32(out, P, Q, 0.5, mp)
+    lib = 0.5 * torch.matmul(Q.expand(b, -1, -1), P.expand(b, -1, -1).transpose(1, 2))
+    print(f"gemm_f32s err {err:.2e} of sum|PQ| (hipBLASLt fp32 {_check32(lib, P, Q, 1.0, mp):.2e})")
+    assert err <= 2e-6, err
+    pad = torch.as_strided(out, (b, mq, 20), out.stride(), out.storage_offset() + mp)
+    assert bool(torch.isnan(pad).all()), "the GEMM wrote outside the logical output"
+
+
+@pytest.mark.parametrize("mp,mq,k,fold", [(1, 1, 64, 1), (129, 127, 64, 1), (4, 640, 1024, 1), (640, 4, 2048, 1),
+                                           (512, 300, 1000, 3), (1024, 512, 640, 2)])
+def test_gemm_f32s_edge_shapes_and_fold(mp, mq, k, fold):
+    """Single elements, tile remainders, long K, and the folded weight-gradient form (groups of batches summed)."""
+    g = torch.Generator(device=DEV).manual_seed(mp * 37 + mq + fold)
+    b = 2 * fold
+    P = _operand32(b, mp, k, True, g)
+    Q = _operand32(b, mq, k, False, g)
+    out = torch.empty((b // fold, mq, mp + (-mp) % 4), device=DEV)[..., :mp]
+    K().gemm_f32s(P, Q, out, fold=fold)
+    assert _check32(out, P, Q, 1.0, mp, fold) <= 2e-6
+
+
+def test_gemm_f32s_c3_layouts_vs_fp64():
+    """The four Mamba-TasNet-L fp32 projection layouts at reduced batch (in_proj fwd and input gradient, out_proj fwd,
+    weight gradient with fold), each within 2e-6 of sum |PQ| of the fp64 product."""
+    g = torch.Generator(device=DEV).manual_seed(99)
+    b, l, dm, di = 2, 600, 512, 1024
+    h = torch.randn(b, l, dm, device=DEV, generator=g)                   # (b, l, d_model)
+    w_in = 0.05 * torch.randn(2 * di, dm, device=DEV, generator=g)
+    xz = torch.empty(b, 2 * di, l + 8, device=DEV)[..., :l]
+    K().gemm_f32s(h, w_in[None], xz)                                     # xz = W_in h^T  (P = h, p = l)
+    assert _check32(xz, h, w_in[None], 1.0, l) <= 2e-6
+    dxz = torch.randn(b, 2 * di, l, device=DEV, generator=g)
+    dh = torch.empty(b, l, dm, device=DEV)
+    K().gemm_f32s(w_in.t()[None], dxz.transpose(1, 2), dh)               # dh = dxz^T W_in
+    assert _check32(dh, w_in.t()[None], dxz.transpose(1, 2), 1.0, dm) <= 2e-6
+    y = torch.randn(b, di, l, device=DEV, generator=g)
+    w_out = 0.05 * torch.randn(dm, di, device=DEV, generator=g)
+    o = torch.empty(b, l, dm, device=DEV)
+    K().gemm_f32s(w_out[None], y.transpose(1, 2), o, 0.5)                 # out = 0.5 y^T W_out^T
+    assert _check32(o, w_out[None], y.transpose(1, 2), 0.5, dm) <= 2e-6
+    dw = torch.empty(1, 2 * di, dm, device=DEV)
+    K().gemm_f32s(h.transpose(1, 2), dxz, dw, fold=b)                    # dW_in = sum_b dxz h
+    assert _check32(dw, h.transpose(1, 2), dxz, 1.0, dm, b) <= 2e-6

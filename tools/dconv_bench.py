@@ -1,6 +1,7 @@
 """Micro-benchmark of the avse1 AudioFeatNet dilated 64->64 5x5 convolutions at the C2 shape (B=32, 376 x 257,
-channels-last): weight gradient on the HIP MFMA kernel (K.dconv_wgrad) vs MIOpen (torch.nn.grad.conv2d_weight), plus
-MIOpen forward / input-gradient for reference.  FLOPs per launch 2*B*64*64*25*H*W (633.3 GF at C2); HIP events.
+channels-last): weight gradient on the HIP MFMA kernel (K.dconv_wgrad) vs MIOpen (torch.nn.grad.conv2d_weight); forward
+and input gradient on the split-fp16 MFMA kernel (K.dconv_fwd: split + weight prep + conv, and the conv launch alone)
+vs MIOpen.  FLOPs per launch 2*B*64*64*25*H*W (633.3 GF at C2, fp32-equivalent); HIP events.
 python tools/dconv_bench.py [--batch 32] [--iters 5]"""
 import argparse
 import json
@@ -45,6 +46,19 @@ def main():
         rec = {"dilation": d, "batch": B, "gflop": round(flops / 1e9, 1)}
         ms = timeit(lambda: K.dconv_wgrad(x, dy, d), a.iters)
         rec["hip_wgrad"] = {"ms": round(ms, 3), "tflops": round(flops / ms / 1e9, 1), "frac": round(flops / ms / 1e9 / 157.3, 3)}
+        L = K._lib.lib()
+        mb = torch.empty(2, device="cuda", dtype=torch.int32)
+        xq = K.split16(x, mb)
+        wq = K.dconv_wprep(w, False, mb)
+        y = torch.empty_like(x)
+        conv = lambda: K.check(L.avse_dconv_fwd(B, H, W, d, K.ptr(xq), K.ptr(wq), K.ptr(mb), None, K.ptr(y),  # noqa: E731
+                                                K.stream_ptr()), "dconv_fwd")
+        for name, fn in (("split_fwd_total", lambda: K.dconv_fwd(x, w, d)),
+                         ("split_dgrad_total", lambda: K.dconv_fwd(dy, w, d, transposed=True)),
+                         ("split_conv_only", conv), ("split16_only", lambda: K.split16(x, mb))):
+            ms = timeit(fn, a.iters)
+            rec[name] = {"ms": round(ms, 3), "tflops": round(flops / ms / 1e9, 1), "frac_fp32": round(flops / ms / 1e9 / 157.3, 3),
+                         "frac_f16x3": round(3 * flops / ms / 1e9 / 2500.0, 3)}
         if not a.no_miopen:
             for name, fn in (("miopen_wgrad", lambda: torch.nn.grad.conv2d_weight(x, w.shape, dy, 1, 2 * d, d)),
                              ("miopen_fwd", lambda: torch.nn.functional.conv2d(x, w, None, 1, 2 * d, d)),
