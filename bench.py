@@ -174,20 +174,27 @@ class Avse1Step:
                 "stft_frames": 376, "lip_frames": 75, "lip_hw": self.lip_hw, "parallelism": f"dp{world}"}
 
     def roofline(self, dev):
-        """Dominant kernel class of the step: the weight gradient of AudioFeatNet's 64->64 5x5 dilated Conv2d on the
-        hand-written MFMA kernel (csrc/dconv_wgrad.hip; 4 launches per step, d = 2, 4, 8, 16, the largest per-step
-        kernel time in the rocprofv3 trace).  FLOPs per launch = 2*B*64*64*25*376*257.
-          * ``achieved`` / ``frac`` / ``avg_ms``: IN-STEP — every launch of the kernel inside 3 eager train steps of the
-            benchmarked model itself (lip branch on its side stream, as the timed step runs), each bracketed by HIP
-            events on its launch stream (kernels.LAUNCH_TAPS).  The audio branch's kernels share the CUs with the lip
-            branch's, so this is what the step gets from the kernel;
+        """Dominant hand-written kernel class of the step: the AudioFeatNet 64->64 5x5 dilated Conv2d (conv2..5, d = 2,
+        4, 8, 16).  With the split-fp16 path (csrc/dconv.hip, default) its forward + input-gradient launches
+        (avse_dconv_fwd, 8 per step) and its weight gradient (avse_dconv_wgrad16, 4 per step); otherwise the fp32-MFMA
+        weight gradient (avse_dconv_wgrad).  Algorithmic FLOPs per launch = 2*B*64*64*25*376*257 (fp32 math); the split
+        kernels run 3 f16 MFMAs per fp32 product, so their peak is the dense f16 peak / 3 (833 TFLOP/s), the fp32-MFMA
+        kernel's the fp32 peak (157.3).
+          * ``achieved`` / ``frac`` / ``avg_ms``: IN-STEP — every launch inside 3 eager train steps of the benchmarked
+            model itself (lip branch on its side stream, as the timed step runs), each bracketed by HIP events on its
+            launch stream (kernels.LAUNCH_TAPS); ``roofline`` is the entry point with the most kernel time in them;
           * ``isolated``: conv3's launch (d = 4) alone on the idle GPU, random operands of the step's shape;
           * ``roofline_library``: the MIOpen forward of the same conv, alone."""
         from avse_challenge_amd import kernels as K
+        from avse_challenge_amd import layers
         cl = torch.channels_last
         flops = 2.0 * self.B * 64 * 64 * 25 * 376 * 257
+        split = layers._DCONV_SPLIT
+        names = ("avse_dconv_fwd", "avse_dconv_wgrad16") if split else ("avse_dconv_wgrad",)
+        peak = BF16_PEAK_TFS / 3 if split else FP32_PEAK_TFS
         mark = os.environ.get("AVSE_PROFILE_MARK", "0") == "1"        # tools/ktrace_window.py OUT_ROOF.csv
-        K.LAUNCH_TAPS["avse_dconv_wgrad"] = taps = []
+        for n in names:
+            K.LAUNCH_TAPS[n] = []
         try:
             if mark:
                 torch.cuda._sleep(1000)
@@ -196,32 +203,64 @@ class Avse1Step:
             if mark:
                 torch.cuda._sleep(1000)
             torch.cuda.synchronize()
+            per = {n: [a.elapsed_time(b) for a, b in K.LAUNCH_TAPS[n]] for n in names}
         finally:
-            K.LAUNCH_TAPS.pop("avse_dconv_wgrad", None)
-        per = [a.elapsed_time(b) for a, b in taps]
-        ms_in = sum(per) / max(1, len(per))
-        ach_in = flops / (ms_in * 1e-3) / 1e12
+            for n in names:
+                K.LAUNCH_TAPS.pop(n, None)
         x = torch.randn(self.B, 64, 376, 257, device=dev).contiguous(memory_format=cl)
         dy = torch.randn(self.B, 64, 376, 257, device=dev).contiguous(memory_format=cl)
-        ms = _event_ms(lambda: K.dconv_wgrad(x, dy, 4), n=10, warm=3)
-        ach = flops / (ms * 1e-3) / 1e12
-        roof = _with_traffic({"kernel": "avse_dconv_wgrad (AudioFeatNet conv2..5 weight gradient: Conv2d 64->64 5x5 "
-                                        "dil 2/4/8/16, HIP MFMA implicit GEMM)", "bound": "mfma",
-                              "achieved": round(ach_in, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
-                              "frac": round(ach_in / FP32_PEAK_TFS, 4), "traffic": None, "avg_ms": round(ms_in, 4),
-                              "measured": f"in-step: {len(per)} launches in 3 eager train steps of the benchmarked "
-                                          "model (two streams), HIP events on the launch stream",
-                              "per_launch_ms": [round(v, 3) for v in per[:4]],
-                              "algorithmic_flops_per_launch": flops,
-                              "isolated": {"what": "conv3 (d = 4) alone on the idle GPU", "avg_ms": round(ms, 4),
-                                           "achieved": round(ach, 2), "frac": round(ach / FP32_PEAK_TFS, 4)}},
-                             "dconv_wgrad" if self.B == 32 else "-")
+        w = 0.05 * torch.randn(64, 64, 5, 5, device=dev)
+        recs = []
+        for n in names:
+            v = per[n]
+            if not v:
+                continue
+            ms_in = sum(v) / len(v)
+            ach_in = flops / (ms_in * 1e-3) / 1e12
+            if n == "avse_dconv_fwd":
+                mb = torch.empty(2, device=dev, dtype=torch.int32)
+                xq = K.split16(x, mb)
+                wq = K.dconv_wprep(w, False, mb)
+                y = torch.empty_like(x)
+                L = K._lib.lib()
+                iso = lambda: K.check(L.avse_dconv_fwd(self.B, 376, 257, 4, K.ptr(xq), K.ptr(wq), K.ptr(mb), None,  # noqa: E731
+                                                       K.ptr(y), K.stream_ptr(dev)), "avse_dconv_fwd")
+                desc = ("avse_dconv_fwd (AudioFeatNet conv2..5 forward and input gradient: Conv2d 64->64 5x5 dil "
+                        "2/4/8/16 as a split-fp16 MFMA implicit GEMM, fp32-accurate)")
+            elif n == "avse_dconv_wgrad16":
+                xm, dm = torch.empty(2, device=dev, dtype=torch.int32), torch.empty(2, device=dev, dtype=torch.int32)
+                xq, dq = K.split16(x, xm), K.split16(dy, dm)
+                iso = lambda: K.dconv_wgrad16((xq, xm[:1]), (dq, dm[:1]), tuple(x.shape), 4)  # noqa: E731
+                desc = "avse_dconv_wgrad16 (AudioFeatNet conv2..5 weight gradient, split-fp16 MFMA implicit GEMM)"
+            else:
+                iso = lambda: K.dconv_wgrad(x, dy, 4)  # noqa: E731
+                desc = ("avse_dconv_wgrad (AudioFeatNet conv2..5 weight gradient: Conv2d 64->64 5x5 dil 2/4/8/16, "
+                        "fp32 HIP MFMA implicit GEMM)")
+            ms = _event_ms(iso, n=10, warm=3)
+            ach = flops / (ms * 1e-3) / 1e12
+            recs.append({"kernel": desc, "bound": "mfma", "achieved": round(ach_in, 2), "peak": round(peak, 1),
+                         "unit": "TFLOP/s", "frac": round(ach_in / peak, 4), "traffic": None, "avg_ms": round(ms_in, 4),
+                         "launches": len(v), "step_ms": round(sum(v) / 3, 3),
+                         "measured": f"in-step: {len(v)} launches in 3 eager train steps of the benchmarked model (two "
+                                     "streams), HIP events on the launch stream",
+                         "per_launch_ms": [round(t, 3) for t in v[:4]], "algorithmic_flops_per_launch": flops,
+                         "isolated": {"what": "conv3 (d = 4) alone on the idle GPU", "avg_ms": round(ms, 4),
+                                      "achieved": round(ach, 2), "frac": round(ach / peak, 4)}})
+        if not recs:
+            return None
+        roof = dict(max(recs, key=lambda r: r["step_ms"]))
+        if split:
+            roof["peak_note"] = ("split-fp16 kernels: 3 f16 MFMAs per fp32 product, peak = dense f16 2500 TFLOP/s / 3; "
+                                 "achieved counts the fp32 algorithmic FLOPs")
+            roof["other_conv_kernels"] = [{k: r[k] for k in ("kernel", "avg_ms", "achieved", "frac", "launches",
+                                                             "step_ms")} for r in recs if r is not roof]
+        _with_traffic(roof, "dconv_wgrad" if (self.B == 32 and not split) else "-")
         conv = self.model.net_audiofeat.conv3
-        with torch.no_grad():
+        with torch.no_grad(), _dconv_library():
             ms_f = _event_ms(lambda: conv(x), n=10, warm=3)
         ach_f = flops / (ms_f * 1e-3) / 1e12
         roof["roofline_library"] = {"kernel": "AudioFeatNet.conv3 fwd (MIOpen), alone", "achieved": round(ach_f, 2),
-                                    "frac": round(ach_f / FP32_PEAK_TFS, 4), "avg_ms": round(ms_f, 4)}
+                                    "frac_fp32": round(ach_f / FP32_PEAK_TFS, 4), "avg_ms": round(ms_f, 4)}
         return roof
 
     def cpu_baseline(self):
@@ -669,6 +708,19 @@ def _in_step_hbm(work, name, byts, desc, isolated=None, traffic_phase=None):
     if isolated is not None:
         rec["isolated"] = isolated
     return rec
+
+
+class _dconv_library:
+    """Context: the dilated convs on MIOpen (layers._DCONV_SPLIT off) — the library figure beside the own kernels."""
+
+    def __enter__(self):
+        from avse_challenge_amd import layers
+        self.prev, layers._DCONV_SPLIT = layers._DCONV_SPLIT, False
+
+    def __exit__(self, *exc):
+        from avse_challenge_amd import layers
+        layers._DCONV_SPLIT = self.prev
+        return False
 
 
 def _time_hbm(fn, byts, name, n=10):
