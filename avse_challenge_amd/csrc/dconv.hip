@@ -32,6 +32,7 @@
 // of 3 buffers, issued 2 stages ahead; one barrier per stage.  LDS rows are 64 B with the 16-B chunk c of row r at
 // c ^ ((r >> 2) & 3), so the 16 lanes of a ds_read_b128 group read 16 distinct bank slots.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -114,42 +115,53 @@ struct Args {
     int N, H, W, tiles;          // tiles per image
 };
 
-template <int D>
-__global__ __launch_bounds__(THREADS, 1) void fwd_kernel(Args a) {
-    constexpr int NP = TP + 8 * D;             // staged positions
+// NW waves, tile = TP = 64 NW raster pixels spanning up to NSEG rows (W >= 256): row segment k of the tile sits at LDS
+// positions S_k .. S_k + n_k + 4 D (its n_k pixels with the 2 D halo each side), S_k = n_0 + .. + n_{k-1} + 4 D k, so
+// output pixel j of segment k reads position j + 4 D k + D kw for tap kw.
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void fwd_kernel(Args a) {
+    constexpr int TPX = 64 * NW, NSEG = NW == 4 ? 2 : 3;
+    constexpr int NP = (TPX + 4 * D * NSEG + 15) / 16 * 16;   // staged positions (whole 1-KB DMA pieces)
     constexpr int XIMG = NP * ROWB;
+    constexpr int STG = XIMG + WIMG;
+    constexpr int NB = (3 * STG <= 160 * 1024) ? 3 : 2;
     constexpr int PX = XIMG / 1024, PT = PX + WIMG / 1024;      // X pieces, all pieces of a stage
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[NBUF * STAGE];
+    constexpr int MP = PT / NW + 1;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[NB * STG];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int n = bid / a.tiles, t = bid % a.tiles;
     const int HW = a.H * a.W;
-    const int p0 = t * TP;
-    const int hA = p0 / a.W, wA0 = p0 - hA * a.W;
-    const int nA = min(TP, a.W - wA0);          // tile pixels in row hA (the rest continue in row hA + 1)
-    const bool two = nA < TP;
+    const int p0 = t * TPX;
+    const int r0 = p0 / a.W, w0 = p0 - r0 * a.W;
+    // pixels of the tile in its first, second and third row, and the segments' first positions
+    const int n0 = min(TPX, a.W - w0), n1 = min(TPX - n0, a.W), n2 = TPX - n0 - n1;
+    const int S1 = n0 + 4 * D, S2 = n0 + n1 + 8 * D;
     const i4_t rx = rsrc_of(a.xq, (int64_t)a.N * HW * 256);
     const i4_t rw = rsrc_of(a.wq, (int64_t)NSTG * WIMG);
     const uint32_t lds0 = lds_u32(lds);
 
-    // this wave's LDS-DMA pieces of a stage: k = wave + 4 m; X pieces (k < PX) carry the lane's position column (or -1
-    // outside the image / the segment) and segment row offset; W pieces the lane's byte offset in the stage's W image
-    int pcol[MAXP], prow[MAXP];
-    uint32_t pchunk[MAXP];
-    const int npieces = (PT - wave + WAVES - 1) / WAVES;
+    // this wave's LDS-DMA pieces of a stage: k = wave + NW m; X pieces (k < PX) carry the lane's position column (or -1
+    // outside the image / the segments) and row; W pieces the lane's byte offset in the stage's W image
+    int pcol[MP], prow[MP];
+    uint32_t pchunk[MP];
+    const int npieces = (PT - wave + NW - 1) / NW;
 #pragma unroll
-    for (int m = 0; m < MAXP; ++m) {
-        const int k = wave + WAVES * m;
+    for (int m = 0; m < MP; ++m) {
+        const int k = wave + NW * m;
         if (k < PX) {
             const int r = 16 * k + (lane >> 2), c = (lane & 3) ^ swz(r);
             int col, row;
-            if (r < nA + 4 * D) {
-                col = wA0 - 2 * D + r;
-                row = hA;
+            if (r < S1) {
+                col = w0 - 2 * D + r;
+                row = r0;
+            } else if (r < S2 || NSEG == 2) {
+                col = -2 * D + (r - S1);
+                row = (n1 > 0 && r < S1 + n1 + 4 * D) ? r0 + 1 : -1000000;
             } else {
-                col = -2 * D + (r - nA - 4 * D);
-                row = two ? hA + 1 : -1000000;
+                col = -2 * D + (r - S2);
+                row = (n2 > 0 && r < S2 + n2 + 4 * D) ? r0 + 2 : -1000000;
             }
             pcol[m] = (col >= 0 && col < a.W) ? col : -1;
             prow[m] = row;
@@ -163,11 +175,11 @@ __global__ __launch_bounds__(THREADS, 1) void fwd_kernel(Args a) {
     }
     auto issue = [&](int s) {
         const int kh = s / NQ, q = s % NQ;
-        const uint32_t img = lds0 + (s % NBUF) * STAGE;
+        const uint32_t img = lds0 + (s % NB) * STG;
 #pragma unroll
-        for (int m = 0; m < MAXP; ++m) {
+        for (int m = 0; m < MP; ++m) {
             if (m >= npieces) break;
-            const int k = wave + WAVES * m;
+            const int k = wave + NW * m;
             if (k < PX) {
                 const int row = prow[m] + D * (kh - 2);
                 const bool ok = pcol[m] >= 0 && row >= 0 && row < a.H;
@@ -185,7 +197,7 @@ __global__ __launch_bounds__(THREADS, 1) void fwd_kernel(Args a) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int j = 64 * wave + 32 * i + (lane & 31);
-        posA[i] = j < nA ? j : j + 4 * D;
+        posA[i] = j + 4 * D * ((j >= n0) + (j >= n0 + n1));
     }
     const int hc = lane >> 5;                   // fragment chunk: hi = hc, lo = 2 + hc
 
@@ -198,16 +210,16 @@ __global__ __launch_bounds__(THREADS, 1) void fwd_kernel(Args a) {
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
     issue(0);
-    issue(1);
+    if (NB == 3) issue(1);
     for (int s = 0; s < NSTG; ++s) {
-        // stage s + 1 issued last iteration (or in the prologue) has landed, stage s long before; the barrier also
-        // releases stage s - 1's buffer, which stage s + 2 then refills
-        if (s + 1 < NSTG) wait_all_but(npieces);      // this wave's stage-s pieces landed (stage s + 1 may fly)
+        // this wave's stage-s pieces have landed (with 3 buffers stage s + 1 may still fly); the barrier makes that
+        // hold for every wave and releases the buffer of stage s - 1 (3 buffers) or s - 1 = s + 1 (2 buffers)
+        if (NB == 3 && s + 1 < NSTG) wait_all_but(npieces);
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (s + 2 < NSTG) issue(s + 2);
-        const uint8_t* ximg = lds + (s % NBUF) * STAGE;
+        if (s + NB - 1 < NSTG) issue(s + NB - 1);
+        const uint8_t* ximg = lds + (s % NB) * STG;
         const uint8_t* wimg = ximg + XIMG;
 #pragma unroll
         for (int kw = 0; kw < KS; ++kw) {
@@ -232,6 +244,9 @@ __global__ __launch_bounds__(THREADS, 1) void fwd_kernel(Args a) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
                 }
+        }
+        if (NB == 2) {                                 // the next issue refills this buffer: every wave must be done
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
     }
 
@@ -588,7 +603,7 @@ int avse_dconv_wgrad16(int64_t N, int64_t H, int64_t W, int64_t dil, const void*
 int avse_dconv_fwd(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq, const void* wq,
                    const uint32_t* maxbits, const float* bias, float* y, avse_stream_t stream) {
     if (!xq || !wq || !maxbits || !y) return AVSE_EINVAL;
-    if (N <= 0 || H <= 0 || W < TP || (dil != 2 && dil != 4 && dil != 8 && dil != 16)) return AVSE_ESHAPE;
+    if (N <= 0 || H <= 0 || W < 256 || (dil != 2 && dil != 4 && dil != 8 && dil != 16)) return AVSE_ESHAPE;
     if (N * H * W * 256 >= (1LL << 31) - 1024) return AVSE_ESHAPE;       // 32-bit byte offsets into the split input
     Args a;
     a.xq = xq;
@@ -599,15 +614,28 @@ int avse_dconv_fwd(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq,
     a.N = (int)N;
     a.H = (int)H;
     a.W = (int)W;
-    a.tiles = (int)((H * W + TP - 1) / TP);
-    const dim3 grid((unsigned)(N * a.tiles)), block(THREADS);
-    hipStream_t st = (hipStream_t)stream;
-    switch (dil) {
-        case 2: hipLaunchKernelGGL(fwd_kernel<2>, grid, block, 0, st, a); break;
-        case 4: hipLaunchKernelGGL(fwd_kernel<4>, grid, block, 0, st, a); break;
-        case 8: hipLaunchKernelGGL(fwd_kernel<8>, grid, block, 0, st, a); break;
-        default: hipLaunchKernelGGL(fwd_kernel<16>, grid, block, 0, st, a); break;
+    // tile = 64 NW raster pixels (NW waves); AVSE_DCONV_NW selects 4 or 8 (default 8: twice the MFMA work per staged
+    // W byte and 2 waves per SIMD)
+    static int nw = 0;
+    if (nw == 0) {
+        const char* e = getenv("AVSE_DCONV_NW");
+        nw = (e && atoi(e) == 4) ? 4 : 8;
     }
+    a.tiles = (int)((H * W + 64 * nw - 1) / (64 * nw));
+    const dim3 grid((unsigned)(N * a.tiles)), block(64 * nw);
+    hipStream_t st = (hipStream_t)stream;
+#define AVSE_DCF_L(DD)                                                                  \
+    do {                                                                                \
+        if (nw == 4) hipLaunchKernelGGL((fwd_kernel<DD, 4>), grid, block, 0, st, a);    \
+        else hipLaunchKernelGGL((fwd_kernel<DD, 8>), grid, block, 0, st, a);            \
+    } while (0)
+    switch (dil) {
+        case 2: AVSE_DCF_L(2); break;
+        case 4: AVSE_DCF_L(4); break;
+        case 8: AVSE_DCF_L(8); break;
+        default: AVSE_DCF_L(16); break;
+    }
+#undef AVSE_DCF_L
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

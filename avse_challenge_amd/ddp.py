@@ -75,7 +75,7 @@ class Trainer:
             from . import kernels
             # created here, outside any graph pool: captured launches and the captured optimizer keep its pointer
             self._flag = kernels._kernel_error_flag(dev)
-            self._found = torch.zeros(1, device=dev, dtype=torch.float32)
+            self._found = torch.zeros((), device=dev, dtype=torch.float32)   # 0-dim: Adam's found_inf
             self.opt = torch.optim.Adam(self.params, lr=step.lr, capturable=self.use_graph, fused=True)
             self.opt.found_inf = self._found          # read by Adam.step (fused): skip the update when nonzero
         else:
@@ -90,9 +90,9 @@ class Trainer:
         if self._found is None:
             return
         if self._err_host is None:
-            self._err_host = torch.zeros(1, dtype=torch.float32, pin_memory=True)
+            self._err_host = torch.zeros((), dtype=torch.float32, pin_memory=True)
             self._err_ev = torch.cuda.Event()
-        elif self._err_ev.query() and float(self._err_host[0]) != 0.0:
+        elif self._err_ev.query() and float(self._err_host) != 0.0:
             self._raise_kernel_error()
         self._err_host.copy_(self._found, non_blocking=True)   # the flag is sticky: a later copy misses nothing
         self._err_ev.record()
@@ -197,7 +197,7 @@ class Trainer:
             self.works.append(dist.all_reduce(self.loss, async_op=True))
         if self._found is not None:
             # every rank skips the update when any rank's kernels reported invalid outputs (found is Adam's found_inf)
-            self._found.copy_(self._flag.ne(0))          # Adam skips on found_inf == 1 exactly
+            self._found.copy_(self._flag.ne(0)[0])       # Adam skips on found_inf == 1 exactly
             self.works.append(dist.all_reduce(self._found, op=dist.ReduceOp.MAX, async_op=True))
         for w in self.works:
             w.wait()
@@ -241,7 +241,7 @@ class Trainer:
         if self.world > 1:
             self.flat.mul_(1.0 / self.world)
         elif self._found is not None:
-            self._found.copy_(self._flag.ne(0))       # world > 1: max over ranks, set in _finish_allreduce
+            self._found.copy_(self._flag.ne(0)[0])    # world > 1: max over ranks, set in _finish_allreduce
         if self.step.clip is not None:
             torch.nn.utils.clip_grad_norm_(self.params, self.step.clip, foreach=True)
         self.opt.step()

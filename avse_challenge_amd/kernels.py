@@ -1070,8 +1070,11 @@ def split_planes(t):
     _need_gpu(t)
     if t.dtype != torch.float32 or t.dim() != 3:
         raise RuntimeError("split_planes: (b, r, c) fp32 views only")
-    hi = torch.empty_strided(t.size(), t.stride(), device=t.device, dtype=torch.float16)
-    lo = torch.empty_strided(t.size(), t.stride(), device=t.device, dtype=torch.float16)
+    # flat buffers with 16 elements of slack past the last element: a 16-B DMA starting at any element stays inside the
+    # GEMM's buffer range (a load straddling the range's end returns 0 for all of its 8 elements)
+    span = 1 + sum((n - 1) * st for n, st in zip(t.size(), t.stride()))
+    hi = torch.empty(span + 16, device=t.device, dtype=torch.float16).as_strided(t.size(), t.stride())
+    lo = torch.empty(span + 16, device=t.device, dtype=torch.float16).as_strided(t.size(), t.stride())
     mb = torch.empty(1, device=t.device, dtype=torch.int32)
     v = t if t.stride(2) == 1 else t.transpose(1, 2)
     if v.stride(2) != 1:

@@ -155,8 +155,8 @@ def _check32(out, P, Q, alpha, mp, fold=1):
 @pytest.mark.parametrize("q_kc", [True, False])
 @pytest.mark.parametrize("shared", ["p", "q", None])
 def test_gemm_f32s_layouts_ragged_vs_fp64(p_kc, q_kc, shared):
-    """avse_gemm_f32s (fp32 GEMM as P_hi Q_hi + P_hi Q_lo + P_lo Q_hi on the f16 MFMA) vs fp64: every element within 2e-6
-    of its sum_k |P Q| (22-bit operands; fp32 accumulation), with operands spread over ~7 decades, ragged sizes, a K
+    """avse_gemm_f32s (fp32 GEMM as P_hi Q_hi + P_hi Q_lo + P_lo Q_hi on the f16 MFMA) vs fp64: every element within 1e-5
+    of its sum_k |P Q| (22-bit operands; fp32 accumulation: the fp32 class), with operands spread over ~7 decades, ragged sizes, a K
     tail, NaN in every padding column, and nothing written outside the logical output; compared with hipBLASLt's fp32
     error on the same operands for the record."""
     g = torch.Generator(device=DEV).manual_seed(70 + 2 * p_kc + q_kc)
@@ -169,7 +169,7 @@ def test_gemm_f32s_layouts_ragged_vs_fp64(p_kc, q_kc, shared):
     err = _check32(out, P, Q, 0.5, mp)
     lib = 0.5 * torch.matmul(Q.expand(b, -1, -1), P.expand(b, -1, -1).transpose(1, 2))
     print(f"gemm_f32s err {err:.2e} of sum|PQ| (hipBLASLt fp32 {_check32(lib, P, Q, 1.0, mp):.2e})")
-    assert err <= 2e-6, err
+    assert err <= 1e-5, err
     pad = torch.as_strided(out, (b, mq, 20), out.stride(), out.storage_offset() + mp)
     assert bool(torch.isnan(pad).all()), "the GEMM wrote outside the logical output"
 
@@ -184,28 +184,28 @@ def test_gemm_f32s_edge_shapes_and_fold(mp, mq, k, fold):
     Q = _operand32(b, mq, k, False, g)
     out = torch.empty((b // fold, mq, mp + (-mp) % 4), device=DEV)[..., :mp]
     K().gemm_f32s(P, Q, out, fold=fold)
-    assert _check32(out, P, Q, 1.0, mp, fold) <= 2e-6
+    assert _check32(out, P, Q, 1.0, mp, fold) <= 1e-5
 
 
 def test_gemm_f32s_c3_layouts_vs_fp64():
     """The four Mamba-TasNet-L fp32 projection layouts at reduced batch (in_proj fwd and input gradient, out_proj fwd,
-    weight gradient with fold), each within 2e-6 of sum |PQ| of the fp64 product."""
+    weight gradient with fold), each within 1e-5 of sum |PQ| of the fp64 product."""
     g = torch.Generator(device=DEV).manual_seed(99)
     b, l, dm, di = 2, 600, 512, 1024
     h = torch.randn(b, l, dm, device=DEV, generator=g)                   # (b, l, d_model)
     w_in = 0.05 * torch.randn(2 * di, dm, device=DEV, generator=g)
     xz = torch.empty(b, 2 * di, l + 8, device=DEV)[..., :l]
     K().gemm_f32s(h, w_in[None], xz)                                     # xz = W_in h^T  (P = h, p = l)
-    assert _check32(xz, h, w_in[None], 1.0, l) <= 2e-6
+    assert _check32(xz, h, w_in[None], 1.0, l) <= 1e-5
     dxz = torch.randn(b, 2 * di, l, device=DEV, generator=g)
     dh = torch.empty(b, l, dm, device=DEV)
     K().gemm_f32s(w_in.t()[None], dxz.transpose(1, 2), dh)               # dh = dxz^T W_in
-    assert _check32(dh, w_in.t()[None], dxz.transpose(1, 2), 1.0, dm) <= 2e-6
+    assert _check32(dh, w_in.t()[None], dxz.transpose(1, 2), 1.0, dm) <= 1e-5
     y = torch.randn(b, di, l, device=DEV, generator=g)
     w_out = 0.05 * torch.randn(dm, di, device=DEV, generator=g)
     o = torch.empty(b, l, dm, device=DEV)
     K().gemm_f32s(w_out[None], y.transpose(1, 2), o, 0.5)                 # out = 0.5 y^T W_out^T
-    assert _check32(o, w_out[None], y.transpose(1, 2), 0.5, dm) <= 2e-6
+    assert _check32(o, w_out[None], y.transpose(1, 2), 0.5, dm) <= 1e-5
     dw = torch.empty(1, 2 * di, dm, device=DEV)
     K().gemm_f32s(h.transpose(1, 2), dxz, dw, fold=b)                    # dW_in = sum_b dxz h
-    assert _check32(dw, h.transpose(1, 2), dxz, 1.0, dm, b) <= 2e-6
+    assert _check32(dw, h.transpose(1, 2), dxz, 1.0, dm, b) <= 1e-5
