@@ -30,6 +30,8 @@
 // The swizzle is applied to the DMA's per-lane SOURCE address (the LDS side of an LDS-DMA is lane-linear).
 // Tile order: the shared weight's tile index runs fastest, and the 32 workgroups of an XCD take 32 consecutive tiles
 // per round, so an activation block is fetched from HBM once and re-read from that XCD's L2.
+#include <algorithm>
+
 #include "common.h"
 
 namespace avse {
@@ -524,30 +526,86 @@ using namespace avse::pg;
 // ------------------------------------------------------------------------------------------------ split planes
 // x (b, r, c) fp32, c contiguous -> hi / lo fp16 planes with x's strides: hi = fp16(x 2^e), lo = fp16(x 2^e - hi) with
 // max |x| 2^e in [2^14, 2^15) (dconv.hip's split, the same 22 significant bits); the planes' padding is not written.
-__global__ void planes_absmax_kernel(const float* x, int64_t b, int64_t r, int64_t c, int64_t bs, int64_t rs,
-                                     uint32_t* out) {
+// Two streaming passes (max, then split): a workgroup takes rpb consecutive rows, float4 accesses when the rows are
+// 16-B aligned (VEC), the row's last c % 4 elements one by one; 4 accesses in flight per thread.
+struct PlanesArgs {
+    const float* x;
+    int64_t rows, r, c, bs, rs;
+    int rpb;
+    uint32_t* maxbits;
+    _Float16* hi;
+    _Float16* lo;
+};
+
+__device__ inline int64_t planes_row_off(const PlanesArgs& a, int64_t row) { return (row / a.r) * a.bs + (row % a.r) * a.rs; }
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void planes_absmax_kernel(PlanesArgs a) {
     float m = 0.f;
-    const int64_t rows = b * r;
-    for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
-        const float* xr = x + (row / r) * bs + (row % r) * rs;
-        for (int64_t i = threadIdx.x; i < c; i += blockDim.x) m = fmaxf(m, fabsf(xr[i]));
+    const int64_t c4 = VEC ? a.c / 4 : 0;
+    for (int rr = 0; rr < a.rpb; ++rr) {
+        const int64_t row = (int64_t)blockIdx.x * a.rpb + rr;
+        if (row >= a.rows) break;
+        const float* xr = a.x + planes_row_off(a, row);
+        if constexpr (VEC) {
+            for (int64_t j0 = threadIdx.x; j0 < c4; j0 += 4 * 256) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    v[u] = j0 + u * 256 < c4 ? reinterpret_cast<const float4*>(xr)[j0 + u * 256] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+            }
+        }
+        for (int64_t i = 4 * c4 + threadIdx.x; i < a.c; i += 256) m = fmaxf(m, fabsf(xr[i]));
     }
     uint32_t v = __float_as_uint(m);
     for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    if ((threadIdx.x & 63) == 0 && v) atomicMax(out, v);
+    if ((threadIdx.x & 63) == 0 && v) atomicMax(a.maxbits, v);
 }
 
-__global__ void planes_split_kernel(const float* x, int64_t b, int64_t r, int64_t c, int64_t bs, int64_t rs,
-                                    const uint32_t* maxbits, _Float16* hi, _Float16* lo) {
-    const float sc = __builtin_ldexpf(1.f, split_exp_pg(*maxbits));
-    const int64_t rows = b * r;
-    for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
-        const int64_t off = (row / r) * bs + (row % r) * rs;
-        for (int64_t i = threadIdx.x; i < c; i += blockDim.x) {
-            const float v = x[off + i] * sc;
+__device__ inline uint32_t split_pair(float x0, float x1, float sc, uint32_t& lo) {
+    const float s0 = x0 * sc, s1 = x1 * sc;
+    const _Float16 h0 = (_Float16)s0, h1 = (_Float16)s1;
+    const _Float16 l0 = (_Float16)(s0 - (float)h0), l1 = (_Float16)(s1 - (float)h1);
+    lo = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+    return (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void planes_split_kernel(PlanesArgs a) {
+    const float sc = __builtin_ldexpf(1.f, split_exp_pg(*a.maxbits));
+    const int64_t c4 = VEC ? a.c / 4 : 0;
+    for (int rr = 0; rr < a.rpb; ++rr) {
+        const int64_t row = (int64_t)blockIdx.x * a.rpb + rr;
+        if (row >= a.rows) break;
+        const int64_t off = planes_row_off(a, row);
+        const float* xr = a.x + off;
+        if constexpr (VEC) {
+            uint2* hr = reinterpret_cast<uint2*>(a.hi + off);
+            uint2* lr = reinterpret_cast<uint2*>(a.lo + off);
+            for (int64_t j0 = threadIdx.x; j0 < c4; j0 += 4 * 256) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (j0 + u * 256 < c4) v[u] = reinterpret_cast<const float4*>(xr)[j0 + u * 256];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (j0 + u * 256 >= c4) break;
+                    uint2 h, l;
+                    h.x = split_pair(v[u].x, v[u].y, sc, l.x);
+                    h.y = split_pair(v[u].z, v[u].w, sc, l.y);
+                    hr[j0 + u * 256] = h;
+                    lr[j0 + u * 256] = l;
+                }
+            }
+        }
+        for (int64_t i = 4 * c4 + threadIdx.x; i < a.c; i += 256) {
+            const float v = xr[i] * sc;
             const _Float16 h = (_Float16)v;
-            hi[off + i] = h;
-            lo[off + i] = (_Float16)(v - (float)h);
+            a.hi[off + i] = h;
+            a.lo[off + i] = (_Float16)(v - (float)h);
         }
     }
 }
@@ -668,12 +726,32 @@ int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t
     if (b <= 0 || r <= 0 || c <= 0 || x_rs < c || (b > 1 && x_bs < (r - 1) * x_rs + c)) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
-    const int64_t rows = b * r;
-    const unsigned blocks = (unsigned)(rows < 8192 ? rows : 8192);
-    hipLaunchKernelGGL(planes_absmax_kernel, dim3(blocks), dim3(256), 0, st, x, b, r, c, x_bs, x_rs, maxbits);
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(planes_split_kernel, dim3(blocks), dim3(256), 0, st, x, b, r, c, x_bs, x_rs, maxbits,
-                       (_Float16*)hi, (_Float16*)lo);
+    PlanesArgs a;
+    a.x = x;
+    a.rows = b * r;
+    a.r = r;
+    a.c = c;
+    a.bs = x_bs;
+    a.rs = x_rs;
+    a.maxbits = maxbits;
+    a.hi = (_Float16*)hi;
+    a.lo = (_Float16*)lo;
+    // rows per workgroup: ~1024 float4 of work each
+    const int64_t c4 = (c + 3) / 4;
+    a.rpb = (int)std::max<int64_t>(1, std::min<int64_t>(1024 / std::max<int64_t>(c4, 1), 64));
+    const int64_t blocks = (a.rows + a.rpb - 1) / a.rpb;
+    if (blocks >= (1LL << 31)) return AVSE_ESHAPE;
+    const bool vec = ((uintptr_t)x % 16 == 0) && ((uintptr_t)hi % 8 == 0) && ((uintptr_t)lo % 8 == 0) &&
+                     (x_rs % 4 == 0) && (b == 1 || x_bs % 4 == 0);
+    if (vec) {
+        hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(planes_split_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL(planes_split_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    }
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

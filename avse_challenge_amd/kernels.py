@@ -1064,8 +1064,19 @@ def gemm_bf16(P, Q, out, alpha=1.0, fold=1):
 
 # ------------------------------------------------------------------------ fp32 GEMM on split fp16 planes (C3 projections)
 
+class Split:
+    """fp16 hi / lo planes of an fp32 tensor (same shape and strides) and its max-|x| bits (split_planes); ``t()`` is the
+    transposed (1, 2) view of both planes, for the GEMM operand that reads the tensor transposed."""
+
+    def __init__(self, hi, lo, mb):
+        self.hi, self.lo, self.mb = hi, lo, mb
+
+    def t(self):
+        return Split(self.hi.transpose(1, 2), self.lo.transpose(1, 2), self.mb)
+
+
 def split_planes(t):
-    """t (b, r, c) fp32 view with stride(2) == 1 or stride(1) == 1 -> (hi, lo, maxbits): fp16 planes of t's shape and
+    """t (b, r, c) fp32 view with stride(2) == 1 or stride(1) == 1 -> Split(hi, lo, maxbits): fp16 planes of t's shape and
     strides holding fp16(t 2^e) and the remainder (csrc/projgemm.hip avse_split16_planes), and max |t|'s bits."""
     _need_gpu(t)
     if t.dtype != torch.float32 or t.dim() != 3:
@@ -1083,12 +1094,17 @@ def split_planes(t):
     check(_lib.lib().avse_split16_planes(b, r, c, ptr(v), v.stride(0) if b > 1 else (r - 1) * v.stride(1) + c,
                                          v.stride(1), ptr(hi), ptr(lo), ptr(mb), stream_ptr(t.device)),
           "avse_split16_planes")
-    return hi, lo, mb
+    return Split(hi, lo, mb)
 
 
 def gemm_f32s_supported(P, Q, out, fold=1):
     """True when avse_gemm_f32s takes out[g, q, p] = sum_{b in g} sum_k P[b, p, k] Q[b, q, k] for these fp32 views."""
-    if not (P.is_cuda and P.dtype == Q.dtype == out.dtype == torch.float32):
+    return P.is_cuda and P.dtype == Q.dtype == torch.float32 and _f32s_layout_ok(P, Q, out, fold)
+
+
+def _f32s_layout_ok(P, Q, out, fold=1):
+    """The shape / stride rules of avse_gemm_f32s (P, Q: the operands or their split planes; out fp32)."""
+    if out.dtype != torch.float32:
         return False
     if P.dim() != 3 or Q.dim() != 3 or out.dim() != 3 or P.shape[2] != Q.shape[2] or P.shape[2] < 1:
         return False
@@ -1102,16 +1118,31 @@ def gemm_f32s_supported(P, Q, out, fold=1):
     return _gemm_operand(P) is not None and _gemm_operand(Q) is not None
 
 
-def gemm_f32s(P, Q, out, alpha=1.0, fold=1):
+def gemm_f32s(P, Q, out, alpha=1.0, fold=1, ps=None, qs=None):
     """out[g, q, p] = alpha * sum_{b in group g} sum_k P[b, p, k] * Q[b, q, k] in fp32 on the split-fp16 MFMA GEMM
     (csrc/projgemm.hip avse_gemm_f32s: both operands split into hi / lo fp16 planes, three MFMAs per product, fp32
-    accumulation, fp32-accurate).  Same operand rules as gemm_bf16; out fp32.  Returns out."""
+    accumulation, fp32-accurate).  Same operand rules as gemm_bf16; out fp32.  ps / qs: the operands' Split when the
+    caller already made it (an operand used by two GEMMs is split once).  Returns out."""
     _need_gpu(P, Q, out)
     if not gemm_f32s_supported(P, Q, out, fold):
         raise RuntimeError(f"avse_gemm_f32s: unsupported operands P {tuple(P.shape)}/{P.stride()} "
                            f"Q {tuple(Q.shape)}/{Q.stride()} out {tuple(out.shape)}/{out.stride()} (fold {fold})")
-    ph, pl, pm = split_planes(P)
-    qh, ql, qm = split_planes(Q)
+    for t, sp in ((P, ps), (Q, qs)):
+        if sp is not None and (sp.hi.shape != t.shape or sp.hi.stride() != t.stride()):
+            raise RuntimeError(f"gemm_f32s: split planes {tuple(sp.hi.shape)}/{sp.hi.stride()} do not match the operand "
+                               f"{tuple(t.shape)}/{t.stride()}")
+    return gemm_f32s_split(ps or split_planes(P), qs or split_planes(Q), out, alpha, fold)
+
+
+def gemm_f32s_split(sp, sq, out, alpha=1.0, fold=1):
+    """gemm_f32s on operands given only by their Splits (the fp32 tensors need not be kept)."""
+    _need_gpu(sp.hi, sq.hi, out)
+    if not _f32s_layout_ok(sp.hi, sq.hi, out, fold):
+        raise RuntimeError(f"avse_gemm_f32s: unsupported planes P {tuple(sp.hi.shape)}/{sp.hi.stride()} "
+                           f"Q {tuple(sq.hi.shape)}/{sq.hi.stride()} out {tuple(out.shape)}/{out.stride()}")
+    P = sp.hi
+    ph, pl, pm = sp.hi, sp.lo, sp.mb
+    qh, ql, qm = sq.hi, sq.lo, sq.mb
     a = _lib.GemmF32sArgs()
     a.batch, a.mp, a.mq, a.k, a.fold = out.shape[0] * fold, P.shape[1], Q.shape[1], P.shape[2], fold
     a.p_hi, a.p_lo, (a.p_bs, a.p_sx, a.p_sk), a.p_extent, a.p_max = ph.data_ptr(), pl.data_ptr(), _gemm_operand(ph), \

@@ -60,11 +60,16 @@ def _hip_gemm(P, Q, out, alpha=1.0, fold=1):
 _F32_SPLIT = os.environ.get("AVSE_F32_SPLIT", "1") == "1"
 
 
+def _f32_ok(P, Q, out, fold=1):
+    return (_F32_SPLIT and min(P.shape[1], Q.shape[1]) >= 128 and P.shape[2] >= 64
+            and K.gemm_f32s_supported(P, Q, out, fold))
+
+
 def _f32_gemm(P, Q, out, alpha=1.0, fold=1):
     """out[g, q, p] = alpha sum_{b in group g} sum_k P[b, p, k] Q[b, q, k] in fp32 on avse_gemm_f32s; None when it does
-    not take them (the x_proj / dt_proj rank-sized projections stay on the library)."""
-    if _F32_SPLIT and min(P.shape[1], Q.shape[1]) >= 128 and P.shape[2] >= 64 and \
-            K.gemm_f32s_supported(P, Q, out, fold):
+    not take them (the x_proj / dt_proj rank-sized projections stay on the library).  The in / out projections call
+    gemm_f32s themselves with shared Splits (an activation used by two GEMMs is split once)."""
+    if _f32_ok(P, Q, out, fold):
         return K.gemm_f32s(P, Q, out, alpha, fold)
     return None
 
@@ -128,6 +133,28 @@ class _Fork(torch.autograd.Function):
         return _padded_add(g1, g2)
 
 
+def _unit_stride(t):
+    """t, or a contiguous copy when neither of its last two dims has unit stride (split_planes needs one)"""
+    return t if t.stride(2) == 1 or t.stride(1) == 1 else t.contiguous()
+
+
+def _fold_for(nb, m, n):
+    """batches folded into groups so that a weight-gradient launch has about one 256 x 256 tile per CU"""
+    fold = max(1, nb * (-(-m // 256)) * (-(-n // 256)) // 256)
+    while nb % fold:
+        fold -= 1
+    return fold
+
+
+def _bsum_split(a_split, bt_split, m, n, alpha=1.0):
+    """alpha sum_b a[b] @ bt[b] (m, n) fp32 from the Splits of a (b, m, l) and bt (b, l, n) (avse_gemm_f32s, folded)."""
+    nb = a_split.hi.shape[0]
+    fold = _fold_for(nb, m, n)
+    out = torch.empty(nb // fold, m, n, device=a_split.hi.device, dtype=torch.float32)
+    K.gemm_f32s_split(bt_split.t(), a_split, out, alpha, fold)
+    return out.sum(0)
+
+
 def _bsum_mm(a, bt, alpha=1.0):
     """alpha sum_b a[b] @ bt[b] for a (b, m, l), bt (b, l, n): the weight gradient of a batched projection, fp32.
     Under bf16 autocast with AVSE_PROJ_GEMM=all: the HIP GEMM with fp32 accumulation (avse_gemm_bf16, batches folded
@@ -140,9 +167,7 @@ def _bsum_mm(a, bt, alpha=1.0):
     dt = _autocast_dtype()
     if (dt == torch.bfloat16 and _HIP_GEMM_ALL) or (dt is None and _F32_SPLIT and a.dtype == bt.dtype == torch.float32):
         # batches folded into groups so that the launch has about one 256 x 256 tile per CU; groups summed after
-        fold = max(1, nb * (-(-m // 256)) * (-(-n // 256)) // 256)
-        while nb % fold:
-            fold -= 1
+        fold = _fold_for(nb, m, n)
         out = torch.empty(nb // fold, m, n, device=a.device, dtype=torch.float32)
         if dt is None:
             if _f32_gemm(bt.transpose(1, 2), a, out, alpha, fold=fold) is not None:
@@ -232,12 +257,33 @@ class _InProj(torch.autograd.Function):
     @staticmethod
     @_FWD
     def forward(ctx, h, w):
+        if _autocast_dtype() is None and h.dtype == w.dtype == torch.float32:
+            # fp32 (C3): h's split planes serve the forward GEMM and, saved in place of h, the weight gradient
+            out = K.bdl_empty(h.shape[0], w.shape[0], h.shape[1], torch.float32, h.device)
+            if _f32_ok(h, w[None], out):
+                hs = K.split_planes(h)
+                K.gemm_f32s(h, w[None], out, ps=hs)
+                ctx.save_for_backward(hs.hi, hs.lo, hs.mb, w)
+                ctx.split = True
+                return out
         ctx.save_for_backward(h, w)
+        ctx.split = False
         return _wbmm(w, h.transpose(1, 2))
 
     @staticmethod
     @_BWD
     def backward(ctx, dxz):
+        if ctx.split:
+            # fp32 split path: dxz split once for both GEMMs; h only as its planes
+            hhi, hlo, hmb, w = ctx.saved_tensors
+            dxz = _unit_stride(dxz)
+            out = torch.empty(dxz.shape[0], dxz.shape[2], w.shape[1], device=dxz.device, dtype=torch.float32)
+            ds = K.split_planes(dxz)
+            if _f32_ok(w.t()[None], dxz.transpose(1, 2), out):
+                dh = K.gemm_f32s(w.t()[None], dxz.transpose(1, 2), out, qs=ds.t())
+            else:
+                dh = torch.bmm(dxz.transpose(1, 2), w.expand(dxz.shape[0], *w.shape))
+            return dh, _bsum_split(ds, K.Split(hhi, hlo, hmb), dxz.shape[1], hhi.shape[2])
         h, w = ctx.saved_tensors
         dt = _autocast_dtype()
         dh = None
@@ -246,8 +292,8 @@ class _InProj(torch.autograd.Function):
             dh = _hip_gemm(wc.t()[None], dxc.transpose(1, 2),
                            torch.empty(dxz.shape[0], dxz.shape[2], w.shape[1], device=dxz.device, dtype=dt))
         elif dxz.dtype == torch.float32:
-            dh = _f32_gemm(w.t()[None], dxz.transpose(1, 2),
-                           torch.empty(dxz.shape[0], dxz.shape[2], w.shape[1], device=dxz.device, dtype=torch.float32))
+            out = torch.empty(dxz.shape[0], dxz.shape[2], w.shape[1], device=dxz.device, dtype=torch.float32)
+            dh = _f32_gemm(w.t()[None], dxz.transpose(1, 2), out)
         if dh is None:
             dh = torch.bmm(dxz.transpose(1, 2), w.expand(dxz.shape[0], *w.shape))
         dw = _bsum_mm(dxz, h)
@@ -263,8 +309,18 @@ class _BiOutProj(torch.autograd.Function):
     @_FWD
     def forward(ctx, f, bk, w):
         y = _padded_add(f, bk)
-        ctx.save_for_backward(y, w)
         dt = _autocast_dtype()
+        ctx.split = False
+        if dt is None and y.dtype == w.dtype == torch.float32:
+            # fp32 (C3): y's split planes serve the forward GEMM and, saved in place of y, the weight gradient
+            out = torch.empty(y.shape[0], y.shape[2], w.shape[0], device=y.device, dtype=torch.float32)
+            if _f32_ok(w[None], y.transpose(1, 2), out):
+                ys = K.split_planes(y)
+                K.gemm_f32s(w[None], y.transpose(1, 2), out, 0.5, qs=ys.t())
+                ctx.save_for_backward(ys.hi, ys.lo, ys.mb, w)
+                ctx.split = True
+                return out
+        ctx.save_for_backward(y, w)
         if dt is not None and _HIP_GEMM_ALL:
             wc, yc = w.to(dt), y.to(dt)
             out = _hip_gemm(wc[None], yc.transpose(1, 2),
@@ -282,6 +338,18 @@ class _BiOutProj(torch.autograd.Function):
     @staticmethod
     @_BWD
     def backward(ctx, dout):
+        if ctx.split:
+            yhi, ylo, ymb, w = ctx.saved_tensors
+            ys = K.Split(yhi, ylo, ymb)
+            dout = _unit_stride(dout)
+            dy = K.bdl_empty(dout.shape[0], w.shape[1], dout.shape[1], torch.float32, dout.device)
+            dsp = K.split_planes(dout)                 # (b, l, d_model): shared by the input and the weight gradient
+            if _f32_ok(dout, w.t()[None], dy):
+                K.gemm_f32s(dout, w.t()[None], dy, 0.5, ps=dsp)                      # dy = 0.5 W^T dout^T
+            else:
+                torch.bmm((0.5 * w.t()).expand(dout.shape[0], *w.t().shape), dout.transpose(1, 2), out=dy)
+            dw = _bsum_split(dsp.t(), ys.t(), w.shape[0], w.shape[1], 0.5)         # 0.5 sum_b dout^T y^T
+            return dy, dy, dw
         y, w = ctx.saved_tensors
         dy = _wbmm(w.t(), dout.transpose(1, 2), 0.5)                             # (b, d_inner, l)
         dw = _bsum_mm(dout.transpose(1, 2), y.transpose(1, 2), 0.5)               # (d_model, d_inner)

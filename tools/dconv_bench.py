@@ -55,7 +55,9 @@ def main():
                                                 K.stream_ptr()), "dconv_fwd")
         for name, fn in (("split_fwd_total", lambda: K.dconv_fwd(x, w, d)),
                          ("split_dgrad_total", lambda: K.dconv_fwd(dy, w, d, transposed=True)),
-                         ("split_conv_only", conv), ("split16_only", lambda: K.split16(x, mb))):
+                         ("split_conv_only", conv), ("split16_only", lambda: K.split16(x, mb)),
+                         ("split_wgrad16", lambda: K.dconv_wgrad16((xq, mb[:1]), (xq, mb[:1]), tuple(x.shape), d,
+                                                                   bias_grad=True))):
             ms = timeit(fn, a.iters)
             rec[name] = {"ms": round(ms, 3), "tflops": round(flops / ms / 1e9, 1), "frac_fp32": round(flops / ms / 1e9 / 157.3, 3),
                          "frac_f16x3": round(3 * flops / ms / 1e9 / 2500.0, 3)}

@@ -59,8 +59,9 @@ def main():
     ]
     for name, flops, (P, Q, out, alpha, fold), lib in cases:
         ms = timed(lambda: K.gemm_f32s(P, Q, out, alpha, fold), args.reps)
-        ph, pl, pm = K.split_planes(P)
-        qh, ql, qm = K.split_planes(Q)
+        sp, sq = K.split_planes(P), K.split_planes(Q)
+        ph, pl, pm, qh, ql, qm = sp.hi, sp.lo, sp.mb, sq.hi, sq.lo, sq.mb
+        ms_s = timed(lambda: K.split_planes(Q), args.reps)
         a = K._lib.GemmF32sArgs()
         a.batch, a.mp, a.mq, a.k, a.fold = out.shape[0] * fold, P.shape[1], Q.shape[1], P.shape[2], fold
         a.p_hi, a.p_lo, (a.p_bs, a.p_sx, a.p_sk), a.p_extent, a.p_max = ph.data_ptr(), pl.data_ptr(), \
@@ -71,7 +72,8 @@ def main():
         ms_g = timed(lambda: K.check(K._lib.lib().avse_gemm_f32s(a, K.stream_ptr(dev)), "gemm"), args.reps)
         ms_l = timed(lib, args.reps)
         rec = {"gemm": name, "shape": [b, L, dm, di], "gflop": round(flops / 1e9, 1),
-               "f32s_total_ms": round(ms, 3), "f32s_gemm_ms": round(ms_g, 3), "lib_ms": round(ms_l, 3),
+               "f32s_total_ms": round(ms, 3), "f32s_gemm_ms": round(ms_g, 3), "split_q_ms": round(ms_s, 3),
+               "q_elems": Q.numel(), "lib_ms": round(ms_l, 3),
                "f32s_gemm_frac_f16x3": round(3 * flops / ms_g / 1e9 / F16_PEAK, 3),
                "f32s_total_tflops_fp32eq": round(flops / ms / 1e9, 1), "lib_frac_fp32": round(flops / ms_l / 1e9 / FP32_PEAK, 3)}
         print(json.dumps(rec), flush=True)
