@@ -1140,7 +1140,7 @@ def gemm_f32s_split(sp, sq, out, alpha=1.0, fold=1):
     if not _f32s_layout_ok(sp.hi, sq.hi, out, fold):
         raise RuntimeError(f"avse_gemm_f32s: unsupported planes P {tuple(sp.hi.shape)}/{sp.hi.stride()} "
                            f"Q {tuple(sq.hi.shape)}/{sq.hi.stride()} out {tuple(out.shape)}/{out.stride()}")
-    P = sp.hi
+    P, Q = sp.hi, sq.hi
     ph, pl, pm = sp.hi, sp.lo, sp.mb
     qh, ql, qm = sq.hi, sq.lo, sq.mb
     a = _lib.GemmF32sArgs()
