@@ -226,8 +226,20 @@ def _branch_stream(device):
     if device.type != "cuda" or os.environ.get("AVSE_AVSE1_STREAMS", "1") != "1":
         return None
     if device not in _STREAMS:
-        _STREAMS[device] = torch.cuda.Stream(device)
+        # AVSE_AVSE1_SIDE_PRIO: the side stream's priority (0 = the default; lower = dispatched first)
+        _STREAMS[device] = torch.cuda.Stream(device, priority=int(os.environ.get("AVSE_AVSE1_SIDE_PRIO", "0")))
     return _STREAMS[device]
+
+
+def _audio_stream(device):
+    """AVSE_AVSE1_AUDIO_PRIO=<p> (A/B knob): run the audio branch on its own stream of priority p, else None."""
+    v = os.environ.get("AVSE_AVSE1_AUDIO_PRIO")
+    if device.type != "cuda" or v is None:
+        return None
+    key = (device, "audio")
+    if key not in _STREAMS:
+        _STREAMS[key] = torch.cuda.Stream(device, priority=int(v))
+    return _STREAMS[key]
 
 
 class _JoinFromSide(torch.autograd.Function):
@@ -283,7 +295,18 @@ class AVNet(nn.Module):
             with torch.cuda.stream(side):
                 vis = self.net_visualfeat(lips)          # (B, 75, 512); lips.float() of model.py:122 in the conv
             lips.record_stream(side)
-        audio = self.net_audiofeat(spec)
+        ast = _audio_stream(spec.device) if side is not None else None
+        if ast is not None:
+            main = torch.cuda.current_stream(spec.device)
+            ast.wait_stream(main)
+            with torch.cuda.stream(ast):
+                audio = self.net_audiofeat(spec)
+            spec.record_stream(ast)
+            main.wait_stream(ast)
+            audio.record_stream(main)
+            audio = _JoinFromSide.apply(audio, ast)
+        else:
+            audio = self.net_audiofeat(spec)
         if side is not None:
             main.wait_stream(side)
             vis.record_stream(main)

@@ -539,12 +539,16 @@ struct PlanesArgs {
 
 __device__ inline int64_t planes_row_off(const PlanesArgs& a, int64_t row) { return (row / a.r) * a.bs + (row % a.r) * a.rs; }
 
+// grid-stride over the row blocks (a bounded grid), one atomicMax per workgroup: one per wave over 10^5 row blocks
+// serialised on the single word (6.8 ms for a C3 activation, profiles/r05i_gemm_f32s_probe.jsonl)
 template <bool VEC>
-__global__ __launch_bounds__(256) void planes_absmax_kernel(PlanesArgs a) {
+__global__ __launch_bounds__(256) void planes_absmax_kernel(PlanesArgs a, int64_t nrb) {
+    __shared__ uint32_t red[4];
     float m = 0.f;
     const int64_t c4 = VEC ? a.c / 4 : 0;
+    for (int64_t rb = blockIdx.x; rb < nrb; rb += gridDim.x)
     for (int rr = 0; rr < a.rpb; ++rr) {
-        const int64_t row = (int64_t)blockIdx.x * a.rpb + rr;
+        const int64_t row = rb * a.rpb + rr;
         if (row >= a.rows) break;
         const float* xr = a.x + planes_row_off(a, row);
         if constexpr (VEC) {
@@ -562,7 +566,12 @@ __global__ __launch_bounds__(256) void planes_absmax_kernel(PlanesArgs a) {
     }
     uint32_t v = __float_as_uint(m);
     for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    if ((threadIdx.x & 63) == 0 && v) atomicMax(a.maxbits, v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        v = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (v) atomicMax(a.maxbits, v);
+    }
 }
 
 __device__ inline uint32_t split_pair(float x0, float x1, float sc, uint32_t& lo) {
@@ -743,12 +752,13 @@ int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t
     if (blocks >= (1LL << 31)) return AVSE_ESHAPE;
     const bool vec = ((uintptr_t)x % 16 == 0) && ((uintptr_t)hi % 8 == 0) && ((uintptr_t)lo % 8 == 0) &&
                      (x_rs % 4 == 0) && (b == 1 || x_bs % 4 == 0);
+    const unsigned mgrid = (unsigned)std::min<int64_t>(blocks, 2048);
     if (vec) {
-        hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3(mgrid), dim3(256), 0, st, a, blocks);
         AVSE_CHECK_LAUNCH();
         hipLaunchKernelGGL(planes_split_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
     } else {
-        hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3(mgrid), dim3(256), 0, st, a, blocks);
         AVSE_CHECK_LAUNCH();
         hipLaunchKernelGGL(planes_split_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
     }

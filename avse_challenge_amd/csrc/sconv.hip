@@ -1,0 +1,576 @@
+// 3x3 convolutions of the lip-encoder ResNet trunks for gfx950: forward, stride-1 input gradient and weight gradient
+// as implicit GEMMs on the fp16 MFMA with fp32-accurate split operands (the "fp16x3" scheme of dconv.hip).
+//
+// Replaces the trunk convolutions nn.Conv2d(cin, cout, 3, stride s in {1, 2}, padding=1, bias=False) of
+//   /root/reference/baseline/avse1/utils/resnet.py:9-10 (conv3x3, used by BasicBlock :26-67, ResNet :70-124) and
+//   /root/reference/baseline/avse4/utils.py:40-84 (ResNetLayer conv1a / conv2a / conv1b / conv2b),
+// channels 64 .. 512 on 2400 (avse1) / 1200 (avse4) lip frames of 3 .. 28 pixels square.  MIOpen ran them in fp32 at
+// 0.6-0.8 of the fp32 MFMA peak; they are most of the avse1 lip branch, the critical path of the avse1 C2 step once
+// the AudioFeatNet convolutions moved to dconv.hip.
+//
+//   Y[n][ho][wo][o] = sum_{i,kh,kw} X[n][s ho + kh - 1][s wo + kw - 1][i] W[o][i][kh][kw]          (0 outside)
+//   input gradient (s = 1): the same with X = dY and W'[o = ci][i = co][kh][kw] = W[co][ci][2 - kh][2 - kw]
+//   weight gradient: dW[o][i][kh][kw] = sum_{n,ho,wo} dY[n][ho][wo][o] X[n][s ho + kh - 1][s wo + kw - 1][i]
+//
+// Operands are NHWC tensors split once into the Q layout: per pixel, C / 16 chunks of 64 B = [hi 16 ch][lo 16 ch]
+// (avse_split16 over the tensor viewed as (pixels C / 64, 64): the same chunk order), hi = fp16(x 2^e),
+// lo = fp16(x 2^e - hi), max |x| 2^e in [2^14, 2^15); products hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16
+// (fp32 accumulation), scaled back by 2^-(e_x + e_w).  Weights: avse_sconv_wprep -> [kh][ci chunk q][kw][o][64 B].
+//
+// Forward tile: TM consecutive output pixels of the flat (n, ho, wo) raster x TN output channels, 8 waves of
+// 64 pixels x 64 channels (2 x 2 MFMA blocks, 64 accumulators per lane): TN = 64, TM = 512 for 64 output channels,
+// TN = 128, TM = 256 otherwise.  Reduction in stages (kernel row kh, 16-channel chunk q); a stage stages, by LDS-DMA,
+// every input row the tile's output rows read at kernel row kh as a padded segment of RS = s Wo + 2 positions (one
+// per input column -1 .. s Wo, zeros outside the image), so output pixel (row k of the tile, column wo) reads position
+// k RS + s wo + kw for tap kw: the 3 kw taps share one staged segment.  Per stage and wave: 3 taps x 4 blocks x 3
+// products = 36 MFMAs.  Two LDS buffers, the next stage issued right after the barrier that frees its buffer.
+#include <algorithm>
+
+#include "common.h"
+
+namespace avse {
+namespace scv {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef int i4_t __attribute__((ext_vector_type(4)));
+typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+
+constexpr int ROWB = 64;                 // LDS / Q bytes per staged (position, 16-channel chunk)
+constexpr int NPOS_MAX = 720;            // staged positions per forward stage (host-checked)
+constexpr int XIMG = NPOS_MAX * ROWB;    // 45 KB
+constexpr uint32_t OOB = 0x7FFFFFF0u;    // DMA offset past every buffer range: lands as zeros
+
+__device__ inline int swz(int r) { return (r >> 2) & 3; }
+
+// same function as dconv.hip / projgemm.hip: max |x| 2^e in [2^14, 2^15)
+__device__ inline int split_exp(uint32_t mb) {
+    const int ef = (int)((mb >> 23) & 0xff);
+    if (mb == 0) return 0;
+    const int k = ef == 0 ? -127 : ef - 127;
+    return min(100, max(-100, 14 - k));
+}
+
+__device__ inline i4_t rsrc_of(const void* base, int64_t bytes) {
+    if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+    const uint64_t a = (uint64_t)base;
+    return i4_t{__builtin_amdgcn_readfirstlane((int)(uint32_t)a), __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff)),
+                __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
+
+// one 16-B-per-lane LDS-DMA wave-instruction (inline asm: the builtin makes the compiler wait vmcnt(0) before every
+// ds_read of the array).  Nothing else in these kernels uses M0.
+__device__ inline void dma16(i4_t r, uint32_t lds_addr, uint32_t voff) {
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds_addr)
+                 : "memory");
+}
+
+__device__ inline uint32_t lds_u32(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_void_t*)p);
+}
+
+__device__ inline half8 frag(const uint8_t* img, int row, int c) {
+    return *reinterpret_cast<const half8*>(img + row * ROWB + 16 * (c ^ swz(row)));
+}
+
+// t / d and t % d for 0 <= t < 2^22, d >= 1 (float reciprocal + one correction step)
+__device__ inline void divmod_small(int t, int d, float inv_d, int& q, int& r) {
+    q = (int)((float)t * inv_d);
+    r = t - q * d;
+    if (r >= d) { r -= d; ++q; }
+    if (r < 0) { r += d; --q; }
+}
+
+struct FArgs {
+    const void* xq;            // Q-split input (N Hi Wi pixels x Ci 4 B)
+    const void* wq;            // avse_sconv_wprep image
+    const uint32_t* xmax;
+    const uint32_t* wmax;
+    float* y;                  // NHWC fp32 (N Ho Wo x Co)
+    int N, Hi, Wi, Ci, Ho, Wo, Co;
+    int tiles_n;               // Co / TN
+    int RS, npos;              // staged segment length, positions per stage (multiple of 16, <= NPOS_MAX)
+};
+
+template <int S, int TN>
+__global__ __launch_bounds__(512, 1) void fwd_kernel(FArgs a) {
+    constexpr int WAVES = 8, WN = TN / 64, WM = WAVES / WN, TM = 64 * WM;
+    constexpr int WIMG = 3 * TN * ROWB;
+    constexpr int STG = XIMG + WIMG;
+    constexpr int PW = WIMG / 1024;                                // W pieces per stage
+    constexpr int MP = (NPOS_MAX / 16 + PW + WAVES - 1) / WAVES;   // pieces per wave and stage (upper bound)
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * STG];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tn = bid % a.tiles_n, tm = bid / a.tiles_n;         // the o tiles of one pixel tile run together
+    const int p0 = tm * TM, o0 = tn * TN;
+    const int NHWo = a.N * a.Ho * a.Wo, NHo = a.N * a.Ho;
+    const int g0 = p0 / a.Wo;                                      // first output row (flat n, ho) of the tile
+    const int NQ = a.Ci / 16, NSTG = 3 * NQ;
+    const i4_t rx = rsrc_of(a.xq, (int64_t)a.N * a.Hi * a.Wi * a.Ci * 4);
+    const i4_t rw = rsrc_of(a.wq, (int64_t)9 * a.Ci * a.Co * 4);
+    const uint32_t lds0 = lds_u32(lds);
+    const int PX = a.npos / 16, PT = PX + PW;
+    const int npieces = (PT - wave + WAVES - 1) / WAVES;
+    const uint32_t pixb = (uint32_t)a.Ci * 4u;
+
+    // this wave's DMA pieces: X pieces (position r = 16 k + lane / 4) carry (n Hi, s ho - 1, input column or -1) and
+    // the lane's source chunk; W pieces the lane's byte offset inside a stage's weight rows
+    int pnh[MP], ph[MP], pcol[MP];
+    uint32_t pchunk[MP];
+#pragma unroll
+    for (int m = 0; m < MP; ++m) {
+        const int k = wave + WAVES * m;
+        if (k < PX) {
+            const int r = 16 * k + (lane >> 2), c = (lane & 3) ^ swz(r);
+            const int rk = r / a.RS, col = r - rk * a.RS, g = g0 + rk;
+            const int n = g / a.Ho, ho = g - n * a.Ho, wi = col - 1;
+            const bool ok = g < NHo && wi >= 0 && wi < a.Wi;
+            pnh[m] = n * a.Hi;
+            ph[m] = S * ho - 1;
+            pcol[m] = ok ? wi : -1;
+            pchunk[m] = 16u * c;
+        } else {
+            const int r = 16 * (k - PX) + (lane >> 2), c = (lane & 3) ^ swz(r);    // W row r = kw TN + ol
+            const int kw = r / TN, ol = r - kw * TN;
+            pnh[m] = 0;
+            ph[m] = 0;
+            pcol[m] = kw * a.Co + o0 + ol;                                           // row within the stage's block
+            pchunk[m] = 16u * c;
+        }
+    }
+    auto issue = [&](int s) {
+        const int kh = s / NQ, q = s - kh * NQ;
+        const uint32_t img = lds0 + (s & 1) * STG;
+#pragma unroll
+        for (int m = 0; m < MP; ++m) {
+            if (m >= npieces) break;
+            const int k = wave + WAVES * m;
+            if (k < PX) {
+                const int hi = ph[m] + kh;
+                const bool ok = pcol[m] >= 0 && hi >= 0 && hi < a.Hi;
+                const uint32_t pix = (uint32_t)(pnh[m] + hi) * (uint32_t)a.Wi + (uint32_t)pcol[m];
+                dma16(rx, img + k * 1024, ok ? pix * pixb + (uint32_t)(q * 64) + pchunk[m] : OOB);
+            } else {
+                const uint32_t row = (uint32_t)(kh * NQ + q) * 3u * (uint32_t)a.Co + (uint32_t)pcol[m];
+                dma16(rw, img + XIMG + (k - PX) * 1024, row * 64u + pchunk[m]);
+            }
+        }
+    };
+
+    const int wm = wave / WN, wn = wave % WN;
+    // the lane's fragment rows: output pixel p = p0 + 64 wm + 32 i + (lane & 31) reads position pos + kw
+    int posA[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int p = min(p0 + 64 * wm + 32 * i + (lane & 31), NHWo - 1);
+        const int gr = p / a.Wo, wo = p - gr * a.Wo;
+        posA[i] = (gr - g0) * a.RS + S * wo;
+    }
+    const int hc = lane >> 5;                                       // fragment chunk: hi = hc, lo = 2 + hc
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    issue(0);
+    for (int s = 0; s < NSTG; ++s) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this wave's stage-s pieces have landed
+        __builtin_amdgcn_s_barrier();                              // ... every wave's; stage s - 1's buffer is free
+        asm volatile("" ::: "memory");
+        if (s + 1 < NSTG) issue(s + 1);
+        const uint8_t* ximg = lds + (s & 1) * STG;
+        const uint8_t* wimg = ximg + XIMG;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+            half8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int r = posA[i] + kw;
+                ah[i] = frag(ximg, r, hc);
+                al[i] = frag(ximg, r, 2 + hc);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = kw * TN + 64 * wn + 32 * j + (lane & 31);
+                bh[j] = frag(wimg, r, hc);
+                bl[j] = frag(wimg, r, 2 + hc);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // the buffer is refilled after the next barrier
+    }
+
+    // epilogue: acc[i][j] register 4 g + e = pixel p0 + 64 wm + 32 i + 8 g + 4 (lane >> 5) + e, channel
+    // o0 + 64 wn + 32 j + (lane & 31): 32 lanes write 128 contiguous bytes of one pixel
+    const float scale = __builtin_ldexpf(1.f, -(split_exp(*a.xmax) + split_exp(*a.wmax)));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int o = o0 + 64 * wn + 32 * j + (lane & 31);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int p = p0 + 64 * wm + 32 * i + 8 * g + 4 * (lane >> 5) + e;
+                    if (p < NHWo) a.y[(int64_t)p * a.Co + o] = acc[i][j][4 * g + e] * scale;
+                }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ weight gradient
+// Per kernel row kh: dW[o][i][kh][kw] for the 3 kw taps, a GEMM with M = o, N = i and the reduction over output pixels.
+// Workgroup (pixel-chunk range, o block of 64, i block of 64, kh): 4 waves of 32 x 32 (o, i) blocks x 3 taps (48
+// accumulators).  Per 64-pixel raster chunk: the dY rows (64 pixels x the o block: 256 B each) and the input segment
+// rows the chunk reads at kernel row kh (positions as in the forward, 256 B each for the i block) staged by LDS-DMA;
+// fragments by ds_read_b64_tr_b16 from 256-B rows whose 16-B chunk c sits at c ^ ((r & 3) << 2).  Per chunk and wave:
+// 4 k-steps x 3 taps x 3 products = 36 MFMAs.  Per-workgroup partial slabs, summed by a second kernel (deterministic).
+constexpr int WG_CHUNK = 64;
+constexpr int PIXB = 256;
+constexpr int NPW_MAX = 192;                    // staged input positions per chunk (host-checked)
+
+__device__ inline int tswz(int r, int c) { return c ^ ((r & 3) << 2); }
+
+// 32 channels (block cb of the staged 64) x 16 pixels, plane pl (0 hi, 1 lo); rows given per lane (see dconv.hip tfrag)
+__device__ inline half8 tfrag(const uint8_t* img, const int (&row)[2], int cb, int pl, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    const int q = 2 * cb + (g & 1);
+    s4_t v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int r = row[u];
+        const int byte = q * 64 + pl * 32 + 8 * (i & 3);
+        const int off = r * PIXB + 16 * tswz(r, byte >> 4) + (byte & 15);
+        v[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(img + off));
+    }
+    const s4_t w0 = v[0], w1 = v[1];
+    const short __attribute__((ext_vector_type(8))) w = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+    return __builtin_bit_cast(half8, w);
+}
+
+struct WArgs {
+    const void* xq;
+    const void* dyq;
+    const uint32_t* xmax;
+    const uint32_t* dymax;
+    float* part;                 // [ranges][kh][kw][o][i]
+    int N, Hi, Wi, Ci, Ho, Wo, Co;
+    int RS, npw;                 // staged segment length, positions staged per chunk (multiple of 4, <= NPW_MAX)
+    int chunks, ranges, nob, nib;
+    float inv_ho, inv_wo;
+};
+
+template <int S>
+__global__ __launch_bounds__(256, 1) void wgrad_kernel(WArgs a) {
+    constexpr int YIMG = WG_CHUNK * PIXB, STG = YIMG + NPW_MAX * PIXB;
+    constexpr int PY = YIMG / 1024;                              // 16 dY pieces (4 pixels each)
+    constexpr int MP = (PY + NPW_MAX / 4 + 3) / 4;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * STG];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    int t = bid;
+    const int kh = t % 3;
+    t /= 3;
+    const int ib = t % a.nib;
+    t /= a.nib;
+    const int ob = t % a.nob;
+    const int r = t / a.nob;
+    const int c_lo = (int)((int64_t)r * a.chunks / a.ranges), c_hi = (int)((int64_t)(r + 1) * a.chunks / a.ranges);
+    const int NHWo = a.N * a.Ho * a.Wo, NHo = a.N * a.Ho;
+    const i4_t rx = rsrc_of(a.xq, (int64_t)a.N * a.Hi * a.Wi * a.Ci * 4);
+    const i4_t ry = rsrc_of(a.dyq, (int64_t)NHWo * a.Co * 4);
+    const uint32_t lds0 = lds_u32(lds);
+    const int PT = PY + a.npw / 4;
+    const int npieces = (PT - wave + 3) / 4;
+    const int pr = lane >> 4, pc = lane & 15;                    // a piece's lane: pixel row (of 4), physical chunk
+    const uint32_t xpixb = (uint32_t)a.Ci * 4u, ypixb = (uint32_t)a.Co * 4u;
+
+    // the lane's staged position of each X piece: (row of the chunk's segment list, column)
+    int qrk[MP], qcol[MP];
+#pragma unroll
+    for (int m = 0; m < MP; ++m) {
+        const int k = wave + 4 * m;
+        const int q = 4 * (k - PY) + pr;
+        qrk[m] = k >= PY ? q / a.RS : 0;
+        qcol[m] = k >= PY ? q - qrk[m] * a.RS : 0;
+    }
+    auto issue = [&](int c, int buf) {
+        const int p0 = c * WG_CHUNK, g0 = p0 / a.Wo;
+        int n0, ho0;
+        divmod_small(g0, a.Ho, a.inv_ho, n0, ho0);
+        const uint32_t img = lds0 + buf * STG;
+#pragma unroll
+        for (int m = 0; m < MP; ++m) {
+            if (m >= npieces) break;
+            const int k = wave + 4 * m;
+            if (k < PY) {                                        // dY rows: chunk pixel j = 4 k + pr
+                const int j = 4 * k + pr, p = p0 + j;
+                const uint32_t off = p < NHWo ? (uint32_t)p * ypixb + (uint32_t)(ob * 256) + 16u * tswz(j, pc) : OOB;
+                dma16(ry, img + k * 1024, off);
+            } else {
+                const int q = 4 * (k - PY) + pr;
+                int dn, ho;
+                divmod_small(ho0 + qrk[m], a.Ho, a.inv_ho, dn, ho);
+                const int g = g0 + qrk[m], n = n0 + dn;
+                const int hi = S * ho - 1 + kh, wi = qcol[m] - 1;
+                const bool ok = q < a.npw && g < NHo && hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi;
+                const uint32_t pix = (uint32_t)(n * a.Hi + hi) * (uint32_t)a.Wi + (uint32_t)wi;
+                dma16(rx, img + YIMG + (k - PY) * 1024, ok ? pix * xpixb + (uint32_t)(ib * 256) + 16u * tswz(q, pc) : OOB);
+            }
+        }
+    };
+
+    const int obw = wave >> 1, ibw = wave & 1;                   // this wave's (o, i) 32 x 32 block
+    floatx16 acc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[k][e] = 0.f;
+
+    const int g = lane >> 4, li = lane & 15;
+    if (c_lo < c_hi) issue(c_lo, 0);
+    for (int c = c_lo; c < c_hi; ++c) {
+        const int it = c - c_lo;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (c + 1 < c_hi) issue(c + 1, (it + 1) & 1);
+        const uint8_t* yimg = lds + (it & 1) * STG;
+        const uint8_t* ximg = yimg + YIMG;
+        const int p0 = c * WG_CHUNK, g0 = p0 / a.Wo, w0 = p0 - g0 * a.Wo;
+#pragma unroll
+        for (int s = 0; s < WG_CHUNK / 16; ++s) {
+            int ry_[2], rx_[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int j = 16 * s + 8 * (g >> 1) + (li >> 2) + 4 * u;       // the lane's pixel of the k-step
+                int dr, wo;
+                divmod_small(w0 + j, a.Wo, a.inv_wo, dr, wo);
+                ry_[u] = j;
+                rx_[u] = dr * a.RS + S * wo;
+            }
+            const half8 ah = tfrag(yimg, ry_, obw, 0, lane), al = tfrag(yimg, ry_, obw, 1, lane);
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int rk[2] = {rx_[0] + kw, rx_[1] + kw};
+                const half8 bh = tfrag(ximg, rk, ibw, 0, lane), bl = tfrag(ximg, rk, ibw, 1, lane);
+                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[kw], 0, 0, 0);
+                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[kw], 0, 0, 0);
+                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[kw], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    // partial tiles: acc[kw] register 4 q + e = row o = 64 ob + 32 obw + 8 q + 4 (lane >> 5) + e, column
+    // i = 64 ib + 32 ibw + (lane & 31)
+    const float sc = __builtin_ldexpf(1.f, -(split_exp(*a.xmax) + split_exp(*a.dymax)));
+    float* pp = a.part + ((int64_t)r * 9 + kh * 3) * a.Co * a.Ci;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = 64 * ob + 32 * obw + 8 * q + 4 * (lane >> 5) + e, i = 64 * ib + 32 * ibw + (lane & 31);
+                pp[((int64_t)kw * a.Co + o) * a.Ci + i] = acc[kw][4 * q + e] * sc;
+            }
+}
+
+// dW[o][i][kh][kw] = sum over ranges of part[range][kh][kw][o][i]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int ranges, int Co, int Ci, float* __restrict__ dw) {
+    const int64_t total = (int64_t)9 * Co * Ci;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+        float v = 0.f;
+        for (int g = 0; g < ranges; ++g) v += part[(int64_t)g * total + idx];
+        const int i = (int)(idx % Ci), o = (int)((idx / Ci) % Co), tap = (int)(idx / ((int64_t)Ci * Co));
+        dw[((int64_t)o * Ci + i) * 9 + tap] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ weights
+__global__ void wmax_kernel(const float* w, int n, uint32_t* out) {
+    __shared__ uint32_t red[4];
+    float m = 0.f;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) m = fmaxf(m, fabsf(w[i]));
+    uint32_t b = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        b = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (b) atomicMax(out, b);
+    }
+}
+
+// W (Co, Ci, 3, 3) fp32 -> [kh][q][kw][o][hi 16 | lo 16]; transposed: the input gradient's W'[o = ci][i = co][kh][kw] =
+// W[co][ci][2 - kh][2 - kw] (then o runs over Ci and i over Co of W)
+__global__ void wsplit_kernel(const float* w, int Co, int Ci, int transposed, const uint32_t* maxbits, uint16_t* wq) {
+    const int O = transposed ? Ci : Co, I = transposed ? Co : Ci, NQ = I / 16;
+    const int64_t total = (int64_t)9 * O * I;
+    const float sc = __builtin_ldexpf(1.f, split_exp(*maxbits));
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e % 16);
+        const int64_t rrow = e / 16;                            // ((kh NQ + q) 3 + kw) O + o
+        const int o = (int)(rrow % O), kw = (int)((rrow / O) % 3), s = (int)(rrow / ((int64_t)O * 3));
+        const int kh = s / NQ, q = s % NQ, i = q * 16 + c;
+        const float v = transposed ? w[(((int64_t)i * Ci + o) * 3 + (2 - kh)) * 3 + (2 - kw)]
+                                   : w[(((int64_t)o * Ci + i) * 3 + kh) * 3 + kw];
+        const float sv = v * sc;
+        const _Float16 h = (_Float16)sv, l = (_Float16)(sv - (float)h);
+        wq[rrow * 32 + c] = __builtin_bit_cast(uint16_t, h);
+        wq[rrow * 32 + 16 + c] = __builtin_bit_cast(uint16_t, l);
+    }
+}
+
+inline int out_dim(int x, int s) { return (x - 1) / s + 1; }     // k 3, padding 1
+
+// forward geometry: the tile's rows span at most (TM - 1 + Wo - 1) / Wo + 1 output rows
+inline int fwd_npos(int TM, int Wo, int RS) {
+    const int rows = (TM - 1 + Wo - 1) / Wo + 1;
+    return (rows * RS + 15) / 16 * 16;
+}
+inline int wg_npw(int Wo, int RS) {
+    const int rows = (WG_CHUNK - 1 + Wo - 1) / Wo + 1;
+    return (rows * RS + 3) / 4 * 4;
+}
+inline int wg_ranges(int chunks, int blocks_per_range) {
+    return std::max(1, std::min(chunks, (512 + blocks_per_range - 1) / blocks_per_range));
+}
+
+}  // namespace scv
+}  // namespace avse
+
+using namespace avse::scv;
+
+extern "C" {
+
+int64_t avse_sconv_wprep_bytes(int64_t co, int64_t ci) { return 9 * co * ci * 4; }
+
+int avse_sconv_wprep(int64_t co, int64_t ci, const float* w, int32_t transposed, void* wq, uint32_t* wmax,
+                     avse_stream_t stream) {
+    if (!w || !wq || !wmax) return AVSE_EINVAL;
+    if (co <= 0 || ci <= 0 || co % 64 || ci % 64 || co > 4096 || ci > 4096) return AVSE_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(wmax, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
+    const int n = (int)(9 * co * ci);
+    hipLaunchKernelGGL(wmax_kernel, dim3((unsigned)std::min(256, (n + 255) / 256)), dim3(256), 0, st, w, n, wmax);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(wsplit_kernel, dim3((unsigned)std::min(2048, (n + 255) / 256)), dim3(256), 0, st, w, (int)co,
+                       (int)ci, transposed, wmax, reinterpret_cast<uint16_t*>(wq));
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_sconv_fwd(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride, const void* xq,
+                   const uint32_t* xmax, const void* wq, const uint32_t* wmax, float* y, avse_stream_t stream) {
+    if (!xq || !xmax || !wq || !wmax || !y) return AVSE_EINVAL;
+    if (N <= 0 || Hi <= 0 || Wi <= 0 || ci <= 0 || co <= 0 || ci % 64 || co % 64 || (stride != 1 && stride != 2))
+        return AVSE_ESHAPE;
+    if (N * Hi * Wi * ci * 4 >= (1LL << 31) - 4096 || 9 * ci * co * 4 >= (1LL << 31)) return AVSE_ESHAPE;
+    FArgs a;
+    a.xq = xq;
+    a.wq = wq;
+    a.xmax = xmax;
+    a.wmax = wmax;
+    a.y = y;
+    a.N = (int)N;
+    a.Hi = (int)Hi;
+    a.Wi = (int)Wi;
+    a.Ci = (int)ci;
+    a.Co = (int)co;
+    a.Ho = out_dim((int)Hi, (int)stride);
+    a.Wo = out_dim((int)Wi, (int)stride);
+    a.RS = (int)stride * a.Wo + 2;
+    const int TN = co % 128 ? 64 : 128, TM = TN == 64 ? 512 : 256;
+    a.npos = fwd_npos(TM, a.Wo, a.RS);
+    if (a.npos > NPOS_MAX) return AVSE_ESHAPE;
+    const int64_t NHWo = N * a.Ho * a.Wo;
+    if (NHWo * co >= (1LL << 31)) return AVSE_ESHAPE;
+    a.tiles_n = (int)(co / TN);
+    const int64_t tiles = (NHWo + TM - 1) / TM * a.tiles_n;
+    if (tiles >= (1LL << 31)) return AVSE_ESHAPE;
+    const dim3 grid((unsigned)tiles), block(512);
+    hipStream_t st = (hipStream_t)stream;
+    if (stride == 1) {
+        if (TN == 64) hipLaunchKernelGGL((fwd_kernel<1, 64>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((fwd_kernel<1, 128>), grid, block, 0, st, a);
+    } else {
+        if (TN == 64) hipLaunchKernelGGL((fwd_kernel<2, 64>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((fwd_kernel<2, 128>), grid, block, 0, st, a);
+    }
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+static int wg_setup(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride, WArgs& a) {
+    if (N <= 0 || Hi <= 0 || Wi <= 0 || ci <= 0 || co <= 0 || ci % 64 || co % 64 || (stride != 1 && stride != 2))
+        return AVSE_ESHAPE;
+    if (N * Hi * Wi * ci * 4 >= (1LL << 31) - 4096) return AVSE_ESHAPE;
+    a.N = (int)N;
+    a.Hi = (int)Hi;
+    a.Wi = (int)Wi;
+    a.Ci = (int)ci;
+    a.Co = (int)co;
+    a.Ho = out_dim((int)Hi, (int)stride);
+    a.Wo = out_dim((int)Wi, (int)stride);
+    a.RS = (int)stride * a.Wo + 2;
+    a.npw = wg_npw(a.Wo, a.RS);
+    if (a.npw > NPW_MAX) return AVSE_ESHAPE;
+    const int64_t NHWo = N * a.Ho * a.Wo;
+    if (NHWo * co * 4 >= (1LL << 31) - 4096) return AVSE_ESHAPE;
+    a.chunks = (int)((NHWo + WG_CHUNK - 1) / WG_CHUNK);
+    a.nob = (int)(co / 64);
+    a.nib = (int)(ci / 64);
+    a.ranges = wg_ranges(a.chunks, 3 * a.nob * a.nib);
+    a.inv_ho = 1.f / (float)a.Ho;
+    a.inv_wo = 1.f / (float)a.Wo;
+    return AVSE_OK;
+}
+
+int64_t avse_sconv_wgrad_workspace_bytes(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride) {
+    WArgs a;
+    if (wg_setup(N, Hi, Wi, ci, co, stride, a) != AVSE_OK) return -1;
+    return (int64_t)a.ranges * 9 * co * ci * 4;
+}
+
+int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride, const void* xq,
+                     const uint32_t* xmax, const void* dyq, const uint32_t* dymax, float* dw, float* workspace,
+                     avse_stream_t stream) {
+    if (!xq || !xmax || !dyq || !dymax || !dw || !workspace) return AVSE_EINVAL;
+    WArgs a;
+    const int rc = wg_setup(N, Hi, Wi, ci, co, stride, a);
+    if (rc != AVSE_OK) return rc;
+    a.xq = xq;
+    a.dyq = dyq;
+    a.xmax = xmax;
+    a.dymax = dymax;
+    a.part = workspace;
+    const dim3 grid((unsigned)(a.ranges * 3 * a.nob * a.nib)), block(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (stride == 1) hipLaunchKernelGGL(wgrad_kernel<1>, grid, block, 0, st, a);
+    else hipLaunchKernelGGL(wgrad_kernel<2>, grid, block, 0, st, a);
+    AVSE_CHECK_LAUNCH();
+    const int64_t total = 9 * co * ci;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0,
+                       st, a.part, a.ranges, (int)co, (int)ci, dw);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+}  // extern "C"

@@ -535,6 +535,83 @@ def dconv_wgrad16(xs, dys, shape, dilation, bias_grad=False):
     return (dw, db) if bias_grad else dw
 
 
+# ------------------------------------------------------------------------ ResNet trunk 3x3 Conv2d (split fp16 MFMA)
+
+def sconv_ok(x, cout, stride):
+    """True when csrc/sconv.hip takes Conv2d(cin, cout, 3, stride, padding=1, bias=False) on x: (N, cin, H, W) fp32 GPU
+    tensor, cin and cout multiples of 64, stride 1 or 2, the pixel counts inside the kernels' 32-bit offsets."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and stride in (1, 2)):
+        return False
+    n, cin, h, w = x.shape
+    if cin % 64 or cout % 64 or n * h * w * max(cin, cout) * 4 >= (1 << 31) - 4096:
+        return False
+    return _lib.lib().avse_sconv_wgrad_workspace_bytes(n, h, w, cin, cout, stride) > 0
+
+
+def split_nhwc(x, maxbits):
+    """x (N, C, H, W) fp32, C % 64 == 0 (channels-last memory read as it lies, anything else made so) -> its fp16
+    hi / lo split in the Q layout (uint8 (N*H*W, 4 C): per pixel C / 16 chunks of [hi 16][lo 16]); writes max |x| bits
+    into maxbits[0] (avse_split16 over the tensor viewed as (N H W C / 64, 64))."""
+    _need_gpu(x)
+    x = x.contiguous(memory_format=torch.channels_last)
+    n, c, h, w = x.shape
+    xq = torch.empty((n * h * w, 4 * c), device=x.device, dtype=torch.uint8)
+    check(_lib.lib().avse_split16(n * h * w * (c // 64), ptr(x), ptr(xq), ptr(maxbits), stream_ptr(x.device)),
+          "avse_split16")
+    return xq
+
+
+def sconv_wprep(w, transposed, wmax):
+    """W (co, ci, 3, 3) -> sconv.hip's split weight image (transposed: the stride-1 input gradient's flipped W')."""
+    _need_gpu(w)
+    co, ci = w.shape[0], w.shape[1]
+    L = _lib.lib()
+    wq = torch.empty(int(L.avse_sconv_wprep_bytes(co, ci)), device=w.device, dtype=torch.uint8)
+    check(L.avse_sconv_wprep(co, ci, ptr(w.float().contiguous()), int(bool(transposed)), ptr(wq), ptr(wmax),
+                             stream_ptr(w.device)), "avse_sconv_wprep")
+    return wq
+
+
+def sconv_fwd(xs, xshape, w, stride, transposed=False):
+    """conv2d(x, w, stride=stride, padding=1) on csrc/sconv.hip from x's split xs = (xq, xmax) (split_nhwc) and shape
+    (N, ci, H, W); transposed=True: the stride-1 input gradient (x = dY, w the forward's (co, ci, 3, 3) weight).
+    Returns the (N, co, Ho, Wo) output in channels-last memory."""
+    xq, xm = xs
+    _need_gpu(xq, w)
+    n, ci, h, wd = xshape
+    co = w.shape[1] if transposed else w.shape[0]
+    if transposed and stride != 1:
+        raise RuntimeError("sconv_fwd: the transposed (input gradient) form is stride 1 only")
+    wm = torch.empty(1, device=w.device, dtype=torch.int32)
+    wq = sconv_wprep(w, transposed, wm)
+    ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
+    y = torch.empty((n, co, ho, wo), device=xq.device, dtype=torch.float32, memory_format=torch.channels_last)
+    tap = _tap_begin("avse_sconv_fwd", xq.device)
+    check(_lib.lib().avse_sconv_fwd(n, h, wd, ci, co, stride, ptr(xq), ptr(xm), ptr(wq), ptr(wm), ptr(y),
+                                    stream_ptr(xq.device)), "avse_sconv_fwd")
+    _tap_end(tap)
+    return y
+
+
+def sconv_wgrad(xs, dys, xshape, cout, stride):
+    """dW (cout, ci, 3, 3) of Conv2d(ci, cout, 3, stride, padding=1, bias=False) from the splits of the input
+    (xs = (xq, xmax), shape xshape = (N, ci, H, W)) and of the output gradient (dys), csrc/sconv.hip."""
+    (xq, xm), (dyq, dym) = xs, dys
+    _need_gpu(xq, dyq)
+    n, ci, h, wd = xshape
+    L = _lib.lib()
+    nb = L.avse_sconv_wgrad_workspace_bytes(n, h, wd, ci, cout, stride)
+    if nb <= 0:
+        raise RuntimeError(f"sconv_wgrad: unsupported shape {tuple(xshape)} -> {cout}, stride {stride}")
+    dw = torch.empty((cout, ci, 3, 3), device=xq.device, dtype=torch.float32)
+    ws = torch.empty((nb + 3) // 4, device=xq.device, dtype=torch.float32)
+    tap = _tap_begin("avse_sconv_wgrad", xq.device)
+    check(L.avse_sconv_wgrad(n, h, wd, ci, cout, stride, ptr(xq), ptr(xm), ptr(dyq), ptr(dym), ptr(dw), ptr(ws),
+                             stream_ptr(xq.device)), "avse_sconv_wgrad")
+    _tap_end(tap)
+    return dw
+
+
 # ------------------------------------------------------------------------ ResNet trunk 3x3 Conv2d dW
 
 def rconv_wgrad_supported(x, cout, stride):

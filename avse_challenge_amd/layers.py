@@ -543,16 +543,57 @@ class PointwiseConv2d(nn.Conv2d):
         return super().forward(x)
 
 
+# 3x3 trunk convs on csrc/sconv.hip (split-fp16 MFMA, fp32-accurate) for channels-last activations; "0": MIOpen
+_SCONV = os.environ.get("AVSE_SCONV", "1") == "1"
+
+
+class _SConvFn(torch.autograd.Function):
+    """Conv2d(ci, co, 3, stride, padding=1, bias=False) on csrc/sconv.hip: forward, weight gradient and the stride-1
+    input gradient as split-fp16 MFMA implicit GEMMs (the stride-2 input gradient, 3 of the 16 trunk convs, stays on
+    MIOpen).  The input's split is made once and kept for the weight gradient in place of the input (same bytes);
+    the output gradient is split once for both of its GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride):
+        xm = torch.empty(1, device=x.device, dtype=torch.int32)
+        xq = K.split_nhwc(x, xm)
+        ctx.shape, ctx.stride = tuple(x.shape), stride
+        ctx.save_for_backward(xq, xm, w)
+        return K.sconv_fwd((xq, xm), ctx.shape, w, stride)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xq, xm, w = ctx.saved_tensors
+        s, shape = ctx.stride, ctx.shape
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dym = torch.empty(1, device=dy.device, dtype=torch.int32)
+        dyq = K.split_nhwc(dy, dym)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if s == 1:
+                dx = K.sconv_fwd((dyq, dym), tuple(dy.shape), w, 1, transposed=True)
+            else:
+                x_like = torch.empty(shape, device=dy.device, dtype=torch.float32, memory_format=torch.channels_last)
+                dx = _conv2d_dgrad(x_like, w, dy, s, 1, 1)
+        if ctx.needs_input_grad[1]:
+            dw = K.sconv_wgrad((xq, xm), (dyq, dym), shape, w.shape[0], s)
+        return dx, dw, None
+
+
 class TrunkConv2d(nn.Conv2d):
     """nn.Conv2d(cin, cout, 3, stride, padding=1, bias=False) of the lip-encoder ResNet trunks (same parameters and
-    state_dict keys).  NCHW fp32 GPU activations with channel counts that are multiples of 64 take their weight
-    gradient from csrc/rconv_wgrad.hip; channels-last activations (use_channels_last) run the library convolution."""
+    state_dict keys).  Channels-last fp32 GPU activations with channel counts that are multiples of 64 run on
+    csrc/sconv.hip (_SConvFn; AVSE_SCONV=0: MIOpen); NCHW ones can take their weight gradient from csrc/rconv_wgrad.hip
+    (AVSE_RCONV_WGRAD)."""
 
     def __init__(self, cin, cout, stride=1):
         super().__init__(cin, cout, 3, stride=stride, padding=1, bias=False)
 
     def forward(self, x):
         s = self.stride[0]
+        if (_SCONV and x.is_contiguous(memory_format=torch.channels_last) and x.dtype == self.weight.dtype
+                and K.sconv_ok(x, self.out_channels, s)):
+            return _SConvFn.apply(x, self.weight, s)
         if gemm_conv_ok(x, 3, s):                          # small frames: one GEMM over all pixels (_GemmConvFn)
             return _GemmConvFn.apply(x, self.weight, s)
         if ((x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last)) and self._use_hip(x, s)

@@ -897,12 +897,18 @@ def roofline_hip(dev):
             with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=on, cache_enabled=False):
                 ms = _event_ms(fn)
             ach = flops / (ms * 1e-3) / 1e12
+            split = not on and M._F32_SPLIT
+            pk = BF16_PEAK_TFS / 3 if split else peak
             proj.append({"gemm": f"BiMambaV2 {pname} ({tag})", "shape": [b, l, dm, di], "dtype": str(dt)[6:],
                          "path": ("avse_gemm_bf16 (csrc/projgemm.hip)"
                                   if on and (M._HIP_GEMM_ALL or (M._HIP_GEMM and pname == "in_proj"))
+                                  else "avse_gemm_f32s (csrc/projgemm.hip: split-fp16 planes, 3 f16 MFMAs per product; "
+                                       "time includes splitting the activation)" if split
                                   else "hipBLASLt (torch.bmm)"),
                          "bound": "mfma", "flops_per_launch": flops, "avg_ms": round(ms, 4),
-                         "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4)})
+                         "achieved": round(ach, 2), "peak": pk, "unit": "TFLOP/s", "frac": round(ach / pk, 4)}
+                        | ({"peak_note": "dense f16 2500 TFLOP/s / 3 (three f16 MFMAs per fp32 product); achieved "
+                                         "counts the fp32 algorithmic FLOPs"} if split else {}))
         del h, f, bk
         torch.cuda.empty_cache()
     return hbm, proj

@@ -405,6 +405,27 @@ int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t
 int64_t avse_dconv_wprep_bytes(void);
 int avse_split16(int64_t n_pix, const float* x, void* xq, uint32_t* maxbits, avse_stream_t stream);
 int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* maxbits, avse_stream_t stream);
+
+/* 3x3 convolutions of the lip-encoder ResNet trunks (csrc/sconv.hip), replacing
+ * nn.Conv2d(ci, co, 3, stride, padding=1, bias=False) of baseline/avse1/utils/resnet.py:9-10 (BasicBlock :26-67)
+ * and baseline/avse4/utils.py:40-84 (ResNetLayer); ci, co multiples of 64, stride 1 or 2, NHWC fp32 activations.
+ * Split-fp16 MFMA implicit GEMMs (fp32-accurate, as avse_dconv_fwd).  Operands in the Q layout of avse_split16 (a
+ * (pixels, C) tensor split as (pixels C / 64, 64)); max |x| bits from avse_split16, max |w| bits from avse_sconv_wprep.
+ *   avse_sconv_wprep: W (co, ci, 3, 3) fp32 -> wq (avse_sconv_wprep_bytes(co, ci)); transposed = 1 prepares the
+ *     stride-1 input gradient's W'[ci][co][kh][kw] = W[co][ci][2 - kh][2 - kw] (then call avse_sconv_fwd with ci, co
+ *     swapped);
+ *   avse_sconv_fwd: y (N, Ho, Wo, co) fp32, Ho = (Hi - 1) / stride + 1;
+ *   avse_sconv_wgrad: dW (co, ci, 3, 3) from the split input (N, Hi, Wi, ci) and output gradient (N, Ho, Wo, co);
+ *     workspace of avse_sconv_wgrad_workspace_bytes (< 0: shape not supported). */
+int64_t avse_sconv_wprep_bytes(int64_t co, int64_t ci);
+int avse_sconv_wprep(int64_t co, int64_t ci, const float* w, int32_t transposed, void* wq, uint32_t* wmax,
+                     avse_stream_t stream);
+int avse_sconv_fwd(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride, const void* xq,
+                   const uint32_t* xmax, const void* wq, const uint32_t* wmax, float* y, avse_stream_t stream);
+int64_t avse_sconv_wgrad_workspace_bytes(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride);
+int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride, const void* xq,
+                     const uint32_t* xmax, const void* dyq, const uint32_t* dymax, float* dw, float* workspace,
+                     avse_stream_t stream);
 int avse_dconv_fwd(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq, const void* wq,
                    const uint32_t* maxbits, const float* bias, float* y, avse_stream_t stream);
 /* Weight (and bias) gradient of the same convolution from the split input xq (max bits *xmax) and the split output

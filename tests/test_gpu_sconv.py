@@ -1,0 +1,117 @@
+"""GPU parity tests of csrc/sconv.hip: the lip-encoder ResNet trunk 3x3 convolutions (baseline/avse1/utils/resnet.py:9-10,
+baseline/avse4/utils.py:40-84) as split-fp16 MFMA implicit GEMMs, against fp64.
+
+Bar (the fp32 class, as the AudioFeatNet split convs in test_gpu_kernels.py): every element within 1e-5 of its sum of
+|terms| (the split operands carry 22 significant bits, accumulation is fp32; an fp32 K = 4608 dot product rounds to a
+few 1e-6 of it); MIOpen's own fp32 error is printed beside ours.  Shapes: every trunk layer of both models (frames of
+28 / 24 down to 3 / 4 pixels, 64 .. 512 channels, stride 1 and 2) at small batch counts that leave the last tile
+partial, inputs spanning several decades."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle.det_init import det_input
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CL = torch.channels_last
+
+# (N, ci, H, W, co, stride): avse1 (96-px lips -> 24 x 24 trunk input) and avse4 (112 -> 28 x 28) layers
+SHAPES = [(3, 64, 24, 24, 64, 1), (2, 64, 24, 24, 128, 2), (5, 128, 12, 12, 128, 1), (3, 128, 12, 12, 256, 2),
+          (7, 256, 6, 6, 256, 1), (9, 256, 6, 6, 512, 2), (11, 512, 3, 3, 512, 1), (2, 64, 28, 28, 64, 1),
+          (3, 256, 7, 7, 512, 2), (5, 512, 4, 4, 512, 1), (1, 64, 5, 7, 192, 1)]
+
+
+def K():
+    from avse_challenge_amd import kernels
+    return kernels
+
+
+def _rel(got, truth, bound):
+    return float(((got.double().cpu() - truth).abs() / (bound + 1e-30)).max())
+
+
+def _inputs(N, ci, H, W, co, seed):
+    x = det_input((N, ci, H, W), seed) * torch.exp(3.0 * det_input((N, ci, H, W), seed + 1))    # ~1e-6 .. 1e2
+    w = 0.05 * det_input((co, ci, 3, 3), seed + 2)
+    return x, w
+
+
+@pytest.mark.parametrize("N,ci,H,W,co,s", SHAPES)
+def test_sconv_fwd_vs_fp64(N, ci, H, W, co, s):
+    """K.sconv_fwd: conv2d(x, W, stride=s, padding=1) vs fp64, bit-identical on rerun."""
+    x, w = _inputs(N, ci, H, W, co, 2100 + ci + co + H)
+    truth = F.conv2d(x.double(), w.double(), None, s, 1)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), None, s, 1)
+    xg = x.to(DEV).contiguous(memory_format=CL)
+    assert K().sconv_ok(xg, co, s)
+    xm = torch.empty(1, device=DEV, dtype=torch.int32)
+    xq = K().split_nhwc(xg, xm)
+    got = K().sconv_fwd((xq, xm), tuple(x.shape), w.to(DEV), s)
+    assert got.is_contiguous(memory_format=CL) and got.shape == truth.shape
+    worst = _rel(got, truth, bound)
+    lib = _rel(F.conv2d(xg, w.to(DEV), None, s, 1), truth, bound)
+    print(f"sconv fwd {N, ci, H, W, co, s}: {worst:.2e} of sum|terms| (MIOpen fp32 {lib:.2e})")
+    assert worst <= 1e-5, (worst, lib)
+    assert torch.equal(K().sconv_fwd((xq, xm), tuple(x.shape), w.to(DEV), s), got)
+
+
+@pytest.mark.parametrize("N,ci,H,W,co,s", [sh for sh in SHAPES if sh[5] == 1])
+def test_sconv_dgrad_vs_fp64(N, ci, H, W, co, s):
+    """K.sconv_fwd(transposed=True): the stride-1 input gradient conv_transpose2d(dy, W, padding=1) vs fp64."""
+    _, w = _inputs(N, ci, H, W, co, 2200 + ci + co + H)
+    dy = det_input((N, co, H, W), 2203 + co) * torch.exp(2.0 * det_input((N, co, H, W), 2204))
+    truth = F.conv_transpose2d(dy.double(), w.double(), None, 1, 1)
+    bound = F.conv_transpose2d(dy.double().abs(), w.double().abs(), None, 1, 1)
+    dyg = dy.to(DEV).contiguous(memory_format=CL)
+    dm = torch.empty(1, device=DEV, dtype=torch.int32)
+    dq = K().split_nhwc(dyg, dm)
+    got = K().sconv_fwd((dq, dm), tuple(dy.shape), w.to(DEV), 1, transposed=True)
+    assert got.shape == truth.shape
+    worst = _rel(got, truth, bound)
+    print(f"sconv dgrad {N, ci, H, W, co}: {worst:.2e} of sum|terms|")
+    assert worst <= 1e-5, worst
+
+
+@pytest.mark.parametrize("N,ci,H,W,co,s", SHAPES)
+def test_sconv_wgrad_vs_fp64(N, ci, H, W, co, s):
+    """K.sconv_wgrad: the weight gradient from the split input and output gradient vs fp64 (64-pixel chunks spanning
+    rows and images, the last chunk partial), deterministic."""
+    x, _ = _inputs(N, ci, H, W, co, 2300 + ci + co + H)
+    ho, wo = (H - 1) // s + 1, (W - 1) // s + 1
+    dy = det_input((N, co, ho, wo), 2305 + co + ho)
+    truth = torch.nn.grad.conv2d_weight(x.double(), (co, ci, 3, 3), dy.double(), s, 1)
+    bound = torch.nn.grad.conv2d_weight(x.double().abs(), (co, ci, 3, 3), dy.double().abs(), s, 1)
+    xm = torch.empty(1, device=DEV, dtype=torch.int32)
+    dm = torch.empty(1, device=DEV, dtype=torch.int32)
+    xq = K().split_nhwc(x.to(DEV).contiguous(memory_format=CL), xm)
+    dq = K().split_nhwc(dy.to(DEV).contiguous(memory_format=CL), dm)
+    dw = K().sconv_wgrad((xq, xm), (dq, dm), tuple(x.shape), co, s)
+    worst = _rel(dw, truth, bound)
+    print(f"sconv wgrad {N, ci, H, W, co, s}: {worst:.2e} of sum|terms|")
+    assert worst <= 1e-5, worst
+    assert torch.equal(K().sconv_wgrad((xq, xm), (dq, dm), tuple(x.shape), co, s), dw)
+
+
+@pytest.mark.parametrize("ci,co,s,H", [(64, 64, 1, 24), (128, 256, 2, 12), (512, 512, 1, 3)])
+def test_trunk_conv2d_module_vs_fp64(ci, co, s, H):
+    """layers.TrunkConv2d on channels-last activations (the _SConvFn path: forward, input gradient -- the stride-2 one on
+    MIOpen -- and weight gradient) vs nn.Conv2d in fp64 on the same weight."""
+    from avse_challenge_amd.layers import TrunkConv2d
+    torch.manual_seed(7)
+    ref = torch.nn.Conv2d(ci, co, 3, stride=s, padding=1, bias=False).double()
+    ours = TrunkConv2d(ci, co, s).to(DEV).to(memory_format=CL)
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = det_input((4, ci, H, H), 2400 + ci)
+    ho = (H - 1) // s + 1
+    gy = det_input((4, co, ho, ho), 2401 + co)
+    xr = x.double().requires_grad_(True)
+    (ref(xr) * gy.double()).sum().backward()
+    xg = x.to(DEV).contiguous(memory_format=CL).requires_grad_(True)
+    y = ours(xg)
+    assert y.grad_fn is not None and "SConv" in type(y.grad_fn).__name__, type(y.grad_fn).__name__
+    (y * gy.to(DEV)).sum().backward()
+    for got, want, what in ((y, ref(xr), "y"), (xg.grad, xr.grad, "dx"), (ours.weight.grad, ref.weight.grad, "dw")):
+        err = float((got.detach().double().cpu() - want.detach()).abs().max())
+        sc = float(want.detach().abs().max())
+        assert err <= 2e-5 * sc, (what, err, sc)
