@@ -19,7 +19,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import losses
-from .layers import LipConv3d, _PReLUFn, bn_act, dwconv1d, dwconv_prelu_gln, maxpool3d, prelu_gln
+from .layers import (LipConv3d, PointwiseConv2d, TrunkConv2d, _PReLUFn, bn_act, dwconv1d, dwconv_prelu_gln, frames_nhwc,
+                     maxpool3d, prelu_gln)
 
 NORM_MEAN, NORM_STD = 0.4161, 0.1688
 
@@ -204,15 +205,17 @@ class ResNetLayer(nn.Module):
     def __init__(self, cin, cout, stride):
         super().__init__()
         bn = dict(momentum=0.01, eps=0.001)
-        self.conv1a = nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
+        # the reference's nn.Conv2d 3x3 / 1x1 (same parameters and keys): channels-last activations run the 3x3 convs
+        # on csrc/sconv.hip and the strided 1x1 shortcut as one GEMM (layers.TrunkConv2d / PointwiseConv2d)
+        self.conv1a = TrunkConv2d(cin, cout, stride)
         self.bn1a = nn.BatchNorm2d(cout, **bn)
-        self.conv2a = nn.Conv2d(cout, cout, 3, padding=1, bias=False)
+        self.conv2a = TrunkConv2d(cout, cout, 1)
         self.stride = stride
-        self.downsample = nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+        self.downsample = PointwiseConv2d(cin, cout, stride)
         self.outbna = nn.BatchNorm2d(cout, **bn)
-        self.conv1b = nn.Conv2d(cout, cout, 3, padding=1, bias=False)
+        self.conv1b = TrunkConv2d(cout, cout, 1)
         self.bn1b = nn.BatchNorm2d(cout, **bn)
-        self.conv2b = nn.Conv2d(cout, cout, 3, padding=1, bias=False)
+        self.conv2b = TrunkConv2d(cout, cout, 1)
         self.outbnb = nn.BatchNorm2d(cout, **bn)
 
     def forward(self, x):
@@ -245,12 +248,24 @@ class VisualFrontend(nn.Module):
             LipConv3d(1, 64, (5, 7, 7), (1, 2, 2), (2, 3, 3)), nn.BatchNorm3d(64, momentum=0.01, eps=0.001), nn.ReLU(),
             nn.MaxPool3d((1, 3, 3), stride=(1, 2, 2), padding=(0, 1, 1)))
         self.resnet = ResNet()
+        self.channels_last = False
+
+    def use_channels_last(self, on=True):
+        """NHWC ResNet trunk: the frames enter as (B*T, H, W, C) memory (csrc/transpose.hip), the 3x3 convs run on
+        csrc/sconv.hip, BatchNorm -> ReLU on bnact's channels-last view (the same kernels as the avse1 lip trunk)."""
+        self.channels_last = on
+        self.resnet.to(memory_format=torch.channels_last if on else torch.contiguous_format)
+        return self
 
     def forward(self, x):                                   # (B, 1, T, 112, 112) -> (B, T, 512)
         bsz = x.shape[0]
         conv, bn, _, pool = self.frontend3D
-        y = maxpool3d(bn_act(conv((x - NORM_MEAN) / NORM_STD), bn, "relu"), pool).transpose(1, 2)
-        y = y.reshape(y.shape[0] * y.shape[1], y.shape[2], y.shape[3], y.shape[4])
+        y = maxpool3d(bn_act(conv((x - NORM_MEAN) / NORM_STD), bn, "relu"), pool)
+        if self.channels_last:
+            y = frames_nhwc(y)
+        else:
+            y = y.transpose(1, 2)
+            y = y.reshape(y.shape[0] * y.shape[1], y.shape[2], y.shape[3], y.shape[4])
         return self.resnet(y).reshape(bsz, -1, 512)
 
 

@@ -500,6 +500,8 @@ class Avse4Step:
         from avse_challenge_amd import avse4, data
         self.B = B
         self.model = avse4.AVSE4BaselineModule(num_channels=2).to(dev).train()
+        if int(os.environ.get("AVSE_LIP_CHANNELS_LAST", "1")):  # NHWC lip ResNet: 3x3 convs on csrc/sconv.hip
+            self.model.visual_frontend.use_channels_last()
         self.lr, self.clip = self.model.lr, None
         self.batch = data.avse4_batch(B, dev, 777 + rank)
 

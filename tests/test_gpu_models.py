@@ -363,7 +363,8 @@ def test_avse4_full_train_step_vs_oracle():
         assert e_gpu <= max(3 * e_torch, floor) and cos > 1 - 1e-4, (k, e_gpu, e_torch, float(cos))
 
 
-def test_avse4_full_train_step_vs_masked_oracle():
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_avse4_full_train_step_vs_masked_oracle(channels_last):
     """The reduced AVSE4BaselineModule train step (lip front-end included) vs the fp64 oracle with OUR activation
     masks imposed (tests/avse4_parity.py): every sign disagreement at a rounding-level pre-activation; loss within
     1e-5; per parameter the max error relative to the masked fp64 gradient's max within max(3x the stock PyTorch-ROCm
@@ -380,6 +381,8 @@ def test_avse4_full_train_step_vs_masked_oracle():
     bg = {k: v.to(DEV) for k, v in batch.items()}
     b64 = {k: v.double() for k, v in batch.items()}
     ours = det_init_(avse4.AVSE4BaselineModule(num_channels=2, **kw), 61).to(DEV).train()
+    if channels_last:                                 # the bench's NHWC lip ResNet (3x3 convs on csrc/sconv.hip)
+        ours.visual_frontend.use_channels_last()
     with capture_masks(ours) as masks:
         loss = ours.training_step(bg)
     loss.backward()
