@@ -203,14 +203,15 @@ __global__ __launch_bounds__(512, 1) void fwd_kernel(FArgs a) {
                 bh[j] = frag(wimg, r, hc);
                 bl[j] = frag(wimg, r, 2 + hc);
             }
+            // product-major: consecutive MFMAs feed the 4 blocks' independent accumulators
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int pr = 0; pr < 3; ++pr)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                }
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr == 2 ? al[i] : ah[i], pr == 1 ? bl[j] : bh[j],
+                                                                           acc[i][j], 0, 0, 0);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // the buffer is refilled after the next barrier
     }
@@ -235,18 +236,21 @@ __global__ __launch_bounds__(512, 1) void fwd_kernel(FArgs a) {
 
 // ------------------------------------------------------------------------------------------------ weight gradient
 // Per kernel row kh: dW[o][i][kh][kw] for the 3 kw taps, a GEMM with M = o, N = i and the reduction over output pixels.
-// Workgroup (pixel-chunk range, o block of 64, i block of 64, kh): 4 waves of 32 x 32 (o, i) blocks x 3 taps (48
-// accumulators).  Per 64-pixel raster chunk: the dY rows (64 pixels x the o block: 256 B each) and the input segment
-// rows the chunk reads at kernel row kh (positions as in the forward, 256 B each for the i block) staged by LDS-DMA;
-// fragments by ds_read_b64_tr_b16 from 256-B rows whose 16-B chunk c sits at c ^ ((r & 3) << 2).  Per chunk and wave:
-// 4 k-steps x 3 taps x 3 products = 36 MFMAs.  Per-workgroup partial slabs, summed by a second kernel (deterministic).
+// Workgroup (pixel-chunk range, o block of OB = 64 or 128, i block of 64, kh): OB / 32 x 2 waves of 32 x 32 (o, i)
+// blocks x 3 taps (48 accumulators).  Per 64-pixel raster chunk: the dY rows (64 pixels x the o block) and the input
+// segment rows the chunk reads at kernel row kh (positions as in the forward, 256 B each for the i block) staged by
+// LDS-DMA; fragments by ds_read_b64_tr_b16 from pixel rows whose 16-B chunk c sits at c ^ ((r & 3) << 2).  Per chunk
+// and wave: 4 k-steps x 3 products x 3 taps = 36 MFMAs, issued product-major so that consecutive MFMAs feed the 3
+// taps' independent accumulators.  Per-workgroup partial slabs, summed by a second kernel (deterministic).
 constexpr int WG_CHUNK = 64;
-constexpr int PIXB = 256;
-constexpr int NPW_MAX = 192;                    // staged input positions per chunk (host-checked)
+constexpr int XROWB = 256;                      // staged input position: the 64-channel i block
+constexpr int NPW_MAX = 184;                    // staged input positions per chunk (host-checked)
 
 __device__ inline int tswz(int r, int c) { return c ^ ((r & 3) << 2); }
 
-// 32 channels (block cb of the staged 64) x 16 pixels, plane pl (0 hi, 1 lo); rows given per lane (see dconv.hip tfrag)
+// 32 channels (block cb of a staged row) x 16 pixels, plane pl (0 hi, 1 lo), rows given per lane (dconv.hip tfrag);
+// RB = bytes per staged row
+template <int RB>
 __device__ inline half8 tfrag(const uint8_t* img, const int (&row)[2], int cb, int pl, int lane) {
     const int g = lane >> 4, i = lane & 15;
     const int q = 2 * cb + (g & 1);
@@ -255,7 +259,7 @@ __device__ inline half8 tfrag(const uint8_t* img, const int (&row)[2], int cb, i
     for (int u = 0; u < 2; ++u) {
         const int r = row[u];
         const int byte = q * 64 + pl * 32 + 8 * (i & 3);
-        const int off = r * PIXB + 16 * tswz(r, byte >> 4) + (byte & 15);
+        const int off = r * RB + 16 * tswz(r, byte >> 4) + (byte & 15);
         v[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(img + off));
     }
     const s4_t w0 = v[0], w1 = v[1];
@@ -275,11 +279,12 @@ struct WArgs {
     float inv_ho, inv_wo;
 };
 
-template <int S>
-__global__ __launch_bounds__(256, 1) void wgrad_kernel(WArgs a) {
-    constexpr int YIMG = WG_CHUNK * PIXB, STG = YIMG + NPW_MAX * PIXB;
-    constexpr int PY = YIMG / 1024;                              // 16 dY pieces (4 pixels each)
-    constexpr int MP = (PY + NPW_MAX / 4 + 3) / 4;
+template <int S, int OB>
+__global__ __launch_bounds__(OB * 4, 1) void wgrad_kernel(WArgs a) {
+    constexpr int WAVES = OB / 16, YRB = OB * 4;                  // dY row bytes: the o block
+    constexpr int YIMG = WG_CHUNK * YRB, STG = YIMG + NPW_MAX * XROWB;
+    constexpr int PY = YIMG / 1024, YPP = 1024 / YRB;             // dY pieces; pixels per piece
+    constexpr int MP = (PY + NPW_MAX / 4 + WAVES - 1) / WAVES;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * STG];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -297,16 +302,17 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WArgs a) {
     const i4_t ry = rsrc_of(a.dyq, (int64_t)NHWo * a.Co * 4);
     const uint32_t lds0 = lds_u32(lds);
     const int PT = PY + a.npw / 4;
-    const int npieces = (PT - wave + 3) / 4;
-    const int pr = lane >> 4, pc = lane & 15;                    // a piece's lane: pixel row (of 4), physical chunk
+    const int npieces = (PT - wave + WAVES - 1) / WAVES;
     const uint32_t xpixb = (uint32_t)a.Ci * 4u, ypixb = (uint32_t)a.Co * 4u;
+    const int ypr = lane / (YRB / 16), ypc = lane % (YRB / 16);  // dY piece lane: pixel of the piece, physical chunk
+    const int xpr = lane >> 4, xpc = lane & 15;                    // X piece lane: position of the piece, chunk
 
     // the lane's staged position of each X piece: (row of the chunk's segment list, column)
     int qrk[MP], qcol[MP];
 #pragma unroll
     for (int m = 0; m < MP; ++m) {
-        const int k = wave + 4 * m;
-        const int q = 4 * (k - PY) + pr;
+        const int k = wave + WAVES * m;
+        const int q = 4 * (k - PY) + xpr;
         qrk[m] = k >= PY ? q / a.RS : 0;
         qcol[m] = k >= PY ? q - qrk[m] * a.RS : 0;
     }
@@ -318,20 +324,22 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WArgs a) {
 #pragma unroll
         for (int m = 0; m < MP; ++m) {
             if (m >= npieces) break;
-            const int k = wave + 4 * m;
-            if (k < PY) {                                        // dY rows: chunk pixel j = 4 k + pr
-                const int j = 4 * k + pr, p = p0 + j;
-                const uint32_t off = p < NHWo ? (uint32_t)p * ypixb + (uint32_t)(ob * 256) + 16u * tswz(j, pc) : OOB;
+            const int k = wave + WAVES * m;
+            if (k < PY) {                                        // dY rows: chunk pixel j = YPP k + ypr
+                const int j = YPP * k + ypr, p = p0 + j;
+                const uint32_t off =
+                    p < NHWo ? (uint32_t)p * ypixb + (uint32_t)(ob * YRB) + 16u * tswz(j, ypc) : OOB;
                 dma16(ry, img + k * 1024, off);
             } else {
-                const int q = 4 * (k - PY) + pr;
+                const int q = 4 * (k - PY) + xpr;
                 int dn, ho;
                 divmod_small(ho0 + qrk[m], a.Ho, a.inv_ho, dn, ho);
                 const int g = g0 + qrk[m], n = n0 + dn;
                 const int hi = S * ho - 1 + kh, wi = qcol[m] - 1;
                 const bool ok = q < a.npw && g < NHo && hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi;
                 const uint32_t pix = (uint32_t)(n * a.Hi + hi) * (uint32_t)a.Wi + (uint32_t)wi;
-                dma16(rx, img + YIMG + (k - PY) * 1024, ok ? pix * xpixb + (uint32_t)(ib * 256) + 16u * tswz(q, pc) : OOB);
+                dma16(rx, img + YIMG + (k - PY) * 1024,
+                      ok ? pix * xpixb + (uint32_t)(ib * XROWB) + 16u * tswz(q, xpc) : OOB);
             }
         }
     };
@@ -365,19 +373,24 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WArgs a) {
                 ry_[u] = j;
                 rx_[u] = dr * a.RS + S * wo;
             }
-            const half8 ah = tfrag(yimg, ry_, obw, 0, lane), al = tfrag(yimg, ry_, obw, 1, lane);
+            const half8 ah = tfrag<YRB>(yimg, ry_, obw, 0, lane), al = tfrag<YRB>(yimg, ry_, obw, 1, lane);
+            half8 bh[3], bl[3];
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw) {
                 const int rk[2] = {rx_[0] + kw, rx_[1] + kw};
-                const half8 bh = tfrag(ximg, rk, ibw, 0, lane), bl = tfrag(ximg, rk, ibw, 1, lane);
-                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[kw], 0, 0, 0);
-                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[kw], 0, 0, 0);
-                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[kw], 0, 0, 0);
+                bh[kw] = tfrag<XROWB>(ximg, rk, ibw, 0, lane);
+                bl[kw] = tfrag<XROWB>(ximg, rk, ibw, 1, lane);
             }
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[kw], acc[kw], 0, 0, 0);
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[kw], acc[kw], 0, 0, 0);
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[kw], acc[kw], 0, 0, 0);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    // partial tiles: acc[kw] register 4 q + e = row o = 64 ob + 32 obw + 8 q + 4 (lane >> 5) + e, column
+    // partial tiles: acc[kw] register 4 q + e = row o = OB ob + 32 obw + 8 q + 4 (lane >> 5) + e, column
     // i = 64 ib + 32 ibw + (lane & 31)
     const float sc = __builtin_ldexpf(1.f, -(split_exp(*a.xmax) + split_exp(*a.dymax)));
     float* pp = a.part + ((int64_t)r * 9 + kh * 3) * a.Co * a.Ci;
@@ -387,7 +400,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WArgs a) {
         for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const int o = 64 * ob + 32 * obw + 8 * q + 4 * (lane >> 5) + e, i = 64 * ib + 32 * ibw + (lane & 31);
+                const int o = OB * ob + 32 * obw + 8 * q + 4 * (lane >> 5) + e, i = 64 * ib + 32 * ibw + (lane & 31);
                 pp[((int64_t)kw * a.Co + o) * a.Ci + i] = acc[kw][4 * q + e] * sc;
             }
 }
@@ -535,7 +548,7 @@ static int wg_setup(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, i
     const int64_t NHWo = N * a.Ho * a.Wo;
     if (NHWo * co * 4 >= (1LL << 31) - 4096) return AVSE_ESHAPE;
     a.chunks = (int)((NHWo + WG_CHUNK - 1) / WG_CHUNK);
-    a.nob = (int)(co / 64);
+    a.nob = (int)(co % 128 ? co / 64 : co / 128);               // o blocks of OB = 128 when they tile co, else 64
     a.nib = (int)(ci / 64);
     a.ranges = wg_ranges(a.chunks, 3 * a.nob * a.nib);
     a.inv_ho = 1.f / (float)a.Ho;
@@ -561,10 +574,16 @@ int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, 
     a.xmax = xmax;
     a.dymax = dymax;
     a.part = workspace;
-    const dim3 grid((unsigned)(a.ranges * 3 * a.nob * a.nib)), block(256);
+    const bool ob128 = co % 128 == 0;
+    const dim3 grid((unsigned)(a.ranges * 3 * a.nob * a.nib)), block(ob128 ? 512 : 256);
     hipStream_t st = (hipStream_t)stream;
-    if (stride == 1) hipLaunchKernelGGL(wgrad_kernel<1>, grid, block, 0, st, a);
-    else hipLaunchKernelGGL(wgrad_kernel<2>, grid, block, 0, st, a);
+    if (ob128) {
+        if (stride == 1) hipLaunchKernelGGL((wgrad_kernel<1, 128>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((wgrad_kernel<2, 128>), grid, block, 0, st, a);
+    } else {
+        if (stride == 1) hipLaunchKernelGGL((wgrad_kernel<1, 64>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((wgrad_kernel<2, 64>), grid, block, 0, st, a);
+    }
     AVSE_CHECK_LAUNCH();
     const int64_t total = 9 * co * ci;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0,
