@@ -127,9 +127,9 @@ SIGNATURES = {
     "avse_transpose_cp": (c_i32, [c_i64] * 3 + [c_vp, c_vp, c_vp]),
     "avse_bnact_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "avse_bnact_fwd": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_f32, c_f32,
-                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "avse_bnact_bwd": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32,
                                c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_bnact_bwd": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32,
+                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_prelu_nhwc_fwd": (c_i32, [c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "avse_prelu_nhwc_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_prelu_nhwc_bwd": (c_i32, [c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -157,6 +157,7 @@ SIGNATURES = {
     "avse_split16_planes": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_dconv_wprep_bytes": (c_i64, []),
     "avse_split16": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "avse_split16_known": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_dconv_wprep": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp]),
     "avse_dconv_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_dconv_wgrad16_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),

@@ -111,6 +111,22 @@ __device__ inline void block_partials(const Geo& g, float (&p)[NQ][V], bool vali
     }
 }
 
+// max |out| of the workgroup -> one atomicMax on the float bits (non-negative floats order like their bits) into
+// omax: the producer-side max of the split operands (the convolution that consumes the output skips its absmax pass)
+__device__ inline void block_max_out(float m, uint32_t* omax) {
+    __shared__ uint32_t red[THREADS / 64];
+    uint32_t b = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        b = red[0];
+#pragma unroll
+        for (int w = 1; w < THREADS / 64; ++w) b = max(b, red[w]);
+        if (b) atomicMax(omax, b);
+    }
+}
+
 // ---- forward: statistics partials (shifted sums), finalize, apply
 template <int V>
 __global__ __launch_bounds__(THREADS) void stats_kernel(Geo g, const float* __restrict__ x, float* __restrict__ ws) {
@@ -183,8 +199,9 @@ __global__ __launch_bounds__(THREADS) void chan_partial_kernel(Geo g, const floa
 
 __global__ void stats_combine(Geo g, const float* __restrict__ x, const double* __restrict__ fin, int G, float eps,
                               float momentum, float* __restrict__ running_mean, float* __restrict__ running_var,
-                              float* __restrict__ stats) {
+                              float* __restrict__ stats, uint32_t* __restrict__ omax) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0 && omax) *omax = 0u;                      // the apply pass's max, reset in stream order before it
     if (c >= g.C) return;
     double s1 = 0.0, s2 = 0.0;
     for (int gi = 0; gi < G; ++gi) {
@@ -206,8 +223,9 @@ __global__ void stats_combine(Geo g, const float* __restrict__ x, const double* 
 }
 
 __global__ void eval_stats_kernel(int C, const float* __restrict__ rm, const float* __restrict__ rv, float eps,
-                                  float* __restrict__ stats) {
+                                  float* __restrict__ stats, uint32_t* __restrict__ omax) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0 && omax) *omax = 0u;
     if (c < C) {
         stats[4 * c] = rm[c];
         stats[4 * c + 1] = 0.f;
@@ -220,25 +238,29 @@ template <int V, int ACT, bool RES>
 __global__ __launch_bounds__(THREADS) void apply_kernel(Geo g, const float* __restrict__ x, const float* __restrict__ res,
                                                         const float* __restrict__ stats, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, const float* __restrict__ alpha,
-                                                        int alpha_n, float* __restrict__ y) {
+                                                        int alpha_n, float* __restrict__ y, uint32_t* __restrict__ ymax) {
     const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
     const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
-    if (j0 >= g.CS) return;
-    ColConst<V, ACT> cc;
-    cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
-    for (int64_t r = (int64_t)blockIdx.y * g.RPI + ty; r < g.N; r += (int64_t)gridDim.y * g.RPI) {
-        const int64_t o = r * g.CS + j0;
-        float v[V], rv[V];
-        vld<V>::ld(x + o, v);
-        if (RES) vld<V>::ld(res + o, rv);
+    float m = 0.f;
+    if (j0 < g.CS) {
+        ColConst<V, ACT> cc;
+        cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
+        for (int64_t r = (int64_t)blockIdx.y * g.RPI + ty; r < g.N; r += (int64_t)gridDim.y * g.RPI) {
+            const int64_t o = r * g.CS + j0;
+            float v[V], rv[V];
+            vld<V>::ld(x + o, v);
+            if (RES) vld<V>::ld(res + o, rv);
 #pragma unroll
-        for (int k = 0; k < V; ++k) {
-            float z = fmaf(cc.centred(v[k], k), cc.a[k], cc.b[k]);
-            if (RES) z += rv[k];
-            v[k] = act_fwd<ACT>(z, cc.al[k]);
+            for (int k = 0; k < V; ++k) {
+                float z = fmaf(cc.centred(v[k], k), cc.a[k], cc.b[k]);
+                if (RES) z += rv[k];
+                v[k] = act_fwd<ACT>(z, cc.al[k]);
+                m = fmaxf(m, fabsf(v[k]));
+            }
+            vld<V>::st(y + o, v);
         }
-        vld<V>::st(y + o, v);
     }
+    if (ymax) block_max_out(m, ymax);                    // workgroup-uniform condition
 }
 
 // ---- backward: partials of sum dz, sum dz*xhat, PReLU slope; finalize; apply
@@ -281,8 +303,10 @@ __global__ __launch_bounds__(THREADS) void bwd_partial_kernel(Geo g, const float
 }
 
 __global__ void bwd_combine(Geo g, const double* __restrict__ fin, int G, int training, float* __restrict__ dgamma,
-                            float* __restrict__ dbeta, float* __restrict__ dalpha_c, float* __restrict__ kbuf) {
+                            float* __restrict__ dbeta, float* __restrict__ dalpha_c, float* __restrict__ kbuf,
+                            uint32_t* __restrict__ omax) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0 && omax) *omax = 0u;                      // the apply pass's max, reset in stream order before it
     if (c >= g.C) return;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     for (int gi = 0; gi < G; ++gi) {
@@ -299,15 +323,11 @@ __global__ void bwd_combine(Geo g, const double* __restrict__ fin, int G, int tr
 }
 
 template <int V, int ACT, bool RES>
-__global__ __launch_bounds__(THREADS) void bwd_apply_kernel(Geo g, const float* __restrict__ x,
-                                                            const float* __restrict__ dy, const float* __restrict__ dres,
-                                                            const float* __restrict__ stats,
-                                                            const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                            const float* __restrict__ alpha, int alpha_n,
-                                                            const float* __restrict__ kbuf, float* __restrict__ dx) {
-    const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
-    const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
-    if (j0 >= g.CS) return;
+__device__ inline void bwd_apply_cols(const Geo& g, int64_t j0, int ty, const float* __restrict__ x,
+                                      const float* __restrict__ dy, const float* __restrict__ dres,
+                                      const float* __restrict__ stats, const float* __restrict__ gamma,
+                                      const float* __restrict__ beta, const float* __restrict__ alpha, int alpha_n,
+                                      const float* __restrict__ kbuf, float* __restrict__ dx, float& m) {
     ColConst<V, ACT> cc;
     cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
     float k1[V], k2[V];
@@ -333,9 +353,25 @@ __global__ __launch_bounds__(THREADS) void bwd_apply_kernel(Geo g, const float* 
         for (int k = 0; k < V; ++k) {
             const float xh = cc.centred(v[k], k) * cc.rstd[k];
             v[k] = cc.a[k] * (dz[k] - k1[k] - xh * k2[k]);
+            m = fmaxf(m, fabsf(v[k]));
         }
         vld<V>::st(dx + o, v);
     }
+}
+
+template <int V, int ACT, bool RES>
+__global__ __launch_bounds__(THREADS) void bwd_apply_kernel(Geo g, const float* __restrict__ x,
+                                                            const float* __restrict__ dy, const float* __restrict__ dres,
+                                                            const float* __restrict__ stats,
+                                                            const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                            const float* __restrict__ alpha, int alpha_n,
+                                                            const float* __restrict__ kbuf, float* __restrict__ dx,
+                                                            uint32_t* __restrict__ dxmax) {
+    const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
+    const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
+    float m = 0.f;
+    if (j0 < g.CS) bwd_apply_cols<V, ACT, RES>(g, j0, ty, x, dy, dres, stats, gamma, beta, alpha, alpha_n, kbuf, dx, m);
+    if (dxmax) block_max_out(m, dxmax);                  // workgroup-uniform condition
 }
 
 // ---- host side
@@ -409,7 +445,7 @@ int64_t avse_bnact_workspace_bytes(int64_t N, int64_t C, int64_t S) {
 int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* gamma,
                    const float* beta, int32_t act, const float* alpha, int32_t alpha_n, int32_t training, float eps,
                    float momentum, float* running_mean, float* running_var, float* stats, float* y, float* workspace,
-                   avse_stream_t stream) {
+                   uint32_t* y_max, avse_stream_t stream) {
     if (!x || !y || !stats || !workspace || (act == ACT_PRELU && !alpha)) return AVSE_EINVAL;
     if (!training && (!running_mean || !running_var)) return AVSE_EINVAL;
     if (!shape_ok(N, C, S) || act < ACT_NONE || act > ACT_PRELU) return AVSE_ESHAPE;
@@ -429,14 +465,14 @@ int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float*
                            fin);
         AVSE_CHECK_LAUNCH();
         hipLaunchKernelGGL(stats_combine, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, g, x, (const double*)fin,
-                           G, eps, momentum, running_mean, running_var, stats);
+                           G, eps, momentum, running_mean, running_var, stats, y_max);
     } else {
         hipLaunchKernelGGL(eval_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, (int)C, running_mean,
-                           running_var, eps, stats);
+                           running_var, eps, stats, y_max);
     }
     AVSE_CHECK_LAUNCH();
     dispatch<ApplyK>::run(V, act, res != nullptr, grid, st, g, x, res, (const float*)stats, gamma, beta, alpha,
-                          (int)alpha_n, y);
+                          (int)alpha_n, y, y_max);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
@@ -444,7 +480,7 @@ int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float*
 int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* dy, const float* stats,
                    const float* gamma, const float* beta, int32_t act, const float* alpha, int32_t alpha_n,
                    int32_t training, float* dx, float* dres, float* dgamma, float* dbeta, float* dalpha_c,
-                   float* workspace, avse_stream_t stream) {
+                   float* workspace, uint32_t* dx_max, avse_stream_t stream) {
     if (!x || !dy || !stats || !dx || !workspace || (act == ACT_PRELU && (!alpha || !dalpha_c)) || (res && !dres))
         return AVSE_EINVAL;
     if (!shape_ok(N, C, S) || act < ACT_NONE || act > ACT_PRELU) return AVSE_ESHAPE;
@@ -464,10 +500,10 @@ int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float*
                        fin);
     AVSE_CHECK_LAUNCH();
     hipLaunchKernelGGL(bwd_combine, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, g, (const double*)fin, G,
-                       (int)training, dgamma, dbeta, dalpha_c, kbuf);
+                       (int)training, dgamma, dbeta, dalpha_c, kbuf, dx_max);
     AVSE_CHECK_LAUNCH();
     dispatch<BwdApplyK>::run(V, act, res != nullptr, grid, st, g, x, dy, (const float*)dres, stats, gamma, beta, alpha,
-                             (int)alpha_n, (const float*)kbuf, dx);
+                             (int)alpha_n, (const float*)kbuf, dx, dx_max);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

@@ -552,6 +552,18 @@ int avse_split16(int64_t n_pix, const float* x, void* xq, uint32_t* maxbits, avs
     return AVSE_OK;
 }
 
+int avse_split16_known(int64_t n_pix, const float* x, void* xq, const uint32_t* maxbits, avse_stream_t stream) {
+    if (!x || !xq || !maxbits) return AVSE_EINVAL;
+    if (n_pix <= 0) return AVSE_ESHAPE;
+    if (((uintptr_t)x & 15) || ((uintptr_t)xq & 15)) return AVSE_EALIGN;
+    const int64_t nq = n_pix * NQ;
+    const int blocks = (int)std::min<int64_t>((nq + 255) / 256, 8192);
+    hipLaunchKernelGGL(split_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, nq, maxbits,
+                       reinterpret_cast<uint4*>(xq));
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
 int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* maxbits, avse_stream_t stream) {
     if (!w || !wq || !maxbits) return AVSE_EINVAL;
     hipLaunchKernelGGL(wprep_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, w, transposed, maxbits,

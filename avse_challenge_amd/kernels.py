@@ -475,10 +475,16 @@ def split16(x, maxbits):
     """x (N, 64, H, W) fp32 (channels-last memory is read as it lies, anything else made so) -> its fp16 hi / lo split
     in dconv.hip's Q4 layout (uint8 (N*H*W, 256)); writes max |x| (float bits) into maxbits[0]."""
     _need_gpu(x)
+    known = _known_absmax(x)
     x = x.contiguous(memory_format=torch.channels_last)
     npix = x.shape[0] * x.shape[2] * x.shape[3]
     xq = torch.empty((npix, 256), device=x.device, dtype=torch.uint8)
-    check(_lib.lib().avse_split16(npix, ptr(x), ptr(xq), ptr(maxbits), stream_ptr(x.device)), "avse_split16")
+    if known is not None:                          # the producer's max: the split pass only
+        maxbits[:1].copy_(known)
+        check(_lib.lib().avse_split16_known(npix, ptr(x), ptr(xq), ptr(maxbits), stream_ptr(x.device)),
+              "avse_split16_known")
+    else:
+        check(_lib.lib().avse_split16(npix, ptr(x), ptr(xq), ptr(maxbits), stream_ptr(x.device)), "avse_split16")
     return xq
 
 
@@ -559,6 +565,23 @@ def split_nhwc(x, maxbits):
     check(_lib.lib().avse_split16(n * h * w * (c // 64), ptr(x), ptr(xq), ptr(maxbits), stream_ptr(x.device)),
           "avse_split16")
     return xq
+
+
+def split_q(x):
+    """-> (xq, xmax): split_nhwc with the producer's max when x carries one (no absmax pass), else a fresh max."""
+    known = _known_absmax(x)
+    if known is None:
+        xm = torch.empty(1, device=x.device, dtype=torch.int32)
+        return split_nhwc(x, xm), xm
+    _need_gpu(x)
+    x = x.contiguous(memory_format=torch.channels_last)
+    n, c, h, w = x.shape
+    if c % 64:
+        raise RuntimeError(f"split_q: channels must be a multiple of 64, got {c}")
+    xq = torch.empty((n * h * w, 4 * c), device=x.device, dtype=torch.uint8)
+    check(_lib.lib().avse_split16_known(n * h * w * (c // 64), ptr(x), ptr(xq), ptr(known), stream_ptr(x.device)),
+          "avse_split16_known")
+    return xq, known
 
 
 def sconv_wprep(w, transposed, wmax):
@@ -785,11 +808,28 @@ def bnact_fwd(x, gamma, beta, running_mean, running_var, training, momentum, eps
     L = _lib.lib()
     ws = torch.empty((L.avse_bnact_workspace_bytes(N, C, S) + 3) // 4, device=x.device, dtype=torch.float32)
     a = alpha.float().contiguous() if alpha is not None else None
+    ymax = torch.empty(1, device=x.device, dtype=torch.int32)
     check(L.avse_bnact_fwd(N, C, S, ptr(x), _opt(res), _opt(gamma), _opt(beta), int(act), _opt(a),
                            a.numel() if a is not None else 0, int(bool(training)), float(eps), float(momentum),
-                           _opt(running_mean), _opt(running_var), ptr(stats), ptr(y), ptr(ws), stream_ptr(x.device)),
-          "avse_bnact_fwd")
+                           _opt(running_mean), _opt(running_var), ptr(stats), ptr(y), ptr(ws), ptr(ymax),
+                           stream_ptr(x.device)), "avse_bnact_fwd")
+    _set_absmax(y, ymax)
     return y, stats
+
+
+# The producer-side max |t| of a tensor (float bits in a 1-element int32 device tensor), attached to the tensor object by
+# the kernels that compute it in their output pass (bnact fwd / bwd): a split consumer (split16 / split_q) then skips its
+# absmax pass.  Only fresh outputs carry it, and nothing writes them in place before their consumers read them.
+ABSMAX_ATTR = "_avse_absmax"
+
+
+def _set_absmax(t, mb):
+    setattr(t, ABSMAX_ATTR, mb)
+
+
+def _known_absmax(t):
+    mb = getattr(t, ABSMAX_ATTR, None)
+    return mb if isinstance(mb, torch.Tensor) and mb.device == t.device else None
 
 
 def bnact_bwd(x, res, dy, stats, gamma, beta, act, alpha, training):
@@ -807,9 +847,11 @@ def bnact_bwd(x, res, dy, stats, gamma, beta, act, alpha, training):
     dalpha_c = torch.empty((C,), device=x.device, dtype=torch.float32) if a is not None else None
     L = _lib.lib()
     ws = torch.empty((L.avse_bnact_workspace_bytes(N, C, S) + 3) // 4, device=x.device, dtype=torch.float32)
+    dxmax = torch.empty(1, device=x.device, dtype=torch.int32)
     check(L.avse_bnact_bwd(N, C, S, ptr(x), _opt(res), ptr(dy), ptr(stats), _opt(gamma), _opt(beta), int(act), _opt(a),
                            a.numel() if a is not None else 0, int(bool(training)), ptr(dx), _opt(dres), ptr(dgamma),
-                           ptr(dbeta), _opt(dalpha_c), ptr(ws), stream_ptr(x.device)), "avse_bnact_bwd")
+                           ptr(dbeta), _opt(dalpha_c), ptr(ws), ptr(dxmax), stream_ptr(x.device)), "avse_bnact_bwd")
+    _set_absmax(dx, dxmax)
     dalpha = None
     if a is not None:
         dalpha = (dalpha_c if a.numel() == C else dalpha_c.sum().reshape(1)).view_as(alpha)

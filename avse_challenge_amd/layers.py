@@ -555,8 +555,7 @@ class _SConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, stride):
-        xm = torch.empty(1, device=x.device, dtype=torch.int32)
-        xq = K.split_nhwc(x, xm)
+        xq, xm = K.split_q(x)                      # the producing BatchNorm pass's max when it comes with x
         ctx.shape, ctx.stride = tuple(x.shape), stride
         ctx.save_for_backward(xq, xm, w)
         return K.sconv_fwd((xq, xm), ctx.shape, w, stride)
@@ -565,9 +564,8 @@ class _SConvFn(torch.autograd.Function):
     def backward(ctx, dy):
         xq, xm, w = ctx.saved_tensors
         s, shape = ctx.stride, ctx.shape
+        dyq, dym = K.split_q(dy)                   # (the incoming gradient keeps its producer's max, if any)
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dym = torch.empty(1, device=dy.device, dtype=torch.int32)
-        dyq = K.split_nhwc(dy, dym)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             if s == 1:

@@ -248,17 +248,18 @@ int avse_prelu_nhwc_bwd(int64_t R, int64_t C, int32_t num_params, const float* x
  * dalpha_c (C; sum it for a single slope) and, with res, dres (= the gradient of the pre-activation).
  * Replaces nn.BatchNorm3d/2d + nn.PReLU / F.relu (+ the residual add) of the avse1 lip front-end and ResNet
  * BasicBlock (/root/reference/baseline/avse1/model.py:29-34, utils/resnet.py:40-67) and of the avse1 audio net
- * (model.py:181-267).  workspace: avse_bnact_workspace_bytes.
+ * (model.py:181-267).  workspace: avse_bnact_workspace_bytes.  y_max / dx_max (may be null): max |y| / |dx| as float
+ * bits, the producer-side max of a split operand (avse_split16_known then skips its absmax pass).
  */
 int64_t avse_bnact_workspace_bytes(int64_t N, int64_t C, int64_t S);
 int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* gamma,
                    const float* beta, int32_t act, const float* alpha, int32_t alpha_n, int32_t training, float eps,
                    float momentum, float* running_mean, float* running_var, float* stats, float* y, float* workspace,
-                   avse_stream_t stream);
+                   uint32_t* y_max, avse_stream_t stream);
 int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* dy, const float* stats,
                    const float* gamma, const float* beta, int32_t act, const float* alpha, int32_t alpha_n,
                    int32_t training, float* dx, float* dres, float* dgamma, float* dbeta, float* dalpha_c,
-                   float* workspace, avse_stream_t stream);
+                   float* workspace, uint32_t* dx_max, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- max pooling over planes -------
  * nn.MaxPool3d((1, KH, KW), (1, SH, SW), (0, PH, PW)) of the lip front-ends (avse1 model.py:29-34, avse4
@@ -404,6 +405,8 @@ int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t
  *                 most two rows), n_pix * 256 < 2^31. */
 int64_t avse_dconv_wprep_bytes(void);
 int avse_split16(int64_t n_pix, const float* x, void* xq, uint32_t* maxbits, avse_stream_t stream);
+/* avse_split16 with max |x| already in maxbits[0] (e.g. avse_bnact_fwd's y_max): the split pass only */
+int avse_split16_known(int64_t n_pix, const float* x, void* xq, const uint32_t* maxbits, avse_stream_t stream);
 int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* maxbits, avse_stream_t stream);
 
 /* 3x3 convolutions of the lip-encoder ResNet trunks (csrc/sconv.hip), replacing

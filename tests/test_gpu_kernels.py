@@ -575,9 +575,14 @@ def test_bnact_vs_fp64(shape, cl, act, res, training, mean, scale):
     yg = bn_act(xg, bn, m_act, res=rg)
     assert yg.stride() == xg.stride()
     close(yg, y, 2e-5, 1e-5, "y")
+    # the producer-side max the split convolutions take instead of an absmax pass: exactly max |y| as stored
+    assert int(getattr(yg, K().ABSMAX_ATTR).item()) == int(yg.detach().abs().max().view(torch.int32).item())
     yg.backward(gy.float().to(DEV).contiguous(memory_format=fmt))
     gs = float(x.grad.abs().max())
     close(xg.grad, x.grad, 2e-5 * gs, 1e-4, "dx")
+    mb = getattr(xg.grad, K().ABSMAX_ATTR, None)          # the backward's dx max (when autograd kept the object)
+    if mb is not None:
+        assert int(mb.item()) == int(xg.grad.abs().max().view(torch.int32).item())
     if res:
         close(rg.grad, r.grad, 1e-6, 1e-6, "dres")
     close(bn.weight.grad, ref.weight.grad, 1e-4 * float(ref.weight.grad.abs().max()), 1e-4, "dgamma")
