@@ -16,7 +16,8 @@
 //   - fp32 operands: the split of dconv.hip / projgemm.hip with per-TILE power-of-two scales (the tile's x slab and
 //     W rows are in LDS anyway): hi = fp16(v 2^e), lo = fp16(v 2^e - hi), products hi*hi + hi*lo + lo*hi on the f16
 //     MFMA, scaled back by 2^-(e_x + e_w) (22-bit operands: the fp32 class).
-// Workgroup = 64 channels x 256 steps of one batch row, 4 waves of 64 channels x 64 steps (2 x 2 MFMA blocks).  x rows
+// Workgroup = 64 channels x 256 steps of one batch row, 4 waves of 64 channels x 64 steps (2 x 2 MFMA blocks, the
+// steps as the MFMA rows: each lane stores 4 consecutive steps of one channel).  x rows
 // [0, R) x 256 steps are staged in LDS as 16-bit k-rows of 512 B (16-B chunk c of k-row r at c ^ ((r & 3) << 2),
 // fragments by ds_read_b64_tr_b16), W's 64 rows as R-long 16-bit rows padded by 16 B (conflict-free 16-B reads).
 // The workgroups of one x slab (its D / 64 channel tiles) are consecutive, so the slab is re-read from L2.
@@ -215,62 +216,87 @@ __global__ __launch_bounds__(THREADS) void dtproj_kernel(Args a) {
     }
     __syncthreads();
 
-    floatx16 acc[2][2];
+    // C[t][d] = sum_r x[r][t] W[d][r]: the steps are the MFMA rows, so each lane ends with 4 consecutive steps of one
+    // channel (one 16-B / 8-B store per 4 outputs)
+    floatx16 acc[2][2];                                       // [t block j][channel block i]
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    const int tc = 64 * wave;                                 // this wave's steps tc .. tc + 63 of the tile
-    for (int s = 0; s < a.RP / 16; ++s) {
-        half8 ah[2], bh[2], al[2], bl[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            ah[i] = wfrag(wimg, wrow, 32 * i, s, lane);
-            if constexpr (F32) al[i] = wfrag(wimg + WB, wrow, 32 * i, s, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            bh[j] = xfrag(ximg, tc + 32 * j, s, lane);
-            if constexpr (F32) bl[j] = xfrag(ximg + XB, tc + 32 * j, s, lane);
-        }
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if constexpr (F32) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                } else {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ah[i]),
-                                                                        __builtin_bit_cast(bf16x8, bh[j]), acc[i][j], 0,
-                                                                        0, 0);
+            for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+    const int tc = 64 * wave;                                 // this wave's steps tc .. tc + 63 of the tile
+    for (int s = 0; s < a.RP / 16; ++s) {
+        half8 wh[2], xh[2], wl[2], xl[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            wh[i] = wfrag(wimg, wrow, 32 * i, s, lane);
+            if constexpr (F32) wl[i] = wfrag(wimg + WB, wrow, 32 * i, s, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            xh[j] = xfrag(ximg, tc + 32 * j, s, lane);
+            if constexpr (F32) xl[j] = xfrag(ximg + XB, tc + 32 * j, s, lane);
+        }
+#pragma unroll
+        for (int pr = 0; pr < (F32 ? 3 : 1); ++pr)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if constexpr (F32) {
+                        acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr == 2 ? xl[j] : xh[j], pr == 1 ? wl[i] : wh[i],
+                                                                           acc[j][i], 0, 0, 0);
+                    } else {
+                        acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, xh[j]),
+                                                                            __builtin_bit_cast(bf16x8, wh[i]), acc[j][i],
+                                                                            0, 0, 0);
+                    }
                 }
-            }
     }
 
-    // epilogue: acc[i][j] register 4 g + e = channel d0 + 32 i + 8 g + 4 (lane >> 5) + e, step t0 + tc + 32 j +
-    // (lane & 31): 32 lanes store 32 consecutive steps of one channel
+    // epilogue: acc[j][i] register 4 g + e = step t0 + tc + 32 j + 8 g + 4 (lane >> 5) + e, channel d0 + 32 i +
+    // (lane & 31)
     T* ob = reinterpret_cast<T*>(a.out) + (int64_t)b * a.o_bs;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
+        const int d = d0 + 32 * i + (lane & 31);
+        if (d >= a.D) continue;
+        const float bv = a.bias ? a.bias[d] : 0.f;
+        T* orow = ob + (int64_t)d * a.o_ds;
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int d = d0 + 32 * i + 8 * g + 4 * (lane >> 5) + e;
-                if (d >= a.D) continue;
-                const float bv = a.bias ? a.bias[d] : 0.f;
+            for (int g = 0; g < 4; ++g) {
+                const int t = t0 + tc + 32 * j + 8 * g + 4 * (lane >> 5);
+                if (t >= a.L) continue;
+                float v[4];
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int t = t0 + tc + 32 * j + (lane & 31);
-                    float v = acc[i][j][4 * g + e] * unscale + bv;
-                    if (a.softplus) v = softplus2(v);
-                    if (t < a.L) io<T>::st(ob + (int64_t)d * a.o_ds + t, v);
+                for (int e = 0; e < 4; ++e) {
+                    v[e] = acc[j][i][4 * g + e] * unscale + bv;
+                    if (a.softplus) v[e] = softplus2(v[e]);
                 }
+                T* o = orow + t;
+                if constexpr (F32) {
+                    if (t + 3 < a.L && ((uintptr_t)o & 15) == 0) {
+                        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+                        continue;
+                    }
+                } else {
+                    if (t + 3 < a.L && ((uintptr_t)o & 7) == 0) {
+                        bf16_t h[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) io<bf16_t>::st(&h[e], v[e]);
+                        *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)h[0].x | ((uint32_t)h[1].x << 16),
+                                                                  (uint32_t)h[2].x | ((uint32_t)h[3].x << 16));
+                        continue;
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (t + e < a.L) io<T>::st(o + e, v[e]);
             }
+    }
 }
 
 }  // namespace dtp

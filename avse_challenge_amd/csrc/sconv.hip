@@ -280,8 +280,10 @@ struct WArgs {
 };
 
 template <int S, int OB>
-__global__ __launch_bounds__(OB * 4, 1) void wgrad_kernel(WArgs a) {
-    constexpr int WAVES = OB / 16, YRB = OB * 4;                  // dY row bytes: the o block
+__global__ __launch_bounds__(512, 1) void wgrad_kernel(WArgs a) {
+    // OB = 128: 8 waves of (o, i) blocks; OB = 64: the 4 blocks twice, each copy over half of a chunk's 4 k-steps
+    // (KG = 2 k-step groups, two partial slabs per range): 8 waves either way
+    constexpr int KG = OB == 64 ? 2 : 1, BW = OB / 16, WAVES = BW * KG, YRB = OB * 4;   // dY row bytes: the o block
     constexpr int YIMG = WG_CHUNK * YRB, STG = YIMG + NPW_MAX * XROWB;
     constexpr int PY = YIMG / 1024, YPP = 1024 / YRB;             // dY pieces; pixels per piece
     constexpr int MP = (PY + NPW_MAX / 4 + WAVES - 1) / WAVES;
@@ -344,7 +346,8 @@ __global__ __launch_bounds__(OB * 4, 1) void wgrad_kernel(WArgs a) {
         }
     };
 
-    const int obw = wave >> 1, ibw = wave & 1;                   // this wave's (o, i) 32 x 32 block
+    const int kg = wave / BW, lw = wave % BW;
+    const int obw = lw >> 1, ibw = lw & 1;                       // this wave's (o, i) 32 x 32 block
     floatx16 acc[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k)
@@ -363,7 +366,8 @@ __global__ __launch_bounds__(OB * 4, 1) void wgrad_kernel(WArgs a) {
         const uint8_t* ximg = yimg + YIMG;
         const int p0 = c * WG_CHUNK, g0 = p0 / a.Wo, w0 = p0 - g0 * a.Wo;
 #pragma unroll
-        for (int s = 0; s < WG_CHUNK / 16; ++s) {
+        for (int s2 = 0; s2 < WG_CHUNK / 16 / KG; ++s2) {
+            const int s = kg * (WG_CHUNK / 16 / KG) + s2;
             int ry_[2], rx_[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(OB * 4, 1) void wgrad_kernel(WArgs a) {
     // partial tiles: acc[kw] register 4 q + e = row o = OB ob + 32 obw + 8 q + 4 (lane >> 5) + e, column
     // i = 64 ib + 32 ibw + (lane & 31)
     const float sc = __builtin_ldexpf(1.f, -(split_exp(*a.xmax) + split_exp(*a.dymax)));
-    float* pp = a.part + ((int64_t)r * 9 + kh * 3) * a.Co * a.Ci;
+    float* pp = a.part + ((int64_t)(r * KG + kg) * 9 + kh * 3) * a.Co * a.Ci;
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
@@ -559,7 +563,7 @@ static int wg_setup(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, i
 int64_t avse_sconv_wgrad_workspace_bytes(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride) {
     WArgs a;
     if (wg_setup(N, Hi, Wi, ci, co, stride, a) != AVSE_OK) return -1;
-    return (int64_t)a.ranges * 9 * co * ci * 4;
+    return (int64_t)a.ranges * (co % 128 ? 2 : 1) * 9 * co * ci * 4;      // KG partial slabs per range
 }
 
 int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride, const void* xq,
@@ -575,7 +579,7 @@ int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, 
     a.dymax = dymax;
     a.part = workspace;
     const bool ob128 = co % 128 == 0;
-    const dim3 grid((unsigned)(a.ranges * 3 * a.nob * a.nib)), block(ob128 ? 512 : 256);
+    const dim3 grid((unsigned)(a.ranges * 3 * a.nob * a.nib)), block(512);
     hipStream_t st = (hipStream_t)stream;
     if (ob128) {
         if (stride == 1) hipLaunchKernelGGL((wgrad_kernel<1, 128>), grid, block, 0, st, a);
@@ -587,7 +591,7 @@ int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, 
     AVSE_CHECK_LAUNCH();
     const int64_t total = 9 * co * ci;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0,
-                       st, a.part, a.ranges, (int)co, (int)ci, dw);
+                       st, a.part, a.ranges * (ob128 ? 1 : 2), (int)co, (int)ci, dw);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
