@@ -541,6 +541,43 @@ def dconv_wgrad16(xs, dys, shape, dilation, bias_grad=False):
     return (dw, db) if bias_grad else dw
 
 
+# ------------------------------------------------------------------------ AudioFeatNet.conv1 (1 -> 64, 5x5)
+
+def conv1_fwd(x, w, b=None):
+    """conv2d(x, w, b, padding=2) for x (N, 1, H, W) fp32 contiguous, w (64, 1, 5, 5) (csrc/conv1.hip) -> (N, 64, H, W)
+    in channels-last memory."""
+    _need_gpu(x, w, b)
+    n, _, h, wd = x.shape
+    y = torch.empty((n, 64, h, wd), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+    tap = _tap_begin("avse_conv1_fwd", x.device)
+    check(_lib.lib().avse_conv1_fwd(n, h, wd, ptr(x.contiguous()), ptr(w.float().contiguous()),
+                                    ptr(None if b is None else b.float().contiguous()), ptr(y), stream_ptr(x.device)),
+          "avse_conv1_fwd")
+    _tap_end(tap)
+    return y
+
+
+def conv1_bwd(x, w, dy, need_dx=True, need_dw=True):
+    """(dx (N, 1, H, W) or None, dW (64, 1, 5, 5) or None, db (64) or None) of conv1_fwd from its input x and the
+    output gradient dy (N, 64, H, W) (read as channels-last memory)."""
+    _need_gpu(x, w, dy)
+    n, _, h, wd = x.shape
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    L = _lib.lib()
+    dx = dw = db = None
+    if need_dx:
+        dx = torch.empty((n, 1, h, wd), device=x.device, dtype=torch.float32)
+        check(L.avse_conv1_dgrad(n, h, wd, ptr(dy), ptr(w.float().contiguous()), ptr(dx), stream_ptr(x.device)),
+              "avse_conv1_dgrad")
+    if need_dw:
+        dw = torch.empty((64, 1, 5, 5), device=x.device, dtype=torch.float32)
+        db = torch.empty(64, device=x.device, dtype=torch.float32)
+        ws = torch.empty((L.avse_conv1_wgrad_workspace_bytes(n, h, wd) + 3) // 4, device=x.device, dtype=torch.float32)
+        check(L.avse_conv1_wgrad(n, h, wd, ptr(x.contiguous()), ptr(dy), ptr(dw), ptr(db), ptr(ws),
+                                 stream_ptr(x.device)), "avse_conv1_wgrad")
+    return dx, dw, db
+
+
 # ------------------------------------------------------------------------ ResNet trunk 3x3 Conv2d (split fp16 MFMA)
 
 def sconv_ok(x, cout, stride):

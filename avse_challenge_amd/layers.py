@@ -291,6 +291,10 @@ def frames_nhwc(x):
     return x.permute(0, 2, 3, 4, 1).reshape(B * T, H, W, C).permute(0, 3, 1, 2)
 
 
+# AudioFeatNet.conv1 on csrc/conv1.hip (direct HBM-streaming kernels); "0": the im2col GEMM form below
+_CONV1_HIP = os.environ.get("AVSE_CONV1_HIP", "1") == "1"
+
+
 class _Conv1Fn(torch.autograd.Function):
     """AudioFeatNet.conv1 = Conv2d(1, 64, 5, padding=2) (model.py:199-215) as GEMMs over all B·T·F pixels, writing its
     output straight into channels-last memory.  MIOpen ran this single-input-channel conv in NCHW (for C = 1 the
@@ -313,6 +317,10 @@ class _Conv1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, add_bias):
         n, _, h, ww = x.shape
+        ctx.hip = _CONV1_HIP and ww >= 128
+        if ctx.hip:                                 # csrc/conv1.hip: direct kernels, x (not the im2col rows) kept
+            ctx.save_for_backward(x, w)
+            return K.conv1_fwd(x, w, b if add_bias else None)
         a = _Conv1Fn._rows(x)
         wb = torch.cat([w.reshape(w.shape[0], 25), (b if add_bias else torch.zeros_like(b)).reshape(-1, 1)], 1)
         y = a @ wb.t()                                                                # (n h w, 64): NHWC memory
@@ -322,6 +330,11 @@ class _Conv1Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.hip:
+            x, w = ctx.saved_tensors
+            dx, dw, db = K.conv1_bwd(x, w, dy, ctx.needs_input_grad[0],
+                                     ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+            return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None, None)
         a, w = ctx.saved_tensors
         n, h, ww = ctx.shape
         cout = w.shape[0]

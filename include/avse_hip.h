@@ -420,6 +420,17 @@ int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* max
  *   avse_sconv_fwd: y (N, Ho, Wo, co) fp32, Ho = (Hi - 1) / stride + 1;
  *   avse_sconv_wgrad: dW (co, ci, 3, 3) from the split input (N, Hi, Wi, ci) and output gradient (N, Ho, Wo, co);
  *     workspace of avse_sconv_wgrad_workspace_bytes (< 0: shape not supported). */
+/* AudioFeatNet.conv1 = nn.Conv2d(1, 64, 5, padding=2) (baseline/avse1/model.py:199-215) on x (N, 1, H, W) fp32
+ * (csrc/conv1.hip): y (N, H, W, 64) NHWC fp32 = conv(x, w (64, 1, 5, 5)) + b (b may be null); dx (N, 1, H, W) from
+ * dy (N, H, W, 64); dW (64, 1, 5, 5) and db (64, may be null) from x and dy (workspace:
+ * avse_conv1_wgrad_workspace_bytes).  W >= 128 for the forward. */
+int avse_conv1_fwd(int64_t N, int64_t H, int64_t W, const float* x, const float* w, const float* b, float* y,
+                   avse_stream_t stream);
+int avse_conv1_dgrad(int64_t N, int64_t H, int64_t W, const float* dy, const float* w, float* dx, avse_stream_t stream);
+int64_t avse_conv1_wgrad_workspace_bytes(int64_t N, int64_t H, int64_t W);
+int avse_conv1_wgrad(int64_t N, int64_t H, int64_t W, const float* x, const float* dy, float* dw, float* db,
+                     float* workspace, avse_stream_t stream);
+
 int64_t avse_sconv_wprep_bytes(int64_t co, int64_t ci);
 int avse_sconv_wprep(int64_t co, int64_t ci, const float* w, int32_t transposed, void* wq, uint32_t* wmax,
                      avse_stream_t stream);

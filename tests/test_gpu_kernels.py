@@ -1185,18 +1185,20 @@ def test_frames_nhwc_transpose(shape):
     assert torch.equal(gx, gy.view(B, T, C, H, W).permute(0, 2, 1, 3, 4))
 
 
-def test_conv1_module_nhwc_vs_torch():
-    """AudioFeatNet.conv1 (DilatedConv2d(1, 64, 5, padding=2) with nhwc_out: layers._Conv1Fn on hipBLASLt) at an avse1
-    spectrogram shape: channels-last output, and output / input / weight / bias gradients vs nn.Conv2d in fp64; with
-    bias_to_bn the bias is left out of the output and its gradient is unchanged."""
+@pytest.mark.parametrize("N,H,W", [(2, 376, 257), (3, 37, 130)])
+def test_conv1_module_nhwc_vs_torch(N, H, W):
+    """AudioFeatNet.conv1 (DilatedConv2d(1, 64, 5, padding=2) with nhwc_out: layers._Conv1Fn on csrc/conv1.hip) at the
+    avse1 spectrogram shape and a ragged one (partial row tiles and 8 x 32 gradient tiles): channels-last output, and
+    output / input / weight / bias gradients vs nn.Conv2d in fp64; with bias_to_bn the bias is left out of the output
+    and its gradient is unchanged."""
     from avse_challenge_amd.layers import DilatedConv2d
     torch.manual_seed(4)
     ref = torch.nn.Conv2d(1, 64, 5, padding=2).double()
     ours = DilatedConv2d(1, 64, 5, padding=2, dilation=1).to(DEV)
     ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
     ours.nhwc_out = True
-    x = det_input((2, 1, 376, 257), 1860)
-    gy = det_input((2, 64, 376, 257), 1861)
+    x = det_input((N, 1, H, W), 1860)
+    gy = det_input((N, 64, H, W), 1861)
     xr = x.double().requires_grad_(True)
     yr = ref(xr)
     (yr * gy.double()).sum().backward()

@@ -14,9 +14,13 @@ from collections import defaultdict
 trace, steps, out = sys.argv[1], float(sys.argv[2]), sys.argv[3]
 post_out = sys.argv[4] if len(sys.argv) > 4 else None
 rows = []
+queue_of = {}
 with open(trace) as f:
     for r in csv.DictReader(f):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+        q = r.get("Stream_Id") or r.get("Queue_Id")
+        if q is not None:
+            queue_of[rows[-1]] = q
 rows.sort()
 marks = [i for i, r in enumerate(rows) if "spin_kernel" in r[2]]
 if len(marks) < 2:
@@ -46,3 +50,30 @@ if roof_out and len(marks) >= 4:
     write_stats(rows[marks[2] + 1:marks[3]], roof_out)
 print(f"timed window: {span / 1e6:.2f} ms wall, {tot / 1e6:.2f} ms kernel busy "
       f"({tot / 1e6 / steps:.2f} ms/step over {steps:g} steps, {len(win)} launches)")
+
+
+def union_ns(iv):
+    """total length of the union of [s, e) intervals"""
+    tot, cur_s, cur_e = 0, None, None
+    for s_, e_ in sorted(iv):
+        if cur_e is None or s_ > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = s_, e_
+        else:
+            cur_e = max(cur_e, e_)
+    if cur_e is not None:
+        tot += cur_e - cur_s
+    return tot
+
+
+if queue_of:
+    # per stream / queue: the union of its kernels' intervals in the timed window (the branch with the most busy time
+    # bounds the step when the branches overlap); all streams together: the GPU's busy union
+    per = defaultdict(list)
+    for r in win:
+        per[queue_of.get(r, "?")].append((r[0], r[1]))
+    allb = union_ns([(r[0], r[1]) for r in win])
+    print(f"busy union of all streams: {allb / 1e6 / steps:.2f} ms/step (wall {span / 1e6 / steps:.2f})")
+    for q, iv in sorted(per.items(), key=lambda kv: -union_ns(kv[1])):
+        print(f"  stream/queue {q}: {union_ns(iv) / 1e6 / steps:.2f} ms/step busy, {len(iv) / steps:.0f} launches/step")
