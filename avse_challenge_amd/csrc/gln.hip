@@ -11,6 +11,8 @@
 // finalize kernels reduce (deterministic, double accumulation across rows).  Statistics use sums
 // shifted by the sample's first element, which removes the E[x^2]-E[x]^2 cancellation.
 // HBM: fwd = 2 reads + 1 write of x, bwd = 2 reads of (x, dy) + 1 write of dx.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace avse {
@@ -634,13 +636,19 @@ __global__ void dw_tail_kernel(const float* __restrict__ ws_dw, const float2* __
 
 using namespace avse::gln;
 
-// Samples per launch pair of a two-pass kernel: the group's inputs of the first pass (bytes_per_sample) stay within
-// 64 MiB, so the second pass re-reads them from the 256 MiB Infinity Cache instead of HBM (with every sample in one
-// launch, C4's 262 MB of (x, dy) had left the cache by the time the second pass reached it: PMC 1.67x the algorithmic
-// bytes, profiles/r04_traffic.json).  The passes' own bytes in between (the first pass's reads, the second's writes)
-// stay inside the cache's reuse window (MI355X_MICROARCH.md 'Infinity Cache').
+// Samples per launch pair of a two-pass kernel.  Grouping the samples so that a group's first-pass inputs stay within
+// the 256 MiB Infinity Cache for the second pass (AVSE_GLN_GROUP_MB=64: PMC traffic of C4's prelu_gln_bwd was 1.67x the
+// algorithmic bytes with one launch, profiles/r04_traffic.json) measured SLOWER in isolation: C4 dwconv_gln fwd
+// 0.095 -> 0.136 ms, prelu_gln_bwd 0.131 -> 0.151 ms (profiles/r05k: the serialised launch pairs and their tails cost
+// more than the re-reads), so the default is one launch pair over all samples.
 static int64_t group_samples(int64_t B, int64_t bytes_per_sample) {
-    const int64_t cap = (64LL << 20) / (bytes_per_sample > 0 ? bytes_per_sample : 1);
+    static int64_t mb = -1;
+    if (mb < 0) {
+        const char* e = getenv("AVSE_GLN_GROUP_MB");
+        mb = e ? atoll(e) : 0;
+    }
+    if (mb <= 0) return B;
+    const int64_t cap = (mb << 20) / (bytes_per_sample > 0 ? bytes_per_sample : 1);
     return cap < 1 ? 1 : (cap > B ? B : cap);
 }
 
