@@ -419,6 +419,8 @@ class AVMambaStep:
         from avse_challenge_amd import avmamba, data
         self.B, self.size = B, size
         self.model = avmamba.AVMambaTasNet(**avmamba.AV_MAMBA_SIZES[size]).to(dev).train()
+        if int(os.environ.get("AVSE_LIP_CHANNELS_LAST", "1")):  # NHWC lip ResNet: 3x3 convs on csrc/sconv.hip
+            self.model.visual_frontend.use_channels_last()
         self.lr, self.clip = 1.5e-4, 5.0
         g = torch.Generator(device=dev).manual_seed(999 + rank)
         noisy, clean, _ = data.avse1_batch(B, dev, 999 + rank, lip_hw=8)
