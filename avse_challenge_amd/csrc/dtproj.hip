@@ -16,12 +16,14 @@
 //   - fp32 operands: the split of dconv.hip / projgemm.hip with per-TILE power-of-two scales (the tile's x slab and
 //     W rows are in LDS anyway): hi = fp16(v 2^e), lo = fp16(v 2^e - hi), products hi*hi + hi*lo + lo*hi on the f16
 //     MFMA, scaled back by 2^-(e_x + e_w) (22-bit operands: the fp32 class).
-// Workgroup = 64 channels x 256 steps of one batch row, 4 waves of 64 channels x 64 steps (2 x 2 MFMA blocks, the
-// steps as the MFMA rows: each lane stores 4 consecutive steps of one channel).  x rows
+// Workgroup = 64 channels x 256 steps of one batch row, 4 waves of 64 channels x 64 steps (2 x 2 MFMA blocks); the
+// output tile goes out through LDS in 1-KB coalesced rows (stores straight from the accumulators -- 32-B runs per
+// row -- ran the C3 call at 0.60 ms against 0.48 for the VALU version).  x rows
 // [0, R) x 256 steps are staged in LDS as 16-bit k-rows of 512 B (16-B chunk c of k-row r at c ^ ((r & 3) << 2),
 // fragments by ds_read_b64_tr_b16), W's 64 rows as R-long 16-bit rows padded by 16 B (conflict-free 16-B reads).
 // The workgroups of one x slab (its D / 64 channel tiles) are consecutive, so the slab is re-read from L2.
 // bias + softplus in the epilogue; the bf16 output is rounded once.
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -216,15 +218,13 @@ __global__ __launch_bounds__(THREADS) void dtproj_kernel(Args a) {
     }
     __syncthreads();
 
-    // C[t][d] = sum_r x[r][t] W[d][r]: the steps are the MFMA rows, so each lane ends with 4 consecutive steps of one
-    // channel (one 16-B / 8-B store per 4 outputs)
-    floatx16 acc[2][2];                                       // [t block j][channel block i]
+    floatx16 acc[2][2];                                       // [channel block i][step block j]
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
     const int tc = 64 * wave;                                 // this wave's steps tc .. tc + 63 of the tile
     for (int s = 0; s < a.RP / 16; ++s) {
         half8 wh[2], xh[2], wl[2], xl[2];
@@ -241,61 +241,71 @@ __global__ __launch_bounds__(THREADS) void dtproj_kernel(Args a) {
 #pragma unroll
         for (int pr = 0; pr < (F32 ? 3 : 1); ++pr)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
+                for (int j = 0; j < 2; ++j) {
                     if constexpr (F32) {
-                        acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr == 2 ? xl[j] : xh[j], pr == 1 ? wl[i] : wh[i],
-                                                                           acc[j][i], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr == 2 ? wl[i] : wh[i], pr == 1 ? xl[j] : xh[j],
+                                                                           acc[i][j], 0, 0, 0);
                     } else {
-                        acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, xh[j]),
-                                                                            __builtin_bit_cast(bf16x8, wh[i]), acc[j][i],
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wh[i]),
+                                                                            __builtin_bit_cast(bf16x8, xh[j]), acc[i][j],
                                                                             0, 0, 0);
                     }
                 }
     }
 
-    // epilogue: acc[j][i] register 4 g + e = step t0 + tc + 32 j + 8 g + 4 (lane >> 5) + e, channel d0 + 32 i +
-    // (lane & 31)
+    // epilogue through LDS, 32 channels at a time: acc[i][j] register 4 g + e = channel d0 + 32 i + 8 g + 4 (lane >> 5)
+    // + e, step t0 + tc + 32 j + (lane & 31) -> ot[channel][step] (rows padded by 4 floats: the two half-waves' rows
+    // land on different banks), then every thread stores whole 16-B pieces of 32 rows x 256 steps (1 KB per wave
+    // instruction, coalesced): the output is the kernel's bytes
+    float* ot = reinterpret_cast<float*>(lds);                // [32][OS]
+    constexpr int OS = TT + 4;
     T* ob = reinterpret_cast<T*>(a.out) + (int64_t)b * a.o_bs;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        const int d = d0 + 32 * i + (lane & 31);
-        if (d >= a.D) continue;
-        const float bv = a.bias ? a.bias[d] : 0.f;
-        T* orow = ob + (int64_t)d * a.o_ds;
+        __syncthreads();                                      // the images / the previous half's reads are done
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int g = 0; g < 4; ++g)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int t = t0 + tc + 32 * j + 8 * g + 4 * (lane >> 5);
-                if (t >= a.L) continue;
-                float v[4];
+            for (int e = 0; e < 4; ++e) {
+                const int dl = 8 * g + 4 * (lane >> 5) + e, d = d0 + 32 * i + dl;
+                const float bv = (a.bias && d < a.D) ? a.bias[d] : 0.f;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    v[e] = acc[j][i][4 * g + e] * unscale + bv;
-                    if (a.softplus) v[e] = softplus2(v[e]);
+                for (int j = 0; j < 2; ++j) {
+                    float v = acc[i][j][4 * g + e] * unscale + bv;
+                    if (a.softplus) v = softplus2(v);
+                    ot[dl * OS + tc + 32 * j + (lane & 31)] = v;
                 }
-                T* o = orow + t;
-                if constexpr (F32) {
-                    if (t + 3 < a.L && ((uintptr_t)o & 15) == 0) {
-                        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-                        continue;
-                    }
-                } else {
-                    if (t + 3 < a.L && ((uintptr_t)o & 7) == 0) {
-                        bf16_t h[4];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) io<bf16_t>::st(&h[e], v[e]);
-                        *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)h[0].x | ((uint32_t)h[1].x << 16),
-                                                                  (uint32_t)h[2].x | ((uint32_t)h[3].x << 16));
-                        continue;
-                    }
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (t + e < a.L) io<T>::st(o + e, v[e]);
             }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 32 * TT / 4 / THREADS; ++k) {
+            const int idx = tid + k * THREADS, row = idx / (TT / 4), c4 = idx % (TT / 4);
+            const int d = d0 + 32 * i + row, t = t0 + 4 * c4;
+            if (d >= a.D || t >= a.L) continue;
+            const float4 v4 = *reinterpret_cast<const float4*>(&ot[row * OS + 4 * c4]);
+            T* o = ob + (int64_t)d * a.o_ds + t;
+            const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+            if constexpr (F32) {
+                if (t + 3 < a.L && ((uintptr_t)o & 15) == 0) {
+                    *reinterpret_cast<float4*>(o) = v4;
+                    continue;
+                }
+            } else {
+                if (t + 3 < a.L && ((uintptr_t)o & 7) == 0) {
+                    bf16_t h[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) io<bf16_t>::st(&h[e], v[e]);
+                    *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)h[0].x | ((uint32_t)h[1].x << 16),
+                                                              (uint32_t)h[2].x | ((uint32_t)h[3].x << 16));
+                    continue;
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (t + e < a.L) io<T>::st(o + e, v[e]);
+        }
     }
 }
 
@@ -338,7 +348,8 @@ int avse_dtproj(int64_t batch, int64_t dim, int64_t rank, int64_t seqlen, int32_
     const int64_t nblocks = batch * a.nt * a.nd;
     if (nblocks >= (1LL << 31)) return AVSE_ESHAPE;
     const int npl = dtype == AVSE_F32 ? 2 : 1;
-    const size_t lds = (size_t)npl * (a.RP * 512 + CH * (2 * a.RP + 16));
+    // the operand images, later the 32 x (256 + 4)-float output staging
+    const size_t lds = std::max<size_t>((size_t)npl * (a.RP * 512 + CH * (2 * a.RP + 16)), (size_t)32 * (TT + 4) * 4);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == AVSE_F32)
         hipLaunchKernelGGL(dtproj_kernel<float>, dim3((unsigned)nblocks), dim3(THREADS), lds, st, a);
