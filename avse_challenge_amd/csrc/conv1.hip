@@ -120,33 +120,38 @@ __global__ __launch_bounds__(DT) void dgrad_kernel(int N, int H, int W, int rblo
 // ------------------------------------------------------------------------------------------------ weight gradient
 constexpr int WT = 256, WROWS = 4;             // threads; image rows per workgroup
 
+// a bounded grid of workgroups, each looping over row blocks (N H / WROWS of them) with its accumulators in registers:
+// few partials to reduce (3008 per-row-block partials summed serially took 1.6 ms at avse1 C2)
 __global__ __launch_bounds__(WT) void wgrad_kernel(int N, int H, int W, int rblocks, const float* __restrict__ x,
                                                    const float* __restrict__ dy, float* __restrict__ part) {
     extern __shared__ float xs[];              // [WROWS + 4][W + 4]
-    const int bid = blockIdx.x;
-    const int n = bid / rblocks, h0 = (bid % rblocks) * WROWS;
     const int WP = W + 4, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const float* xn = x + (int64_t)n * H * W;
-    for (int i = threadIdx.x; i < (WROWS + 4) * WP; i += WT) {
-        const int rr = i / WP, cc = i % WP;
-        const int hi = h0 - PAD + rr, wi = cc - PAD;
-        xs[i] = (hi >= 0 && hi < H && wi >= 0 && wi < W) ? xn[hi * W + wi] : 0.f;
-    }
-    __syncthreads();
-    // lane = output channel; wave w takes the pixels w, w + 4, ... of the workgroup's rows
     float acc[TAPS + 1];
 #pragma unroll
     for (int t = 0; t <= TAPS; ++t) acc[t] = 0.f;
-    const int np = min(WROWS, H - h0) * W;
-    for (int i = wave; i < np; i += WT / 64) {
-        const int r = i / W, c = i % W;
-        const float g = dy[(((int64_t)n * H + h0 + r) * W + c) * CO + lane];
+    for (int rb = blockIdx.x; rb < N * rblocks; rb += gridDim.x) {
+        const int n = rb / rblocks, h0 = (rb % rblocks) * WROWS;
+        const float* xn = x + (int64_t)n * H * W;
+        __syncthreads();                       // the previous row block's tile reads are done
+        for (int i = threadIdx.x; i < (WROWS + 4) * WP; i += WT) {
+            const int rr = i / WP, cc = i % WP;
+            const int hi = h0 - PAD + rr, wi = cc - PAD;
+            xs[i] = (hi >= 0 && hi < H && wi >= 0 && wi < W) ? xn[hi * W + wi] : 0.f;
+        }
+        __syncthreads();
+        // lane = output channel; wave w takes the pixels w, w + 4, ... of the row block
+        const int np = min(WROWS, H - h0) * W;
+        for (int i = wave; i < np; i += WT / 64) {
+            const int r = i / W, c = i % W;
+            const float g = dy[(((int64_t)n * H + h0 + r) * W + c) * CO + lane];
 #pragma unroll
-        for (int kh = 0; kh < KS; ++kh)
+            for (int kh = 0; kh < KS; ++kh)
 #pragma unroll
-            for (int kw = 0; kw < KS; ++kw) acc[kh * KS + kw] = fmaf(g, xs[(r + kh) * WP + c + kw], acc[kh * KS + kw]);
-        acc[TAPS] += g;
+                for (int kw = 0; kw < KS; ++kw) acc[kh * KS + kw] = fmaf(g, xs[(r + kh) * WP + c + kw], acc[kh * KS + kw]);
+            acc[TAPS] += g;
+        }
     }
+    const int bid = blockIdx.x;
     // the 4 waves' partials through LDS (after every wave has finished reading the x tile)
     __syncthreads();
     float* red = xs;                           // [4][26][64]
@@ -158,16 +163,23 @@ __global__ __launch_bounds__(WT) void wgrad_kernel(int N, int H, int W, int rblo
                                                    red[3 * (TAPS + 1) * CO + i];
 }
 
-// dW[o][t] (= W's (64, 1, 5, 5) layout), db[o]: sum of the workgroups' partials [blk][t][o] in a fixed order
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int blocks, float* __restrict__ dw,
-                                    float* __restrict__ db) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;        // i = t * 64 + o
-    if (i >= (TAPS + 1) * CO) return;
+// dW[o][t] (= W's (64, 1, 5, 5) layout), db[o]: sum of the workgroups' partials [blk][t][o]; one workgroup per
+// output, its threads over the partials, then a fixed tree (deterministic)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int blocks,
+                                                           float* __restrict__ dw, float* __restrict__ db) {
+    __shared__ float red[4];
+    const int i = blockIdx.x;                                   // i = t * 64 + o
     float s = 0.f;
-    for (int k = 0; k < blocks; ++k) s += part[(int64_t)k * (TAPS + 1) * CO + i];
-    const int t = i / CO, o = i % CO;
-    if (t < TAPS) dw[o * TAPS + t] = s;
-    else if (db) db[o] = s;
+    for (int k = threadIdx.x; k < blocks; k += 256) s += part[(int64_t)k * (TAPS + 1) * CO + i];
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s = (red[0] + red[1]) + (red[2] + red[3]);
+        const int t = i / CO, o = i % CO;
+        if (t < TAPS) dw[o * TAPS + t] = s;
+        else if (db) db[o] = s;
+    }
 }
 
 }  // namespace cv1
@@ -203,9 +215,11 @@ int avse_conv1_dgrad(int64_t N, int64_t H, int64_t W, const float* dy, const flo
     return AVSE_OK;
 }
 
+constexpr int WG_GRID = 512;
+
 int64_t avse_conv1_wgrad_workspace_bytes(int64_t N, int64_t H, int64_t W) {
     (void)W;
-    return N * ((H + WROWS - 1) / WROWS) * (TAPS + 1) * CO * 4;
+    return std::min<int64_t>(N * ((H + WROWS - 1) / WROWS), WG_GRID) * (TAPS + 1) * CO * 4;
 }
 
 int avse_conv1_wgrad(int64_t N, int64_t H, int64_t W, const float* x, const float* dy, float* dw, float* db,
@@ -213,16 +227,15 @@ int avse_conv1_wgrad(int64_t N, int64_t H, int64_t W, const float* x, const floa
     if (!x || !dy || !dw || !workspace) return AVSE_EINVAL;
     if (N <= 0 || H <= 0 || W <= 0 || W > 4096) return AVSE_ESHAPE;
     const int rblocks = (int)((H + WROWS - 1) / WROWS);
-    const int64_t blocks = N * rblocks;
-    if (blocks >= (1LL << 31)) return AVSE_ESHAPE;
+    if (N * rblocks >= (1LL << 31)) return AVSE_ESHAPE;
+    const int64_t blocks = std::min<int64_t>(N * rblocks, WG_GRID);
     // LDS: the x tile, reused for the 4 x 26 x 64 wave partials
     const size_t lds = std::max<size_t>((size_t)(WROWS + 4) * (W + 4), (size_t)4 * (TAPS + 1) * CO) * 4;
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)blocks), dim3(WT), lds, st, (int)N, (int)H, (int)W, rblocks, x, dy,
                        workspace);
     AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(((TAPS + 1) * CO + 255) / 256), dim3(256), 0, st, workspace, (int)blocks,
-                       dw, db);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((TAPS + 1) * CO), dim3(256), 0, st, workspace, (int)blocks, dw, db);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

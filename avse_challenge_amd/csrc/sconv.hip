@@ -409,12 +409,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WArgs a) {
             }
 }
 
-// dW[o][i][kh][kw] = sum over ranges of part[range][kh][kw][o][i]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int ranges, int Co, int Ci, float* __restrict__ dw) {
+// dW[o][i][kh][kw] = sum over ranges of part[range][kh][kw][o][i]: workgroup = 64 consecutive elements x 4 range
+// slices (coalesced 256-B reads per slice and range), the slices combined in a fixed order (deterministic)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int ranges, int Co, int Ci,
+                                                           float* __restrict__ dw) {
+    __shared__ float red[4][64];
     const int64_t total = (int64_t)9 * Co * Ci;
-    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
-        float v = 0.f;
-        for (int g = 0; g < ranges; ++g) v += part[(int64_t)g * total + idx];
+    const int64_t idx = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int sl = threadIdx.x >> 6;
+    float v = 0.f;
+    if (idx < total)
+        for (int g = sl; g < ranges; g += 4) v += part[(int64_t)g * total + idx];
+    red[sl][threadIdx.x & 63] = v;
+    __syncthreads();
+    if (sl == 0 && idx < total) {
+        v = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
         const int i = (int)(idx % Ci), o = (int)((idx / Ci) % Co), tap = (int)(idx / ((int64_t)Ci * Co));
         dw[((int64_t)o * Ci + i) * 9 + tap] = v;
     }
@@ -590,8 +599,8 @@ int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, 
     }
     AVSE_CHECK_LAUNCH();
     const int64_t total = 9 * co * ci;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0,
-                       st, a.part, a.ranges * (ob128 ? 1 : 2), (int)co, (int)ci, dw);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, a.part,
+                       a.ranges * (ob128 ? 1 : 2), (int)co, (int)ci, dw);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
