@@ -16,6 +16,10 @@
 // the 2 planes' input window (2 * 7 + 7 rows x 101 columns, zero outside the frame / clip) is staged in LDS with even
 // and odd columns in separate arrays (the stride-2 pixel walk becomes unit stride: no bank conflicts), and the
 // pair's weights as [tap][plane][co]; the next pair is loaded into registers while the current one's MFMAs run.
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 
 namespace avse {
@@ -167,11 +171,247 @@ __global__ __launch_bounds__(THREADS, 2) void fwd_kernel(int B, int TT, const T*
     }
 }
 
+// ------------------------------------------------------------------------------------------------ uint8 lips on f16
+// uint8 frames are exact in fp16, so the products need only the weights split: W 2^e = hi + lo (fp16 each, 22 bits;
+// max |W| 2^e in [2^14, 2^15)), y = 2^-e (x hi + x lo) on v_mfma_f32_32x32x16_f16 -- 2 MFMAs per product against
+// 1/16-rate fp32 MFMAs, fp32-accurate (x exact, W to 22 bits, fp32 accumulation).
+// K per input plane (ci, kt): 8 kernel rows (7 + a zero row) x 8 columns (7 + a zero column) = 4 k16-steps; k-step s,
+// lane half h = kernel row 2 s + h, the lane's 8 k = kernel columns 0..7 = input columns 2 wo - 3 .. 2 wo + 4 of input
+// row 2 ho + kh - 3: 8 consecutive fp16 of the staged row, two 8-B reads from one of two copies of the row (copy 0
+// starts at column -3, copy 1 at column -1, so that either wo parity reads 8-B aligned words).
+constexpr int F16_KSTEPS = 4;                    // k16-steps per plane
+constexpr int WB_HALF = F16_KSTEPS * COUT * 16 * 2;   // bytes of one plane's hi (or lo) weights
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+
+// W (64, NPL, 5*... flattened to (64, NPL, 7, 7)) -> wq[pl][s][co][16] hi, then lo (same layout), scaled by 2^e
+__global__ void wmax16_kernel(const float* __restrict__ w, int n, uint32_t* __restrict__ mb) {
+    float m = 0.f;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
+    uint32_t b = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
+    __shared__ uint32_t red[16];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) b = max(b, red[k]);
+        *mb = b;
+    }
+}
+
+typedef int i4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ inline i4_t rsrc16(const void* base, int64_t bytes) {
+    if (bytes > 0x7FFFFFF0LL) bytes = 0x7FFFFFF0LL;
+    const uint64_t a = (uint64_t)base;
+    return i4_t{__builtin_amdgcn_readfirstlane((int)(uint32_t)a), __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff)),
+                __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
+// one 16-B-per-lane LDS-DMA wave-instruction (inline asm: the builtin makes the compiler wait vmcnt(0) before every
+// ds_read of the array).  Nothing else in this kernel uses M0.
+__device__ inline void dma16(i4_t r, uint32_t lds_addr, uint32_t voff) {
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(lds_addr)
+                 : "memory");
+}
+
+__device__ inline int split_exp16(uint32_t mb) {
+    const int ef = (int)((mb >> 23) & 0xff);
+    if (mb == 0) return 0;
+    const int k = ef == 0 ? -127 : ef - 127;
+    return min(100, max(-100, 14 - k));
+}
+
+__global__ void wprep16_kernel(const float* __restrict__ w, int npl, const uint32_t* __restrict__ mb,
+                               uint16_t* __restrict__ wq) {
+    const int n = npl * F16_KSTEPS * COUT * 16;
+    const float sc = __builtin_ldexpf(1.f, split_exp16(*mb));
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int k = i % 16, co = (i / 16) % COUT, st = (i / (16 * COUT)) % F16_KSTEPS, pl = i / (16 * COUT * F16_KSTEPS);
+        const int kh = 2 * st + k / 8, kw = k % 8;
+        const float v = (kh < KH && kw < KW) ? w[(((int64_t)co * npl + pl) * KH + kh) * KW + kw] * sc : 0.f;
+        const _Float16 hi = (_Float16)v, lo = (_Float16)(v - (float)hi);
+        wq[i] = __builtin_bit_cast(uint16_t, hi);
+        wq[n + i] = __builtin_bit_cast(uint16_t, lo);
+    }
+}
+
+template <int CIN, int H, int W>
+struct Geo16 {
+    using G = Geo<CIN, H, W>;
+    static constexpr int RC = ((G::IC + 2 + 3) / 4) * 4;          // staged fp16 per row copy (columns -3 .. IC - 3 + 2)
+    static constexpr int IRS = G::IR + 1;                         // staged rows: + a zero row for kernel row 7
+    static constexpr int XB = 2 * IRS * RC * 2;                   // bytes: 2 copies x IRS rows
+    static constexpr int WB = F16_KSTEPS * COUT * 16 * 2 * 2;    // hi + lo
+    static constexpr int STG = ((XB + 15) / 16) * 16 + WB;
+    static constexpr int XPT = (G::IR * G::IC + THREADS - 1) / THREADS;
+};
+
+template <int CIN, int H, int W>
+__global__ __launch_bounds__(THREADS, 2) void fwd16_kernel(int B, int TT, const uint8_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ wq, const uint32_t* __restrict__ mb,
+                                                           float* __restrict__ y) {
+    using G = Geo<CIN, H, W>;
+    using G16 = Geo16<CIN, H, W>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * G16::STG];
+    const int lane = threadIdx.x & 63, half = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = bid % G::NT, bt = bid / G::NT;
+    const int t = bt % TT, b = bt / TT;
+    const int p0 = tile * TILE_PX;
+    const int r0 = p0 / G::WO;
+    const int hi0 = 2 * r0 - PH;
+    const int64_t nx = (int64_t)B * CIN * TT * H * W;
+    const auto rx = make_rsrc(x, nx);
+    const int OOB = (int)nx;
+
+    // B-operand byte offsets (without the k-step row) per pixel tile: copy (wo & 1), row 2 (ho - r0), the word of
+    // column 2 wo - 3
+    int boff[TILES_PER_WAVE];
+#pragma unroll
+    for (int j = 0; j < TILES_PER_WAVE; ++j) {
+        int p = p0 + (wave * TILES_PER_WAVE + j) * 32 + (lane & 31);
+        if (p >= G::PLANE_PX) p = p0;
+        const int ho = p / G::WO, wo = p % G::WO;
+        const int cp = wo & 1;                                    // copy 1 starts 2 columns later
+        boff[j] = ((cp * G16::IRS + 2 * (ho - r0)) * G16::RC + (2 * wo - 2 * cp)) * 2;
+    }
+    uint32_t xr[G16::XPT];
+    const i4_t rwq = rsrc16(wq, (int64_t)2 * G::NPL * WB_HALF);
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_void_t*)lds);
+    constexpr int WOFF = ((G16::XB + 15) / 16) * 16;            // the weight image inside a stage buffer
+    // x of plane pl into registers; its weights (hi 8 KB, lo 8 KB) by LDS-DMA straight into buffer buf (free: its
+    // last readers passed the barrier before this call)
+    auto prefetch = [&](int pl, int buf) {
+        const int ci = pl / KT, kt = pl % KT, ti = t + kt - PT;
+#pragma unroll
+        for (int i = 0; i < G16::XPT; ++i) {
+            const int e = threadIdx.x + i * THREADS;
+            const int c = e % G::IC, row = e / G::IC;
+            const int hi = hi0 + row, wi = c - PW;
+            const bool ok = e < G::IR * G::IC && ti >= 0 && ti < TT && hi >= 0 && hi < H && wi >= 0 && wi < W;
+            xr[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rx, ok ? (((b * CIN + ci) * TT + ti) * H + hi) * W + wi
+                                                                        : OOB, 0, 0);
+        }
+        // 16 pieces of 1 KB (wq: all planes' hi, then all planes' lo), 4 per wave
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = wave * 4 + i, hl = k / 8, kk = k % 8;
+            dma16(rwq, lds0 + buf * G16::STG + WOFF + hl * WB_HALF + kk * 1024,
+                  (uint32_t)((hl * G::NPL + pl) * WB_HALF + kk * 1024 + lane * 16));
+        }
+    };
+    auto stage = [&](int buf) {
+        uint8_t* img = lds + buf * G16::STG;
+        _Float16* xs = reinterpret_cast<_Float16*>(img);
+#pragma unroll
+        for (int i = 0; i < G16::XPT; ++i) {
+            const int e = threadIdx.x + i * THREADS;
+            if (e < G::IR * G::IC) {
+                const int c = e % G::IC, row = e / G::IC;
+                const _Float16 v = (_Float16)(float)xr[i];
+                xs[row * G16::RC + c] = v;                                      // copy 0: column c - 3 at c
+                if (c >= 2) xs[(G16::IRS + row) * G16::RC + c - 2] = v;         // copy 1: column c - 3 at c - 2
+            }
+        }
+        // zeros: each copy's columns past the window (read by the zero-weight 8th kernel column) and the zero row
+        // IR of both copies (the zero-weight 8th kernel row): NaN-free operands for the padded k
+        for (int i = threadIdx.x; i < 2 * G16::IRS * 8; i += THREADS) {
+            const int cp = i / (G16::IRS * 8), row = (i / 8) % G16::IRS, k = i % 8;
+            const int c0 = cp ? G::IC - 2 : G::IC;
+            if (row == G::IR) {
+                for (int c = k; c < G16::RC; c += 8) xs[(cp * G16::IRS + row) * G16::RC + c] = (_Float16)0.f;
+            } else if (c0 + k < G16::RC) {
+                xs[(cp * G16::IRS + row) * G16::RC + c0 + k] = (_Float16)0.f;
+            }
+        }
+    };
+
+    floatx16 acc[2][TILES_PER_WAVE];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int j = 0; j < TILES_PER_WAVE; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][j][r] = 0.f;
+
+    prefetch(0, 0);
+    for (int pl = 0; pl < G::NPL; ++pl) {
+        const int buf = pl & 1;
+        stage(buf);                                 // the buffer last read two planes ago (a barrier in between)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's weight pieces of plane pl have landed
+        __syncthreads();
+        if (pl + 1 < G::NPL) prefetch(pl + 1, buf ^ 1);
+        const uint8_t* img = lds + buf * G16::STG;
+        const uint8_t* wimg = img + ((G16::XB + 15) / 16) * 16;
+#pragma unroll
+        for (int st = 0; st < F16_KSTEPS; ++st) {
+            half8 ah[2], al[2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const int co = 32 * m + (lane & 31);
+                ah[m] = *reinterpret_cast<const half8*>(wimg + ((st * COUT + co) * 16 + 8 * half) * 2);
+                al[m] = *reinterpret_cast<const half8*>(wimg + WB_HALF + ((st * COUT + co) * 16 + 8 * half) * 2);
+            }
+            const int rowb = (2 * st + half) * G16::RC * 2;       // kernel row 2 st + half
+#pragma unroll
+            for (int j = 0; j < TILES_PER_WAVE; ++j) {
+                const uint8_t* p = img + boff[j] + rowb;
+                const half4 v0 = *reinterpret_cast<const half4*>(p);
+                const half4 v1 = *reinterpret_cast<const half4*>(p + 8);
+                const half8 bv = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bv, acc[m][j], 0, 0, 0);
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bv, acc[m][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+    const float unscale = __builtin_ldexpf(1.f, -split_exp16(*mb));
+    float* yb = y + ((int64_t)b * COUT * TT + t) * G::PLANE_PX;
+#pragma unroll
+    for (int j = 0; j < TILES_PER_WAVE; ++j) {
+        const int p = p0 + (wave * TILES_PER_WAVE + j) * 32 + (lane & 31);
+        if (p < G::PLANE_PX) {
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int co = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    yb[(int64_t)co * TT * G::PLANE_PX + p] = acc[m][j][r] * unscale;
+                }
+        }
+    }
+}
+
 template <typename T, int CIN, int H, int W>
 int launch(int64_t B, int64_t TT, const void* x, const float* w, float* y, float* workspace, hipStream_t st) {
     using G = Geo<CIN, H, W>;
     if ((int64_t)B * CIN * TT * H * W >= (1LL << 31) / (int64_t)sizeof(T)) return AVSE_ESHAPE;   // 32-bit offsets
     if (B * TT * G::NT >= (1LL << 31)) return AVSE_ESHAPE;
+    static int f16 = -1;
+    if (f16 < 0) {
+        const char* e = getenv("AVSE_C3F_F16");
+        f16 = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    if constexpr (std::is_same<T, uint8_t>::value) {
+        if (f16) {                              // uint8 lips: the f16 MFMA with split weights
+            uint16_t* wq = reinterpret_cast<uint16_t*>(workspace);
+            uint32_t* mb = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(workspace) + 2 * G::NPL * WB_HALF);
+            hipLaunchKernelGGL(wmax16_kernel, dim3(1), dim3(1024), 0, st, w, G::NPL * COUT * TAPS, mb);
+            AVSE_CHECK_LAUNCH();
+            const int n = G::NPL * F16_KSTEPS * COUT * 16;
+            hipLaunchKernelGGL(wprep16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w, G::NPL, (const uint32_t*)mb,
+                               wq);
+            AVSE_CHECK_LAUNCH();
+            hipLaunchKernelGGL((fwd16_kernel<CIN, H, W>), dim3((unsigned)(B * TT * G::NT)), dim3(THREADS), 0, st, (int)B,
+                               (int)TT, (const uint8_t*)x, (const uint16_t*)wq, (const uint32_t*)mb, y);
+            AVSE_CHECK_LAUNCH();
+            return AVSE_OK;
+        }
+    }
     const int nw = G::NQ * G::WEL;
     hipLaunchKernelGGL(prep_weights_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, w, G::NPL, G::NQ, workspace);
     AVSE_CHECK_LAUNCH();
@@ -190,7 +430,9 @@ extern "C" {
 
 // shapes compiled in: the avse1 front-end (3 x 96 x 96 lips)
 int64_t avse_conv3d_fwd_workspace_bytes(int64_t CIN, int64_t H, int64_t W) {
-    if (CIN == 3 && H == 96 && W == 96) return 4 * (int64_t)Geo<3, 96, 96>::NQ * Geo<3, 96, 96>::WEL;
+    if (CIN == 3 && H == 96 && W == 96)
+        return std::max<int64_t>(4 * (int64_t)Geo<3, 96, 96>::NQ * Geo<3, 96, 96>::WEL,
+                                 2 * (int64_t)Geo<3, 96, 96>::NPL * WB_HALF + 16);
     return 0;
 }
 

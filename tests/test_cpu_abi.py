@@ -60,7 +60,8 @@ def test_host_side_validation_without_gpu():
     assert L.avse_dconv_wgrad(2, 10, 257, 17, dummy, dummy, dummy, dummy, dummy, None) == -2
     assert L.avse_dconv_wgrad_workspace_bytes(32, 376, 257, 16) % (4 * (25 * 64 * 64 + 64)) == 0
     # lip Conv3d forward: compiled shape table, null pointers, unsupported shape / dtype
-    assert L.avse_conv3d_fwd_workspace_bytes(3, 96, 96) == 4 * 8 * 49 * 2 * 64
+    # the fp32 path's prepped weights, or the f16 path's split weights (15 planes x 4 k-steps x 64 x 16 x hi/lo) + max
+    assert L.avse_conv3d_fwd_workspace_bytes(3, 96, 96) == max(4 * 8 * 49 * 2 * 64, 2 * 15 * 4 * 64 * 16 * 2 + 16)
     assert L.avse_conv3d_fwd_workspace_bytes(1, 88, 88) == 0
     assert L.avse_conv3d_fwd(2, 3, 75, 96, 96, 2, None, dummy, dummy, dummy, None) == -1
     assert L.avse_conv3d_fwd(2, 1, 75, 88, 88, 2, dummy, dummy, dummy, dummy, None) == -2

@@ -419,8 +419,9 @@ def test_conv3d_wgrad_uint8_equals_fp32():
 def test_conv3d_fwd_vs_fp64(dtype, T):
     """K.conv3d_fwd (csrc/conv3d_fwd.hip) vs the fp64 Conv3d(3, 64, (5,7,7), (1,2,2), (2,3,3)) of the avse1 lip
     front-end (baseline/avse1/model.py:29-34) at its 96 x 96 frames: every output within 1e-6 of its sum of |terms|
-    (one rounding per exact-f32 MFMA product-accumulate); clips of 1 .. 7 frames cover the zero time padding on
-    both sides; uint8 frames are read as stored."""
+    (fp32 frames: exact-f32 MFMA; uint8 frames, read as stored, on the f16 MFMA -- exact in fp16 -- against the
+    weights split into hi + lo fp16 (22 bits), fp32 accumulation); clips of 1 .. 7 frames cover the zero time padding
+    on both sides."""
     g = torch.Generator().manual_seed(707 + T)
     if dtype == torch.uint8:
         x = torch.randint(0, 256, (2, 3, T, 96, 96), generator=g, dtype=torch.uint8)
