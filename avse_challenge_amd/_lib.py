@@ -112,6 +112,7 @@ SIGNATURES = {
     "avse_conv3d_wgrad_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "avse_conv3d_wgrad": (c_i32, [c_i64] * 11 + [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "avse_conv3d_wgrad_u8": (c_i32, [c_i64] * 11 + [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
+    "avse_conv3d_wgrad_u8_split": (c_i32, [c_i64] * 11 + [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "avse_conv3d_fwd_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "avse_conv3d_fwd": (c_i32, [c_i64] * 5 + [c_i32] + [c_vp] * 5),
     "avse_dconv_wgrad_workspace_bytes": (c_i64, [c_i64] * 4),

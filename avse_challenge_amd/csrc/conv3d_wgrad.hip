@@ -16,6 +16,7 @@
 // then every wave runs WO/2 K-steps of 2 x NTW 32x32x2 MFMAs (M = 64 = 2 tiles, N split over waves).
 // Partial 64 x N tiles per workgroup go to a workspace; a second kernel sums them (deterministic).
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -151,6 +152,175 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(Shape s, const T* __r
         }
 }
 
+// ------------------------------------------------------------------------------------------------ uint8 frames, f16
+// The same decomposition on the f16 MFMA for uint8 frames (exact in fp16) with dY split per element into hi + lo
+// fp16 under one power-of-two scale (max |dY| 2^e in [2^14, 2^15): the producing BatchNorm -> act backward reports
+// max |dY|): dW = 2^-e (dY_hi X + dY_lo X), fp32 accumulation -- 2 MFMAs per product against 1/16-rate fp32 MFMAs.
+// Per output row (b, t, ho): K = wo in k16-steps; A = dY (64 co x 16 wo, hi / lo rows in LDS, 16-B reads); B = the
+// input columns 2 wo + kw - 3 of the staged rows: stride 2 along wo, so every staged row is kept as its two column
+// parities, each twice (the second copy one element later), and a lane's 8 values (8 consecutive wo of one (row,
+// kw) tap) are 4 aligned 4-B words of one copy.
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+constexpr int PARW = MAX_WO + 8;                    // fp16 per parity copy (column pairs of one staged row)
+constexpr int YS16 = MAX_WO + 8;                    // fp16 per dY row (hi, lo planes)
+
+__device__ inline int split_exp_w(uint32_t mb) {
+    const int ef = (int)((mb >> 23) & 0xff);
+    if (mb == 0) return 0;
+    const int k = ef == 0 ? -127 : ef - 127;
+    return min(100, max(-100, 14 - k));
+}
+
+template <int NTW, int RPW>
+__global__ __launch_bounds__(THREADS, 2) void wgrad16_kernel(Shape s, const uint8_t* __restrict__ x,
+                                                             const float* __restrict__ dy,
+                                                             const uint32_t* __restrict__ dymax,
+                                                             float* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];
+    const int WIN = 2 * (s.WO - 1) + s.KW;
+    const int lane = threadIdx.x & 63, half = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nxrow = s.CIN * s.KT * s.KH;
+    const int n_lo = blockIdx.y * 4 * NTW * 32;
+    const int n_hi = min(s.N, n_lo + 4 * NTW * 32);
+    const int r_lo = n_lo / s.KW, r_hi = min(nxrow, (n_hi + s.KW - 1) / s.KW);
+    const int nrs = r_hi - r_lo;
+    const int ks = (s.WO + 15) / 16;                             // k16-steps per output row
+    // LDS: dY hi, lo [64][YS16]; staged rows [nrs + 1][parity 2][copy 2][PARW] (row nrs: zeros, the N padding)
+    _Float16* yh = reinterpret_cast<_Float16*>(lds8);
+    _Float16* yl = yh + COUT * YS16;
+    _Float16* xs = yl + COUT * YS16;
+    const int XROW = 4 * PARW;                                   // fp16 per staged row
+    for (int i = threadIdx.x; i < XROW; i += THREADS) xs[nrs * XROW + i] = (_Float16)0.f;
+
+    // B fragment base per N tile: staged row, parity p = kw & 1, copy q = (kw >> 1) & 1, element m0 - q with
+    // m0 = wo + kw >> 1 (wo added per k-step), so the lane reads words 2 i of copy q: (m0 - q) is even for even wo
+    int bbase[NTW], bshift[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = n_lo + (wave * NTW + j) * 32 + (lane & 31);
+        const bool ok = n < n_hi;
+        const int rr = ok ? n / s.KW - r_lo : nrs, kw = ok ? n % s.KW : 0;
+        const int p = kw & 1, q = (kw >> 1) & 1;
+        bbase[j] = rr * XROW + (2 * p + q) * PARW;
+        bshift[j] = (kw >> 1) - q;                               // even
+    }
+    floatx16 acc[2][NTW];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][j][r] = 0.f;
+
+    const int64_t plane = (int64_t)s.H * s.W;
+    const int64_t yplane = (int64_t)s.HO * s.WO;
+    const int nx = (int)((int64_t)s.B * s.CIN * s.T * plane);
+    const int ny = (int)((int64_t)s.B * COUT * s.TO * yplane);
+    const auto rx = make_rsrc(x, nx);
+    const auto ry = make_rsrc(dy, ny);
+    const float sc = __builtin_ldexpf(1.f, split_exp_w(*dymax));
+    float xr[RPW][2], yr[16];
+    const int wo16 = ks * 16;
+
+    auto prefetch = [&](int row) {
+        const int ho = row % s.HO, t = (row / s.HO) % s.TO, b = row / (s.HO * s.TO);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const int r = r_lo + wave + 4 * i;
+            const int kh = r % s.KH, kt = (r / s.KH) % s.KT, ci = r / (s.KH * s.KT);
+            const int ti = t - s.PT + kt, hi = 2 * ho - s.PH + kh;
+            const bool rowok = r < r_hi && ti >= 0 && ti < s.T && hi >= 0 && hi < s.H;
+            const int base = (int)(((int64_t)(b * s.CIN + ci) * s.T + ti) * plane + (int64_t)hi * s.W) - s.PW;
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const int c = lane + 64 * qq, wi = c - s.PW;
+                const bool ok = rowok && c < WIN && wi >= 0 && wi < s.W;
+                xr[i][qq] = bufld<uint8_t>::ld(rx, ok ? base + c : nx, 0);
+            }
+        }
+        const int64_t yb = ((int64_t)b * COUT * s.TO + t) * yplane + (int64_t)ho * s.WO;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int co = wave + 4 * i;
+            const bool ok = lane < s.WO;
+            yr[i] = bufld<float>::ld(ry, ok ? (int)(yb + (int64_t)co * s.TO * yplane) + lane : ny, 0);
+        }
+    };
+
+    int row = blockIdx.x;
+    if (row < s.rows) prefetch(row);
+    for (; row < s.rows; row += gridDim.x) {
+        __syncthreads();                                 // previous row's MFMAs are done with LDS
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const int rr = wave + 4 * i;
+            if (rr < nrs) {
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    const int c = lane + 64 * qq;               // staged column c: input column c - PW
+                    if (c < 2 * PARW) {
+                        // beyond the window: zeros (the zero-weight 8th tap reads up to 2 columns past it)
+                        const _Float16 v = (_Float16)(c < WIN ? xr[i][qq] : 0.f);
+                        const int p = c & 1, mm = c >> 1;
+                        xs[rr * XROW + (2 * p) * PARW + mm] = v;                     // copy 0
+                        if (mm >= 1) xs[rr * XROW + (2 * p + 1) * PARW + mm - 1] = v; // copy 1: one element later
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (lane < wo16) {
+                const float v = (lane < s.WO ? yr[i] : 0.f) * sc;
+                const _Float16 h = (_Float16)v;
+                yh[(wave + 4 * i) * YS16 + lane] = h;
+                yl[(wave + 4 * i) * YS16 + lane] = (_Float16)(v - (float)h);
+            }
+        }
+        __syncthreads();
+        if (row + (int)gridDim.x < s.rows) prefetch(row + gridDim.x);
+        for (int kk = 0; kk < ks; ++kk) {
+            const int wo0 = 16 * kk + 8 * half;                  // the lane's 8 k = wo0 .. wo0 + 7
+            half8 ah[2], al[2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const int co = 32 * m + (lane & 31);
+                ah[m] = *reinterpret_cast<const half8*>(&yh[co * YS16 + wo0]);
+                al[m] = *reinterpret_cast<const half8*>(&yl[co * YS16 + wo0]);
+            }
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                const _Float16* src = xs + bbase[j] + wo0 + bshift[j];
+                const uint32_t* w32 = reinterpret_cast<const uint32_t*>(src);
+                const uint32_t u0 = w32[0], u1 = w32[1], u2 = w32[2], u3 = w32[3];
+                const uint32_t __attribute__((ext_vector_type(4))) u = {u0, u1, u2, u3};
+                const half8 bv = __builtin_bit_cast(half8, u);
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bv, acc[m][j], 0, 0, 0);
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bv, acc[m][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+    const float unscale = __builtin_ldexpf(1.f, -split_exp_w(*dymax));
+    float* pp = part + (int64_t)blockIdx.x * COUT * s.N;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+            const int n = n_lo + (wave * NTW + j) * 32 + (lane & 31);
+            if (n < n_hi) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int co = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    pp[(int64_t)co * s.N + n] = acc[m][j][r] * unscale;
+                }
+            }
+        }
+}
+
 __global__ void reduce_kernel(const float* __restrict__ part, int nparts, int total, float* __restrict__ dw, int accumulate) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
@@ -169,7 +339,8 @@ using namespace avse::c3w;
 template <typename XT>
 static int conv3d_wgrad_impl(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH,
                              int64_t KW, int64_t PT, int64_t PH, int64_t PW, const XT* x, const float* dy, float* dw,
-                             int32_t accumulate, float* workspace, avse_stream_t stream) {
+                             int32_t accumulate, float* workspace, avse_stream_t stream,
+                             const uint32_t* dymax = nullptr) {
     if (!x || !dy || !dw || !workspace) return AVSE_EINVAL;
     Shape s;
     s.B = (int)B; s.CIN = (int)CIN; s.T = (int)T; s.H = (int)H; s.W = (int)W;
@@ -198,10 +369,23 @@ static int conv3d_wgrad_impl(int64_t B, int64_t CIN, int64_t T, int64_t H, int64
         max_nrs = std::max(max_nrs, nrs);
     }
     if (max_nrs > 4 * RPW) return AVSE_ESHAPE;
-    const size_t lds = 4 * ((size_t)max_nrs * (WIN + 1) + 2 * MAX_WO + 8 + COUT * YS);
-    if (lds > 64 * 1024) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid(s.nparts, nsplit), block(THREADS);
+    if constexpr (std::is_same<XT, uint8_t>::value) {
+        if (dymax) {                            // the f16 MFMA with dY split under the given max
+            if (2 * ((s.KW - 1) / 2) + 2 * MAX_WO > 2 * PARW || WIN > 128) return AVSE_ESHAPE;
+            const size_t lds16 = 2 * ((size_t)2 * COUT * YS16 + (size_t)(max_nrs + 1) * 4 * PARW);
+            hipLaunchKernelGGL((wgrad16_kernel<NTW, RPW>), grid, block, lds16, st, s, x, dy, dymax, workspace);
+            AVSE_CHECK_LAUNCH();
+            const int total = COUT * s.N;
+            hipLaunchKernelGGL(reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, workspace, s.nparts, total, dw,
+                               (int)accumulate);
+            AVSE_CHECK_LAUNCH();
+            return AVSE_OK;
+        }
+    }
+    const size_t lds = 4 * ((size_t)max_nrs * (WIN + 1) + 2 * MAX_WO + 8 + COUT * YS);
+    if (lds > 64 * 1024) return AVSE_ESHAPE;
     hipLaunchKernelGGL((wgrad_kernel<XT, NTW, RPW>), grid, block, lds, st, s, x, dy, workspace);
     AVSE_CHECK_LAUNCH();
     const int total = COUT * s.N;
@@ -221,6 +405,15 @@ int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, i
                       int64_t PT, int64_t PH, int64_t PW, const float* x, const float* dy, float* dw,
                       int32_t accumulate, float* workspace, avse_stream_t stream) {
     return conv3d_wgrad_impl<float>(B, CIN, T, H, W, KT, KH, KW, PT, PH, PW, x, dy, dw, accumulate, workspace, stream);
+}
+
+int avse_conv3d_wgrad_u8_split(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH,
+                               int64_t KW, int64_t PT, int64_t PH, int64_t PW, const uint8_t* x, const float* dy,
+                               const uint32_t* dymax, float* dw, int32_t accumulate, float* workspace,
+                               avse_stream_t stream) {
+    if (!dymax) return AVSE_EINVAL;
+    return conv3d_wgrad_impl<uint8_t>(B, CIN, T, H, W, KT, KH, KW, PT, PH, PW, x, dy, dw, accumulate, workspace, stream,
+                                      dymax);
 }
 
 int avse_conv3d_wgrad_u8(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,

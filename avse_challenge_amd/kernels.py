@@ -374,6 +374,8 @@ def istft(mag, phase_spec, length):
 # ------------------------------------------------------------------------ lip front-end Conv3d dW
 
 CONV3D_WGRAD_MAX_WO = 64      # output width the MFMA kernel stages per LDS row (conv3d_wgrad.hip MAX_WO)
+# uint8 frames: the f16 MFMA weight gradient with dy split (avse_conv3d_wgrad_u8_split); "0": the exact-fp32 kernel
+C3W_F16 = os.environ.get("AVSE_C3W_F16", "1") == "1"
 
 
 def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
@@ -382,7 +384,10 @@ def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
     _need_gpu(x, dy)
     u8 = x.dtype == torch.uint8
     x = x.contiguous() if u8 else x.float().contiguous()
+    dymax = _known_absmax(dy) if u8 and C3W_F16 else None     # the BatchNorm -> act backward's max |dy|
     dy = dy.float().contiguous()
+    if u8 and C3W_F16 and dymax is None:
+        dymax = dy.abs().amax().reshape(1).view(torch.int32)
     Bn, Cin, Tn, H, W = x.shape
     KT, KH, KW = kernel_size
     PT, PH, PW = padding
@@ -395,6 +400,11 @@ def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
     L = _lib.lib()
     ws = torch.empty((L.avse_conv3d_wgrad_workspace_bytes(Bn, dy.shape[2], dy.shape[3], N) + 3) // 4,
                      device=x.device, dtype=torch.float32)
+    if dymax is not None:              # uint8 frames on the f16 MFMA, dy split under its max
+        check(L.avse_conv3d_wgrad_u8_split(Bn, Cin, Tn, H, W, KT, KH, KW, PT, PH, PW, ptr(x), ptr(dy), ptr(dymax),
+                                           ptr(out), int(bool(accumulate)), ptr(ws), stream_ptr(x.device)),
+              "avse_conv3d_wgrad_u8_split")
+        return out
     fn = L.avse_conv3d_wgrad_u8 if u8 else L.avse_conv3d_wgrad
     check(fn(Bn, Cin, Tn, H, W, KT, KH, KW, PT, PH, PW, ptr(x), ptr(dy), ptr(out),
              int(bool(accumulate)), ptr(ws), stream_ptr(x.device)), "avse_conv3d_wgrad")

@@ -194,6 +194,12 @@ int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, i
                       int64_t PT, int64_t PH, int64_t PW, const float* x, const float* dy, float* dw,
                       int32_t accumulate, float* workspace, avse_stream_t stream);
 /* the same with x the uint8 lip frames (values 0..255 read as floats: the cast of baseline/avse1/model.py:122) */
+/* avse_conv3d_wgrad_u8 on the f16 MFMA: uint8 frames (exact in fp16) against dy split into hi + lo fp16 under the
+ * power-of-two scale of max |dy| (float bits in *dymax, e.g. avse_bnact_bwd's dx_max): fp32-accurate. */
+int avse_conv3d_wgrad_u8_split(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH,
+                               int64_t KW, int64_t PT, int64_t PH, int64_t PW, const uint8_t* x, const float* dy,
+                               const uint32_t* dymax, float* dw, int32_t accumulate, float* workspace,
+                               avse_stream_t stream);
 int avse_conv3d_wgrad_u8(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,
                          int64_t PT, int64_t PH, int64_t PW, const uint8_t* x, const float* dy, float* dw,
                          int32_t accumulate, float* workspace, avse_stream_t stream);

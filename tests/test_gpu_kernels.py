@@ -403,16 +403,35 @@ def test_conv3d_wgrad_vs_fp64(cin, T, H, W):
     close(got2, 2 * ref, 4e-6 * scale * (1 + x.numel() / 1e5) ** 0.5, 0, "dW accumulate")
 
 
-def test_conv3d_wgrad_uint8_equals_fp32():
-    """avse_conv3d_wgrad_u8 reads the uint8 lip frames themselves: bitwise the fp32 kernel's result on their float
-    values (same products, same order)."""
-    g = torch.Generator().manual_seed(704)
-    xu = torch.randint(0, 256, (2, 3, 5, 96, 96), generator=g, dtype=torch.uint8)
+@pytest.mark.parametrize("T", [5, 1])
+def test_conv3d_wgrad_uint8_vs_fp64(T):
+    """avse_conv3d_wgrad_u8(_split) reads the uint8 lip frames themselves (no fp32 copy of the clip) at the avse1
+    96 x 96 shape: the f16 MFMA path (frames exact in fp16, dy split into hi + lo under its max, given by the producing
+    BatchNorm backward or computed here) vs fp64, every element within 1e-5 of its sum of |terms| (the fp32 class);
+    AVSE_C3W_F16=0's exact-fp32 kernel is bitwise the fp32-frames kernel (same products, same order); deterministic."""
+    import importlib
+    g = torch.Generator().manual_seed(704 + T)
+    xu = torch.randint(0, 256, (2, 3, T, 96, 96), generator=g, dtype=torch.uint8)
     y = torch.nn.functional.conv3d(xu.double(), det_input((64, 3, 5, 7, 7), 705).double(), None, (1, 2, 2), (2, 3, 3))
-    dy = det_input(tuple(y.shape), 706).to(DEV)
-    a = K().conv3d_wgrad(xu.to(DEV), dy, (5, 7, 7), (2, 3, 3))
-    b = K().conv3d_wgrad(xu.to(DEV).float(), dy, (5, 7, 7), (2, 3, 3))
-    assert torch.equal(a, b)
+    dy = det_input(tuple(y.shape), 706) * torch.exp(2.0 * det_input(tuple(y.shape), 707))
+    truth = torch.nn.grad.conv3d_weight(xu.double(), (64, 3, 5, 7, 7), dy.double(), (1, 2, 2), (2, 3, 3))
+    bound = torch.nn.grad.conv3d_weight(xu.double(), (64, 3, 5, 7, 7), dy.double().abs(), (1, 2, 2), (2, 3, 3))
+    a = K().conv3d_wgrad(xu.to(DEV), dy.to(DEV), (5, 7, 7), (2, 3, 3))
+    worst = float(((a.double().cpu() - truth).abs() / (bound + 1e-30)).max())
+    print(f"conv3d wgrad u8 split vs fp64: {worst:.2e} of sum|terms|")
+    assert worst <= 1e-5, worst
+    assert torch.equal(a, K().conv3d_wgrad(xu.to(DEV), dy.to(DEV), (5, 7, 7), (2, 3, 3)))
+    dyg = dy.to(DEV)
+    setattr(dyg, K().ABSMAX_ATTR, dyg.abs().amax().reshape(1).view(torch.int32))   # a producer's max: same result
+    assert torch.equal(a, K().conv3d_wgrad(xu.to(DEV), dyg, (5, 7, 7), (2, 3, 3)))
+    old = K().C3W_F16
+    try:
+        K().C3W_F16 = False
+        b = K().conv3d_wgrad(xu.to(DEV), dy.to(DEV), (5, 7, 7), (2, 3, 3))
+        c = K().conv3d_wgrad(xu.to(DEV).float(), dy.to(DEV), (5, 7, 7), (2, 3, 3))
+    finally:
+        K().C3W_F16 = old
+    assert torch.equal(b, c)
 
 
 @pytest.mark.parametrize("dtype,T", [(torch.uint8, 7), (torch.float32, 6), (torch.uint8, 1)])
