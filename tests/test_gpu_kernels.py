@@ -467,8 +467,10 @@ def test_conv3d_fwd_unsupported_shapes():
 
 
 def test_lip_conv3d_module_uint8_frames():
-    """LipConv3d on the uint8 frames (the HIP forward and the uint8 weight gradient) equals it on their float
-    values, output and weight gradient bitwise."""
+    """LipConv3d on the uint8 frames (the HIP forward and weight gradient on the f16 MFMA, frames read as stored) and
+    on their float values (the exact-fp32 kernels) both hold the fp32 class against fp64: output within 1e-6 and
+    weight gradient within 1e-5 of each element's sum of |terms| (round 5: the two paths no longer share products, so
+    they agree to that bar, not bitwise)."""
     from avse_challenge_amd.layers import LipConv3d
     m = LipConv3d(3, 64, (5, 7, 7)).to(DEV)
     g = torch.Generator().manual_seed(711)
@@ -480,7 +482,14 @@ def test_lip_conv3d_module_uint8_frames():
     m.weight.grad = None
     y2 = m(xu.float())
     y2.backward(gy)
-    assert torch.equal(y, y2) and torch.equal(w1, m.weight.grad)
+    x64, w64, g64 = xu.double().cpu(), m.weight.detach().double().cpu(), gy.double().cpu()
+    conv = lambda a, b: torch.nn.functional.conv3d(a, b, None, (1, 2, 2), (2, 3, 3))  # noqa: E731
+    wgr = lambda a, d: torch.nn.grad.conv3d_weight(a, tuple(w64.shape), d, (1, 2, 2), (2, 3, 3))  # noqa: E731
+    yt, yb = conv(x64, w64), conv(x64, w64.abs())
+    dwt, dwb = wgr(x64, g64), wgr(x64, g64.abs())
+    for out, dw in ((y, w1), (y2, m.weight.grad)):
+        assert float(((out.detach().double().cpu() - yt).abs() / (yb + 1e-30)).max()) <= 1e-6
+        assert float(((dw.double().cpu() - dwt).abs() / (dwb + 1e-30)).max()) <= 1e-5
 
 
 def test_lip_conv3d_module_grad():
