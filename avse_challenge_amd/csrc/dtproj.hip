@@ -9,23 +9,21 @@
 //   delta[b][d][t] = softplus(sum_r W[d][r] * x[b][r][t] + bias[d])        (torch's threshold: x > 20 -> x)
 //
 // A GEMM with M = D, N = L and a short reduction K = R (dt_rank = 8 .. 32 at every Mamba-TasNet size) whose output
-// (b, D, l) is the bulk of its bytes: the kernel has to stream at HBM rate, and 2R fp32 FMAs per output element on
-// the VALU did not (round-5 first version: 0.28 of HBM at C3, 0.16 at C5, VALU-bound).  So the products run on the
-// MFMA (v_mfma_f32_32x32x16_*), fp32 accumulation:
+// (b, D, l) is nearly all of its bytes: a write stream.  The products run on the MFMA (v_mfma_f32_32x32x16_*, fp32
+// accumulation):
 //   - bf16 operands: bf16 MFMA on the values as they are (bf16 x bf16 products are exact in fp32);
-//   - fp32 operands: the split of dconv.hip / projgemm.hip with per-TILE power-of-two scales (the tile's x slab and
-//     W rows are in LDS anyway): hi = fp16(v 2^e), lo = fp16(v 2^e - hi), products hi*hi + hi*lo + lo*hi on the f16
-//     MFMA, scaled back by 2^-(e_x + e_w) (22-bit operands: the fp32 class).
-// Workgroup = 64 channels x 256 steps of one batch row, 4 waves of 64 channels x 64 steps (2 x 2 MFMA blocks); the
-// output tile goes out through LDS in 1-KB coalesced rows (stores straight from the accumulators -- 32-B runs per
-// row -- ran the C3 call at 0.60 ms against 0.48 for the VALU version).  x rows
-// [0, R) x 256 steps are staged in LDS as 16-bit k-rows of 512 B (16-B chunk c of k-row r at c ^ ((r & 3) << 2),
-// fragments by ds_read_b64_tr_b16), W's 64 rows as R-long 16-bit rows padded by 16 B (conflict-free 16-B reads).
-// The workgroups of one x slab (its D / 64 channel tiles) are consecutive, so the slab is re-read from L2.
-// bias + softplus in the epilogue; the bf16 output is rounded once.
-#include <algorithm>
-#include <type_traits>
-
+//   - fp32 operands: the split of dconv.hip / projgemm.hip with power-of-two scales per x tile and per W tile:
+//     hi = fp16(v 2^e), lo = fp16(v 2^e - hi), products hi*hi + hi*lo + lo*hi on the f16 MFMA, scaled back by
+//     2^-(e_x + e_w) (22-bit operands: the fp32 class).
+// Schedule (round 5, fourth version): one workgroup per (batch row, 256-step tile) walks ALL channels.  The x slab
+// (R rows x 256 steps) is staged once through LDS (16-bit k-rows of 512 B, 16-B chunk c of k-row r at
+// c ^ ((r & 3) << 2), read by ds_read_b64_tr_b16) into per-wave MFMA A fragments (steps as the rows) that stay in
+// registers; the channel loop then reads no LDS and has no barrier: W fragments (lane = channel, 8 consecutive k: one
+// or two 16-B loads) are loaded one 32-channel tile ahead, so a tile's stores drain while the next one multiplies.
+// Each lane ends with 4 consecutive steps of one channel: one 16-B (fp32) / 8-B (bf16) store.  bias + softplus in
+// the epilogue; the bf16 output is rounded once.  <= 128 VGPRs (4 waves per SIMD at dt_rank <= 32).
+// Isolated (tools/dtproj_bench.py, profiles/r05v_dtproj_ab.jsonl): C5 bf16 0.18 ms (the VALU version 0.28, the
+// earlier MFMA versions with one workgroup per (64 channels, 256 steps) 0.31-0.34), C3 fp32 0.43 (VALU 0.41).
 #include "common.h"
 
 namespace avse {
@@ -37,10 +35,11 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef short s4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4_t lds_s4_t;
 
-constexpr int THREADS = 256, CH = 64, TT = 256, RMAX = 64;
+constexpr int THREADS = 256, CH = 32, TT = 256, RMAX = 64;
 
 struct Args {
-    int D, R, RP, L, nt, nd;
+    int D, R, L, nt, nd;
+    bool wvec;
     const void* w;
     int64_t w_ds;
     const void* x;
@@ -92,31 +91,47 @@ __device__ inline half8 xfrag(const uint8_t* img, int cb, int s, int lane) {
     const short __attribute__((ext_vector_type(8))) w = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     return __builtin_bit_cast(half8, w);
 }
-// A operand fragment (32 channels x 16 k) of channels rb .. rb + 31: lane l holds channel rb + (l & 31),
-// k = 16 s + 8 (l >> 5) + 0..7 (one 16-B read of the channel's row)
-__device__ inline half8 wfrag(const uint8_t* img, int wrow, int rb, int s, int lane) {
-    return *reinterpret_cast<const half8*>(img + (rb + (lane & 31)) * wrow + 2 * (16 * s + 8 * (lane >> 5)));
+// One lane's 8 W values of an MFMA B fragment: channel d, k = k0 .. k0 + 7 (0 past D or R).  wvec: rows of 8-element
+// multiples, 16-B aligned, R % 8 == 0 (the model's dt_proj.weight) -> 16-B loads; otherwise element loads.
+template <typename T>
+__device__ inline void wload(const T* __restrict__ w, int64_t w_ds, int D, int R, int d, int k0, bool wvec, float (&o)[8]) {
+    if (d < D && k0 < R && wvec) {
+        const T* p = w + (int64_t)d * w_ds + k0;
+        if constexpr (std::is_same<T, float>::value) {
+            const float4 v0 = *reinterpret_cast<const float4*>(p), v1 = *reinterpret_cast<const float4*>(p + 4);
+            o[0] = v0.x; o[1] = v0.y; o[2] = v0.z; o[3] = v0.w;
+            o[4] = v1.x; o[5] = v1.y; o[6] = v1.z; o[7] = v1.w;
+        } else {
+            const uint4 v = *reinterpret_cast<const uint4*>(p);
+            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o[2 * e] = __uint_as_float(u[e] << 16);
+                o[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (d < D && k0 + e < R) ? io<T>::ld(w + (int64_t)d * w_ds + k0 + e) : 0.f;
 }
 
-template <typename T>
-__global__ __launch_bounds__(THREADS) void dtproj_kernel(Args a) {
+template <typename T, int NKS>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void dtproj_kernel(Args a) {
     constexpr bool F32 = std::is_same<T, float>::value;
-    constexpr int NPL = F32 ? 2 : 1;                          // planes: hi, lo (fp32) or the bf16 values
+    constexpr int RP = 16 * NKS;
+    constexpr int XB = RP * 512;                              // one plane of the x image
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    __shared__ uint32_t red[2][4];
-    const int XB = a.RP * 512, wrow = 2 * a.RP + 16, WB = CH * wrow;
-    uint8_t* ximg = lds;                                      // [plane][RP k-rows][512 B]
-    uint8_t* wimg = lds + NPL * XB;                           // [plane][64 rows][wrow]
+    __shared__ uint32_t red[4];
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int db = bid % a.nd, tb = (bid / a.nd) % a.nt, b = bid / (a.nd * a.nt);
-    const int t0 = tb * TT, d0 = db * CH;
+    const int tb = bid % a.nt, b = bid / a.nt;
+    const int t0 = tb * TT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-    // x slab: thread -> (k-row r, 4 steps); steps past L read 0 (the range ends at the row's last element) or row
-    // padding (inside the range): either way they feed only unstored outputs
+    // x slab: thread -> (k-row r, 4 steps); steps past L and rows past R are 0 (the tile's split scale sees only data)
     const T* xb = reinterpret_cast<const T*>(a.x) + (int64_t)b * a.x_bs;
     const auto rx = make_rsrc(xb, (int64_t)(a.R - 1) * a.x_rs + a.L);
-    constexpr int XPT = RMAX * (TT / 4) / THREADS;            // float4 per thread (upper bound: R <= 64)
+    constexpr int XPT = RP * (TT / 4) / THREADS;
     float4 xv[XPT];
     float mx = 0.f;
 #pragma unroll
@@ -136,46 +151,20 @@ __global__ __launch_bounds__(THREADS) void dtproj_kernel(Args a) {
         }
         mx = fmaxf(mx, fmaxf(fmaxf(fabsf(xv[k].x), fabsf(xv[k].y)), fmaxf(fabsf(xv[k].z), fabsf(xv[k].w))));
     }
-    // W rows of the tile: thread -> (row, 4 k); rows past D and k past R are 0
-    const T* w = reinterpret_cast<const T*>(a.w);
-    constexpr int WPT = CH * RMAX / 4 / THREADS;
-    float4 wv[WPT];
-#pragma unroll
-    for (int k = 0; k < WPT; ++k) {
-        const int i = tid + k * THREADS, row = i / (RMAX / 4), k4 = 4 * (i % (RMAX / 4)), d = d0 + row;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (d < a.D && k4 + e < a.R) ? io<T>::ld(w + (int64_t)d * a.w_ds + k4 + e) : 0.f;
-        wv[k] = make_float4(v[0], v[1], v[2], v[3]);
-    }
-    float sx = 1.f, sw = 1.f, unscale = 1.f;
+    float sx = 1.f;
+    int ex = 0;
     if constexpr (F32) {
-        float mw = 0.f;
-#pragma unroll
-        for (int k = 0; k < WPT; ++k)
-            mw = fmaxf(mw, fmaxf(fmaxf(fabsf(wv[k].x), fabsf(wv[k].y)), fmaxf(fabsf(wv[k].z), fabsf(wv[k].w))));
-        uint32_t bx = __float_as_uint(mx), bw = __float_as_uint(mw);
-        for (int o = 32; o >= 1; o >>= 1) {
-            bx = max(bx, (uint32_t)__shfl_xor((int)bx, o, 64));
-            bw = max(bw, (uint32_t)__shfl_xor((int)bw, o, 64));
-        }
-        if (lane == 0) {
-            red[0][wave] = bx;
-            red[1][wave] = bw;
-        }
+        uint32_t bx = __float_as_uint(mx);
+        for (int o = 32; o >= 1; o >>= 1) bx = max(bx, (uint32_t)__shfl_xor((int)bx, o, 64));
+        if (lane == 0) red[wave] = bx;
         __syncthreads();
-        bx = max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3]));
-        bw = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
-        const int ex = split_exp(bx), ew = split_exp(bw);
+        bx = max(max(red[0], red[1]), max(red[2], red[3]));
+        ex = split_exp(bx);
         sx = __builtin_ldexpf(1.f, ex);
-        sw = __builtin_ldexpf(1.f, ew);
-        unscale = __builtin_ldexpf(1.f, -(ex + ew));
     }
-    // LDS images (k-rows R .. RP - 1 of x are zero: their thread slots loaded 0)
 #pragma unroll
     for (int k = 0; k < XPT; ++k) {
         const int i = tid + k * THREADS, r = i / (TT / 4), c4 = i % (TT / 4);
-        if (r >= a.RP) continue;
         const float v[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
         uint16_t h[4], l[4];
 #pragma unroll
@@ -190,122 +179,125 @@ __global__ __launch_bounds__(THREADS) void dtproj_kernel(Args a) {
             }
         }
         const int off = ximg_off(r, 4 * c4);
-        *reinterpret_cast<uint2*>(ximg + off) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+        *reinterpret_cast<uint2*>(lds + off) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
         if constexpr (F32)
-            *reinterpret_cast<uint2*>(ximg + XB + off) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
-    }
-#pragma unroll
-    for (int k = 0; k < WPT; ++k) {
-        const int i = tid + k * THREADS, row = i / (RMAX / 4), k4 = 4 * (i % (RMAX / 4));
-        if (k4 >= a.RP) continue;
-        const float v[4] = {wv[k].x, wv[k].y, wv[k].z, wv[k].w};
-        uint16_t h[4], l[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            if constexpr (F32) {
-                const float sv = v[e] * sw;
-                const _Float16 hh = (_Float16)sv;
-                h[e] = __builtin_bit_cast(uint16_t, hh);
-                l[e] = h16(sv - (float)hh);
-            } else {
-                h[e] = (uint16_t)(__float_as_uint(v[e]) >> 16);
-            }
-        }
-        const int off = row * wrow + 2 * k4;
-        *reinterpret_cast<uint2*>(wimg + off) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-        if constexpr (F32)
-            *reinterpret_cast<uint2*>(wimg + WB + off) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+            *reinterpret_cast<uint2*>(lds + XB + off) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
     }
     __syncthreads();
-
-    floatx16 acc[2][2];                                       // [channel block i][step block j]
+    // the wave's x fragments (steps tc .. tc + 63 as the MFMA rows) stay in registers for every channel tile: the
+    // loop below reads no LDS and has no barrier, so one tile's stores drain while the next one computes
+    const int tc = 64 * wave;
+    half8 xh[2][NKS], xl[2][NKS];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            xh[j][s] = xfrag(lds, tc + 32 * j, s, lane);
+            if constexpr (F32) xl[j][s] = xfrag(lds + XB, tc + 32 * j, s, lane);
+        }
+
+    const T* w = reinterpret_cast<const T*>(a.w);
+    T* ob = reinterpret_cast<T*>(a.out) + (int64_t)b * a.o_bs;
+    const int tl = t0 + tc + 4 * (lane >> 5);                 // + 32 j + 8 g + e: this lane's steps
+    const int kl = 8 * (lane >> 5);
+    // channel tiles of 32 (one MFMA column block): 32 accumulators, the x fragments and the next tile's W in flight
+    // fit ~100 VGPRs, i.e. 4+ waves per SIMD to cover the loads' and stores' latency
+    float wn[NKS][8];                                         // this tile's W fragment (loaded one tile ahead)
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) wload<T>(w, a.w_ds, a.D, a.R, lane & 31, 16 * s + kl, a.wvec, wn[s]);
+    for (int d0 = 0; d0 < a.D; d0 += CH) {
+        const int d = d0 + (lane & 31);
+        // B fragments (lane = channel d, k = 16 s + kl .. + 7); fp32: split with the tile's scale (every wave holds
+        // all 32 x RP W values of the tile: one wave max)
+        half8 wh[NKS], wl[NKS];
+        float unscale = 1.f;
+        if constexpr (F32) {
+            float mw = 0.f;
+#pragma unroll
+            for (int s = 0; s < NKS; ++s)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) mw = fmaxf(mw, fabsf(wn[s][e]));
+            uint32_t bw = __float_as_uint(mw);
+            for (int o = 32; o >= 1; o >>= 1) bw = max(bw, (uint32_t)__shfl_xor((int)bw, o, 64));
+            const int ew = split_exp(bw);
+            const float sw = __builtin_ldexpf(1.f, ew);
+            unscale = __builtin_ldexpf(1.f, -(ex + ew));
+#pragma unroll
+            for (int s = 0; s < NKS; ++s)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float sv = wn[s][e] * sw;
+                    const _Float16 hh = (_Float16)sv;
+                    wh[s][e] = hh;
+                    wl[s][e] = (_Float16)(sv - (float)hh);
+                }
+        } else {
+#pragma unroll
+            for (int s = 0; s < NKS; ++s)
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    wh[s][e] = __builtin_bit_cast(_Float16, (uint16_t)(__float_as_uint(wn[s][e]) >> 16));
+        }
+        if (d0 + CH < a.D) {                                  // the next tile's W, in flight during this tile
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) wload<T>(w, a.w_ds, a.D, a.R, d + CH, 16 * s + kl, a.wvec, wn[s]);
+        }
+        const float bv = (a.bias && d < a.D) ? a.bias[d] : 0.f;
+        floatx16 acc[2];                                      // [step block j]
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    const int tc = 64 * wave;                                 // this wave's steps tc .. tc + 63 of the tile
-    for (int s = 0; s < a.RP / 16; ++s) {
-        half8 wh[2], xh[2], wl[2], xl[2];
+            for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            wh[i] = wfrag(wimg, wrow, 32 * i, s, lane);
-            if constexpr (F32) wl[i] = wfrag(wimg + WB, wrow, 32 * i, s, lane);
-        }
+        for (int s = 0; s < NKS; ++s)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            xh[j] = xfrag(ximg, tc + 32 * j, s, lane);
-            if constexpr (F32) xl[j] = xfrag(ximg + XB, tc + 32 * j, s, lane);
-        }
-#pragma unroll
-        for (int pr = 0; pr < (F32 ? 3 : 1); ++pr)
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int pr = 0; pr < (F32 ? 3 : 1); ++pr)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     if constexpr (F32) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr == 2 ? wl[i] : wh[i], pr == 1 ? xl[j] : xh[j],
-                                                                           acc[i][j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr == 2 ? xl[j][s] : xh[j][s],
+                                                                        pr == 1 ? wl[s] : wh[s], acc[j], 0, 0, 0);
                     } else {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wh[i]),
-                                                                            __builtin_bit_cast(bf16x8, xh[j]), acc[i][j],
-                                                                            0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, xh[j][s]),
+                                                                         __builtin_bit_cast(bf16x8, wh[s]), acc[j], 0, 0, 0);
                     }
                 }
-    }
-
-    // epilogue through LDS, 32 channels at a time: acc[i][j] register 4 g + e = channel d0 + 32 i + 8 g + 4 (lane >> 5)
-    // + e, step t0 + tc + 32 j + (lane & 31) -> ot[channel][step] (rows padded by 4 floats: the two half-waves' rows
-    // land on different banks), then every thread stores whole 16-B pieces of 32 rows x 256 steps (1 KB per wave
-    // instruction, coalesced): the output is the kernel's bytes
-    float* ot = reinterpret_cast<float*>(lds);                // [32][OS]
-    constexpr int OS = TT + 4;
-    T* ob = reinterpret_cast<T*>(a.out) + (int64_t)b * a.o_bs;
+        // epilogue: acc[j] register 4 g + e = step tl + 32 j + 8 g + e of channel d: four consecutive steps per lane
+        // -> one 16-B (fp32) / 8-B (bf16) store; a wave instruction writes 32 B into each of 32 channel rows
+        if (d >= a.D) continue;
+        T* orow = ob + (int64_t)d * a.o_ds;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        __syncthreads();                                      // the images / the previous half's reads are done
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
+            for (int g = 0; g < 4; ++g) {
+                const int t = tl + 32 * j + 8 * g;
+                if (t >= a.L) continue;
+                float v[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int dl = 8 * g + 4 * (lane >> 5) + e, d = d0 + 32 * i + dl;
-                const float bv = (a.bias && d < a.D) ? a.bias[d] : 0.f;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    float v = acc[i][j][4 * g + e] * unscale + bv;
-                    if (a.softplus) v = softplus2(v);
-                    ot[dl * OS + tc + 32 * j + (lane & 31)] = v;
+                for (int e = 0; e < 4; ++e) {
+                    v[e] = acc[j][4 * g + e] * unscale + bv;
+                    if (a.softplus) v[e] = softplus2(v[e]);
                 }
+                T* o = orow + t;
+                if constexpr (F32) {
+                    if (t + 3 < a.L && ((uintptr_t)o & 15) == 0) {
+                        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+                        continue;
+                    }
+                } else {
+                    if (t + 3 < a.L && ((uintptr_t)o & 7) == 0) {
+                        bf16_t h[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) io<bf16_t>::st(&h[e], v[e]);
+                        *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)h[0].x | ((uint32_t)h[1].x << 16),
+                                                                  (uint32_t)h[2].x | ((uint32_t)h[3].x << 16));
+                        continue;
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (t + e < a.L) io<T>::st(o + e, v[e]);
             }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 32 * TT / 4 / THREADS; ++k) {
-            const int idx = tid + k * THREADS, row = idx / (TT / 4), c4 = idx % (TT / 4);
-            const int d = d0 + 32 * i + row, t = t0 + 4 * c4;
-            if (d >= a.D || t >= a.L) continue;
-            const float4 v4 = *reinterpret_cast<const float4*>(&ot[row * OS + 4 * c4]);
-            T* o = ob + (int64_t)d * a.o_ds + t;
-            const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-            if constexpr (F32) {
-                if (t + 3 < a.L && ((uintptr_t)o & 15) == 0) {
-                    *reinterpret_cast<float4*>(o) = v4;
-                    continue;
-                }
-            } else {
-                if (t + 3 < a.L && ((uintptr_t)o & 7) == 0) {
-                    bf16_t h[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) io<bf16_t>::st(&h[e], v[e]);
-                    *reinterpret_cast<uint2*>(o) = make_uint2((uint32_t)h[0].x | ((uint32_t)h[1].x << 16),
-                                                              (uint32_t)h[2].x | ((uint32_t)h[3].x << 16));
-                    continue;
-                }
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (t + e < a.L) io<T>::st(o + e, v[e]);
-        }
     }
 }
 
@@ -331,12 +323,13 @@ int avse_dtproj(int64_t batch, int64_t dim, int64_t rank, int64_t seqlen, int32_
     Args a;
     a.D = (int)dim;
     a.R = (int)rank;
-    a.RP = (int)((rank + 15) / 16 * 16);
     a.L = (int)seqlen;
     a.nt = (int)((seqlen + TT - 1) / TT);
     a.nd = (int)((dim + CH - 1) / CH);
     a.w = w;
     a.w_ds = w_ds;
+    // 16-B W fragment loads: rows of 8-element multiples (bf16: 16 B; fp32: two 16-B halves), 16-B aligned base
+    a.wvec = (rank % 8 == 0) && ((uintptr_t)w % 16 == 0) && ((w_ds * es) % 16 == 0);
     a.x = x;
     a.x_bs = x_bs;
     a.x_rs = x_rs;
@@ -345,16 +338,26 @@ int avse_dtproj(int64_t batch, int64_t dim, int64_t rank, int64_t seqlen, int32_
     a.o_bs = delta_bs;
     a.o_ds = delta_ds;
     a.softplus = softplus;
-    const int64_t nblocks = batch * a.nt * a.nd;
+    // one workgroup per (batch row, 256-step tile), looping over the channel tiles
+    const int64_t nblocks = batch * a.nt;
     if (nblocks >= (1LL << 31)) return AVSE_ESHAPE;
-    const int npl = dtype == AVSE_F32 ? 2 : 1;
-    // the operand images, later the 32 x (256 + 4)-float output staging
-    const size_t lds = std::max<size_t>((size_t)npl * (a.RP * 512 + CH * (2 * a.RP + 16)), (size_t)32 * (TT + 4) * 4);
+    const int nks = (int)((rank + 15) / 16);
+    const size_t lds = (size_t)(dtype == AVSE_F32 ? 2 : 1) * nks * 16 * 512;   // the x image (hi, lo planes)
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == AVSE_F32)
-        hipLaunchKernelGGL(dtproj_kernel<float>, dim3((unsigned)nblocks), dim3(THREADS), lds, st, a);
-    else
-        hipLaunchKernelGGL(dtproj_kernel<avse::bf16_t>, dim3((unsigned)nblocks), dim3(THREADS), lds, st, a);
+    const dim3 grid((unsigned)nblocks), blk(THREADS);
+#define AVSE_DTP_LAUNCH(T)                                                          \
+    switch (nks) {                                                                  \
+        case 1: hipLaunchKernelGGL((dtproj_kernel<T, 1>), grid, blk, lds, st, a); break; \
+        case 2: hipLaunchKernelGGL((dtproj_kernel<T, 2>), grid, blk, lds, st, a); break; \
+        case 3: hipLaunchKernelGGL((dtproj_kernel<T, 3>), grid, blk, lds, st, a); break; \
+        default: hipLaunchKernelGGL((dtproj_kernel<T, 4>), grid, blk, lds, st, a); break; \
+    }
+    if (dtype == AVSE_F32) {
+        AVSE_DTP_LAUNCH(float)
+    } else {
+        AVSE_DTP_LAUNCH(avse::bf16_t)
+    }
+#undef AVSE_DTP_LAUNCH
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
