@@ -131,6 +131,10 @@ SIGNATURES = {
                                c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_bnact_bwd": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32,
                                c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_bnact_fwd_q": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_f32, c_f32, c_vp, c_vp,
+                                 c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_bnact_bwd_q": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp,
+                                 c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_prelu_nhwc_fwd": (c_i32, [c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "avse_prelu_nhwc_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_prelu_nhwc_bwd": (c_i32, [c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -43,8 +43,10 @@ class _BasicBlock(nn.Module):            # utils/resnet.py:26-67 (relu_type='pre
         self.downsample = downsample
 
     def forward(self, x):
-        # BN -> PReLU and BN -> (+ shortcut) -> PReLU as fused passes (csrc/bnact.hip)
-        y = self.conv2(bn_act(self.conv1(x), self.bn1, self.relu1))
+        # BN -> PReLU and BN -> (+ shortcut) -> PReLU as fused passes (csrc/bnact.hip); bn1's output and input gradient
+        # go straight to the split-fp16 trunk convs in their split layout where those take them (bn_act q_fwd / q_bwd)
+        h = self.conv1(x)
+        y = self.conv2(bn_act(h, self.bn1, self.relu1, q_fwd=self.conv2.q_ok(h), q_bwd=self.conv1.q_ok(x, grad=True)))
         if self.downsample is None:
             sc = x
         else:
@@ -197,10 +199,15 @@ class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 conv
             x = x.contiguous(memory_format=torch.channels_last)
         for i in range(1, self.num_conv + 1):
             conv, bn = getattr(self, f"conv{i}"), getattr(self, f"bn{i}")
+            nxt = getattr(self, f"conv{i + 1}") if i < self.num_conv else None
             if bn.training and bn.track_running_stats and bn.momentum is not None and conv.bias is not None \
                     and conv.hip_ok(x):
                 # the conv bias goes into the BatchNorm (no separate bias-add pass): DilatedConv2d docstring
-                x = bn_act(conv(x, bias_to_bn=True), bn, "relu", folded_bias=conv.bias)
+                y = conv(x, bias_to_bn=True)
+                # BN -> ReLU writes its output (input gradient) in the split layout when the next (this) conv is a
+                # split-fp16 kernel: no separate split pass over the (B, 64, T, F) tensor (bn_act q_fwd / q_bwd)
+                x = bn_act(y, bn, "relu", folded_bias=conv.bias, q_fwd=nxt is not None and nxt.q_ok(y),
+                           q_bwd=conv.q_ok(x, grad=True))
             else:
                 x = bn_act(conv(x), bn, "relu")
         x = bn_act(self.convf(x), self.bn_last, "relu")

@@ -86,9 +86,9 @@ __device__ inline float act_bwd(float z, float g, float al) {
     else return g;
 }
 
-// Sum NQ per-thread column partials over the workgroup's RPI row offsets; row offset 0 writes
-// ws[(blockIdx.y * NQ + q) * CS + j].
-template <int V, int NQ>
+// Sum NQ per-thread column partials over the workgroup's RPI row offsets (quantity MAXQ, if in range: their max);
+// row offset 0 writes ws[(blockIdx.y * NQ + q) * CS + j].
+template <int V, int NQ, int MAXQ = -1>
 __device__ inline void block_partials(const Geo& g, float (&p)[NQ][V], bool valid, int64_t j0, float* ws) {
     __shared__ float part[NQ][THREADS * V];
     const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
@@ -105,7 +105,8 @@ __device__ inline void block_partials(const Geo& g, float (&p)[NQ][V], bool vali
             for (int k = 0; k < V; ++k) s[k] = p[q][k];
             for (int t = 1; t < g.RPI; ++t)
 #pragma unroll
-                for (int k = 0; k < V; ++k) s[k] += part[q][(t * g.TW + tx) * V + k];
+                for (int k = 0; k < V; ++k)
+                    s[k] = q == MAXQ ? fmaxf(s[k], part[q][(t * g.TW + tx) * V + k]) : s[k] + part[q][(t * g.TW + tx) * V + k];
             vld<V>::st(ws + ((int64_t)blockIdx.y * NQ + q) * g.CS + j0, s);
         }
     }
@@ -127,16 +128,53 @@ __device__ inline void block_max_out(float m, uint32_t* omax) {
     }
 }
 
-// ---- forward: statistics partials (shifted sums), finalize, apply
-template <int V>
+// ---- split output ("Q": the operand layout of dconv.hip / sconv.hip, round 5)
+// With QOUT the apply passes write their channels-last output (S = 1, C % 64 == 0) directly as the fp16 hi / lo split the
+// next convolution reads -- per pixel C / 16 chunks of 64 B = [hi of 16 channels][lo of 16 channels], the bytes of the
+// fp32 tensor -- instead of fp32 values that a separate split pass (read 4 B + write 4 B per element) would convert.
+// The split scale has to be known before the pass, so it comes from an upper bound of max |out| assembled from the
+// per-channel statistics (a bound is enough: any power-of-two scale with no fp16 overflow keeps the 22-bit split; see
+// stats_combine / bwd_combine), published as float bits where the exact max would be (y_max / dx_max).
+__device__ inline int q_split_exp(uint32_t mb) {          // dconv.hip split_exp: max 2^e in [2^14, 2^15)
+    const int ef = (int)((mb >> 23) & 0xff);
+    if (mb == 0) return 0;
+    const int k = ef == 0 ? -127 : ef - 127;
+    return min(100, max(-100, 14 - k));
+}
+// 4 channels c .. c + 3 (c % 4 == 0) of pixel r: hi at 64 (c / 16) + 2 (c % 16), lo 32 B further
+__device__ inline void q_store4(uint16_t* q, int64_t r, int64_t C, int64_t c, const float* v, float sc) {
+    uint32_t hi[2], lo[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const float s0 = v[2 * k] * sc, s1 = v[2 * k + 1] * sc;
+        const _Float16 h0 = (_Float16)s0, h1 = (_Float16)s1;
+        const _Float16 l0 = (_Float16)(s0 - (float)h0), l1 = (_Float16)(s1 - (float)h1);
+        hi[k] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+        lo[k] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+    }
+    uint16_t* base = q + r * 2 * C + 32 * (c >> 4) + (c & 15);
+    *reinterpret_cast<uint2*>(base) = make_uint2(hi[0], hi[1]);
+    *reinterpret_cast<uint2*>(base + 16) = make_uint2(lo[0], lo[1]);
+}
+// the bound's float bits, rounded up by 2^-10 (the apply pass's own fp32 rounding stays below it)
+__device__ inline void q_bound_out(double bnd, uint32_t* omax) {
+    const float f = (float)(bnd * (1.0 + 1.0 / 1024.0));
+    if (f > 0.f) atomicMax(omax, __float_as_uint(f));
+}
+
+// ---- forward: statistics partials (shifted sums; MAXD: also max |x - shift| per column, for the split bound),
+// finalize, apply
+template <int V, bool MAXD>
 __global__ __launch_bounds__(THREADS) void stats_kernel(Geo g, const float* __restrict__ x, float* __restrict__ ws) {
+    constexpr int NQ = MAXD ? 3 : 2;
     const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
     const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
     const bool valid = j0 < g.CS;
-    float p[2][V], K[V];
+    float p[NQ][V], K[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-        p[0][k] = p[1][k] = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) p[q][k] = 0.f;
         K[k] = valid ? x[((j0 + k) / g.S) * g.S] : 0.f;
     }
     if (valid) {
@@ -148,10 +186,11 @@ __global__ __launch_bounds__(THREADS) void stats_kernel(Geo g, const float* __re
                 const float d = v[k] - K[k];
                 p[0][k] += d;
                 p[1][k] = fmaf(d, d, p[1][k]);
+                if constexpr (MAXD) p[NQ - 1][k] = fmaxf(p[NQ - 1][k], fabsf(d));
             }
         }
     }
-    block_partials<V, 2>(g, p, valid, j0, ws);
+    block_partials<V, NQ, MAXD ? 2 : -1>(g, p, valid, j0, ws);
 }
 
 __device__ inline double block_sum_d(double v, double* red) {
@@ -174,11 +213,24 @@ inline int chan_groups(const Geo& g) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(MAXG, (cnt + 2047) / 2048));
 }
 
-template <int NQ>
+__device__ inline double block_max_d(double v, double* red) {
+    for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s = fmax(s, red[w]);
+    return s;
+}
+
+// quantity MAXQ (if in range) is a column max, reduced by max; reset: the split bound's word, zeroed in stream order
+// before the combine kernel's atomicMax
+template <int NQ, int MAXQ = -1>
 __global__ __launch_bounds__(THREADS) void chan_partial_kernel(Geo g, const float* __restrict__ ws,
-                                                               double* __restrict__ fin) {
+                                                               double* __restrict__ fin, uint32_t* __restrict__ reset) {
     __shared__ double red[THREADS / 64];
     const int c = blockIdx.x, G = gridDim.y, gi = blockIdx.y;
+    if (reset && c == 0 && gi == 0 && threadIdx.x == 0) *reset = 0u;
     const int S = (int)g.S, cnt = g.nrb * S;              // < 2^23: nrb * S <= 4096 * 1024 (make_geo)
     const int per = (cnt + G - 1) / G, i0 = gi * per, i1 = min(cnt, i0 + per);
     double acc[NQ];
@@ -188,25 +240,34 @@ __global__ __launch_bounds__(THREADS) void chan_partial_kernel(Geo g, const floa
         const int y = i / S, sidx = i - y * S;
         const int64_t col = (int64_t)c * g.S + sidx;
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[q] += ws[((int64_t)y * NQ + q) * g.CS + col];
+        for (int q = 0; q < NQ; ++q) {
+            const double v = ws[((int64_t)y * NQ + q) * g.CS + col];
+            acc[q] = q == MAXQ ? fmax(acc[q], v) : acc[q] + v;
+        }
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        const double v = block_sum_d(acc[q], red);
+        const double v = q == MAXQ ? block_max_d(acc[q], red) : block_sum_d(acc[q], red);
         if (threadIdx.x == 0) fin[((int64_t)c * G + gi) * NQ + q] = v;
     }
 }
 
+// fin: sum (x - shift), sum (x - shift)^2, max |x - shift| per channel.  stats[4 c + 3] = a bound of max |x - mean| (the
+// backward's split bound needs it); qb (split output): the channel's bound of |act(BN(x))| goes to omax (zeroed by
+// chan_partial_kernel)
 __global__ void stats_combine(Geo g, const float* __restrict__ x, const double* __restrict__ fin, int G, float eps,
                               float momentum, float* __restrict__ running_mean, float* __restrict__ running_var,
-                              float* __restrict__ stats, uint32_t* __restrict__ omax) {
+                              float* __restrict__ stats, uint32_t* __restrict__ omax, int qb,
+                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                              const float* __restrict__ alpha, int alpha_n, int act) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c == 0 && omax) *omax = 0u;                      // the apply pass's max, reset in stream order before it
+    if (!qb && c == 0 && omax) *omax = 0u;               // the apply pass's max, reset in stream order before it
     if (c >= g.C) return;
-    double s1 = 0.0, s2 = 0.0;
+    double s1 = 0.0, s2 = 0.0, dmax = 0.0;
     for (int gi = 0; gi < G; ++gi) {
-        s1 += fin[((int64_t)c * G + gi) * 2];
-        s2 += fin[((int64_t)c * G + gi) * 2 + 1];
+        s1 += fin[((int64_t)c * G + gi) * 3];
+        s2 += fin[((int64_t)c * G + gi) * 3 + 1];
+        dmax = fmax(dmax, fin[((int64_t)c * G + gi) * 3 + 2]);
     }
     const double n = (double)g.N * (double)g.S;
     const double m1 = s1 / n;
@@ -216,8 +277,17 @@ __global__ void stats_combine(Geo g, const float* __restrict__ x, const double* 
     const float hi = (float)mean;
     stats[4 * c] = hi;
     stats[4 * c + 1] = (float)(mean - (double)hi);
-    stats[4 * c + 2] = (float)(1.0 / sqrt(var + (double)eps));
-    stats[4 * c + 3] = 0.f;
+    const double rstd = 1.0 / sqrt(var + (double)eps);
+    stats[4 * c + 2] = (float)rstd;
+    // |x - mean| <= max |x - shift| + |shift - mean|; |z| <= |gamma rstd| that + |beta|; ReLU / PReLU scale by <= max(1, |slope|)
+    const double dev = dmax + fabs(m1);
+    stats[4 * c + 3] = (float)(dev * (1.0 + 1.0 / 1024.0));
+    if (qb) {
+        const double ga = gamma ? fabs((double)gamma[c]) : 1.0;
+        double bz = ga * rstd * dev + (beta ? fabs((double)beta[c]) : 0.0);
+        if (act == ACT_PRELU) bz *= fmax(1.0, fabs((double)alpha[alpha_n > 1 ? c : 0]));
+        q_bound_out(bz, omax);
+    }
     if (running_mean) running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
     if (running_var) running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * var * n / (n - 1.0));
 }
@@ -234,7 +304,7 @@ __global__ void eval_stats_kernel(int C, const float* __restrict__ rm, const flo
     }
 }
 
-template <int V, int ACT, bool RES>
+template <int V, int ACT, bool RES, bool QOUT = false>
 __global__ __launch_bounds__(THREADS) void apply_kernel(Geo g, const float* __restrict__ x, const float* __restrict__ res,
                                                         const float* __restrict__ stats, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, const float* __restrict__ alpha,
@@ -242,6 +312,21 @@ __global__ __launch_bounds__(THREADS) void apply_kernel(Geo g, const float* __re
     const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
     const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
     float m = 0.f;
+    if constexpr (QOUT) {                                 // S = 1, V = 4, no residual (host-checked)
+        const float sc = __builtin_ldexpf(1.f, q_split_exp(*ymax));
+        if (j0 < g.CS) {
+            ColConst<V, ACT> cc;
+            cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
+            for (int64_t r = (int64_t)blockIdx.y * g.RPI + ty; r < g.N; r += (int64_t)gridDim.y * g.RPI) {
+                float v[V];
+                vld<V>::ld(x + r * g.CS + j0, v);
+#pragma unroll
+                for (int k = 0; k < V; ++k) v[k] = act_fwd<ACT>(fmaf(cc.centred(v[k], k), cc.a[k], cc.b[k]), cc.al[k]);
+                q_store4(reinterpret_cast<uint16_t*>(y), r, g.CS, j0, v, sc);
+            }
+        }
+        return;
+    }
     if (j0 < g.CS) {
         ColConst<V, ACT> cc;
         cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
@@ -264,19 +349,22 @@ __global__ __launch_bounds__(THREADS) void apply_kernel(Geo g, const float* __re
 }
 
 // ---- backward: partials of sum dz, sum dz*xhat, PReLU slope; finalize; apply
-template <int V, int ACT, bool RES>
+template <int V, int ACT, bool RES, bool MAXDZ = false>
 __global__ __launch_bounds__(THREADS) void bwd_partial_kernel(Geo g, const float* __restrict__ x,
                                                               const float* __restrict__ res, const float* __restrict__ dy,
                                                               const float* __restrict__ stats,
                                                               const float* __restrict__ gamma, const float* __restrict__ beta,
                                                               const float* __restrict__ alpha, int alpha_n,
                                                               float* __restrict__ ws, float* __restrict__ dres) {
+    constexpr int NQ = MAXDZ ? 4 : 3;
     const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
     const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
     const bool valid = j0 < g.CS;
-    float p[3][V];
+    float p[NQ][V];
 #pragma unroll
-    for (int k = 0; k < V; ++k) p[0][k] = p[1][k] = p[2][k] = 0.f;
+    for (int k = 0; k < V; ++k)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) p[q][k] = 0.f;
     if (valid) {
         ColConst<V, ACT> cc;
         cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
@@ -295,24 +383,31 @@ __global__ __launch_bounds__(THREADS) void bwd_partial_kernel(Geo g, const float
                 p[0][k] += dz[k];
                 p[1][k] = fmaf(dz[k], xh, p[1][k]);
                 if (ACT == ACT_PRELU && !(z > 0.f)) p[2][k] = fmaf(gv[k], z, p[2][k]);
+                if constexpr (MAXDZ) p[3][k] = fmaxf(p[3][k], fabsf(dz[k]));
             }
             if (RES) vld<V>::st(dres + o, dz);
         }
     }
-    block_partials<V, 3>(g, p, valid, j0, ws);
+    block_partials<V, NQ, MAXDZ ? 3 : -1>(g, p, valid, j0, ws);
 }
 
+// qb (split output): fin carries a fourth quantity, max |dz|; the channel's bound of |dx| goes to omax (zeroed by
+// chan_partial_kernel): |dx| <= |gamma rstd| (max |dz| + |k1| + max |xhat| |k2|), max |xhat| from the forward's
+// stats[4 c + 3] (training; eval: |gamma rstd| max |dz|)
 __global__ void bwd_combine(Geo g, const double* __restrict__ fin, int G, int training, float* __restrict__ dgamma,
                             float* __restrict__ dbeta, float* __restrict__ dalpha_c, float* __restrict__ kbuf,
-                            uint32_t* __restrict__ omax) {
+                            uint32_t* __restrict__ omax, int qb, const float* __restrict__ stats,
+                            const float* __restrict__ gamma) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c == 0 && omax) *omax = 0u;                      // the apply pass's max, reset in stream order before it
+    if (!qb && c == 0 && omax) *omax = 0u;               // the apply pass's max, reset in stream order before it
     if (c >= g.C) return;
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    const int NQ = qb ? 4 : 3;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, dzmax = 0.0;
     for (int gi = 0; gi < G; ++gi) {
-        s0 += fin[((int64_t)c * G + gi) * 3];
-        s1 += fin[((int64_t)c * G + gi) * 3 + 1];
-        s2 += fin[((int64_t)c * G + gi) * 3 + 2];
+        s0 += fin[((int64_t)c * G + gi) * NQ];
+        s1 += fin[((int64_t)c * G + gi) * NQ + 1];
+        s2 += fin[((int64_t)c * G + gi) * NQ + 2];
+        if (qb) dzmax = fmax(dzmax, fin[((int64_t)c * G + gi) * NQ + 3]);
     }
     const double n = (double)g.N * (double)g.S;
     if (dbeta) dbeta[c] = (float)s0;
@@ -320,14 +415,20 @@ __global__ void bwd_combine(Geo g, const double* __restrict__ fin, int G, int tr
     if (dalpha_c) dalpha_c[c] = (float)s2;
     kbuf[2 * c] = training ? (float)(s0 / n) : 0.f;
     kbuf[2 * c + 1] = training ? (float)(s1 / n) : 0.f;
+    if (qb) {
+        const double rstd = (double)stats[4 * c + 2];
+        const double ga = (gamma ? fabs((double)gamma[c]) : 1.0) * rstd;
+        const double b = training ? dzmax + fabs(s0 / n) + (double)stats[4 * c + 3] * rstd * fabs(s1 / n) : dzmax;
+        q_bound_out(ga * b, omax);
+    }
 }
 
-template <int V, int ACT, bool RES>
+template <int V, int ACT, bool RES, bool QOUT = false>
 __device__ inline void bwd_apply_cols(const Geo& g, int64_t j0, int ty, const float* __restrict__ x,
                                       const float* __restrict__ dy, const float* __restrict__ dres,
                                       const float* __restrict__ stats, const float* __restrict__ gamma,
                                       const float* __restrict__ beta, const float* __restrict__ alpha, int alpha_n,
-                                      const float* __restrict__ kbuf, float* __restrict__ dx, float& m) {
+                                      const float* __restrict__ kbuf, float* __restrict__ dx, float& m, float qsc = 1.f) {
     ColConst<V, ACT> cc;
     cc.load(g, j0, stats, gamma, beta, alpha, alpha_n);
     float k1[V], k2[V];
@@ -353,13 +454,14 @@ __device__ inline void bwd_apply_cols(const Geo& g, int64_t j0, int ty, const fl
         for (int k = 0; k < V; ++k) {
             const float xh = cc.centred(v[k], k) * cc.rstd[k];
             v[k] = cc.a[k] * (dz[k] - k1[k] - xh * k2[k]);
-            m = fmaxf(m, fabsf(v[k]));
+            if constexpr (!QOUT) m = fmaxf(m, fabsf(v[k]));
         }
-        vld<V>::st(dx + o, v);
+        if constexpr (QOUT) q_store4(reinterpret_cast<uint16_t*>(dx), r, g.CS, j0, v, qsc);
+        else vld<V>::st(dx + o, v);
     }
 }
 
-template <int V, int ACT, bool RES>
+template <int V, int ACT, bool RES, bool QOUT = false>
 __global__ __launch_bounds__(THREADS) void bwd_apply_kernel(Geo g, const float* __restrict__ x,
                                                             const float* __restrict__ dy, const float* __restrict__ dres,
                                                             const float* __restrict__ stats,
@@ -370,6 +472,12 @@ __global__ __launch_bounds__(THREADS) void bwd_apply_kernel(Geo g, const float* 
     const int tx = threadIdx.x % g.TW, ty = threadIdx.x / g.TW;
     const int64_t j0 = ((int64_t)blockIdx.x * g.TW + tx) * V;
     float m = 0.f;
+    if constexpr (QOUT) {                                 // S = 1, V = 4 (host-checked)
+        const float sc = __builtin_ldexpf(1.f, q_split_exp(*dxmax));
+        if (j0 < g.CS)
+            bwd_apply_cols<V, ACT, RES, true>(g, j0, ty, x, dy, dres, stats, gamma, beta, alpha, alpha_n, kbuf, dx, m, sc);
+        return;
+    }
     if (j0 < g.CS) bwd_apply_cols<V, ACT, RES>(g, j0, ty, x, dy, dres, stats, gamma, beta, alpha, alpha_n, kbuf, dx, m);
     if (dxmax) block_max_out(m, dxmax);                  // workgroup-uniform condition
 }
@@ -405,7 +513,7 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline double* fin_ptr(float* workspace, const Geo& g) {
     const Geo g1 = make_geo(g.N, g.C, g.S, 1), g4 = make_geo(g.N, g.C, g.S, 4);
     const int64_t nrb = std::max(g1.nrb, g4.nrb);
-    const uintptr_t p = (uintptr_t)(workspace + 3 * nrb * g.CS + 2 * (int64_t)g.C);
+    const uintptr_t p = (uintptr_t)(workspace + 4 * nrb * g.CS + 2 * (int64_t)g.C);
     return reinterpret_cast<double*>((p + 15) & ~(uintptr_t)15);
 }
 
@@ -423,6 +531,19 @@ struct dispatch {
     }
 };
 template <int V, int A, bool R> struct ApplyK { static constexpr auto fn = apply_kernel<V, A, R>; };
+template <int V, int A, bool R> struct ApplyQK { static constexpr auto fn = apply_kernel<V, A, R, true>; };
+template <int V, int A, bool R> struct BwdPartQK { static constexpr auto fn = bwd_partial_kernel<V, A, R, true>; };
+template <int V, int A, bool R> struct BwdApplyQK { static constexpr auto fn = bwd_apply_kernel<V, A, R, true>; };
+// the split-output kernels: V = 4, no residual
+template <template <int, int, bool> class K>
+struct dispatch_q {
+    template <typename... A>
+    static void run(int act, dim3 grid, hipStream_t st, A... a) {
+        if (act == ACT_NONE) hipLaunchKernelGGL((K<4, ACT_NONE, false>::fn), grid, dim3(THREADS), 0, st, a...);
+        else if (act == ACT_RELU) hipLaunchKernelGGL((K<4, ACT_RELU, false>::fn), grid, dim3(THREADS), 0, st, a...);
+        else hipLaunchKernelGGL((K<4, ACT_PRELU, false>::fn), grid, dim3(THREADS), 0, st, a...);
+    }
+};
 template <int V, int A, bool R> struct BwdPartK { static constexpr auto fn = bwd_partial_kernel<V, A, R>; };
 template <int V, int A, bool R> struct BwdApplyK { static constexpr auto fn = bwd_apply_kernel<V, A, R>; };
 
@@ -438,41 +559,103 @@ int64_t avse_bnact_workspace_bytes(int64_t N, int64_t C, int64_t S) {
     const Geo g = make_geo(N, C, S, 1);                 // V = 1 has the most row blocks
     const Geo g4 = make_geo(N, C, S, 4);
     const int64_t nrb = std::max(g.nrb, g4.nrb);
-    // column partials (3 rows of C*S per row block), kbuf (2 C floats), then 8-aligned fp64 per-channel partials
-    return 4 * (3 * nrb * C * S + 2 * C) + 16 + 8 * (int64_t)C * MAXG * 3;
+    // column partials (up to 4 rows of C*S per row block), kbuf (2 C floats), then 8-aligned fp64 per-channel partials
+    return 4 * (4 * nrb * C * S + 2 * C) + 16 + 8 * (int64_t)C * MAXG * 4;
 }
 
-int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* gamma,
-                   const float* beta, int32_t act, const float* alpha, int32_t alpha_n, int32_t training, float eps,
-                   float momentum, float* running_mean, float* running_var, float* stats, float* y, float* workspace,
-                   uint32_t* y_max, avse_stream_t stream) {
+static int bnact_fwd_impl(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* gamma,
+                          const float* beta, int32_t act, const float* alpha, int32_t alpha_n, int32_t training, float eps,
+                          float momentum, float* running_mean, float* running_var, float* stats, float* y,
+                          float* workspace, uint32_t* y_max, bool qout, hipStream_t st) {
     if (!x || !y || !stats || !workspace || (act == ACT_PRELU && !alpha)) return AVSE_EINVAL;
     if (!training && (!running_mean || !running_var)) return AVSE_EINVAL;
     if (!shape_ok(N, C, S) || act < ACT_NONE || act > ACT_PRELU) return AVSE_ESHAPE;
     if (act == ACT_PRELU && alpha_n != 1 && alpha_n != C) return AVSE_ESHAPE;
     if (training && N * S < 2) return AVSE_ESHAPE;       // as torch: more than one value per channel
     const int V = ((C * S) % 4 == 0 && al16(x) && al16(y) && (!res || al16(res)) && al16(workspace)) ? 4 : 1;
+    if (qout && (!y_max || !training || res || S != 1 || C % 64 || V != 4)) return AVSE_ESHAPE;
     const Geo g = make_geo(N, C, S, V);
-    hipStream_t st = (hipStream_t)stream;
     const dim3 grid(g.tiles, g.nrb);
     if (training) {
-        if (V == 4) hipLaunchKernelGGL(stats_kernel<4>, grid, dim3(THREADS), 0, st, g, x, workspace);
-        else hipLaunchKernelGGL(stats_kernel<1>, grid, dim3(THREADS), 0, st, g, x, workspace);
+        if (V == 4) hipLaunchKernelGGL((stats_kernel<4, true>), grid, dim3(THREADS), 0, st, g, x, workspace);
+        else hipLaunchKernelGGL((stats_kernel<1, true>), grid, dim3(THREADS), 0, st, g, x, workspace);
         AVSE_CHECK_LAUNCH();
         const int G = chan_groups(g);
         double* fin = fin_ptr(workspace, g);
-        hipLaunchKernelGGL(chan_partial_kernel<2>, dim3((unsigned)C, G), dim3(THREADS), 0, st, g, (const float*)workspace,
-                           fin);
+        hipLaunchKernelGGL((chan_partial_kernel<3, 2>), dim3((unsigned)C, G), dim3(THREADS), 0, st, g,
+                           (const float*)workspace, fin, qout ? y_max : (uint32_t*)nullptr);
         AVSE_CHECK_LAUNCH();
         hipLaunchKernelGGL(stats_combine, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, g, x, (const double*)fin,
-                           G, eps, momentum, running_mean, running_var, stats, y_max);
+                           G, eps, momentum, running_mean, running_var, stats, y_max, (int)qout, gamma, beta, alpha,
+                           (int)alpha_n, (int)act);
     } else {
         hipLaunchKernelGGL(eval_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, (int)C, running_mean,
                            running_var, eps, stats, y_max);
     }
     AVSE_CHECK_LAUNCH();
-    dispatch<ApplyK>::run(V, act, res != nullptr, grid, st, g, x, res, (const float*)stats, gamma, beta, alpha,
-                          (int)alpha_n, y, y_max);
+    if (qout)
+        dispatch_q<ApplyQK>::run(act, grid, st, g, x, res, (const float*)stats, gamma, beta, alpha, (int)alpha_n, y, y_max);
+    else
+        dispatch<ApplyK>::run(V, act, res != nullptr, grid, st, g, x, res, (const float*)stats, gamma, beta, alpha,
+                              (int)alpha_n, y, y_max);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_bnact_fwd(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* gamma,
+                   const float* beta, int32_t act, const float* alpha, int32_t alpha_n, int32_t training, float eps,
+                   float momentum, float* running_mean, float* running_var, float* stats, float* y, float* workspace,
+                   uint32_t* y_max, avse_stream_t stream) {
+    return bnact_fwd_impl(N, C, S, x, res, gamma, beta, act, alpha, alpha_n, training, eps, momentum, running_mean,
+                          running_var, stats, y, workspace, y_max, false, (hipStream_t)stream);
+}
+
+int avse_bnact_fwd_q(int64_t N, int64_t C, int64_t S, const float* x, const float* gamma, const float* beta, int32_t act,
+                     const float* alpha, int32_t alpha_n, float eps, float momentum, float* running_mean,
+                     float* running_var, float* stats, void* yq, float* workspace, uint32_t* y_bound,
+                     avse_stream_t stream) {
+    return bnact_fwd_impl(N, C, S, x, nullptr, gamma, beta, act, alpha, alpha_n, 1, eps, momentum, running_mean,
+                          running_var, stats, (float*)yq, workspace, y_bound, true, (hipStream_t)stream);
+}
+
+static int bnact_bwd_impl(int64_t N, int64_t C, int64_t S, const float* x, const float* res, const float* dy,
+                          const float* stats, const float* gamma, const float* beta, int32_t act, const float* alpha,
+                          int32_t alpha_n, int32_t training, float* dx, float* dres, float* dgamma, float* dbeta,
+                          float* dalpha_c, float* workspace, uint32_t* dx_max, bool qout, hipStream_t st) {
+    if (!x || !dy || !stats || !dx || !workspace || (act == ACT_PRELU && (!alpha || !dalpha_c)) || (res && !dres))
+        return AVSE_EINVAL;
+    if (!shape_ok(N, C, S) || act < ACT_NONE || act > ACT_PRELU) return AVSE_ESHAPE;
+    if (act == ACT_PRELU && alpha_n != 1 && alpha_n != C) return AVSE_ESHAPE;
+    const int V = ((C * S) % 4 == 0 && al16(x) && al16(dy) && al16(dx) && (!res || (al16(res) && al16(dres))) &&
+                   al16(workspace)) ? 4 : 1;
+    if (qout && (!dx_max || res || S != 1 || C % 64 || V != 4)) return AVSE_ESHAPE;
+    const Geo g = make_geo(N, C, S, V);
+    const dim3 grid(g.tiles, g.nrb);
+    float* kbuf = workspace + 4 * (int64_t)g.nrb * g.CS;
+    const int G = chan_groups(g);
+    double* fin = fin_ptr(workspace, g);
+    if (qout) {
+        dispatch_q<BwdPartQK>::run(act, grid, st, g, x, res, dy, stats, gamma, beta, alpha, (int)alpha_n, workspace, dres);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL((chan_partial_kernel<4, 3>), dim3((unsigned)C, G), dim3(THREADS), 0, st, g,
+                           (const float*)workspace, fin, dx_max);
+    } else {
+        dispatch<BwdPartK>::run(V, act, res != nullptr, grid, st, g, x, res, dy, stats, gamma, beta, alpha, (int)alpha_n,
+                                workspace, dres);
+        AVSE_CHECK_LAUNCH();
+        hipLaunchKernelGGL((chan_partial_kernel<3>), dim3((unsigned)C, G), dim3(THREADS), 0, st, g,
+                           (const float*)workspace, fin, (uint32_t*)nullptr);
+    }
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bwd_combine, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, g, (const double*)fin, G,
+                       (int)training, dgamma, dbeta, dalpha_c, kbuf, dx_max, (int)qout, stats, gamma);
+    AVSE_CHECK_LAUNCH();
+    if (qout)
+        dispatch_q<BwdApplyQK>::run(act, grid, st, g, x, dy, (const float*)dres, stats, gamma, beta, alpha, (int)alpha_n,
+                                   (const float*)kbuf, dx, dx_max);
+    else
+        dispatch<BwdApplyK>::run(V, act, res != nullptr, grid, st, g, x, dy, (const float*)dres, stats, gamma, beta,
+                                 alpha, (int)alpha_n, (const float*)kbuf, dx, dx_max);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
@@ -481,31 +664,16 @@ int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float*
                    const float* gamma, const float* beta, int32_t act, const float* alpha, int32_t alpha_n,
                    int32_t training, float* dx, float* dres, float* dgamma, float* dbeta, float* dalpha_c,
                    float* workspace, uint32_t* dx_max, avse_stream_t stream) {
-    if (!x || !dy || !stats || !dx || !workspace || (act == ACT_PRELU && (!alpha || !dalpha_c)) || (res && !dres))
-        return AVSE_EINVAL;
-    if (!shape_ok(N, C, S) || act < ACT_NONE || act > ACT_PRELU) return AVSE_ESHAPE;
-    if (act == ACT_PRELU && alpha_n != 1 && alpha_n != C) return AVSE_ESHAPE;
-    const int V = ((C * S) % 4 == 0 && al16(x) && al16(dy) && al16(dx) && (!res || (al16(res) && al16(dres))) &&
-                   al16(workspace)) ? 4 : 1;
-    const Geo g = make_geo(N, C, S, V);
-    hipStream_t st = (hipStream_t)stream;
-    const dim3 grid(g.tiles, g.nrb);
-    float* kbuf = workspace + 3 * (int64_t)g.nrb * g.CS;
-    dispatch<BwdPartK>::run(V, act, res != nullptr, grid, st, g, x, res, dy, stats, gamma, beta, alpha, (int)alpha_n,
-                            workspace, dres);
-    AVSE_CHECK_LAUNCH();
-    const int G = chan_groups(g);
-    double* fin = fin_ptr(workspace, g);
-    hipLaunchKernelGGL(chan_partial_kernel<3>, dim3((unsigned)C, G), dim3(THREADS), 0, st, g, (const float*)workspace,
-                       fin);
-    AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(bwd_combine, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, g, (const double*)fin, G,
-                       (int)training, dgamma, dbeta, dalpha_c, kbuf, dx_max);
-    AVSE_CHECK_LAUNCH();
-    dispatch<BwdApplyK>::run(V, act, res != nullptr, grid, st, g, x, dy, (const float*)dres, stats, gamma, beta, alpha,
-                             (int)alpha_n, (const float*)kbuf, dx, dx_max);
-    AVSE_CHECK_LAUNCH();
-    return AVSE_OK;
+    return bnact_bwd_impl(N, C, S, x, res, dy, stats, gamma, beta, act, alpha, alpha_n, training, dx, dres, dgamma,
+                          dbeta, dalpha_c, workspace, dx_max, false, (hipStream_t)stream);
+}
+
+int avse_bnact_bwd_q(int64_t N, int64_t C, int64_t S, const float* x, const float* dy, const float* stats,
+                     const float* gamma, const float* beta, int32_t act, const float* alpha, int32_t alpha_n,
+                     int32_t training, void* dxq, float* dgamma, float* dbeta, float* dalpha_c, float* workspace,
+                     uint32_t* dx_bound, avse_stream_t stream) {
+    return bnact_bwd_impl(N, C, S, x, nullptr, dy, stats, gamma, beta, act, alpha, alpha_n, training, (float*)dxq,
+                          nullptr, dgamma, dbeta, dalpha_c, workspace, dx_bound, true, (hipStream_t)stream);
 }
 
 }  // extern "C"

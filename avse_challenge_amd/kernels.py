@@ -483,9 +483,13 @@ def dconv_split_ok(x, dilation):
 
 def split16(x, maxbits):
     """x (N, 64, H, W) fp32 (channels-last memory is read as it lies, anything else made so) -> its fp16 hi / lo split
-    in dconv.hip's Q4 layout (uint8 (N*H*W, 256)); writes max |x| (float bits) into maxbits[0]."""
+    in dconv.hip's Q4 layout (uint8 (N*H*W, 256)); writes max |x| (float bits) into maxbits[0].  A split-output
+    tensor (bnact_fwd / bnact_bwd with q_out) already holds those bytes: returned as its uint8 view, no pass."""
     _need_gpu(x)
     known = _known_absmax(x)
+    if is_split_q(x):
+        maxbits[:1].copy_(known)
+        return q_view(x)
     x = x.contiguous(memory_format=torch.channels_last)
     npix = x.shape[0] * x.shape[2] * x.shape[3]
     xq = torch.empty((npix, 256), device=x.device, dtype=torch.uint8)
@@ -615,8 +619,11 @@ def split_nhwc(x, maxbits):
 
 
 def split_q(x):
-    """-> (xq, xmax): split_nhwc with the producer's max when x carries one (no absmax pass), else a fresh max."""
+    """-> (xq, xmax): split_nhwc with the producer's max when x carries one (no absmax pass), else a fresh max; a
+    split-output tensor as its uint8 view (no pass)."""
     known = _known_absmax(x)
+    if is_split_q(x):
+        return q_view(x), known
     if known is None:
         xm = torch.empty(1, device=x.device, dtype=torch.int32)
         return split_nhwc(x, xm), xm
@@ -840,8 +847,45 @@ def _opt(t):
     return ptr(t) if t is not None else None
 
 
-def bnact_fwd(x, gamma, beta, running_mean, running_var, training, momentum, eps, act=ACT_NONE, alpha=None, res=None):
-    """act(BatchNorm(x) [+ res]); returns (y, stats (C, 4) = mean hi, mean lo, rstd, 0).  y keeps x's format."""
+# Split-output tensors (round 5): bnact_fwd / bnact_bwd with q_out write their channels-last output directly as the
+# fp16 hi / lo split of the split-fp16 convolutions (csrc/bnact.hip, "Q" layout: per pixel C / 16 chunks of [hi 16]
+# [lo 16]) into an fp32 tensor of the output's shape (the same bytes), marked with SPLITQ_ATTR and the bound of its
+# max |.| (ABSMAX_ATTR).  Only a split consumer may read it (split16 / split_q return its bytes as they are): the
+# layers request it where the next convolution (forward) or the previous one (backward) is a split-fp16 kernel.
+SPLITQ_ATTR = "_avse_splitq"
+
+
+def is_split_q(t):
+    return getattr(t, SPLITQ_ATTR, False) is True
+
+
+def q_view(t):
+    """The uint8 (N*H*W, 4 C) view of a split-output (N, C, H, W) channels-last tensor."""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c).view(torch.uint8)
+
+
+def positive(t):
+    """t > 0 elementwise (logical shape), for a split-output tensor from its fp16 hi / lo planes (the sign of hi + lo)."""
+    if not is_split_q(t):
+        return t > 0
+    n, c, h, w = t.shape
+    q = q_view(t).view(torch.float16).reshape(-1, c // 16, 2, 16)
+    pos = (q[:, :, 0, :] > 0) | ((q[:, :, 0, :] == 0) & (q[:, :, 1, :] > 0))
+    return pos.reshape(n, h, w, c).permute(0, 3, 1, 2)
+
+
+def _q_ok(x, res):
+    v = _bn_view(x)
+    return (res is None and x.dim() == 4 and v is not None and v[2] == 1 and x.shape[1] % 64 == 0
+            and not x.is_contiguous() and x.data_ptr() % 16 == 0)
+
+
+def bnact_fwd(x, gamma, beta, running_mean, running_var, training, momentum, eps, act=ACT_NONE, alpha=None, res=None,
+              q_out=False):
+    """act(BatchNorm(x) [+ res]); returns (y, stats (C, 4) = mean hi, mean lo, rstd, bound of max |x - mean|).  y keeps
+    x's format.  q_out (training, channels-last, C % 64 == 0, no residual; otherwise ignored): y is a split-output
+    tensor (SPLITQ_ATTR)."""
     _need_gpu(x)
     if x.dtype != torch.float32:
         raise RuntimeError("bnact kernels are fp32")
@@ -856,6 +900,14 @@ def bnact_fwd(x, gamma, beta, running_mean, running_var, training, momentum, eps
     ws = torch.empty((L.avse_bnact_workspace_bytes(N, C, S) + 3) // 4, device=x.device, dtype=torch.float32)
     a = alpha.float().contiguous() if alpha is not None else None
     ymax = torch.empty(1, device=x.device, dtype=torch.int32)
+    if q_out and training and _q_ok(x, res):
+        check(L.avse_bnact_fwd_q(N, C, S, ptr(x), _opt(gamma), _opt(beta), int(act), _opt(a),
+                                 a.numel() if a is not None else 0, float(eps), float(momentum), _opt(running_mean),
+                                 _opt(running_var), ptr(stats), ptr(y), ptr(ws), ptr(ymax), stream_ptr(x.device)),
+              "avse_bnact_fwd_q")
+        _set_absmax(y, ymax)
+        setattr(y, SPLITQ_ATTR, True)
+        return y, stats
     check(L.avse_bnact_fwd(N, C, S, ptr(x), _opt(res), _opt(gamma), _opt(beta), int(act), _opt(a),
                            a.numel() if a is not None else 0, int(bool(training)), float(eps), float(momentum),
                            _opt(running_mean), _opt(running_var), ptr(stats), ptr(y), ptr(ws), ptr(ymax),
@@ -879,8 +931,9 @@ def _known_absmax(t):
     return mb if isinstance(mb, torch.Tensor) and mb.device == t.device else None
 
 
-def bnact_bwd(x, res, dy, stats, gamma, beta, act, alpha, training):
-    """-> (dx, dres or None, dgamma, dbeta, dalpha (alpha's shape) or None)."""
+def bnact_bwd(x, res, dy, stats, gamma, beta, act, alpha, training, q_out=False):
+    """-> (dx, dres or None, dgamma, dbeta, dalpha (alpha's shape) or None).  q_out (channels-last, C % 64 == 0, no
+    residual; otherwise ignored): dx is a split-output tensor (SPLITQ_ATTR)."""
     _need_gpu(x, dy, stats)
     N, C, S = _bn_view(x)
     dy = _same_layout(dy.float(), x)
@@ -895,9 +948,18 @@ def bnact_bwd(x, res, dy, stats, gamma, beta, act, alpha, training):
     L = _lib.lib()
     ws = torch.empty((L.avse_bnact_workspace_bytes(N, C, S) + 3) // 4, device=x.device, dtype=torch.float32)
     dxmax = torch.empty(1, device=x.device, dtype=torch.int32)
-    check(L.avse_bnact_bwd(N, C, S, ptr(x), _opt(res), ptr(dy), ptr(stats), _opt(gamma), _opt(beta), int(act), _opt(a),
-                           a.numel() if a is not None else 0, int(bool(training)), ptr(dx), _opt(dres), ptr(dgamma),
-                           ptr(dbeta), _opt(dalpha_c), ptr(ws), ptr(dxmax), stream_ptr(x.device)), "avse_bnact_bwd")
+    q = q_out and _q_ok(x, res) and dy.data_ptr() % 16 == 0
+    if q:
+        check(L.avse_bnact_bwd_q(N, C, S, ptr(x), ptr(dy), ptr(stats), _opt(gamma), _opt(beta), int(act), _opt(a),
+                                 a.numel() if a is not None else 0, int(bool(training)), ptr(dx), ptr(dgamma),
+                                 ptr(dbeta), _opt(dalpha_c), ptr(ws), ptr(dxmax), stream_ptr(x.device)),
+              "avse_bnact_bwd_q")
+        setattr(dx, SPLITQ_ATTR, True)
+    else:
+        check(L.avse_bnact_bwd(N, C, S, ptr(x), _opt(res), ptr(dy), ptr(stats), _opt(gamma), _opt(beta), int(act),
+                               _opt(a), a.numel() if a is not None else 0, int(bool(training)), ptr(dx), _opt(dres),
+                               ptr(dgamma), ptr(dbeta), _opt(dalpha_c), ptr(ws), ptr(dxmax), stream_ptr(x.device)),
+              "avse_bnact_bwd")
     _set_absmax(dx, dxmax)
     dalpha = None
     if a is not None:

@@ -57,26 +57,36 @@ class _BNActFn(torch.autograd.Function):
     """act(BatchNorm(x) [+ res]) in two HBM passes forward and two backward (csrc/bnact.hip)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, alpha, res, running_mean, running_var, training, momentum, eps, act):
+    def forward(ctx, x, gamma, beta, alpha, res, running_mean, running_var, training, momentum, eps, act, q_fwd, q_bwd):
         if K._bn_view(x) is None:                  # neither contiguous nor channels-last: the layout the kernels read
             x = x.contiguous()
-        y, stats = K.bnact_fwd(x, gamma, beta, running_mean, running_var, training, momentum, eps, act, alpha, res)
+        y, stats = K.bnact_fwd(x, gamma, beta, running_mean, running_var, training, momentum, eps, act, alpha, res,
+                               q_out=q_fwd)
         ctx.save_for_backward(x, res, stats, gamma, beta, alpha)
-        ctx.act, ctx.training = act, training
+        ctx.act, ctx.training, ctx.q_bwd = act, training, q_bwd
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, res, stats, gamma, beta, alpha = ctx.saved_tensors
-        dx, dres, dgamma, dbeta, dalpha = K.bnact_bwd(x, res, dy, stats, gamma, beta, ctx.act, alpha, ctx.training)
+        dx, dres, dgamma, dbeta, dalpha = K.bnact_bwd(x, res, dy, stats, gamma, beta, ctx.act, alpha, ctx.training,
+                                                      q_out=ctx.q_bwd)
         return (dx, dgamma if ctx.needs_input_grad[1] else None, dbeta if ctx.needs_input_grad[2] else None,
-                dalpha if ctx.needs_input_grad[3] else None, dres, None, None, None, None, None, None)
+                dalpha if ctx.needs_input_grad[3] else None, dres, None, None, None, None, None, None, None, None)
 
 
-def bn_act(x, bn, act=None, res=None, folded_bias=None):
+# split-output BatchNorm passes (bn_act q_fwd / q_bwd); "0": fp32 outputs + the consumer's split pass (A/B)
+_BNACT_Q = os.environ.get("AVSE_BNACT_Q", "1") == "1"
+
+
+def bn_act(x, bn, act=None, res=None, folded_bias=None, q_fwd=False, q_bwd=False):
     """act(bn(x) [+ res]) for an nn.BatchNorm{1,2,3}d `bn` (its parameters, buffers, momentum and eps; running
     statistics and num_batches_tracked updated in train mode as torch does).  act: None, "relu" or a PReLU module.
     x: fp32 contiguous or channels-last; the output keeps x's memory format.
+    q_fwd / q_bwd (round 5): the output / the input gradient as a split-output tensor (kernels.SPLITQ_ATTR) -- ONLY
+    when its sole consumer is a split-fp16 convolution: the next conv's forward (q_fwd; DilatedConv2d.q_ok /
+    TrunkConv2d.q_ok) or the producing conv's backward (q_bwd; q_ok(..., grad=True)).  Ignored where the kernels
+    cannot produce it (eval forward, residual, NCHW).
     folded_bias (training mode only): x is a convolution output whose per-channel bias was left out; the result is
     act(bn(x + bias)) — equal to act(bn(x)), the batch statistics shift with the bias — and the running mean takes
     the bias in (momentum * bias)."""
@@ -84,7 +94,7 @@ def bn_act(x, bn, act=None, res=None, folded_bias=None):
         if not (bn.training and bn.track_running_stats) or res is not None or bn.momentum is None:
             raise RuntimeError("bn_act: folded_bias needs a training-mode BatchNorm with running stats and a momentum "
                                "(not the cumulative average), no residual")
-        y = bn_act(x, bn, act)
+        y = bn_act(x, bn, act, q_fwd=q_fwd, q_bwd=q_bwd)
         # through .data, as the kernel's own running-stat update: no version bump (under DDP the BatchNorm buffers are
         # views of one flat tensor, and a bump would invalidate every library BatchNorm's saved running stats)
         bn.running_mean.data.add_(folded_bias.detach(), alpha=bn.momentum)
@@ -108,7 +118,8 @@ def bn_act(x, bn, act=None, res=None, folded_bias=None):
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
     return _BNActFn.apply(x.float(), bn.weight, bn.bias, alpha, res, rm, rv, training,
-                          bn.momentum if bn.momentum is not None else 0.0, bn.eps, code)
+                          bn.momentum if bn.momentum is not None else 0.0, bn.eps, code, _BNACT_Q and bool(q_fwd),
+                          _BNACT_Q and bool(q_bwd))
 
 
 class _MaxPoolPlanesFn(torch.autograd.Function):
@@ -225,6 +236,8 @@ class _DilatedConvFn(torch.autograd.Function):
     def forward(ctx, x, w, b, dilation, add_bias):
         ctx.dilation = dilation
         ctx.split = _DCONV_SPLIT and K.dconv_split_ok(x, dilation)
+        if K.is_split_q(x) and not ctx.split:
+            raise RuntimeError("_DilatedConvFn: a split-output input needs the split path (DilatedConv2d.q_ok)")
         if ctx.split:
             # the fp16 hi / lo split of x is made once and kept for the weight gradient in place of x (same bytes)
             mb = torch.empty(2, device=x.device, dtype=torch.int32)
@@ -385,6 +398,11 @@ class DilatedConv2d(nn.Conv2d):
                 and self.out_channels == 64 and self.dilation[0] <= K.DCONV_WGRAD_MAX_DIL
                 and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
                 and x.numel() < (1 << 29))
+
+    def q_ok(self, x, grad=False):
+        """True when this conv's forward (or, grad=True, its backward) takes a split-output tensor for an input of x's
+        shape and layout (the split-fp16 path of _DilatedConvFn)."""
+        return (not self.conv1_ok(x)) and self.hip_ok(x) and _DCONV_SPLIT and K.dconv_split_ok(x, self.dilation[0])
 
     def forward(self, x, bias_to_bn=False):
         if self.conv1_ok(x):
@@ -578,6 +596,8 @@ class _SConvFn(torch.autograd.Function):
         xq, xm, w = ctx.saved_tensors
         s, shape = ctx.stride, ctx.shape
         dyq, dym = K.split_q(dy)                   # (the incoming gradient keeps its producer's max, if any)
+        if K.is_split_q(dy) and s != 1 and ctx.needs_input_grad[0]:
+            raise RuntimeError("_SConvFn: the stride-2 input gradient needs an fp32 output gradient (TrunkConv2d.q_ok)")
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
@@ -600,10 +620,18 @@ class TrunkConv2d(nn.Conv2d):
     def __init__(self, cin, cout, stride=1):
         super().__init__(cin, cout, 3, stride=stride, padding=1, bias=False)
 
+    def _sconv(self, x):
+        return (_SCONV and x.is_contiguous(memory_format=torch.channels_last) and x.dtype == self.weight.dtype
+                and K.sconv_ok(x, self.out_channels, self.stride[0]))
+
+    def q_ok(self, x, grad=False):
+        """True when this conv's forward (grad=True: its backward, given its input x) takes a split-output tensor:
+        the sconv path, and for the backward stride 1 (the stride-2 input gradient is MIOpen's, on fp32)."""
+        return self._sconv(x) and (not grad or self.stride[0] == 1)
+
     def forward(self, x):
         s = self.stride[0]
-        if (_SCONV and x.is_contiguous(memory_format=torch.channels_last) and x.dtype == self.weight.dtype
-                and K.sconv_ok(x, self.out_channels, s)):
+        if self._sconv(x):
             return _SConvFn.apply(x, self.weight, s)
         if gemm_conv_ok(x, 3, s):                          # small frames: one GEMM over all pixels (_GemmConvFn)
             return _GemmConvFn.apply(x, self.weight, s)

@@ -249,7 +249,8 @@ int avse_prelu_nhwc_bwd(int64_t R, int64_t C, int32_t num_params, const float* x
  * (S = H*W, T*H*W) or channels-last NHWC (N = batch*H*W, S = 1).  act: 0 none, 1 ReLU, 2 PReLU (alpha_n 1 or C).
  * training != 0: batch statistics (biased variance for the normalisation), running_mean / running_var (may be
  * null) updated with momentum and the unbiased variance, as nn.BatchNorm{1,2,3}d in train mode; training == 0:
- * the running statistics.  stats (C, 4) = (mean as a float pair hi + lo, rstd, 0) written by fwd, read by bwd.  gamma / beta may be null
+ * the running statistics.  stats (C, 4) = (mean as a float pair hi + lo, rstd, bound of max |x - mean| in training /
+ * 0 in eval) written by fwd, read by bwd.  gamma / beta may be null
  * (affine=False).  bwd writes dx, dgamma, dbeta (C, may be null), the per-channel PReLU slope gradient
  * dalpha_c (C; sum it for a single slope) and, with res, dres (= the gradient of the pre-activation).
  * Replaces nn.BatchNorm3d/2d + nn.PReLU / F.relu (+ the residual add) of the avse1 lip front-end and ResNet
@@ -266,6 +267,20 @@ int avse_bnact_bwd(int64_t N, int64_t C, int64_t S, const float* x, const float*
                    const float* gamma, const float* beta, int32_t act, const float* alpha, int32_t alpha_n,
                    int32_t training, float* dx, float* dres, float* dgamma, float* dbeta, float* dalpha_c,
                    float* workspace, uint32_t* dx_max, avse_stream_t stream);
+/* The same passes with the output written as the fp16 hi / lo split the split-fp16 convolutions read (avse_split16's
+ * Q layout: per pixel C / 16 chunks of 64 B = [hi of 16 channels][lo of 16 channels], the size of the fp32 tensor), in
+ * place of fp32 y / dx + a separate split pass.  The scale comes from an upper bound of max |y| / |dx| assembled from
+ * the per-channel statistics, written as float bits to y_bound / dx_bound (which the consumer passes on as the split's
+ * max).  Channels-last only (S = 1, C % 64 == 0, 16-B aligned pointers), no residual; the forward in training mode;
+ * the backward with the stats of a training-mode forward (or eval).  Returns AVSE_ESHAPE otherwise. */
+int avse_bnact_fwd_q(int64_t N, int64_t C, int64_t S, const float* x, const float* gamma, const float* beta, int32_t act,
+                     const float* alpha, int32_t alpha_n, float eps, float momentum, float* running_mean,
+                     float* running_var, float* stats, void* yq, float* workspace, uint32_t* y_bound,
+                     avse_stream_t stream);
+int avse_bnact_bwd_q(int64_t N, int64_t C, int64_t S, const float* x, const float* dy, const float* stats,
+                     const float* gamma, const float* beta, int32_t act, const float* alpha, int32_t alpha_n,
+                     int32_t training, void* dxq, float* dgamma, float* dbeta, float* dalpha_c, float* workspace,
+                     uint32_t* dx_bound, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- max pooling over planes -------
  * nn.MaxPool3d((1, KH, KW), (1, SH, SW), (0, PH, PW)) of the lip front-ends (avse1 model.py:29-34, avse4

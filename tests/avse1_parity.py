@@ -29,13 +29,13 @@ def capture_masks(model):
     names = {id(m): n for n, m in model.named_modules()}
     orig = avse1.bn_act
 
-    def spy(x, bn, act=None, res=None, folded_bias=None):
-        y = orig(x, bn, act, res, folded_bias=folded_bias)
+    def spy(x, bn, act=None, res=None, folded_bias=None, **kw):
+        y = orig(x, bn, act, res, folded_bias=folded_bias, **kw)
         if act is not None:
             key = names[id(bn)] if act == "relu" else names[id(act)]
             if act != "relu":
                 assert bool((act.weight > 0).all()), key
-            masks[key] = (y > 0).detach().cpu()
+            masks[key] = layers.K.positive(y).detach().cpu()      # (split-output tensors: from their planes)
         return y
 
     handles = []

@@ -57,10 +57,10 @@ def _capture(model, masks):
     names = {id(m): n for n, m in model.named_modules()}
     orig = avse1.bn_act
 
-    def spy(x, bn, act=None, res=None, folded_bias=None):
-        y = orig(x, bn, act, res, folded_bias=folded_bias)
+    def spy(x, bn, act=None, res=None, folded_bias=None, **kw):
+        y = orig(x, bn, act, res, folded_bias=folded_bias, **kw)
         if act is not None:
-            masks[names[id(bn)] if act == "relu" else names[id(act)]] = (y > 0).detach().cpu()
+            masks[names[id(bn)] if act == "relu" else names[id(act)]] = layers.K.positive(y).detach().cpu()
         return y
     hs = [m.register_forward_hook(lambda mod, i, o, n=n: masks.__setitem__(n, (o > 0).detach().cpu()))
           for n, m in model.named_modules() if isinstance(m, layers.PReLU)]
@@ -81,7 +81,7 @@ def _impose(model, masks):
     names = {id(m): n for n, m in model.named_modules()}
     orig = avse1.bn_act
 
-    def forced(x, bn, act=None, res=None, folded_bias=None):
+    def forced(x, bn, act=None, res=None, folded_bias=None, **split_output_flags):   # fp32 outputs: masks applied below
         if act is None:
             return orig(x, bn, None, res, folded_bias=folded_bias)
         z = orig(x, bn, None, res, folded_bias=folded_bias)
@@ -229,6 +229,8 @@ def test_two_ranks_one_gpu_side_stream_buckets(workload):
             branches[key] = (be + ei ** 2, bn + ni ** 2)
         for key, (be, bn) in branches.items():
             print(f"    branch {key}: rel err {(be / max(bn, 1e-60)) ** 0.5:.2e}")
+        top = sorted(((ei, ni, name) for name, (ei, ni) in zip(rec["names"], rec["errs"])), reverse=True)[:4]
+        print("    largest absolute errors: " + ", ".join(f"{nm} {ei:.2e} of {ni:.2e}" for ei, ni, nm in top))
         assert e <= 2e-3 * n, (workload, r, e, n)
         for key, (be, bn) in branches.items():
             assert be ** 0.5 <= 2e-3 * bn ** 0.5 + 1e-6 * n, (workload, r, key, be ** 0.5, bn ** 0.5)

@@ -623,6 +623,60 @@ def test_bnact_vs_fp64(shape, cl, act, res, training, mean, scale):
     assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked)
 
 
+def _q_decode(t):
+    """A split-output (N, C, H, W) tensor -> fp64 values (hi + lo) 2^-e, e from its bound (dconv.hip split_exp)."""
+    q = K().q_view(t).view(torch.float16).reshape(-1, t.shape[1] // 16, 2, 16).double()
+    bits = int(getattr(t, K().ABSMAX_ATTR).item())
+    e = max(-100, min(100, 14 - (((bits >> 23) & 0xFF) - 127))) if bits else 0
+    v = (q[:, :, 0, :] + q[:, :, 1, :]) * 2.0 ** -e
+    n, c, h, w = t.shape
+    return v.reshape(n, h, w, c).permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("act", ["relu", "prelu_c", "none"])
+@pytest.mark.parametrize("shape,mean,scale", [((4, 64, 24, 24), 0.0, 1.0), ((2, 128, 9, 11), 30.0, 0.02),
+                                              ((3, 64, 7, 257), -2.0, 5.0)])
+def test_bnact_split_output_vs_fp32(shape, mean, scale, act):
+    """bnact with q_out (csrc/bnact.hip QOUT passes, round 5): the output / input gradient written straight as the fp16
+    hi / lo split the split-fp16 convolutions read.  Against the fp32 passes on the same inputs: same statistics
+    (bitwise), the bound published for the split scale >= max |y| (|dx|) and within 2^6 of it, and every decoded value
+    within 2^-21 of the tensor's max of the fp32 value (the split's 22 bits); split16 / split_q hand the bytes on
+    without a pass."""
+    C = shape[1]
+    g = torch.Generator().manual_seed(C + shape[-1])
+    x = (scale * det_input(shape, 750) + mean).float().to(DEV).contiguous(memory_format=torch.channels_last)
+    gam = (0.5 + torch.rand(C, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    code = {"relu": K().ACT_RELU, "prelu_c": K().ACT_PRELU, "none": K().ACT_NONE}[act]
+    alpha = (0.1 + 0.3 * torch.rand(C, generator=g)).to(DEV) if act == "prelu_c" else None
+    rms = [(torch.zeros(C, device=DEV), torch.ones(C, device=DEV)) for _ in range(2)]
+    y, st = K().bnact_fwd(x, gam, bet, *rms[0], True, 0.1, 1e-5, code, alpha)
+    yq, stq = K().bnact_fwd(x, gam, bet, *rms[1], True, 0.1, 1e-5, code, alpha, q_out=True)
+    assert K().is_split_q(yq) and not K().is_split_q(y)
+    assert torch.equal(st, stq) and torch.equal(rms[0][0], rms[1][0]) and torch.equal(rms[0][1], rms[1][1])
+    for ref, q in ((y, yq),):
+        m = float(ref.abs().max())
+        bound = float(getattr(q, K().ABSMAX_ATTR).view(torch.float32).item())
+        assert m <= bound <= 64 * m + 1e-30, (m, bound)
+        err = float((_q_decode(q).cpu() - ref.double().cpu()).abs().max())
+        assert err <= 2.0 ** -21 * m, (err, m)
+    mb = torch.empty(2, device=DEV, dtype=torch.int32)
+    assert K().split16(yq, mb).data_ptr() == yq.data_ptr() if C == 64 else True
+    xq, xm = K().split_q(yq)
+    assert xq.data_ptr() == yq.data_ptr() and int(xm.item()) == int(getattr(yq, K().ABSMAX_ATTR).item())
+    dy = det_input(shape, 751).float().to(DEV).contiguous(memory_format=torch.channels_last)
+    dx, _, dg, db, da = K().bnact_bwd(x, None, dy, st, gam, bet, code, alpha, True)
+    dxq, _, dgq, dbq, daq = K().bnact_bwd(x, None, dy, st, gam, bet, code, alpha, True, q_out=True)
+    assert K().is_split_q(dxq) and torch.equal(dg, dgq) and torch.equal(db, dbq)
+    if alpha is not None:
+        assert torch.equal(da, daq)
+    m = float(dx.abs().max())
+    bound = float(getattr(dxq, K().ABSMAX_ATTR).view(torch.float32).item())
+    assert m <= bound <= 64 * m, (m, bound)
+    err = float((_q_decode(dxq).cpu() - dx.double().cpu()).abs().max())
+    assert err <= 2.0 ** -21 * m, (err, m)
+
+
 @pytest.mark.parametrize("shape,k,s,p", [((2, 3, 4, 48, 48), 3, 2, 1), ((1, 2, 3, 7, 9), 3, 2, 1),
                                          ((2, 2, 2, 10, 11), 2, 2, 0), ((1, 1, 2, 5, 6), 3, 1, 1),
                                          ((1, 2, 3, 9, 10), 3, 2, 1), ((1, 1, 1, 1, 2), 3, 2, 1),
