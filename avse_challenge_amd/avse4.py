@@ -219,13 +219,17 @@ class ResNetLayer(nn.Module):
         self.outbnb = nn.BatchNorm2d(cout, **bn)
 
     def forward(self, x):
-        # BN -> ReLU pairs as fused passes (csrc/bnact.hip); the residual adds precede their BatchNorm here
-        y = self.conv2a(bn_act(self.conv1a(x), self.bn1a, "relu"))
+        # BN -> ReLU pairs as fused passes (csrc/bnact.hip); the residual adds precede their BatchNorm here.  Where a
+        # BatchNorm's output (input gradient) goes only to a split-fp16 trunk conv's forward (backward), it is written
+        # in that conv's split layout (bn_act q_fwd / q_bwd)
+        h = self.conv1a(x)
+        y = self.conv2a(bn_act(h, self.bn1a, "relu", q_fwd=self.conv2a.q_ok(h), q_bwd=self.conv1a.q_ok(x, grad=True)))
         y = y + (x if self.stride == 1 else self.downsample(x))
         mid = y
-        y = bn_act(y, self.outbna, "relu")
-        y = self.conv2b(bn_act(self.conv1b(y), self.bn1b, "relu")) + mid
-        return bn_act(y, self.outbnb, "relu")
+        y = bn_act(y, self.outbna, "relu", q_fwd=self.conv1b.q_ok(y))
+        h = self.conv1b(y)
+        y = self.conv2b(bn_act(h, self.bn1b, "relu", q_fwd=self.conv2b.q_ok(h), q_bwd=self.conv1b.q_ok(y, grad=True)))
+        return bn_act(y + mid, self.outbnb, "relu")
 
 
 class ResNet(nn.Module):
