@@ -103,9 +103,9 @@ SIGNATURES = {
                                c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "avse_cconv_bwd_bf16": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                                     c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
-    "avse_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
+    "avse_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_rmsnorm_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
-    "avse_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_stft_frames": (c_i64, [c_i64]),
     "avse_stft_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_istft": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -160,6 +160,8 @@ SIGNATURES = {
     "avse_gemm_bf16": (c_i32, [ctypes.POINTER(GemmBf16Args), c_vp]),
     "avse_gemm_f32s": (c_i32, [ctypes.POINTER(GemmF32sArgs), c_vp]),
     "avse_split16_planes": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "avse_add_max": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_split16_planes_known": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_dconv_wprep_bytes": (c_i64, []),
     "avse_split16": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_split16_known": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),

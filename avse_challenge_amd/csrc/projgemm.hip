@@ -619,6 +619,34 @@ __global__ __launch_bounds__(256) void planes_split_kernel(PlanesArgs a) {
     }
 }
 
+// y = a + b over the padded (rows, lp) storage of two (b, c, l) operands (one vectorised pass; the pad columns hold
+// don't-care values) and max |y| over the logical columns c < l: the C3 out_proj input with its producer-side max
+// (the BiMamba direction sum, bimamba.py:253), so the projection's split skips its absmax pass
+__global__ __launch_bounds__(256) void add_max_kernel(int n4, int lp4, int l, const float4* __restrict__ a,
+                                                      const float4* __restrict__ b, float4* __restrict__ y,
+                                                      uint32_t* __restrict__ maxbits) {
+    __shared__ uint32_t red[4];
+    float m = 0.f;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+        const float4 u = a[i], v = b[i];
+        const float4 s = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+        y[i] = s;
+        const int c = 4 * (i % lp4);
+        m = fmaxf(m, c < l ? fabsf(s.x) : 0.f);
+        m = fmaxf(m, c + 1 < l ? fabsf(s.y) : 0.f);
+        m = fmaxf(m, c + 2 < l ? fabsf(s.z) : 0.f);
+        m = fmaxf(m, c + 3 < l ? fabsf(s.w) : 0.f);
+    }
+    uint32_t v = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        v = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (v) atomicMax(maxbits, v);
+    }
+}
+
 static int cu_count_cached() {
     static int cu_count[64];
     int dev = 0, cus = 256;
@@ -729,12 +757,12 @@ int avse_gemm_f32s(const avse_gemm_f32s_args* g, avse_stream_t stream) {
                              g->c, g->c_bs, g->c_sq, g->alpha, AVSE_F32, stream);
 }
 
-int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi, void* lo,
-                        uint32_t* maxbits, avse_stream_t stream) {
+static int split16_planes_impl(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
+                               void* lo, uint32_t* maxbits, bool known, avse_stream_t stream) {
     if (!x || !hi || !lo || !maxbits) return AVSE_EINVAL;
     if (b <= 0 || r <= 0 || c <= 0 || x_rs < c || (b > 1 && x_bs < (r - 1) * x_rs + c)) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
+    if (!known && hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
     PlanesArgs a;
     a.x = x;
     a.rows = b * r;
@@ -754,16 +782,46 @@ int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t
                      (x_rs % 4 == 0) && (b == 1 || x_bs % 4 == 0);
     const unsigned mgrid = (unsigned)std::min<int64_t>(blocks, 2048);
     if (vec) {
-        hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3(mgrid), dim3(256), 0, st, a, blocks);
-        AVSE_CHECK_LAUNCH();
+        if (!known) {
+            hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3(mgrid), dim3(256), 0, st, a, blocks);
+            AVSE_CHECK_LAUNCH();
+        }
         hipLaunchKernelGGL(planes_split_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
     } else {
-        hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3(mgrid), dim3(256), 0, st, a, blocks);
-        AVSE_CHECK_LAUNCH();
+        if (!known) {
+            hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3(mgrid), dim3(256), 0, st, a, blocks);
+            AVSE_CHECK_LAUNCH();
+        }
         hipLaunchKernelGGL(planes_split_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
     }
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
+}
+
+int avse_add_max(int64_t rows, int64_t lp, int64_t l, const float* a, const float* b, float* y, uint32_t* maxbits,
+                 avse_stream_t stream) {
+    if (!a || !b || !y || !maxbits) return AVSE_EINVAL;
+    if (rows <= 0 || l <= 0 || lp < l || lp % 4 || rows * lp / 4 >= (1LL << 31)) return AVSE_ESHAPE;
+    if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)y) % 16) return AVSE_EALIGN;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
+    const int n4 = (int)(rows * lp / 4);
+    const unsigned grid = (unsigned)std::min<int64_t>((n4 + 255) / 256, 8 * cu_count_cached());
+    hipLaunchKernelGGL(add_max_kernel, dim3(grid), dim3(256), 0, st, n4, (int)(lp / 4), (int)l,
+                       reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(b),
+                       reinterpret_cast<float4*>(y), maxbits);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi, void* lo,
+                        uint32_t* maxbits, avse_stream_t stream) {
+    return split16_planes_impl(b, r, c, x, x_bs, x_rs, hi, lo, maxbits, false, stream);
+}
+
+int avse_split16_planes_known(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
+                              void* lo, const uint32_t* maxbits, avse_stream_t stream) {
+    return split16_planes_impl(b, r, c, x, x_bs, x_rs, hi, lo, const_cast<uint32_t*>(maxbits), true, stream);
 }
 
 }  // extern "C"

@@ -21,12 +21,22 @@ __device__ inline float wave_sum(float v) {
     return v;
 }
 
+// the wave's max |out| -> one atomicMax on the float bits (non-negative floats order like their bits): the
+// producer-side max of an operand the split-fp16 projection GEMMs split next (avse_split16_planes_known)
+__device__ inline void wave_max_out(float m, uint32_t* omax) {
+    uint32_t b = __float_as_uint(m);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
+    if ((threadIdx.x & 63) == 0 && b) atomicMax(omax, b);
+}
+
 __global__ __launch_bounds__(THREADS) void fwd_kernel(int rows, int n, const float* __restrict__ h,
                                                       const float* __restrict__ res_in, const float* __restrict__ w,
                                                       float eps, float* __restrict__ y, float* __restrict__ res_out,
-                                                      float* __restrict__ rstd_out) {
+                                                      float* __restrict__ rstd_out, uint32_t* __restrict__ ymax) {
     const int lane = threadIdx.x & 63;
     const int nv = n / 4;
+    float m = 0.f;
     for (int row = blockIdx.x * WPB + (threadIdx.x >> 6); row < rows; row += gridDim.x * WPB) {
         const float4* hr = reinterpret_cast<const float4*>(h + (int64_t)row * n);
         const float4* rr = res_in ? reinterpret_cast<const float4*>(res_in + (int64_t)row * n) : nullptr;
@@ -57,19 +67,24 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(int rows, int n, const flo
                 const float4 ww = wv[c];
                 const float4 a = v[i];
                 ro[c] = a;
-                yr[c] = make_float4(a.x * rs * ww.x, a.y * rs * ww.y, a.z * rs * ww.z, a.w * rs * ww.w);
+                const float4 o = make_float4(a.x * rs * ww.x, a.y * rs * ww.y, a.z * rs * ww.z, a.w * rs * ww.w);
+                yr[c] = o;
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
             }
         }
         if (lane == 0) rstd_out[row] = rs;
     }
+    if (ymax) wave_max_out(m, ymax);                      // wave-uniform condition
 }
 
 // dx = rstd * (dy*w - xhat * mean(dy*w*xhat)) + dres_out ; dw_partial = sum_rows dy * xhat
 __global__ __launch_bounds__(THREADS) void bwd_kernel(int rows, int n, const float* __restrict__ dy,
                                                       const float* __restrict__ dres, const float* __restrict__ x,
                                                       const float* __restrict__ w, const float* __restrict__ rstd,
-                                                      float* __restrict__ dx, float* __restrict__ ws) {
+                                                      float* __restrict__ dx, float* __restrict__ ws,
+                                                      uint32_t* __restrict__ dxmax) {
     __shared__ float4 sdw[WPB][256];
+    float m = 0.f;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nv = n / 4;
     float4 dwacc[MAXV];
@@ -108,9 +123,11 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int rows, int n, const flo
                     o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
                 }
                 dxr[c] = o;
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
             }
         }
     }
+    if (dxmax) wave_max_out(m, dxmax);                    // wave-uniform condition
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
         const int c = lane + i * 64;
@@ -158,11 +175,12 @@ using namespace avse::rms;
 extern "C" {
 
 int avse_add_rmsnorm_fwd(int64_t rows, int64_t n, const float* h, const float* res_in, const float* weight, float eps,
-                         float* y, float* res_out, float* rstd, avse_stream_t stream) {
+                         float* y, float* res_out, float* rstd, uint32_t* y_max, avse_stream_t stream) {
     if (!h || !weight || !y || !res_out || !rstd) return AVSE_EINVAL;
     if (rows <= 0 || n <= 0 || n % 4 || n > 64 * 4 * MAXV || rows > (1LL << 31) - 1) return AVSE_ESHAPE;
+    if (y_max && hipMemsetAsync(y_max, 0, 4, (hipStream_t)stream) != hipSuccess) return AVSE_ELAUNCH;
     hipLaunchKernelGGL(fwd_kernel, dim3(nblocks_for(rows)), dim3(THREADS), 0, (hipStream_t)stream, (int)rows, (int)n,
-                       h, res_in, weight, eps, y, res_out, rstd);
+                       h, res_in, weight, eps, y, res_out, rstd, y_max);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
@@ -171,13 +189,14 @@ int64_t avse_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t n) { return 4 * (
 
 int avse_rmsnorm_bwd(int64_t rows, int64_t n, const float* dy, const float* dres_out, const float* res_out,
                      const float* weight, const float* rstd, float* dx, float* dweight, float* workspace,
-                     avse_stream_t stream) {
+                     uint32_t* dx_max, avse_stream_t stream) {
     if (!dy || !res_out || !weight || !rstd || !dx || !dweight || !workspace) return AVSE_EINVAL;
     if (rows <= 0 || n <= 0 || n % 4 || n > 64 * 4 * MAXV || rows > (1LL << 31) - 1) return AVSE_ESHAPE;
     const int nb = nblocks_for(rows);
     hipStream_t st = (hipStream_t)stream;
+    if (dx_max && hipMemsetAsync(dx_max, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
     hipLaunchKernelGGL(bwd_kernel, dim3(nb), dim3(THREADS), 0, st, (int)rows, (int)n, dy, dres_out, res_out, weight,
-                       rstd, dx, workspace);
+                       rstd, dx, workspace, dx_max);
     AVSE_CHECK_LAUNCH();
     hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64, 16), 0, st, workspace, nb, (int)n,
                        dweight);

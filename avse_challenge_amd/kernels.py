@@ -315,9 +315,12 @@ def add_rmsnorm_fwd(h, res, weight, eps=1e-5):
     y = torch.empty_like(h2)
     res_out = torch.empty_like(h2)
     rstd = torch.empty((rows,), device=h.device, dtype=torch.float32)
+    ymax = torch.empty(1, device=h.device, dtype=torch.int32)
     check(_lib.lib().avse_add_rmsnorm_fwd(rows, n, ptr(h2), ptr(r2), ptr(w), float(eps), ptr(y), ptr(res_out),
-                                          ptr(rstd), stream_ptr(h.device)), "avse_add_rmsnorm_fwd")
-    return y.view(h.shape), res_out.view(h.shape), rstd
+                                          ptr(rstd), ptr(ymax), stream_ptr(h.device)), "avse_add_rmsnorm_fwd")
+    y = y.view(h.shape)
+    _set_absmax(y, ymax)                      # the producer-side max: the projection's split_planes skips its pass
+    return y, res_out.view(h.shape), rstd
 
 
 def rmsnorm_bwd(dy, dres_out, res_out, weight, rstd):
@@ -331,9 +334,13 @@ def rmsnorm_bwd(dy, dres_out, res_out, weight, rstd):
     dw = torch.empty((n,), device=dy.device, dtype=torch.float32)
     ws = torch.empty((_lib.lib().avse_rmsnorm_bwd_workspace_bytes(rows, n) + 3) // 4, device=dy.device,
                      dtype=torch.float32)
+    dxmax = torch.empty(1, device=dy.device, dtype=torch.int32)
     check(_lib.lib().avse_rmsnorm_bwd(rows, n, ptr(dy2), ptr(dr2), ptr(x2), ptr(weight.float().contiguous()),
-                                      ptr(rstd), ptr(dx), ptr(dw), ptr(ws), stream_ptr(dy.device)), "avse_rmsnorm_bwd")
-    return dx.view(res_out.shape), dw
+                                      ptr(rstd), ptr(dx), ptr(dw), ptr(ws), ptr(dxmax), stream_ptr(dy.device)),
+          "avse_rmsnorm_bwd")
+    dx = dx.view(res_out.shape)
+    _set_absmax(dx, dxmax)
+    return dx, dw
 
 
 # ------------------------------------------------------------------------ STFT / iSTFT
@@ -1303,6 +1310,20 @@ class Split:
         return Split(self.hi.transpose(1, 2), self.lo.transpose(1, 2), self.mb)
 
 
+def add_max(a_full, b_full, l):
+    """a + b over two contiguous (b, c, lp) padded storages (kernels.bdl_empty rows) -> (the sum's (b, c, l) view
+    carrying max |sum| over the logical columns as its producer-side max, csrc/projgemm.hip avse_add_max)."""
+    _need_gpu(a_full, b_full)
+    y = torch.empty_like(a_full)
+    mb = torch.empty(1, device=a_full.device, dtype=torch.int32)
+    nb, c, lp = a_full.shape
+    check(_lib.lib().avse_add_max(nb * c, lp, l, ptr(a_full), ptr(b_full), ptr(y), ptr(mb), stream_ptr(a_full.device)),
+          "avse_add_max")
+    v = y[..., :l]
+    _set_absmax(v, mb)
+    return v
+
+
 def split_planes(t):
     """t (b, r, c) fp32 view with stride(2) == 1 or stride(1) == 1 -> Split(hi, lo, maxbits): fp16 planes of t's shape and
     strides holding fp16(t 2^e) and the remainder (csrc/projgemm.hip avse_split16_planes), and max |t|'s bits."""
@@ -1314,14 +1335,15 @@ def split_planes(t):
     span = 1 + sum((n - 1) * st for n, st in zip(t.size(), t.stride()))
     hi = torch.empty(span + 16, device=t.device, dtype=torch.float16).as_strided(t.size(), t.stride())
     lo = torch.empty(span + 16, device=t.device, dtype=torch.float16).as_strided(t.size(), t.stride())
-    mb = torch.empty(1, device=t.device, dtype=torch.int32)
+    known = _known_absmax(t)                  # the producer's max (add_rmsnorm_fwd, rmsnorm_bwd): the split pass only
+    mb = known if known is not None else torch.empty(1, device=t.device, dtype=torch.int32)
     v = t if t.stride(2) == 1 else t.transpose(1, 2)
     if v.stride(2) != 1:
         raise RuntimeError(f"split_planes: no unit stride in {t.stride()}")
     b, r, c = v.shape
-    check(_lib.lib().avse_split16_planes(b, r, c, ptr(v), v.stride(0) if b > 1 else (r - 1) * v.stride(1) + c,
-                                         v.stride(1), ptr(hi), ptr(lo), ptr(mb), stream_ptr(t.device)),
-          "avse_split16_planes")
+    fn = _lib.lib().avse_split16_planes_known if known is not None else _lib.lib().avse_split16_planes
+    check(fn(b, r, c, ptr(v), v.stride(0) if b > 1 else (r - 1) * v.stride(1) + c, v.stride(1), ptr(hi), ptr(lo),
+             ptr(mb), stream_ptr(t.device)), "avse_split16_planes")
     return Split(hi, lo, mb)
 
 

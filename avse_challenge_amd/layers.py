@@ -458,6 +458,7 @@ class _GemmConvFn(torch.autograd.Function):
         return v.reshape(-1, cin * 9), ho, wo
 
     @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, x, w, stride):
         k = w.shape[-1]
         a, ho, wo = _GemmConvFn._rows(x, k, stride)
@@ -468,6 +469,7 @@ class _GemmConvFn(torch.autograd.Function):
         return y if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous() else y.contiguous()
 
     @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")             # the forward's autocast state (bf16 C5 lip encoder)
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         s, (ho, wo) = ctx.stride, ctx.hw

@@ -308,8 +308,14 @@ class _BiOutProj(torch.autograd.Function):
     @staticmethod
     @_FWD
     def forward(ctx, f, bk, w):
-        y = _padded_add(f, bk)
         dt = _autocast_dtype()
+        y = None
+        if dt is None and f.dtype == bk.dtype == w.dtype == torch.float32 and f.stride() == bk.stride():
+            fa, fb = _padded_full(f), _padded_full(bk)
+            if fa is not None and fb is not None and fa.is_contiguous() and fb.is_contiguous():
+                y = K.add_max(fa, fb, f.size(2))        # the sum with its max: the split below skips the absmax pass
+        if y is None:
+            y = _padded_add(f, bk)
         ctx.split = False
         if dt is None and y.dtype == w.dtype == torch.float32:
             # fp32 (C3): y's split planes serve the forward GEMM and, saved in place of y, the weight gradient

@@ -150,15 +150,17 @@ int avse_cconv_bwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t widt
 /* ---------------------------------------------------------------- add + RMSNorm -------
  * Replaces the Block pre-norm of Mamba-TasNet/modules/mamba/bimamba.py:447-451
  * (residual = h + residual; RMSNorm(residual), mamba-ssm Triton RMSNorm, eps 1e-5) and
- * MambaBlocksSequential's final norm_f (mamba_blocks.py:195-197).  Rows of width n.
+ * MambaBlocksSequential's final norm_f (mamba_blocks.py:195-197).  Rows of width n.  y_max / dx_max (or NULL): set to the
+ * bits of max |y| / |dx| (zeroed by the call in stream order), the producer-side max the split-fp16 projection GEMMs
+ * take instead of an absmax pass (avse_split16_planes_known).
  */
 int avse_add_rmsnorm_fwd(int64_t rows, int64_t n, const float* h, const float* res_in /* or NULL */,
-                         const float* weight, float eps, float* y, float* res_out, float* rstd,
+                         const float* weight, float eps, float* y, float* res_out, float* rstd, uint32_t* y_max,
                          avse_stream_t stream);
 int64_t avse_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t n);
 int avse_rmsnorm_bwd(int64_t rows, int64_t n, const float* dy, const float* dres_out /* or NULL */,
                      const float* res_out, const float* weight, const float* rstd,
-                     float* dx, float* dweight, float* workspace, avse_stream_t stream);
+                     float* dx, float* dweight, float* workspace, uint32_t* dx_max, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- STFT / iSTFT --------
  * Replaces the CPU librosa 0.8.1 calls of baseline/avse1/dataset.py:112-118 (stft, n_fft
@@ -410,6 +412,14 @@ int avse_gemm_f32s(const avse_gemm_f32s_args* a, avse_stream_t stream);
  * offsets (their padding untouched) and *maxbits = bits of max |x|. */
 int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi, void* lo,
                         uint32_t* maxbits, avse_stream_t stream);
+/* y = a + b over the padded (rows, lp) storage of two (b, c, l) fp32 operands (16-B aligned, lp % 4 == 0; the pad
+ * columns hold don't-care values) and *maxbits = bits of max |y| over the logical columns < l (the BiMamba v2
+ * direction sum bimamba.py:253 that the C3 out_proj splits next) */
+int avse_add_max(int64_t rows, int64_t lp, int64_t l, const float* a, const float* b, float* y, uint32_t* maxbits,
+                 avse_stream_t stream);
+/* the same with *maxbits already max |x| (e.g. avse_add_rmsnorm_fwd's y_max): the split pass only */
+int avse_split16_planes_known(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
+                              void* lo, const uint32_t* maxbits, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- dilated Conv2d fwd / input gradient ----
  * Replaces the forward and the data gradient of nn.Conv2d(64, 64, 5, padding=2d, dilation=d), d = 2, 4, 8, 16

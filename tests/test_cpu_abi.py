@@ -50,7 +50,7 @@ def test_host_side_validation_without_gpu():
     a.dstate, a.in_dtype = 16, 7
     assert L.avse_scan_fwd(a, None) == -3             # dtype -> EDTYPE
     assert L.avse_cconv_fwd(1, 1, 10, 5, dummy, 10, 10, dummy, None, dummy, 10, 10, 0, 0, None) == -2   # width > 4
-    assert L.avse_add_rmsnorm_fwd(4, 6, dummy, None, dummy, 1e-5, dummy, dummy, dummy, None) == -2   # n % 4
+    assert L.avse_add_rmsnorm_fwd(4, 6, dummy, None, dummy, 1e-5, dummy, dummy, dummy, None, None) == -2   # n % 4
     assert b"shape" in L.avse_strerror(-2)
     ws = L.avse_scan_bwd_workspace_bytes(2, 128, 100, 16)
     assert ws == 4 * (2 * 2 * 32 * 100 + 2 * 128 * 18)

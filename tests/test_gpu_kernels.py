@@ -352,6 +352,16 @@ def test_add_rmsnorm_vs_oracle(n, with_res):
     dx, dw = K().rmsnorm_bwd(gy.float().to(DEV), gr.float().to(DEV), rk, w.detach().float().to(DEV), rstd)
     close(dx, h.grad, 1e-5, 1e-5, "dx")
     close(dw, w.grad, 1e-3, 1e-5, "dw")
+    # the producer-side max the split-fp16 projections take instead of an absmax pass: exactly max |y| / |dx|, and the
+    # planes split from it equal split_planes' own (split16_planes_known vs split16_planes)
+    for t in (yk, dx):
+        mb = getattr(t, K().ABSMAX_ATTR)
+        assert int(mb.item()) == int(t.abs().max().view(torch.int32).item())
+        v = t.view(1, *t.shape)
+        setattr(v, K().ABSMAX_ATTR, mb)
+        sk = K().split_planes(v)
+        sf = K().split_planes(v.clone())
+        assert torch.equal(sk.hi, sf.hi) and torch.equal(sk.lo, sf.lo) and torch.equal(sk.mb, sf.mb)
 
 
 # ------------------------------------------------------------------ STFT / iSTFT (librosa 0.8.1 semantics)

@@ -209,3 +209,27 @@ def test_gemm_f32s_c3_layouts_vs_fp64():
     dw = torch.empty(1, 2 * di, dm, device=DEV)
     K().gemm_f32s(h.transpose(1, 2), dxz, dw, fold=b)                    # dW_in = sum_b dxz h
     assert _check32(dw, h.transpose(1, 2), dxz, 1.0, dm, b) <= 1e-5
+
+
+@pytest.mark.parametrize("b,c,l", [(2, 64, 3999), (3, 40, 17), (1, 8, 4)])
+def test_add_max_padded_rows(b, c, l):
+    """avse_add_max (the C3 out_proj input, bimamba.py:253): the sum over the padded storage equals a + b on the logical
+    columns, and its max is max |a + b| over them exactly, whatever the pad columns hold (NaN here); split_planes then
+    takes that max (no absmax pass) and yields the same planes as from a copy."""
+    from avse_challenge_amd import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(b * c + l)
+    a = K.bdl_empty(b, c, l, torch.float32, torch.device("cuda"))
+    bb = K.bdl_empty(b, c, l, torch.float32, torch.device("cuda"))
+    lp = a.stride(1)
+    fa = a.as_strided((b, c, lp), a.stride())
+    fb = bb.as_strided((b, c, lp), bb.stride())
+    fa.fill_(float("nan"))
+    fb.fill_(float("nan"))
+    a.copy_(torch.randn(b, c, l, device="cuda", generator=g))
+    bb.copy_(3 * torch.randn(b, c, l, device="cuda", generator=g))
+    y = K.add_max(fa, fb, l)
+    assert y.shape == (b, c, l) and torch.equal(y, a + bb)
+    mb = getattr(y, K.ABSMAX_ATTR)
+    assert int(mb.item()) == int((a + bb).abs().max().view(torch.int32).item())
+    s1, s2 = K.split_planes(y), K.split_planes(y.clone())
+    assert torch.equal(s1.hi, s2.hi) and torch.equal(s1.lo, s2.lo) and torch.equal(s1.mb, s2.mb)
