@@ -181,8 +181,11 @@ class Avse1Step:
         kernels run 3 f16 MFMAs per fp32 product, so their peak is the dense f16 peak / 3 (833 TFLOP/s), the fp32-MFMA
         kernel's the fp32 peak (157.3).
           * ``achieved`` / ``frac`` / ``avg_ms``: IN-STEP — every launch inside 3 eager train steps of the benchmarked
-            model itself (lip branch on its side stream, as the timed step runs), each bracketed by HIP events on its
-            launch stream (kernels.LAUNCH_TAPS); ``roofline`` is the entry point with the most kernel time in them;
+            model itself, each bracketed by HIP events on its launch stream (kernels.LAUNCH_TAPS), with the lip branch
+            on the launch stream for these 3 steps: then a launch's event time is its kernel time (with the branch on
+            its side stream, as the timed steps run, the events also count the launch's wait for CUs the lip branch
+            holds: ``in_step_two_streams``, 3 more eager steps); ``roofline`` is the entry point with the most kernel
+            time in them; AVSE_PROFILE_MARK=1 brackets the serial-branch steps (the rocprof window that must agree);
           * ``isolated``: conv3's launch (d = 4) alone on the idle GPU, random operands of the step's shape;
           * ``roofline_library``: the MIOpen forward of the same conv, alone."""
         from avse_challenge_amd import kernels as K
@@ -193,20 +196,31 @@ class Avse1Step:
         names = ("avse_dconv_fwd", "avse_dconv_wgrad16") if split else ("avse_dconv_wgrad",)
         peak = BF16_PEAK_TFS / 3 if split else FP32_PEAK_TFS
         mark = os.environ.get("AVSE_PROFILE_MARK", "0") == "1"        # tools/ktrace_window.py OUT_ROOF.csv
-        for n in names:
-            K.LAUNCH_TAPS[n] = []
-        try:
-            if mark:
-                torch.cuda._sleep(1000)
-            for _ in range(3):
-                self.loss().backward()
-            if mark:
-                torch.cuda._sleep(1000)
-            torch.cuda.synchronize()
-            per = {n: [a.elapsed_time(b) for a, b in K.LAUNCH_TAPS[n]] for n in names}
-        finally:
+
+        def taps(serial):
             for n in names:
-                K.LAUNCH_TAPS.pop(n, None)
+                K.LAUNCH_TAPS[n] = []
+            old = os.environ.get("AVSE_AVSE1_STREAMS")
+            try:
+                if serial:
+                    os.environ["AVSE_AVSE1_STREAMS"] = "0"              # the lip branch on the launch stream
+                if mark and serial:
+                    torch.cuda._sleep(1000)
+                for _ in range(3):
+                    self.loss().backward()
+                if mark and serial:
+                    torch.cuda._sleep(1000)
+                torch.cuda.synchronize()
+                return {n: [a.elapsed_time(b) for a, b in K.LAUNCH_TAPS[n]] for n in names}
+            finally:
+                for n in names:
+                    K.LAUNCH_TAPS.pop(n, None)
+                if old is None:
+                    os.environ.pop("AVSE_AVSE1_STREAMS", None)
+                else:
+                    os.environ["AVSE_AVSE1_STREAMS"] = old
+        per2 = taps(False)
+        per = taps(True)
         x = torch.randn(self.B, 64, 376, 257, device=dev).contiguous(memory_format=cl)
         dy = torch.randn(self.B, 64, 376, 257, device=dev).contiguous(memory_format=cl)
         w = 0.05 * torch.randn(64, 64, 5, 5, device=dev)
@@ -238,11 +252,17 @@ class Avse1Step:
                         "fp32 HIP MFMA implicit GEMM)")
             ms = _event_ms(iso, n=10, warm=3)
             ach = flops / (ms * 1e-3) / 1e12
+            v2 = per2.get(n) or [float("nan")]
+            ms2 = sum(v2) / len(v2)
             recs.append({"kernel": desc, "bound": "mfma", "achieved": round(ach_in, 2), "peak": round(peak, 1),
                          "unit": "TFLOP/s", "frac": round(ach_in / peak, 4), "traffic": None, "avg_ms": round(ms_in, 4),
                          "launches": len(v), "step_ms": round(sum(v) / 3, 3),
-                         "measured": f"in-step: {len(v)} launches in 3 eager train steps of the benchmarked model (two "
-                                     "streams), HIP events on the launch stream",
+                         "measured": f"in-step: {len(v)} launches in 3 eager train steps of the benchmarked model (lip "
+                                     "branch on the launch stream), HIP events on the launch stream",
+                         "in_step_two_streams": {"avg_ms": round(ms2, 4),
+                                                 "frac": round(flops / (ms2 * 1e-3) / 1e12 / peak, 4),
+                                                 "note": "lip branch on its side stream as in the timed steps: the "
+                                                         "events also count each launch's wait for CUs"},
                          "per_launch_ms": [round(t, 3) for t in v[:4]], "algorithmic_flops_per_launch": flops,
                          "isolated": {"what": "conv3 (d = 4) alone on the idle GPU", "avg_ms": round(ms, 4),
                                       "achieved": round(ach, 2), "frac": round(ach / peak, 4)}})
