@@ -17,7 +17,6 @@
 // and odd columns in separate arrays (the stride-2 pixel walk becomes unit stride: no bank conflicts), and the
 // pair's weights as [tap][plane][co]; the next pair is loaded into registers while the current one's MFMAs run.
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -391,13 +390,8 @@ int launch(int64_t B, int64_t TT, const void* x, const float* w, float* y, float
     using G = Geo<CIN, H, W>;
     if ((int64_t)B * CIN * TT * H * W >= (1LL << 31) / (int64_t)sizeof(T)) return AVSE_ESHAPE;   // 32-bit offsets
     if (B * TT * G::NT >= (1LL << 31)) return AVSE_ESHAPE;
-    static int f16 = -1;
-    if (f16 < 0) {
-        const char* e = getenv("AVSE_C3F_F16");
-        f16 = (e && atoi(e) == 0) ? 0 : 1;
-    }
     if constexpr (std::is_same<T, uint8_t>::value) {
-        if (f16) {                              // uint8 lips: the f16 MFMA with split weights
+        {                                       // uint8 lips: the f16 MFMA with split weights (float frames: exact fp32)
             uint16_t* wq = reinterpret_cast<uint16_t*>(workspace);
             uint32_t* mb = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(workspace) + 2 * G::NPL * WB_HALF);
             hipLaunchKernelGGL(wmax16_kernel, dim3(1), dim3(1024), 0, st, w, G::NPL * COUT * TAPS, mb);

@@ -115,6 +115,8 @@ __global__ __launch_bounds__(THREADS, 2) void wgrad_kernel(Shape s, const T* __r
             if (rr < nrs) {
                 if (lane < WIN) xs[rr * WINP + lane] = xr[i][0];          // lanes past the window would
                 if (lane + 64 < WIN) xs[rr * WINP + lane + 64] = xr[i][1];  // spill into the next row
+                // the pad slot: an odd WO's last k-step (dY = 0 there) reads it, and 0 x stale-LDS NaN is NaN
+                if (lane == 0) xs[rr * WINP + WIN] = 0.f;
             }
         }
 #pragma unroll

@@ -32,7 +32,6 @@
 // of 3 buffers, issued 2 stages ahead; one barrier per stage.  LDS rows are 64 B with the 16-B chunk c of row r at
 // c ^ ((r >> 2) & 3), so the 16 lanes of a ds_read_b128 group read 16 distinct bank slots.
 #include <algorithm>
-#include <cstdlib>
 
 #include "common.h"
 
@@ -626,20 +625,15 @@ int avse_dconv_fwd(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq,
     a.N = (int)N;
     a.H = (int)H;
     a.W = (int)W;
-    // tile = 64 NW raster pixels (NW waves); AVSE_DCONV_NW selects 4 or 8 (default 8: twice the MFMA work per staged
-    // W byte and 2 waves per SIMD)
-    static int nw = 0;
-    if (nw == 0) {
-        const char* e = getenv("AVSE_DCONV_NW");
-        nw = (e && atoi(e) == 4) ? 4 : 8;
-    }
+    // tile = 64 NW raster pixels on NW = 8 waves (4 measured slower: half the MFMA work per staged W byte, one wave
+    // per SIMD)
+    constexpr int nw = 8;
     a.tiles = (int)((H * W + 64 * nw - 1) / (64 * nw));
     const dim3 grid((unsigned)(N * a.tiles)), block(64 * nw);
     hipStream_t st = (hipStream_t)stream;
 #define AVSE_DCF_L(DD)                                                                  \
     do {                                                                                \
-        if (nw == 4) hipLaunchKernelGGL((fwd_kernel<DD, 4>), grid, block, 0, st, a);    \
-        else hipLaunchKernelGGL((fwd_kernel<DD, 8>), grid, block, 0, st, a);            \
+        hipLaunchKernelGGL((fwd_kernel<DD, nw>), grid, block, 0, st, a);                \
     } while (0)
     switch (dil) {
         case 2: AVSE_DCF_L(2); break;

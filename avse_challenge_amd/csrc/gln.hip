@@ -11,8 +11,6 @@
 // finalize kernels reduce (deterministic, double accumulation across rows).  Statistics use sums
 // shifted by the sample's first element, which removes the E[x^2]-E[x]^2 cancellation.
 // HBM: fwd = 2 reads + 1 write of x, bwd = 2 reads of (x, dy) + 1 write of dx.
-#include <cstdlib>
-
 #include "common.h"
 
 namespace avse {
@@ -636,21 +634,9 @@ __global__ void dw_tail_kernel(const float* __restrict__ ws_dw, const float2* __
 
 using namespace avse::gln;
 
-// Samples per launch pair of a two-pass kernel.  Grouping the samples so that a group's first-pass inputs stay within
-// the 256 MiB Infinity Cache for the second pass (AVSE_GLN_GROUP_MB=64: PMC traffic of C4's prelu_gln_bwd was 1.67x the
-// algorithmic bytes with one launch, profiles/r04_traffic.json) measured SLOWER in isolation: C4 dwconv_gln fwd
-// 0.095 -> 0.136 ms, prelu_gln_bwd 0.131 -> 0.151 ms (profiles/r05k: the serialised launch pairs and their tails cost
-// more than the re-reads), so the default is one launch pair over all samples.
-static int64_t group_samples(int64_t B, int64_t bytes_per_sample) {
-    static int64_t mb = -1;
-    if (mb < 0) {
-        const char* e = getenv("AVSE_GLN_GROUP_MB");
-        mb = e ? atoll(e) : 0;
-    }
-    if (mb <= 0) return B;
-    const int64_t cap = (mb << 20) / (bytes_per_sample > 0 ? bytes_per_sample : 1);
-    return cap < 1 ? 1 : (cap > B ? B : cap);
-}
+// Each call is one launch pair over all samples: launch pairs per Infinity-Cache-sized sample group measured slower in
+// isolation (round 5: C4 dwconv_gln fwd 0.095 -> 0.136 ms, prelu_gln_bwd 0.131 -> 0.151 ms), and so did a one-launch
+// sample-pipelined form (profiles/r05r_gln_pipelined_ab.jsonl).
 
 extern "C" {
 
@@ -662,8 +648,8 @@ int avse_prelu_gln_fwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     if (B <= 0 || C <= 0 || K <= 0 || B * C > (1LL << 31) - 1) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     float2* ws = (float2*)workspace;
-    // row statistics, then the apply pass, per group of samples (group_samples: x re-read from the Infinity Cache)
-    const int64_t S = group_samples(B, 4 * C * K);
+    // row statistics, then the apply pass (x re-read from the Infinity Cache)
+    const int64_t S = B;
     for (int64_t b0 = 0; b0 < B; b0 += S) {
         const int row0 = (int)(b0 * C);
         const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
@@ -687,7 +673,7 @@ int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     float* ws_a = (float*)(ws + B * C);
     float2* smeans = (float2*)(ws_a + B * C);
     // (x, dy) row reduction, then the apply pass, per group of samples (its (x, dy) re-read from the Infinity Cache)
-    const int64_t S = group_samples(B, 8 * C * K);
+    const int64_t S = B;
     for (int64_t b0 = 0; b0 < B; b0 += S) {
         const int row0 = (int)(b0 * C);
         const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
@@ -737,7 +723,7 @@ int avse_dwconv_gln_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     hipStream_t st = (hipStream_t)stream;
     float2* ws = (float2*)workspace;
     // per group of samples: y1 (written by the first pass) re-read from the Infinity Cache by the apply pass
-    const int64_t S = group_samples(B, 8 * C * K);
+    const int64_t S = B;
     for (int64_t b0 = 0; b0 < B; b0 += S) {
         const int row0 = (int)(b0 * C);
         const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
@@ -765,7 +751,7 @@ int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     float* ws_a = (float*)(ws + B * C);
     float* ws_dw = (float*)((float2*)(ws_a + B * C) + B);
     // per group of samples: dy (read by the reduction) re-read from the Infinity Cache by the main pass
-    const int64_t S = group_samples(B, 8 * C * K);
+    const int64_t S = B;
     for (int64_t b0 = 0; b0 < B; b0 += S) {
     const int row0 = (int)(b0 * C);
     const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);

@@ -44,12 +44,14 @@ def main():
         u, dl, z = aligned(b, d, l, g, dtype=dt), aligned(b, d, l, g, 0.1, dt), aligned(b, d, l, g, dtype=dt)
         A = -torch.rand(d, 16, device=dev, generator=g) - 0.5
         Bm, Cm = aligned(b, 16, l, g, dtype=dt), aligned(b, 16, l, g, dtype=dt)
-        D, bias = torch.ones(d, device=dev), torch.zeros(d, device=dev)
-        fn = lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, bias, True, return_out=False)  # noqa: E731
+        D = torch.ones(d, device=dev)
+        # as the model calls it (round 5): delta already softplus(dt_proj + bias) from avse_dtproj, mode 2
+        dl.copy_(torch.nn.functional.softplus(dl.float()))
+        fn = lambda: K.selective_scan_fwd(u, dl, A, Bm, Cm, D, z, None, 2, return_out=False)  # noqa: E731
         if a.phase.startswith("scan_bwd"):
             _, x, _ = fn()
             dout = aligned(b, d, l, g, dtype=dt)
-            fn = lambda: K.selective_scan_bwd(u, dl, A, Bm, Cm, D, z, bias, dout, x, None, None, True, False)  # noqa: E731
+            fn = lambda: K.selective_scan_bwd(u, dl, A, Bm, Cm, D, z, None, dout, x, None, None, 2, False)  # noqa: E731
     elif a.phase.startswith("prelu_gln"):
         x = torch.randn(*SHAPES["prelu_gln"], device=dev, generator=g)
         al, gm, bt = torch.full((1,), 0.25, device=dev), torch.ones(1, 512, 1, device=dev), torch.zeros(1, 512, 1, device=dev)
