@@ -81,6 +81,7 @@ class GemmF32sArgs(ctypes.Structure):
         ("q_max", c_vp),
         ("c", c_vp), ("c_bs", c_i64), ("c_sq", c_i64),
         ("alpha", c_f32),
+        ("nsub", c_i64), ("p_bs2", c_i64), ("q_bs2", c_i64),
     ]
 
 
@@ -146,6 +147,7 @@ SIGNATURES = {
     "avse_dwconv_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_i64] + [c_vp] * 7),
     "avse_dwconv_gln_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_dwconv_gln_fwd": (c_i32, [c_i64] * 5 + [c_vp] * 5 + [c_f32] + [c_vp] * 5),
+    "avse_dwconv_gln_fwd_q": (c_i32, [c_i64] * 5 + [c_vp] * 5 + [c_f32] + [c_vp] * 3 + [c_i64] + [c_vp] * 4),
     "avse_dwconv_gln_bwd": (c_i32, [c_i64] * 5 + [c_vp] * 14),
     "avse_lstm_padded_hidden": (c_i64, [c_i64]),
     "avse_lstm_group_size": (c_i64, [c_i64, c_i64]),
@@ -162,6 +164,8 @@ SIGNATURES = {
     "avse_split16_planes": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_add_max": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_split16_planes_known": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "avse_split16_planes_to": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i32,
+                                       c_vp]),
     "avse_dconv_wprep_bytes": (c_i64, []),
     "avse_split16": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_split16_known": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),

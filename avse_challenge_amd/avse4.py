@@ -9,15 +9,18 @@ relative to /root/reference/baseline/avse4:
   AVSE4BaselineModule :295-393 (forward :316-321, training_step :323, enhance :335-352, cal_loss :374-383)
 MI355X specifics: every (PReLU -> gLN) pair runs as the fused HIP prelu_gln kernels, every
 depthwise dilated conv1d as the HIP dwconv kernels, the lip Conv3d weight gradient on the HIP
-MFMA implicit GEMM; all 1x1 convolutions / the encoder / the decoder basis are hipBLASLt GEMMs.
+MFMA implicit GEMM; every 1x1 Conv1d (forward, input and weight gradient) on the split-fp16 MFMA GEMM
+(csrc/projgemm.hip avse_gemm_f32s, fp32-accurate); the encoder / decoder basis are hipBLASLt GEMMs.
 """
 import copy
+import os
 
 import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import kernels as K
 from . import losses
 from .layers import (LipConv3d, PointwiseConv2d, TrunkConv2d, _PReLUFn, bn_act, dwconv1d, dwconv_prelu_gln, frames_nhwc,
                      maxpool3d, prelu_gln)
@@ -25,23 +28,77 @@ from .layers import (LipConv3d, PointwiseConv2d, TrunkConv2d, _PReLUFn, bn_act, 
 NORM_MEAN, NORM_STD = 0.4161, 0.1688
 
 
+# "0": the 1x1 convolutions on hipBLASLt fp32 batched GEMMs (torch.bmm) instead of avse_gemm_f32s
+_PW_SPLIT = os.environ.get("AVSE_AVSE4_PW_SPLIT", "1") != "0"
+
+
+def _pw_split_ok(w, x):
+    return (_PW_SPLIT and x.is_cuda and x.dtype == w.dtype == torch.float32 and x.dim() == 3
+            and (x.stride(2) == 1 or x.stride(1) == 1) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0
+            and w.stride(1) == 1)
+
+
+def _padded_rows(sp):
+    """The planes are in the zero-padded row layout (split_rows8, the gLN planes output): rows of a multiple of 8."""
+    h = sp.hi
+    return h.stride(2) == 1 and h.stride(1) % 8 == 0 and h.stride(0) == h.shape[1] * h.stride(1)
+
+
+def _split_act(x):
+    """The split planes of a (B, C, K) activation as a GEMM operand, in the zero-padded row layout (rows of a multiple
+    of 8 elements): the planes its producer wrote (the gLN of DepthwiseSeparableConv, kernels.PLANES_ATTR), else
+    split_rows8 (a channel-contiguous x — the ChannelWiseLayerNorm output — is made time-contiguous first)."""
+    sp = K.planes_of(x)
+    if sp is not None:
+        return sp
+    return K.split_rows8(x if x.stride(2) == 1 else x.contiguous())
+
+
 class _PointwiseFn(torch.autograd.Function):
-    """1x1 Conv1d without bias as batched GEMMs on the (B, C, K) layout, no layout copies:
-    y_b = W x_b;  dx_b = W^T dy_b;  dW = sum_b dy_b x_b^T (batched GEMM + a (B, Cout, Cin) sum)."""
+    """1x1 Conv1d without bias on the (B, C, K) layout, no layout copies (model.py:255-293, nn.Conv1d(cin, cout, 1)):
+    y_b = W x_b;  dx_b = W^T dy_b;  dW = sum_b dy_b x_b^T.  fp32 operands: avse_gemm_f32s (split-fp16 planes, three
+    f16 MFMAs per product, fp32 accumulation) with out[b, q, p] = sum_k P[b, p, k] Q[b, q, k]:
+      y:  P = x^T (B, K, Cin) read along K, Q = W (1, Cout, Cin)
+      dx: P = dy^T (B, K, Cout),            Q = W^T (1, Cin, Cout)
+      dW: P = x (B, Cin, K), Q = dy (B, Cout, K), the B batches folded into one output
+    x and dy are split once each (the planes' rows padded to a multiple of 8: K = 3999), x's planes are what the backward
+    keeps.  Otherwise batched hipBLASLt GEMMs (torch.bmm)."""
 
     @staticmethod
     def forward(ctx, w, x):
-        ctx.save_for_backward(w, x)
-        return torch.bmm(w.expand(x.shape[0], *w.shape), x)
+        ctx.split = _pw_split_ok(w, x)
+        if not ctx.split:
+            ctx.save_for_backward(w, x)
+            return torch.bmm(w.expand(x.shape[0], *w.shape), x)
+        xs = _split_act(x)
+        ws = K.split_planes(w[None])                        # kept for the input gradient (W^T: its transposed view)
+        y = torch.empty(x.shape[0], w.shape[0], x.shape[2], device=x.device, dtype=torch.float32)
+        K.gemm_f32s_split(xs.t(), ws, y)
+        ctx.save_for_backward(w, xs.hi, xs.lo, xs.mb, ws.hi, ws.lo, ws.mb)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
-        w, x = ctx.saved_tensors
         dw = dx = None
+        if not ctx.split:
+            w, x = ctx.saved_tensors
+            if ctx.needs_input_grad[0]:
+                dw = torch.bmm(dy, x.transpose(1, 2)).sum(0)
+            if ctx.needs_input_grad[1]:
+                dx = torch.bmm(w.t().expand(dy.shape[0], w.shape[1], w.shape[0]), dy)
+            return dw, dx
+        w, xh, xl, xm, wh, wl, wm = ctx.saved_tensors
+        dys = _split_act(dy)
         if ctx.needs_input_grad[0]:
-            dw = torch.bmm(dy, x.transpose(1, 2)).sum(0)
+            xs = K.Split(xh, xl, xm)
+            if _padded_rows(xs) and _padded_rows(dys) and xh.stride(1) == dys.hi.stride(1):
+                dw = K.gemm_f32s_time_chunks(xs, dys)       # the time axis shared out over the workgroups
+            else:
+                out = torch.empty(1, w.shape[0], w.shape[1], device=dy.device, dtype=torch.float32)
+                dw = K.gemm_f32s_split(xs, dys, out, fold=dy.shape[0])[0]
         if ctx.needs_input_grad[1]:
-            dx = torch.bmm(w.t().expand(dy.shape[0], w.shape[1], w.shape[0]), dy)
+            dx = torch.empty(dy.shape[0], w.shape[1], dy.shape[2], device=dy.device, dtype=torch.float32)
+            K.gemm_f32s_split(dys.t(), K.Split(wh, wl, wm).t(), dx)
         return dw, dx
 
 
@@ -95,7 +152,9 @@ class DepthwiseSeparableConv(nn.Module):
 
     def forward(self, x):
         dw, pr, nm, pw = self.net
-        y = dwconv_prelu_gln(x, dw.weight, pr.weight, nm.gamma, nm.beta, self.dilation)   # fused passes (gln.hip)
+        # fused passes (gln.hip); with the pointwise conv on the split-fp16 GEMM the gLN writes that GEMM's planes
+        planes = _pw_split_ok(pw.weight[:, :, 0], x)
+        y = dwconv_prelu_gln(x, dw.weight, pr.weight, nm.gamma, nm.beta, self.dilation, planes=planes)
         return _pw(pw, y)
 
 

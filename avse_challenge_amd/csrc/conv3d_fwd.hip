@@ -422,11 +422,13 @@ using namespace avse::c3f;
 
 extern "C" {
 
-// shapes compiled in: the avse1 front-end (3 x 96 x 96 lips)
+// shapes compiled in: the avse1 front-end (3 x 96 x 96 lips, uint8 or fp32) and the avse4 one (1 x 112 x 112
+// normalised grey frames, fp32: baseline/avse4/utils.py:97-118 frontend3D, the exact-fp32 MFMA path)
 int64_t avse_conv3d_fwd_workspace_bytes(int64_t CIN, int64_t H, int64_t W) {
     if (CIN == 3 && H == 96 && W == 96)
         return std::max<int64_t>(4 * (int64_t)Geo<3, 96, 96>::NQ * Geo<3, 96, 96>::WEL,
                                  2 * (int64_t)Geo<3, 96, 96>::NPL * WB_HALF + 16);
+    if (CIN == 1 && H == 112 && W == 112) return 4 * (int64_t)Geo<1, 112, 112>::NQ * Geo<1, 112, 112>::WEL;
     return 0;
 }
 
@@ -438,6 +440,10 @@ int avse_conv3d_fwd(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int
     if (CIN == 3 && H == 96 && W == 96) {
         if (x_dtype == AVSE_U8) return launch<uint8_t, 3, 96, 96>(B, T, x, w, y, workspace, st);
         if (x_dtype == AVSE_F32) return launch<float, 3, 96, 96>(B, T, x, w, y, workspace, st);
+        return AVSE_EDTYPE;
+    }
+    if (CIN == 1 && H == 112 && W == 112) {
+        if (x_dtype == AVSE_F32) return launch<float, 1, 112, 112>(B, T, x, w, y, workspace, st);
         return AVSE_EDTYPE;
     }
     return AVSE_ESHAPE;

@@ -80,6 +80,16 @@ __global__ __launch_bounds__(THREADS) void stats_kernel(int row0, int C, int K, 
     if (threadIdx.x == 0) ws[row] = make_float2(s1, s2);
 }
 
+template <typename T>
+__device__ inline T block_sum_max(T v, T* red) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
 // sample b's (sum_c v.x, sum_c v.y) over its C row partials, in double, by a 256-thread block (fixed order:
 // every caller gets the same bits)
 __device__ inline double2 sample_sums(const float2* __restrict__ ws, int b, int C, double* red /* [8] */,
@@ -119,15 +129,36 @@ __device__ inline float2 sample_stats(double2 sums, int C, int K, float shift, f
 // 0.0965 -> 0.101 ms).
 __device__ inline int second_pass_row() { return gridDim.x - 1 - blockIdx.x; }
 
+// power-of-two scale of the split planes from the bits of an upper bound of max |y| (the projection GEMM's split_exp:
+// bound 2^e in [2^14, 2^15); values up to twice the bound still fit fp16)
+__device__ inline int split_exp_gln(uint32_t mb) {
+    const int ef = (int)((mb >> 23) & 0xff);
+    if (mb == 0) return 0;
+    const int k = ef == 0 ? -127 : ef - 127;
+    return min(100, max(-100, 14 - k));
+}
+
+// Q output: the apply's y as the split-fp16 planes of the 1x1 Conv1d GEMM that consumes it (csrc/projgemm.hip
+// avse_gemm_f32s): hi = fp16(y 2^e), lo = fp16(y 2^e - hi) in rows of kp (a multiple of 8) elements; the padding
+// columns K .. kp - 1 are written as 0 (a weight-gradient GEMM over time chunks sums over them)
+struct QOut {
+    const uint32_t* maxbits;
+    _Float16* hi;
+    _Float16* lo;
+    int kp;
+};
+
 // apply with the finalize folded in: every row block re-derives its sample's statistics from the row partials (the
 // same sums in the same order in every block: bitwise equal), the channel-0 block stores them for the backward.
 // shift_src: the tensor whose (b, 0, 0) element defines the shift (y1 here)
+template <bool QO = false>
 __global__ __launch_bounds__(THREADS) void apply_fused_kernel(int row0, int C, int K, const float* __restrict__ x,
                                                               const float* __restrict__ alpha,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta,
                                                               const float2* __restrict__ ws, float eps,
-                                                              float2* __restrict__ stats, float* __restrict__ y) {
+                                                              float2* __restrict__ stats, float* __restrict__ y,
+                                                              QOut q = QOut{}) {
     __shared__ double red[8];
     const int row = row0 + (int)blockIdx.x, b = row / C, c = row % C;
     const float a = alpha[0];
@@ -135,8 +166,10 @@ __global__ __launch_bounds__(THREADS) void apply_fused_kernel(int row0, int C, i
     if (c == 0 && threadIdx.x == 0) stats[b] = st;
     const float g = gamma[c] * st.y, o = beta[c] - gamma[c] * st.y * st.x;
     const float* xr = x + (int64_t)row * K;
-    float* yr = y + (int64_t)row * K;
-    const auto rx = make_rsrc(xr, K), ry = make_rsrc(yr, K);
+    float* yr = QO ? nullptr : y + (int64_t)row * K;
+    const auto rx = make_rsrc(xr, K), ry = make_rsrc(QO ? xr : yr, K);
+    float sc = 1.f;
+    if constexpr (QO) sc = __builtin_ldexpf(1.f, split_exp_gln(*q.maxbits));
     for (int t0 = 0; t0 < K; t0 += UB4 * V4 * THREADS) {
         float4 xv[UB4];
 #pragma unroll
@@ -147,8 +180,62 @@ __global__ __launch_bounds__(THREADS) void apply_fused_kernel(int row0, int C, i
             float o4[4];
 #pragma unroll
             for (int e = 0; e < V4; ++e) o4[e] = g * prelu(f4at(xv[jj], e), a) + o;
-            st4_row(ry, yr, t, K, o4);
+            if constexpr (QO) {
+                if (t < K) {
+                    uint32_t h[2], l[2];
+#pragma unroll
+                    for (int e2 = 0; e2 < 2; ++e2) {
+                        const float s0 = t + 2 * e2 < K ? o4[2 * e2] * sc : 0.f;
+                        const float s1 = t + 2 * e2 + 1 < K ? o4[2 * e2 + 1] * sc : 0.f;
+                        const _Float16 h0 = (_Float16)s0, h1 = (_Float16)s1;
+                        const _Float16 l0 = (_Float16)(s0 - (float)h0), l1 = (_Float16)(s1 - (float)h1);
+                        h[e2] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+                        l[e2] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+                    }
+                    const int64_t off = (int64_t)row * q.kp + t;
+                    *reinterpret_cast<uint2*>(q.hi + off) = uint2{h[0], h[1]};
+                    *reinterpret_cast<uint2*>(q.lo + off) = uint2{l[0], l[1]};
+                }
+            } else {
+                st4_row(ry, yr, t, K, o4);
+            }
         }
+    }
+    if constexpr (QO) {
+        for (int t = (K + 3) / 4 * 4 + 4 * (int)threadIdx.x; t < q.kp; t += 4 * THREADS) {
+            const int64_t off = (int64_t)row * q.kp + t;
+            *reinterpret_cast<uint2*>(q.hi + off) = uint2{0u, 0u};
+            *reinterpret_cast<uint2*>(q.lo + off) = uint2{0u, 0u};
+        }
+    }
+}
+
+// An upper bound of max |y| for the split planes, before any apply block writes: per row, y = g p + o is affine in
+// p = PReLU(.), so max |y| over the row is max(|g pmin + o|, |g pmax + o|) from the row's PReLU extremes (mm, written
+// by the statistics pass).  One block per sample re-derives its statistics as the apply does and max-reduces its rows.
+__global__ __launch_bounds__(256) void q_bound_kernel(int C, int K, const float* __restrict__ x,
+                                                      const float* __restrict__ alpha, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, const float2* __restrict__ ws,
+                                                      const float2* __restrict__ mm, float eps,
+                                                      uint32_t* __restrict__ maxbits) {
+    __shared__ double red[8];
+    __shared__ float fred[4];
+    const int b = blockIdx.x;
+    const float a = alpha[0];
+    const float2 st = sample_stats(sample_sums(ws, b, C, red), C, K, prelu(x[(int64_t)b * C * K], a), eps);
+    float m = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        const float g = gamma[c] * st.y, o = beta[c] - gamma[c] * st.y * st.x;
+        const float2 e = mm[(int64_t)b * C + c];
+        m = fmaxf(m, fmaxf(fabsf(g * e.x + o), fabsf(g * e.y + o)));
+    }
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) fred[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // a few ulps of headroom over the apply's own rounding of g p + o (the scale only needs an upper bound)
+        const uint32_t v = __float_as_uint(fmaxf(fmaxf(fred[0], fred[1]), fmaxf(fred[2], fred[3])) * 1.0001f);
+        if (v) atomicMax(maxbits, v);
     }
 }
 
@@ -306,11 +393,11 @@ __global__ void alpha_finalize(int rows, const float* __restrict__ ws_alpha, flo
 //        the slope.
 constexpr int DW_MAXP = 7, DW_MAXHALO = 512;
 
-template <int P>
+template <int P, bool MM = false>
 __global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int row0, int C, int K, int dil, const float* __restrict__ x,
                                                                const float* __restrict__ w,
                                                                const float* __restrict__ alpha, float* __restrict__ y1,
-                                                               float2* __restrict__ ws) {
+                                                               float2* __restrict__ ws, float2* __restrict__ mm = nullptr) {
     // streaming form, no LDS: thread t-loop over the row with the taps' neighbours (+-halo) read straight from the
     // cache lines this workgroup just brought in (each x line leaves HBM once); the same k-ordered sums as the tiled
     // form (bitwise equal y1, same per-thread element order for the statistics)
@@ -335,6 +422,7 @@ __global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int row0, int C, 
     }
     const float shift = prelu(y00, a);
     float s1 = 0.f, s2 = 0.f;
+    float pmin = __builtin_inff(), pmax = -__builtin_inff();         // MM: the row's PReLU extremes (the split planes' bound)
     const auto rx = make_rsrc(xr, K);                 // taps outside the row load 0 (buffer range check, no branch)
     for (int t0 = 0; t0 < K; t0 += DW_U * THREADS) {  // DW_U elements per thread in flight
         float acc[DW_U];
@@ -350,15 +438,25 @@ __global__ __launch_bounds__(THREADS) void dwconv_stats_kernel(int row0, int C, 
             const int t = t0 + j * THREADS + threadIdx.x;
             if (t < K) {
                 yr[t] = acc[j];
-                const float v = prelu(acc[j], a) - shift;
+                const float pv = prelu(acc[j], a);
+                const float v = pv - shift;
                 s1 += v;
                 s2 += v * v;
+                if constexpr (MM) {
+                    pmin = fminf(pmin, pv);
+                    pmax = fmaxf(pmax, pv);
+                }
             }
         }
     }
     s1 = block_sum(s1, red);
     s2 = block_sum(s2, red);
     if (threadIdx.x == 0) ws[row] = make_float2(s1, s2);
+    if constexpr (MM) {
+        pmin = -block_sum_max(-pmin, red);
+        pmax = block_sum_max(pmax, red);
+        if (threadIdx.x == 0) mm[row] = make_float2(pmin, pmax);
+    }
 }
 
 template <int P>
@@ -655,7 +753,7 @@ int avse_prelu_gln_fwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
         const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
         hipLaunchKernelGGL(stats_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, ws);
         AVSE_CHECK_LAUNCH();
-        hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
+        hipLaunchKernelGGL(apply_fused_kernel<false>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
                            beta, (const float2*)ws, eps, (float2*)stats, y);
         AVSE_CHECK_LAUNCH();
     }
@@ -732,10 +830,39 @@ int avse_dwconv_gln_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
         AVSE_DW_P_SWITCH(P, L_)
 #undef L_
         AVSE_CHECK_LAUNCH();
-        hipLaunchKernelGGL(apply_fused_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha, gamma,
+        hipLaunchKernelGGL(apply_fused_kernel<false>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha, gamma,
                            beta, (const float2*)ws, eps, (float2*)stats, y);
         AVSE_CHECK_LAUNCH();
     }
+    return AVSE_OK;
+}
+
+int avse_dwconv_gln_fwd_q(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
+                          const float* alpha, const float* gamma, const float* beta, float eps, float* y1, void* y_hi,
+                          void* y_lo, int64_t kp, uint32_t* y_maxbits, float* stats, float* workspace,
+                          avse_stream_t stream) {
+    if (!x || !w || !alpha || !gamma || !beta || !y1 || !y_hi || !y_lo || !y_maxbits || !stats || !workspace)
+        return AVSE_EINVAL;
+    if (int rc = dw_check(B, C, K, P, dil)) return rc;
+    if (kp < K || kp % 8 || B * C * kp >= (1LL << 40)) return AVSE_ESHAPE;
+    if (((uintptr_t)y_hi | (uintptr_t)y_lo) % 16) return AVSE_EALIGN;
+    hipStream_t st = (hipStream_t)stream;
+    float2* ws = (float2*)workspace;
+    float2* mm = ws + B * C;                      // the row extremes (the backward's slope-partial region)
+    const unsigned rows = (unsigned)(B * C);
+    if (hipMemsetAsync(y_maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
+#define L_(PP) hipLaunchKernelGGL((dwconv_stats_kernel<PP, true>), dim3(rows), dim3(THREADS), 0, st, 0, (int)C, (int)K, \
+                              (int)dil, x, w, alpha, y1, ws, mm)
+    AVSE_DW_P_SWITCH(P, L_)
+#undef L_
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(q_bound_kernel, dim3((unsigned)B), dim3(256), 0, st, (int)C, (int)K, y1, alpha, gamma, beta,
+                       (const float2*)ws, (const float2*)mm, eps, y_maxbits);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(apply_fused_kernel<true>, dim3(rows), dim3(THREADS), 0, st, 0, (int)C, (int)K, y1, alpha, gamma,
+                       beta, (const float2*)ws, eps, (float2*)stats, nullptr,
+                       QOut{y_maxbits, (_Float16*)y_hi, (_Float16*)y_lo, (int)kp});
+    AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
 

@@ -84,7 +84,15 @@ struct Args {
     const uint16_t* q_lo;
     const uint32_t* p_max;
     const uint32_t* q_max;
+    // nsub > 1: batch b sits at (b / nsub) bs + (b % nsub) bs2 (a reduction split into nsub chunks of k per batch, e.g.
+    // the time chunks of a 1x1-conv weight gradient, folded and summed as batches); otherwise at b bs
+    int32_t nsub;
+    int64_t p_bs2, q_bs2;
 };
+
+__device__ inline int64_t batch_off(int b, int nsub, int64_t bs, int64_t bs2) {
+    return nsub > 1 ? (int64_t)(b / nsub) * bs + (int64_t)(b % nsub) * bs2 : (int64_t)b * bs;
+}
 
 // power-of-two split scale of a tensor with max |x| bits mb (the same function as dconv.hip's / gemmsplit's)
 __device__ inline int split_exp_pg(uint32_t mb) {
@@ -280,11 +288,12 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
     auto set_tile = [&](int T, int f) {
         const Tile t = tile_of(a, T);
         const int b = t.b * a.fold + f;
-        rp = rsrc_from(a.p + (int64_t)b * a.p_bs, a.p_ext - (int64_t)b * a.p_bs);
-        rq = rsrc_from(a.q + (int64_t)b * a.q_bs, a.q_ext - (int64_t)b * a.q_bs);
+        const int64_t po = batch_off(b, a.nsub, a.p_bs, a.p_bs2), qo = batch_off(b, a.nsub, a.q_bs, a.q_bs2);
+        rp = rsrc_from(a.p + po, a.p_ext - po);
+        rq = rsrc_from(a.q + qo, a.q_ext - qo);
         if constexpr (SPLIT) {
-            rp_lo = rsrc_from(a.p_lo + (int64_t)b * a.p_bs, a.p_ext - (int64_t)b * a.p_bs);
-            rq_lo = rsrc_from(a.q_lo + (int64_t)b * a.q_bs, a.q_ext - (int64_t)b * a.q_bs);
+            rp_lo = rsrc_from(a.p_lo + po, a.p_ext - po);
+            rq_lo = rsrc_from(a.q_lo + qo, a.q_ext - qo);
         }
         piece_offsets<P_KC>(vp, t.p0, a.p_sx, a.mp, wave, lane);
         piece_offsets<Q_KC>(vq, t.q0, a.q_sx, a.mq, wave, lane);
@@ -524,13 +533,14 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_kernel(Args a) {
 using namespace avse::pg;
 
 // ------------------------------------------------------------------------------------------------ split planes
-// x (b, r, c) fp32, c contiguous -> hi / lo fp16 planes with x's strides: hi = fp16(x 2^e), lo = fp16(x 2^e - hi) with
-// max |x| 2^e in [2^14, 2^15) (dconv.hip's split, the same 22 significant bits); the planes' padding is not written.
+// x (b, r, c) fp32, c contiguous -> hi / lo fp16 planes (rows hrs, batches hbs apart: x's strides, or a padded layout
+// whose rows are 16-B aligned for the GEMM's DMA): hi = fp16(x 2^e), lo = fp16(x 2^e - hi) with max |x| 2^e in
+// [2^14, 2^15) (dconv.hip's split, the same 22 significant bits); the planes' padding is not written.
 // Two streaming passes (max, then split): a workgroup takes rpb consecutive rows, float4 accesses when the rows are
-// 16-B aligned (VEC), the row's last c % 4 elements one by one; 4 accesses in flight per thread.
+// 16-B aligned (VEC), the row's last c % 4 elements one by one; 4 accesses in flight per thread either way.
 struct PlanesArgs {
     const float* x;
-    int64_t rows, r, c, bs, rs;
+    int64_t rows, r, c, bs, rs, hbs, hrs;
     int rpb;
     uint32_t* maxbits;
     _Float16* hi;
@@ -538,6 +548,9 @@ struct PlanesArgs {
 };
 
 __device__ inline int64_t planes_row_off(const PlanesArgs& a, int64_t row) { return (row / a.r) * a.bs + (row % a.r) * a.rs; }
+__device__ inline int64_t planes_out_off(const PlanesArgs& a, int64_t row) {
+    return (row / a.r) * a.hbs + (row % a.r) * a.hrs;
+}
 
 // grid-stride over the row blocks (a bounded grid), one atomicMax per workgroup: one per wave over 10^5 row blocks
 // serialised on the single word (6.8 ms for a C3 activation, profiles/r05i_gemm_f32s_probe.jsonl)
@@ -562,7 +575,13 @@ __global__ __launch_bounds__(256) void planes_absmax_kernel(PlanesArgs a, int64_
                     m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
             }
         }
-        for (int64_t i = 4 * c4 + threadIdx.x; i < a.c; i += 256) m = fmaxf(m, fabsf(xr[i]));
+        for (int64_t i0 = 4 * c4 + threadIdx.x; i0 < a.c; i0 += 4 * 256) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = i0 + u * 256 < a.c ? xr[i0 + u * 256] : 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) m = fmaxf(m, fabsf(v[u]));
+        }
     }
     uint32_t v = __float_as_uint(m);
     for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
@@ -589,8 +608,8 @@ __global__ __launch_bounds__(256) void planes_split_kernel(PlanesArgs a) {
     for (int rr = 0; rr < a.rpb; ++rr) {
         const int64_t row = (int64_t)blockIdx.x * a.rpb + rr;
         if (row >= a.rows) break;
-        const int64_t off = planes_row_off(a, row);
-        const float* xr = a.x + off;
+        const int64_t off = planes_out_off(a, row);
+        const float* xr = a.x + planes_row_off(a, row);
         if constexpr (VEC) {
             uint2* hr = reinterpret_cast<uint2*>(a.hi + off);
             uint2* lr = reinterpret_cast<uint2*>(a.lo + off);
@@ -610,11 +629,55 @@ __global__ __launch_bounds__(256) void planes_split_kernel(PlanesArgs a) {
                 }
             }
         }
-        for (int64_t i = 4 * c4 + threadIdx.x; i < a.c; i += 256) {
-            const float v = xr[i] * sc;
-            const _Float16 h = (_Float16)v;
-            a.hi[off + i] = h;
-            a.lo[off + i] = (_Float16)(v - (float)h);
+        for (int64_t i0 = 4 * c4 + threadIdx.x; i0 < a.c; i0 += 4 * 256) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + u * 256 < a.c) v[u] = xr[i0 + u * 256];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t i = i0 + u * 256;
+                if (i >= a.c) break;
+                const float w = v[u] * sc;
+                const _Float16 h = (_Float16)w;
+                a.hi[off + i] = h;
+                a.lo[off + i] = (_Float16)(w - (float)h);
+            }
+        }
+    }
+}
+
+// x rows of any alignment -> planes with 8-B aligned rows of hrs elements (the padded-row layout, hrs >= c): each thread
+// writes 4 consecutive elements of a row as one 8-B store per plane, loading them element by element (lanes read
+// consecutive addresses), 4 quadruples in flight; the pad columns c .. hrs - 1 are written as 0, so a GEMM may sum
+// over them (the time chunks of a weight gradient).
+__global__ __launch_bounds__(256) void planes_split_pad_kernel(PlanesArgs a) {
+    const float sc = __builtin_ldexpf(1.f, split_exp_pg(*a.maxbits));
+    const int64_t q4 = a.hrs / 4;                                  // quadruples per output row
+    for (int rr = 0; rr < a.rpb; ++rr) {
+        const int64_t row = (int64_t)blockIdx.x * a.rpb + rr;
+        if (row >= a.rows) break;
+        const float* xr = a.x + planes_row_off(a, row);
+        uint2* hr = reinterpret_cast<uint2*>(a.hi + planes_out_off(a, row));
+        uint2* lr = reinterpret_cast<uint2*>(a.lo + planes_out_off(a, row));
+        for (int64_t j0 = threadIdx.x; j0 < q4; j0 += 4 * 256) {
+            float v[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int64_t i = 4 * (j0 + u * 256) + e;
+                    v[u][e] = (j0 + u * 256 < q4 && i < a.c) ? xr[i] : 0.f;
+                }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (j0 + u * 256 >= q4) break;
+                uint2 h, l;
+                h.x = split_pair(v[u][0], v[u][1], sc, l.x);
+                h.y = split_pair(v[u][2], v[u][3], sc, l.y);
+                hr[j0 + u * 256] = h;
+                lr[j0 + u * 256] = l;
+            }
         }
     }
 }
@@ -665,18 +728,21 @@ static int launch_gemm(int64_t batch, int64_t mp, int64_t mq, int64_t k, int64_t
                        int64_t p_bs, int64_t p_sx, int64_t p_sk, int64_t p_extent, const uint32_t* p_max, const void* q,
                        const void* q_lo, int64_t q_bs, int64_t q_sx, int64_t q_sk, int64_t q_extent,
                        const uint32_t* q_max, void* c, int64_t c_bs, int64_t c_sq, float alpha, int32_t c_dtype,
-                       avse_stream_t stream) {
+                       avse_stream_t stream, int64_t nsub = 1, int64_t p_bs2 = 0, int64_t q_bs2 = 0) {
     if (!p || !q || !c || (SPLIT && (!p_lo || !q_lo || !p_max || !q_max))) return AVSE_EINVAL;
     if (c_dtype != AVSE_BF16 && c_dtype != AVSE_F32) return AVSE_EDTYPE;
     if (SPLIT && c_dtype != AVSE_F32) return AVSE_EDTYPE;
     const int64_t fold = fold_in > 0 ? fold_in : 1;
-    if (batch <= 0 || mp <= 0 || mq <= 0 || k <= 0 || batch % fold) return AVSE_ESHAPE;
+    if (batch <= 0 || mp <= 0 || mq <= 0 || k <= 0 || batch % fold || nsub >= (1 << 30)) return AVSE_ESHAPE;
     const bool p_kc = p_sk == 1, q_kc = q_sk == 1;
     if (!p_kc && p_sx != 1) return AVSE_ESHAPE;
     if (!q_kc && q_sx != 1) return AVSE_ESHAPE;
     const int64_t p_s = p_kc ? p_sx : p_sk, q_s = q_kc ? q_sx : q_sk;
     const int c_align = c_dtype == AVSE_F32 ? 15 : 7;
-    if (p_s % 8 || q_s % 8 || ((uintptr_t)p & 15) || ((uintptr_t)q & 15) || ((uintptr_t)c & c_align) || c_sq % 4 ||
+    // fp32 out, no folding (the LDS-staged epilogue 2): any row stride (rows not 16-B aligned are stored per element)
+    const bool c_any = SPLIT && fold == 1;
+    if (p_s % 8 || q_s % 8 || ((uintptr_t)p & 15) || ((uintptr_t)q & 15) || ((uintptr_t)c & c_align) ||
+        (!c_any && c_sq % 4) ||
         (SPLIT && (((uintptr_t)p_lo & 15) || ((uintptr_t)q_lo & 15))))
         return AVSE_EALIGN;
     const int64_t tp = (mp + BT - 1) / BT, tq = (mq + BT - 1) / BT, ntb = (k + BK - 1) / BK;
@@ -715,7 +781,11 @@ static int launch_gemm(int64_t batch, int64_t mp, int64_t mq, int64_t k, int64_t
     // the shared weight's tiles vary fastest; otherwise the operand with fewer tiles
     a.q_fast = (q_bs == 0) ? 1 : (p_bs == 0) ? 0 : (tq <= tp);
     a.alpha = alpha;
-    a.c_vec16 = ((uintptr_t)c % 16 == 0) && (c_sq % 8 == 0);
+    a.nsub = nsub > 1 ? (int32_t)nsub : 1;
+    a.p_bs2 = p_bs2;
+    a.q_bs2 = q_bs2;
+    a.c_vec16 = ((uintptr_t)c % 16 == 0) && (c_sq % (c_dtype == AVSE_F32 ? 4 : 8) == 0) &&
+                (c_bs % (c_dtype == AVSE_F32 ? 4 : 8) == 0);
     // persistent: one workgroup per CU (128 KB of LDS each), a multiple of 8 (the XCD tile split)
     int64_t G = ((int64_t)cu_count_cached() + 7) / 8 * 8;
     const int64_t need = (ntiles + 7) / 8 * 8;
@@ -754,13 +824,15 @@ int avse_gemm_f32s(const avse_gemm_f32s_args* g, avse_stream_t stream) {
     if (!g) return AVSE_EINVAL;
     return launch_gemm<true>(g->batch, g->mp, g->mq, g->k, g->fold, g->p_hi, g->p_lo, g->p_bs, g->p_sx, g->p_sk,
                              g->p_extent, g->p_max, g->q_hi, g->q_lo, g->q_bs, g->q_sx, g->q_sk, g->q_extent, g->q_max,
-                             g->c, g->c_bs, g->c_sq, g->alpha, AVSE_F32, stream);
+                             g->c, g->c_bs, g->c_sq, g->alpha, AVSE_F32, stream, g->nsub, g->p_bs2, g->q_bs2);
 }
 
 static int split16_planes_impl(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
-                               void* lo, uint32_t* maxbits, bool known, avse_stream_t stream) {
+                               void* lo, int64_t h_bs, int64_t h_rs, uint32_t* maxbits, bool known,
+                               avse_stream_t stream) {
     if (!x || !hi || !lo || !maxbits) return AVSE_EINVAL;
     if (b <= 0 || r <= 0 || c <= 0 || x_rs < c || (b > 1 && x_bs < (r - 1) * x_rs + c)) return AVSE_ESHAPE;
+    if (h_rs < c || (b > 1 && h_bs < (r - 1) * h_rs + c)) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     if (!known && hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
     PlanesArgs a;
@@ -770,6 +842,8 @@ static int split16_planes_impl(int64_t b, int64_t r, int64_t c, const float* x, 
     a.c = c;
     a.bs = x_bs;
     a.rs = x_rs;
+    a.hbs = h_bs;
+    a.hrs = h_rs;
     a.maxbits = maxbits;
     a.hi = (_Float16*)hi;
     a.lo = (_Float16*)lo;
@@ -778,20 +852,49 @@ static int split16_planes_impl(int64_t b, int64_t r, int64_t c, const float* x, 
     a.rpb = (int)std::max<int64_t>(1, std::min<int64_t>(1024 / std::max<int64_t>(c4, 1), 64));
     const int64_t blocks = (a.rows + a.rpb - 1) / a.rpb;
     if (blocks >= (1LL << 31)) return AVSE_ESHAPE;
-    const bool vec = ((uintptr_t)x % 16 == 0) && ((uintptr_t)hi % 8 == 0) && ((uintptr_t)lo % 8 == 0) &&
-                     (x_rs % 4 == 0) && (b == 1 || x_bs % 4 == 0);
-    const unsigned mgrid = (unsigned)std::min<int64_t>(blocks, 2048);
-    if (vec) {
-        if (!known) {
-            hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3(mgrid), dim3(256), 0, st, a, blocks);
+    const bool xvec = ((uintptr_t)x % 16 == 0) && (x_rs % 4 == 0) && (b == 1 || x_bs % 4 == 0);
+    const bool hvec = ((uintptr_t)hi % 8 == 0) && ((uintptr_t)lo % 8 == 0) && (h_rs % 4 == 0) && (b == 1 || h_bs % 4 == 0);
+    // padded output rows (8-B aligned) differing from x's: the quadruple kernel, which writes the pads as 0
+    const bool pad = hvec && (h_rs != x_rs || (b > 1 && h_bs != x_bs));
+    if (!known) {
+        const int64_t n = b * r * c;
+        if (xvec) {
+            hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3((unsigned)std::min<int64_t>(blocks, 2048)), dim3(256), 0,
+                               st, a, blocks);
+            AVSE_CHECK_LAUNCH();
+        } else if (x_rs == c && (b == 1 || x_bs == r * c) && ((uintptr_t)x % 16 == 0) && n >= 4096) {
+            // contiguous x whose rows are not 16-B aligned: the flat array in 4096-element rows (float4), the tail as
+            // one more row
+            PlanesArgs f = a;
+            f.rows = f.r = n / 4096;
+            f.c = f.rs = 4096;
+            f.bs = 0;
+            f.rpb = 1;
+            hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3((unsigned)std::min<int64_t>(f.rows, 2048)), dim3(256), 0,
+                               st, f, f.rows);
+            AVSE_CHECK_LAUNCH();
+            if (n % 4096) {
+                f.x = x + f.rows * 4096;
+                f.rows = f.r = 1;
+                f.c = f.rs = n % 4096;
+                hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3(1), dim3(256), 0, st, f, (int64_t)1);
+                AVSE_CHECK_LAUNCH();
+            }
+        } else {
+            hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3((unsigned)std::min<int64_t>(blocks, 2048)), dim3(256), 0,
+                               st, a, blocks);
             AVSE_CHECK_LAUNCH();
         }
+    }
+    if (pad) {
+        PlanesArgs p2 = a;
+        p2.rpb = (int)std::max<int64_t>(1, std::min<int64_t>(1024 / std::max<int64_t>(h_rs / 4, 1), 64));
+        const int64_t pblocks = (a.rows + p2.rpb - 1) / p2.rpb;
+        if (pblocks >= (1LL << 31)) return AVSE_ESHAPE;
+        hipLaunchKernelGGL(planes_split_pad_kernel, dim3((unsigned)pblocks), dim3(256), 0, st, p2);
+    } else if (xvec && hvec) {
         hipLaunchKernelGGL(planes_split_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
     } else {
-        if (!known) {
-            hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3(mgrid), dim3(256), 0, st, a, blocks);
-            AVSE_CHECK_LAUNCH();
-        }
         hipLaunchKernelGGL(planes_split_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
     }
     AVSE_CHECK_LAUNCH();
@@ -816,12 +919,17 @@ int avse_add_max(int64_t rows, int64_t lp, int64_t l, const float* a, const floa
 
 int avse_split16_planes(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi, void* lo,
                         uint32_t* maxbits, avse_stream_t stream) {
-    return split16_planes_impl(b, r, c, x, x_bs, x_rs, hi, lo, maxbits, false, stream);
+    return split16_planes_impl(b, r, c, x, x_bs, x_rs, hi, lo, x_bs, x_rs, maxbits, false, stream);
 }
 
 int avse_split16_planes_known(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
                               void* lo, const uint32_t* maxbits, avse_stream_t stream) {
-    return split16_planes_impl(b, r, c, x, x_bs, x_rs, hi, lo, const_cast<uint32_t*>(maxbits), true, stream);
+    return split16_planes_impl(b, r, c, x, x_bs, x_rs, hi, lo, x_bs, x_rs, const_cast<uint32_t*>(maxbits), true, stream);
+}
+
+int avse_split16_planes_to(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
+                           void* lo, int64_t h_bs, int64_t h_rs, uint32_t* maxbits, int32_t known, avse_stream_t stream) {
+    return split16_planes_impl(b, r, c, x, x_bs, x_rs, hi, lo, h_bs, h_rs, maxbits, known != 0, stream);
 }
 
 }  // extern "C"

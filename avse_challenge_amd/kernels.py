@@ -3,6 +3,7 @@
 Each wrapper validates shapes/dtypes/strides, allocates its outputs and workspace with torch
 (caching allocator, stream-ordered) and enqueues the HIP kernels on torch's current stream.
 """
+import functools
 import os
 
 import torch
@@ -422,7 +423,7 @@ def conv3d_fwd_supported(x, w, stride, padding):
     """True when the MFMA forward (conv3d_fwd.hip) is compiled for this lip front-end shape."""
     return (tuple(stride) == (1, 2, 2) and tuple(padding) == (2, 3, 3) and tuple(w.shape[0:1]) == (64,)
             and tuple(w.shape[2:]) == (5, 7, 7) and x.dim() == 5 and x.shape[1] == w.shape[1]
-            and x.dtype in (torch.uint8, torch.float32)
+            and (x.dtype == torch.float32 or (x.dtype == torch.uint8 and x.shape[1] == 3))   # uint8: avse1's f16 path
             and x.numel() * x.element_size() < (1 << 31)          # the kernel's 32-bit buffer offsets
             and _lib.lib().avse_conv3d_fwd_workspace_bytes(x.shape[1], x.shape[3], x.shape[4]) > 0)
 
@@ -1041,16 +1042,54 @@ def dwconv_bwd(x, w, dy, dilation):
 
 # ------------------------------------------------------------------------ fused dwconv <-> PReLU -> gLN (avse4)
 
-def dwconv_gln_fwd(x, w, dilation, alpha, gamma, beta, eps=1e-8):
-    """y1 = depthwise dilated conv1d(x) (w (C, 1, P)), y = gLN(PReLU(y1)); returns (y, y1, stats (B, 2))."""
+# The split planes a producer wrote for the split-fp16 GEMM that consumes its output (PLANES_ATTR: a Split on an fp32
+# "carrier" tensor of the output's shape whose storage holds the two planes; its own elements are not the values, so
+# only that GEMM may read it — avse4._PointwiseFn).
+PLANES_ATTR = "_avse_planes"
+
+
+def planes_of(t):
+    return getattr(t, PLANES_ATTR, None)
+
+
+def _planes_carrier(shape, device):
+    """(carrier, Split) for a (b, r, c) output written as split planes with rows of cp = c rounded up to 8 elements:
+    one allocation of 4 (b r cp + 16) bytes = the hi plane, 16 elements of slack, the lo plane, 16 of slack."""
+    b, r, c = shape
+    cp = (c + 7) // 8 * 8
+    n = b * r * cp + 16
+    store = torch.empty(n, device=device, dtype=torch.float32).untyped_storage()
+    carrier = torch.empty(0, device=device, dtype=torch.float32).set_(store, 0, (b, r, c), (r * cp, cp, 1))
+    hi = torch.empty(0, device=device, dtype=torch.float16).set_(store, 0, (b, r, c), (r * cp, cp, 1))
+    lo = torch.empty(0, device=device, dtype=torch.float16).set_(store, n, (b, r, c), (r * cp, cp, 1))
+    mb = torch.empty(1, device=device, dtype=torch.int32)
+    sp = Split(hi, lo, mb)
+    setattr(carrier, PLANES_ATTR, sp)
+    return carrier, sp, cp
+
+
+def dwconv_gln_fwd(x, w, dilation, alpha, gamma, beta, eps=1e-8, planes=False):
+    """y1 = depthwise dilated conv1d(x) (w (C, 1, P)), y = gLN(PReLU(y1)); returns (y, y1, stats (B, 2)).  planes: y is
+    written only as the split-fp16 planes of its consumer GEMM (avse_dwconv_gln_fwd_q) and returned as their carrier
+    (PLANES_ATTR)."""
     _need_gpu(x, w, alpha, gamma, beta)
     x = x.float().contiguous()
     Bn, C, Kn = x.shape
     w2 = w.reshape(C, -1).float().contiguous()
-    y1, y = torch.empty_like(x), torch.empty_like(x)
     stats = torch.empty((Bn, 2), device=x.device, dtype=torch.float32)
     L = _lib.lib()
     ws = torch.empty((L.avse_dwconv_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    y1 = torch.empty_like(x)
+    if planes:
+        y, sp, cp = _planes_carrier((Bn, C, Kn), x.device)
+        tap = _tap_begin("avse_dwconv_gln_fwd_q", x.device)
+        check(L.avse_dwconv_gln_fwd_q(Bn, C, Kn, w2.shape[1], int(dilation), ptr(x), ptr(w2),
+                                      ptr(alpha.float().contiguous()), ptr(gamma.float().contiguous()),
+                                      ptr(beta.float().contiguous()), float(eps), ptr(y1), ptr(sp.hi), ptr(sp.lo), cp,
+                                      ptr(sp.mb), ptr(stats), ptr(ws), stream_ptr(x.device)), "avse_dwconv_gln_fwd_q")
+        _tap_end(tap)
+        return y, y1, stats
+    y = torch.empty_like(x)
     tap = _tap_begin("avse_dwconv_gln_fwd", x.device)
     check(L.avse_dwconv_gln_fwd(Bn, C, Kn, w2.shape[1], int(dilation), ptr(x), ptr(w2), ptr(alpha.float().contiguous()),
                                 ptr(gamma.float().contiguous()), ptr(beta.float().contiguous()), float(eps), ptr(y1),
@@ -1347,6 +1386,27 @@ def split_planes(t):
     return Split(hi, lo, mb)
 
 
+def split_rows8(t):
+    """t (b, r, c) fp32 with stride(2) == 1 -> Split whose planes are (b, r, c) views of (b, r, cp) storage, cp = c
+    rounded up to a multiple of 8 (csrc/projgemm.hip avse_split16_planes_to): an operand of avse_gemm_f32s read along c
+    or along r whatever c is (the avse4 (B, C, K) activations, K = 3999).  The pad columns are never written; the GEMM
+    only reads them into output rows it does not store (along r) or into the zeroed tail of its last k-stage (along c)."""
+    _need_gpu(t)
+    if t.dtype != torch.float32 or t.dim() != 3 or t.stride(2) != 1:
+        raise RuntimeError("split_rows8: (b, r, c) fp32 views with a unit last stride only")
+    b, r, c = t.shape
+    cp = (c + 7) // 8 * 8
+    n = b * r * cp + 16                        # 16 elements of slack: a 16-B DMA at any element stays in the range
+    hi = torch.empty(n, device=t.device, dtype=torch.float16).as_strided((b, r, c), (r * cp, cp, 1))
+    lo = torch.empty(n, device=t.device, dtype=torch.float16).as_strided((b, r, c), (r * cp, cp, 1))
+    known = _known_absmax(t)
+    mb = known if known is not None else torch.empty(1, device=t.device, dtype=torch.int32)
+    x_bs = t.stride(0) if b > 1 else (r - 1) * t.stride(1) + c
+    check(_lib.lib().avse_split16_planes_to(b, r, c, ptr(t), x_bs, t.stride(1), ptr(hi), ptr(lo), r * cp, cp, ptr(mb),
+                                            int(known is not None), stream_ptr(t.device)), "avse_split16_planes_to")
+    return Split(hi, lo, mb)
+
+
 def gemm_f32s_supported(P, Q, out, fold=1):
     """True when avse_gemm_f32s takes out[g, q, p] = sum_{b in g} sum_k P[b, p, k] Q[b, q, k] for these fp32 views."""
     return P.is_cuda and P.dtype == Q.dtype == torch.float32 and _f32s_layout_ok(P, Q, out, fold)
@@ -1363,7 +1423,8 @@ def _f32s_layout_ok(P, Q, out, fold=1):
         return False
     if max(P.shape[0], Q.shape[0]) != b and fold != 1:
         return False
-    if out.stride(2) != 1 or out.stride(1) % 4 or out.data_ptr() % 16:
+    # fp32 rows of any stride without folding (stored per element when not 16-B aligned); folded: 16-B rows
+    if out.stride(2) != 1 or (fold != 1 and out.stride(1) % 4) or out.data_ptr() % 16:
         return False
     return _gemm_operand(P) is not None and _gemm_operand(Q) is not None
 
@@ -1384,6 +1445,12 @@ def gemm_f32s(P, Q, out, alpha=1.0, fold=1, ps=None, qs=None):
     return gemm_f32s_split(ps or split_planes(P), qs or split_planes(Q), out, alpha, fold)
 
 
+def _plane_extent(sp):
+    """Elements readable from both planes' starts (one range serves both: the planes of a carrier share a storage, the
+    lo plane last)."""
+    return min(_extent(sp.hi), _extent(sp.lo))
+
+
 def gemm_f32s_split(sp, sq, out, alpha=1.0, fold=1):
     """gemm_f32s on operands given only by their Splits (the fp32 tensors need not be kept)."""
     _need_gpu(sp.hi, sq.hi, out)
@@ -1396,12 +1463,67 @@ def gemm_f32s_split(sp, sq, out, alpha=1.0, fold=1):
     a = _lib.GemmF32sArgs()
     a.batch, a.mp, a.mq, a.k, a.fold = out.shape[0] * fold, P.shape[1], Q.shape[1], P.shape[2], fold
     a.p_hi, a.p_lo, (a.p_bs, a.p_sx, a.p_sk), a.p_extent, a.p_max = ph.data_ptr(), pl.data_ptr(), _gemm_operand(ph), \
-        _extent(ph), pm.data_ptr()
+        _plane_extent(sp), pm.data_ptr()
     a.q_hi, a.q_lo, (a.q_bs, a.q_sx, a.q_sk), a.q_extent, a.q_max = qh.data_ptr(), ql.data_ptr(), _gemm_operand(qh), \
-        _extent(qh), qm.data_ptr()
+        _plane_extent(sq), qm.data_ptr()
     a.c, a.c_bs, a.c_sq = out.data_ptr(), out.stride(0), out.stride(1)
     a.alpha = float(alpha)
+    a.nsub = 1
     tap = _tap_begin("avse_gemm_f32s", out.device)
     check(_lib.lib().avse_gemm_f32s(a, stream_ptr(out.device)), "avse_gemm_f32s")
     _tap_end(tap)
     return out
+
+
+@functools.lru_cache(maxsize=None)
+def _chunk_plan(kp, nb, tiles_out, cus=256):
+    """(kc, fold) for a weight gradient summed over nb batches of kp time columns: time chunks of kc columns (kc | kp,
+    kc % 8 == 0) become nb kp / kc batches, folded by ``fold`` into partial outputs summed afterwards; minimises a
+    stage-count model (rounds of workgroups x stages per tile + a partial-sum pass)."""
+    best = None
+    for kc in range(8, kp + 1, 8):
+        if kp % kc:
+            continue
+        nsb = nb * (kp // kc)
+        for fold in range(1, nsb + 1):
+            if nsb % fold:
+                continue
+            g = nsb // fold
+            rounds = -(-(g * tiles_out) // cus)
+            # us: ~3.5 per 32-column stage (3 f16 MFMA segments of a 256 x 256 tile at ~35 % of the peak), ~10 per
+            # tile (ramp, epilogue), the partial outputs written and summed at ~4 TB/s
+            cost = rounds * (fold * (-(-kc // 32)) * 3.5 + 10.0) + g * tiles_out * 65536 * 8 / 4e6
+            if best is None or cost < best[0]:
+                best = (cost, kc, fold)
+    return best[1], best[2]
+
+
+def gemm_f32s_time_chunks(sp, sq, alpha=1.0):
+    """sum_b sum_t P[b, p, t] Q[b, q, t] -> (mq, mp) fp32 for two (b, rows, K) Splits in the padded-row layout (rows of
+    kp % 8 == 0 elements, zero padding: split_rows8 or a gLN planes output) with the same kp: the time axis cut into
+    chunks that run as extra batches (avse_gemm_f32s nsub), folded into partial outputs, then summed — a weight gradient
+    over 16 x 3999 columns has only 2 output tiles, so its reduction is what the workgroups share."""
+    P, Q = sp.hi, sq.hi
+    nb, mp, kn = P.shape
+    mq = Q.shape[1]
+    kp = P.stride(1)
+    if (P.stride(2) != 1 or Q.stride(2) != 1 or Q.stride(1) != kp or kp % 8 or kp < kn or Q.shape[0] != nb
+            or Q.shape[2] != kn or P.stride(0) != mp * kp or Q.stride(0) != mq * kp):
+        raise RuntimeError(f"gemm_f32s_time_chunks: planes {tuple(P.shape)}/{P.stride()} and {tuple(Q.shape)}/"
+                           f"{Q.stride()} are not both in the padded-row layout")
+    kc, fold = _chunk_plan(kp, nb, -(-mp // 256) * -(-mq // 256))
+    nsub = kp // kc
+    out = torch.empty(nb * nsub // fold, mq, mp, device=P.device, dtype=torch.float32)
+    a = _lib.GemmF32sArgs()
+    a.batch, a.mp, a.mq, a.k, a.fold = nb * nsub, mp, mq, kc, fold
+    a.p_hi, a.p_lo, a.p_bs, a.p_sx, a.p_sk, a.p_extent, a.p_max = P.data_ptr(), sp.lo.data_ptr(), mp * kp, kp, 1, \
+        _plane_extent(sp), sp.mb.data_ptr()
+    a.q_hi, a.q_lo, a.q_bs, a.q_sx, a.q_sk, a.q_extent, a.q_max = Q.data_ptr(), sq.lo.data_ptr(), mq * kp, kp, 1, \
+        _plane_extent(sq), sq.mb.data_ptr()
+    a.c, a.c_bs, a.c_sq = out.data_ptr(), out.stride(0), out.stride(1)
+    a.alpha = float(alpha)
+    a.nsub, a.p_bs2, a.q_bs2 = nsub, kc, kc
+    tap = _tap_begin("avse_gemm_f32s", out.device)
+    check(_lib.lib().avse_gemm_f32s(a, stream_ptr(out.device)), "avse_gemm_f32s")
+    _tap_end(tap)
+    return out.sum(0)

@@ -677,8 +677,8 @@ class _DWConvGLNFn(torch.autograd.Function):
     """gLN(PReLU(dwconv(x))) as the two fused passes of csrc/gln.hip (avse_dwconv_gln_fwd / _bwd)."""
 
     @staticmethod
-    def forward(ctx, x, w, alpha, gamma, beta, dilation, eps):
-        y, y1, stats = K.dwconv_gln_fwd(x, w, dilation, alpha, gamma.reshape(-1), beta.reshape(-1), eps)
+    def forward(ctx, x, w, alpha, gamma, beta, dilation, eps, planes=False):
+        y, y1, stats = K.dwconv_gln_fwd(x, w, dilation, alpha, gamma.reshape(-1), beta.reshape(-1), eps, planes)
         ctx.save_for_backward(x, w, y1, alpha, gamma, stats)
         ctx.dilation = dilation
         return y
@@ -687,14 +687,15 @@ class _DWConvGLNFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, y1, alpha, gamma, stats = ctx.saved_tensors
         dx, dw, da, dg, db = K.dwconv_gln_bwd(x, w, ctx.dilation, y1, alpha, gamma.reshape(-1), stats, dy)
-        return dx, dw, da.view_as(alpha), dg.view_as(gamma), db.view_as(gamma), None, None
+        return dx, dw, da.view_as(alpha), dg.view_as(gamma), db.view_as(gamma), None, None, None
 
 
-def dwconv_prelu_gln(x, w, alpha, gamma, beta, dilation, eps=1e-8):
-    """GlobalLayerNorm(PReLU(depthwise dilated 'same' conv1d(x))) for (B, C, K) fp32 GPU tensors (fused passes)."""
+def dwconv_prelu_gln(x, w, alpha, gamma, beta, dilation, eps=1e-8, planes=False):
+    """GlobalLayerNorm(PReLU(depthwise dilated 'same' conv1d(x))) for (B, C, K) fp32 GPU tensors (fused passes).
+    planes: the output is only the split-fp16 planes of the 1x1 Conv1d GEMM that consumes it (kernels.PLANES_ATTR)."""
     if not x.is_cuda:
         raise RuntimeError("dwconv_prelu_gln runs on the GPU kernels only")
-    return _DWConvGLNFn.apply(x, w, alpha, gamma, beta, dilation, eps)
+    return _DWConvGLNFn.apply(x, w, alpha, gamma, beta, dilation, eps, planes)
 
 
 class _DWConvFn(torch.autograd.Function):

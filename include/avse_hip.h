@@ -335,6 +335,14 @@ int64_t avse_dwconv_gln_workspace_bytes(int64_t B, int64_t C);
 int avse_dwconv_gln_fwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
                         const float* alpha, const float* gamma, const float* beta, float eps, float* y1, float* y,
                         float* stats, float* workspace, avse_stream_t stream);
+/* the same with y written as the split-fp16 planes of the 1x1 Conv1d that consumes it (DepthwiseSeparableConv's
+ * pointwise conv, model.py:284-292, on avse_gemm_f32s): y_hi / y_lo rows of kp elements (kp >= K, kp % 8 == 0, 16-B
+ * aligned planes) holding fp16(y 2^e) and fp16(y 2^e - hi), e from *y_maxbits = an upper bound of max |y| (set by the
+ * call from the rows' PReLU extremes before the apply pass; bits of a float) — no fp32 y, no absmax or split pass. */
+int avse_dwconv_gln_fwd_q(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
+                          const float* alpha, const float* gamma, const float* beta, float eps, float* y1, void* y_hi,
+                          void* y_lo, int64_t kp, uint32_t* y_maxbits, float* stats, float* workspace,
+                          avse_stream_t stream);
 int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil, const float* x, const float* w,
                         const float* y1, const float* alpha, const float* gamma, const float* stats, const float* dy,
                         float* dx, float* dw, float* dalpha, float* dgamma, float* dbeta, float* workspace,
@@ -406,6 +414,9 @@ typedef struct {
     const void* q_hi; const void* q_lo;  int64_t q_bs, q_sx, q_sk, q_extent;  const uint32_t* q_max;
     float* c;       int64_t c_bs, c_sq;
     float alpha;
+    /* nsub > 1: batch b of P / Q sits at (b / nsub) p_bs + (b % nsub) p_bs2 (a reduction split into nsub chunks of k
+     * per batch: the avse4 1x1-conv weight gradient over time chunks, folded and summed as batches); 0 or 1: b p_bs */
+    int64_t nsub, p_bs2, q_bs2;
 } avse_gemm_f32s_args;
 int avse_gemm_f32s(const avse_gemm_f32s_args* a, avse_stream_t stream);
 /* x (b, r, c) fp32 with c contiguous (rows x_rs, batches x_bs apart) -> hi / lo fp16 planes at the same element
@@ -420,6 +431,12 @@ int avse_add_max(int64_t rows, int64_t lp, int64_t l, const float* a, const floa
 /* the same with *maxbits already max |x| (e.g. avse_add_rmsnorm_fwd's y_max): the split pass only */
 int avse_split16_planes_known(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
                               void* lo, const uint32_t* maxbits, avse_stream_t stream);
+/* the same into planes with their own strides (rows h_rs, batches h_bs apart: e.g. rows padded to a multiple of 8
+ * elements, so that an (b, c, K) activation with K % 8 != 0 can be a GEMM operand read along K or along c — the avse4
+ * 1x1 Conv1d, baseline/avse4/model.py:255-293); known != 0: *maxbits is already max |x| (no absmax pass).  avse_gemm_f32s
+ * with fold == 1 takes an output row stride c_sq that is not a multiple of 4 (those rows are stored per element). */
+int avse_split16_planes_to(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
+                           void* lo, int64_t h_bs, int64_t h_rs, uint32_t* maxbits, int32_t known, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- dilated Conv2d fwd / input gradient ----
  * Replaces the forward and the data gradient of nn.Conv2d(64, 64, 5, padding=2d, dilation=d), d = 2, 4, 8, 16

@@ -46,8 +46,8 @@ def capture_masks(model):
         masks[pnames[id(alpha)]] = (x > 0).detach().cpu()
         return orig[1](x, alpha, gamma, beta, eps)
 
-    def dpg_spy(x, w, alpha, gamma, beta, dilation, eps=1e-8):
-        y = orig[2](x, w, alpha, gamma, beta, dilation, eps)
+    def dpg_spy(x, w, alpha, gamma, beta, dilation, eps=1e-8, **kw):
+        y = orig[2](x, w, alpha, gamma, beta, dilation, eps, **kw)
         masks[pnames[id(alpha)]] = (y.grad_fn.saved_tensors[2] > 0).detach().cpu()     # y1 = dwconv(x)
         return y
 

@@ -1359,3 +1359,20 @@ def test_trunk_conv2d_module_grads_vs_torch(monkeypatch):
     close(y, yr, 2e-5 * sc(yr), 0, "y")
     close(xg.grad, xr.grad, 2e-5 * sc(xr.grad), 0, "dx")
     close(ours.weight.grad, ref.weight.grad, 2e-5 * sc(ref.weight.grad), 0, "dw")
+
+
+def test_conv3d_fwd_avse4_frontend_vs_fp64():
+    """The avse4 lip front-end Conv3d(1, 64, (5, 7, 7), stride (1, 2, 2), padding (2, 3, 3)) forward on the exact-fp32
+    MFMA kernel (conv3d_fwd.hip, 112 x 112 normalised grey frames; baseline/avse4/utils.py:97-118) vs fp64: within 1e-5
+    of sum |w x| per output, partial last tile of each plane included (56 x 56 = 3136 = 8 x 384 + 64 pixels)."""
+    import torch.nn.functional as F
+    k = K()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = (torch.rand(2, 1, 7, 112, 112, device="cuda", generator=g) - 0.4161) / 0.1688
+    w = 0.05 * torch.randn(64, 1, 5, 7, 7, device="cuda", generator=g)
+    assert k.conv3d_fwd_supported(x, w, (1, 2, 2), (2, 3, 3))
+    y = k.conv3d_fwd(x, w)
+    ref = F.conv3d(x.double(), w.double(), None, (1, 2, 2), (2, 3, 3))
+    mag = F.conv3d(x.double().abs(), w.double().abs(), None, (1, 2, 2), (2, 3, 3))
+    assert y.shape == ref.shape
+    assert float(((y.double() - ref).abs() / (mag + 1e-30)).max()) <= 1e-5

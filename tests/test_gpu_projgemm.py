@@ -233,3 +233,89 @@ def test_add_max_padded_rows(b, c, l):
     assert int(mb.item()) == int((a + bb).abs().max().view(torch.int32).item())
     s1, s2 = K.split_planes(y), K.split_planes(y.clone())
     assert torch.equal(s1.hi, s2.hi) and torch.equal(s1.lo, s2.lo) and torch.equal(s1.mb, s2.mb)
+
+
+@pytest.mark.parametrize("b,c,k", [(2, 24, 3999), (3, 16, 17), (1, 8, 5)])
+def test_split_rows8_planes(b, c, k):
+    """avse_split16_planes_to: the padded-row planes of a (b, c, k) tensor (rows k not 16-B aligned) decode to x within
+    2^-22 of max |x|, equal split_planes' planes of the same tensor element for element, and share its max."""
+    from avse_challenge_amd import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(b * 1000 + k)
+    x = torch.randn(b, c, k, device=DEV, generator=g) * torch.exp(2.0 * torch.randn(b, c, k, device=DEV, generator=g))
+    s = K.split_rows8(x)
+    assert s.hi.shape == x.shape and s.hi.stride(1) % 8 == 0 and s.hi.stride(2) == 1
+    ref = K.split_planes(x)
+    assert torch.equal(s.mb, ref.mb)
+    assert torch.equal(s.hi, ref.hi) and torch.equal(s.lo, ref.lo)
+    bits = int(s.mb.item())
+    e = max(-100, min(100, 14 - (((bits >> 23) & 0xFF) - 127)))
+    dec = (s.hi.double() + s.lo.double()) * 2.0 ** -e
+    assert float((dec - x.double()).abs().max()) <= 2.0 ** -22 * float(x.abs().max())
+    cp = s.hi.stride(1)
+    if cp != k:                               # the padding columns are written as 0 (the time-chunked weight gradient)
+        for pl in (s.hi, s.lo):
+            pad = torch.as_strided(pl, (b, c, cp - k), pl.stride(), pl.storage_offset() + k)
+            assert bool((pad == 0).all())
+
+
+@pytest.mark.parametrize("k", [3999, 125, 64])
+@pytest.mark.parametrize("chan_contig", [False, True])
+def test_avse4_pointwise_conv_split_vs_fp64(k, chan_contig):
+    """The avse4 1x1 Conv1d (baseline/avse4/model.py:255-293) on avse_gemm_f32s: forward, input gradient and weight
+    gradient vs fp64 within 1e-5 of sum |x w| (the fp32 class), K = 3999 (rows not 16-B aligned: padded planes, per-element
+    output rows), the visual K = 125, and a channel-contiguous input (the ChannelWiseLayerNorm output's layout)."""
+    from avse_challenge_amd import avse4
+    g = torch.Generator(device=DEV).manual_seed(k + 7 * chan_contig)
+    b, cin, cout = 3, 256, 512
+    if chan_contig:
+        x = torch.randn(b, k, cin, device=DEV, generator=g).transpose(1, 2)
+    else:
+        x = torch.randn(b, cin, k, device=DEV, generator=g)
+    x.requires_grad_(True)
+    w = (0.05 * torch.randn(cout, cin, device=DEV, generator=g)).requires_grad_(True)
+    assert avse4._pw_split_ok(w, x)
+    y = avse4._PointwiseFn.apply(w, x)
+    dy = torch.randn(b, cout, k, device=DEV, generator=g)
+    y.backward(dy)
+    xd, wd, dyd = x.detach().double(), w.detach().double(), dy.double()
+    ref = torch.matmul(wd, xd)
+    mag = torch.matmul(wd.abs(), xd.abs())
+    assert float(((y.double() - ref).abs() / mag).max()) <= 1e-5
+    dx_ref = torch.matmul(wd.t(), dyd)
+    dx_mag = torch.matmul(wd.t().abs(), dyd.abs())
+    assert float(((x.grad.double() - dx_ref).abs() / dx_mag).max()) <= 1e-5
+    dw_ref = torch.matmul(dyd, xd.transpose(1, 2)).sum(0)
+    dw_mag = torch.matmul(dyd.abs(), xd.abs().transpose(1, 2)).sum(0)
+    assert float(((w.grad.double() - dw_ref).abs() / dw_mag).max()) <= 1e-5
+
+
+@pytest.mark.parametrize("k,dil", [(3999, 128), (37, 1)])
+def test_dwconv_gln_planes_output(k, dil):
+    """avse_dwconv_gln_fwd_q: the gLN output written only as the planes of its consumer GEMM decodes to the fp32 path's y
+    within 2^-21 of max |y|; the bound it scaled by is >= max |y| and within 0.1 % of it; y1 and the statistics equal
+    the fp32 path's bit for bit."""
+    from avse_challenge_amd import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(k + dil)
+    b, c = 2, 64
+    x = torch.randn(b, c, k, device=DEV, generator=g)
+    w = torch.randn(c, 1, 3, device=DEV, generator=g)
+    alpha = torch.full((1,), 0.25, device=DEV)
+    gamma = 1.0 + 0.5 * torch.randn(c, device=DEV, generator=g)
+    beta = 0.1 * torch.randn(c, device=DEV, generator=g)
+    y, y1, st = K.dwconv_gln_fwd(x, w, dil, alpha, gamma, beta)
+    yq, y1q, stq = K.dwconv_gln_fwd(x, w, dil, alpha, gamma, beta, planes=True)
+    assert torch.equal(y1, y1q) and torch.equal(st, stq)
+    sp = K.planes_of(yq)
+    assert sp is not None and sp.hi.shape == y.shape and sp.hi.stride(1) % 8 == 0
+    bound = float(sp.mb.view(torch.float32).item())
+    m = float(y.abs().max())
+    assert m <= bound <= 1.001 * m, (m, bound)
+    bits = int(sp.mb.item())
+    e = max(-100, min(100, 14 - (((bits >> 23) & 0xFF) - 127)))
+    dec = (sp.hi.double() + sp.lo.double()) * 2.0 ** -e
+    assert float((dec - y.double()).abs().max()) <= 2.0 ** -21 * m
+    cp = sp.hi.stride(1)
+    if cp != k:
+        for pl in (sp.hi, sp.lo):
+            pad = torch.as_strided(pl, (b, c, cp - k), pl.stride(), pl.storage_offset() + k)
+            assert bool((pad == 0).all())
