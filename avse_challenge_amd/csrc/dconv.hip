@@ -457,16 +457,29 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float*
 inline int wgrad_ranges(int chunks) { return std::max(1, std::min(chunks, 256 / KS * 1)); }
 
 // ------------------------------------------------------------------------------------------------ operand preparation
-// max |x| over n floats -> atomicMax on the float bits (non-negative floats order like their bits; NaN wins)
-__global__ void absmax_kernel(const float4* x, int64_t n4, uint32_t* out) {
+// max |x| over n floats -> atomicMax on the float bits (non-negative floats order like their bits; NaN wins).  One
+// atomic per 1024-thread workgroup of a 256-workgroup grid: the word's atomics serialise at the memory side (~17 ns
+// each), so one per wave of a 2048 x 256 grid cost ~140 us of a 165 us pass (profiles/r05v3_avse1_timed_window_stats.csv)
+constexpr int AMAX_NT = 1024, AMAX_GRID = 256;
+__global__ __launch_bounds__(AMAX_NT) void absmax_kernel(const float4* x, int64_t n4, uint32_t* out) {
+    __shared__ uint32_t red[AMAX_NT / 64];
     float m = 0.f;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const float4 v = x[i];
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    const int64_t stride = (int64_t)gridDim.x * AMAX_NT;
+    for (int64_t i0 = blockIdx.x * (int64_t)AMAX_NT + threadIdx.x; i0 < n4; i0 += 4 * stride) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = i0 + u * stride < n4 ? x[i0 + u * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
     }
     uint32_t b = __float_as_uint(m);
     for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
-    if ((threadIdx.x & 63) == 0 && b) atomicMax(out, b);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < AMAX_NT / 64; ++k) b = max(b, red[k]);
+        if (b) atomicMax(out, b);
+    }
 }
 
 __device__ inline uint32_t split2(float x0, float x1, float sc, uint32_t& lo) {
@@ -542,7 +555,8 @@ int avse_split16(int64_t n_pix, const float* x, void* xq, uint32_t* maxbits, avs
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
     const int64_t n4 = n_pix * C / 4;
-    hipLaunchKernelGGL(absmax_kernel, dim3(2048), dim3(256), 0, st, reinterpret_cast<const float4*>(x), n4, maxbits);
+    hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(AMAX_GRID, (n4 + AMAX_NT - 1) / AMAX_NT))),
+                       dim3(AMAX_NT), 0, st, reinterpret_cast<const float4*>(x), n4, maxbits);
     AVSE_CHECK_LAUNCH();
     const int64_t nq = n_pix * NQ;
     const int blocks = (int)std::min<int64_t>((nq + 255) / 256, 8192);

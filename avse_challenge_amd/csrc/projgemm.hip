@@ -552,11 +552,14 @@ __device__ inline int64_t planes_out_off(const PlanesArgs& a, int64_t row) {
     return (row / a.r) * a.hbs + (row % a.r) * a.hrs;
 }
 
-// grid-stride over the row blocks (a bounded grid), one atomicMax per workgroup: one per wave over 10^5 row blocks
-// serialised on the single word (6.8 ms for a C3 activation, profiles/r05i_gemm_f32s_probe.jsonl)
+// grid-stride over the row blocks with a bounded grid of 1024-thread workgroups and one atomicMax per workgroup: the
+// max word is shared by every XCD, so its atomics serialise far from the CUs (~17 ns each: one per wave over 10^5 row
+// blocks cost 6.8 ms for a C3 activation, profiles/r05i_gemm_f32s_probe.jsonl; 2048 per call cost ~30 us of a 65 MB
+// pass), while 16 waves per CU keep enough loads in flight
+constexpr int AM_NT = 1024, AM_GRID = 256;
 template <bool VEC>
-__global__ __launch_bounds__(256) void planes_absmax_kernel(PlanesArgs a, int64_t nrb) {
-    __shared__ uint32_t red[4];
+__global__ __launch_bounds__(AM_NT) void planes_absmax_kernel(PlanesArgs a, int64_t nrb) {
+    __shared__ uint32_t red[AM_NT / 64];
     float m = 0.f;
     const int64_t c4 = VEC ? a.c / 4 : 0;
     for (int64_t rb = blockIdx.x; rb < nrb; rb += gridDim.x)
@@ -565,20 +568,20 @@ __global__ __launch_bounds__(256) void planes_absmax_kernel(PlanesArgs a, int64_
         if (row >= a.rows) break;
         const float* xr = a.x + planes_row_off(a, row);
         if constexpr (VEC) {
-            for (int64_t j0 = threadIdx.x; j0 < c4; j0 += 4 * 256) {
+            for (int64_t j0 = threadIdx.x; j0 < c4; j0 += 4 * AM_NT) {
                 float4 v[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    v[u] = j0 + u * 256 < c4 ? reinterpret_cast<const float4*>(xr)[j0 + u * 256] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    v[u] = j0 + u * AM_NT < c4 ? reinterpret_cast<const float4*>(xr)[j0 + u * AM_NT] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
             }
         }
-        for (int64_t i0 = 4 * c4 + threadIdx.x; i0 < a.c; i0 += 4 * 256) {
+        for (int64_t i0 = 4 * c4 + threadIdx.x; i0 < a.c; i0 += 4 * AM_NT) {
             float v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = i0 + u * 256 < a.c ? xr[i0 + u * 256] : 0.f;
+            for (int u = 0; u < 4; ++u) v[u] = i0 + u * AM_NT < a.c ? xr[i0 + u * AM_NT] : 0.f;
 #pragma unroll
             for (int u = 0; u < 4; ++u) m = fmaxf(m, fabsf(v[u]));
         }
@@ -588,7 +591,8 @@ __global__ __launch_bounds__(256) void planes_absmax_kernel(PlanesArgs a, int64_
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
-        v = max(max(red[0], red[1]), max(red[2], red[3]));
+        for (int k = 1; k < AM_NT / 64; ++k) v = max(v, red[k]);
+        v = max(v, red[0]);
         if (v) atomicMax(a.maxbits, v);
     }
 }
@@ -859,7 +863,7 @@ static int split16_planes_impl(int64_t b, int64_t r, int64_t c, const float* x, 
     if (!known) {
         const int64_t n = b * r * c;
         if (xvec) {
-            hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3((unsigned)std::min<int64_t>(blocks, 2048)), dim3(256), 0,
+            hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3((unsigned)std::min<int64_t>(blocks, AM_GRID)), dim3(AM_NT), 0,
                                st, a, blocks);
             AVSE_CHECK_LAUNCH();
         } else if (x_rs == c && (b == 1 || x_bs == r * c) && ((uintptr_t)x % 16 == 0) && n >= 4096) {
@@ -870,18 +874,18 @@ static int split16_planes_impl(int64_t b, int64_t r, int64_t c, const float* x, 
             f.c = f.rs = 4096;
             f.bs = 0;
             f.rpb = 1;
-            hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3((unsigned)std::min<int64_t>(f.rows, 2048)), dim3(256), 0,
+            hipLaunchKernelGGL(planes_absmax_kernel<true>, dim3((unsigned)std::min<int64_t>(f.rows, AM_GRID)), dim3(AM_NT), 0,
                                st, f, f.rows);
             AVSE_CHECK_LAUNCH();
             if (n % 4096) {
                 f.x = x + f.rows * 4096;
                 f.rows = f.r = 1;
                 f.c = f.rs = n % 4096;
-                hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3(1), dim3(256), 0, st, f, (int64_t)1);
+                hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3(1), dim3(AM_NT), 0, st, f, (int64_t)1);
                 AVSE_CHECK_LAUNCH();
             }
         } else {
-            hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3((unsigned)std::min<int64_t>(blocks, 2048)), dim3(256), 0,
+            hipLaunchKernelGGL(planes_absmax_kernel<false>, dim3((unsigned)std::min<int64_t>(blocks, AM_GRID)), dim3(AM_NT), 0,
                                st, a, blocks);
             AVSE_CHECK_LAUNCH();
         }

@@ -21,13 +21,21 @@ __device__ inline float wave_sum(float v) {
     return v;
 }
 
-// the wave's max |out| -> one atomicMax on the float bits (non-negative floats order like their bits): the
-// producer-side max of an operand the split-fp16 projection GEMMs split next (avse_split16_planes_known)
-__device__ inline void wave_max_out(float m, uint32_t* omax) {
+// the workgroup's max |out| -> one atomicMax on the float bits (non-negative floats order like their bits): the
+// producer-side max of an operand the split-fp16 projection GEMMs split next (avse_split16_planes_known).  Per
+// workgroup, not per wave: the word's atomics serialise at the memory side (~17 ns each).  Called by every thread.
+__device__ inline void block_max_out(float m, uint32_t* omax) {
+    __shared__ uint32_t red[WPB];
     uint32_t b = __float_as_uint(m);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
-    if ((threadIdx.x & 63) == 0 && b) atomicMax(omax, b);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int w = 0; w < WPB; ++w) b = max(b, red[w]);
+        if (b) atomicMax(omax, b);
+    }
 }
 
 __global__ __launch_bounds__(THREADS) void fwd_kernel(int rows, int n, const float* __restrict__ h,
@@ -74,7 +82,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(int rows, int n, const flo
         }
         if (lane == 0) rstd_out[row] = rs;
     }
-    if (ymax) wave_max_out(m, ymax);                      // wave-uniform condition
+    if (ymax) block_max_out(m, ymax);                      // wave-uniform condition
 }
 
 // dx = rstd * (dy*w - xhat * mean(dy*w*xhat)) + dres_out ; dw_partial = sum_rows dy * xhat
@@ -127,7 +135,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int rows, int n, const flo
             }
         }
     }
-    if (dxmax) wave_max_out(m, dxmax);                    // wave-uniform condition
+    if (dxmax) block_max_out(m, dxmax);                    // wave-uniform condition
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
         const int c = lane + i * 64;
