@@ -66,8 +66,14 @@ raw = {ph: {c: per_launch(ph, c) for c in ("FETCH_SIZE", "WRITE_SIZE")} for ph i
        if os.path.isdir(os.path.join(root, ph))}
 b, d, l = SHAPES["cconv"]
 known = 4.0 * b * d * l
-cal_r = known / raw["cconv"]["FETCH_SIZE"][0] if raw["cconv"]["FETCH_SIZE"][0] else None
-cal_w = known / raw["cconv"]["WRITE_SIZE"][0] if raw["cconv"]["WRITE_SIZE"][0] else None
+cal_src = "this run's cconv phase"
+if "cconv" in raw:
+    cal_r = known / raw["cconv"]["FETCH_SIZE"][0] if raw["cconv"]["FETCH_SIZE"][0] else None
+    cal_w = known / raw["cconv"]["WRITE_SIZE"][0] if raw["cconv"]["WRITE_SIZE"][0] else None
+else:       # a run of some phases only: the dword corrections of an earlier run's calibration (CAL_FROM=traffic.json)
+    cal_src = os.environ["CAL_FROM"]
+    prev = json.load(open(cal_src))["calibration"]
+    cal_r, cal_w = prev["dword_read_correction"], prev["dword_write_correction"]
 for ph in raw:
     fr, kern = raw[ph]["FETCH_SIZE"]
     wr, _ = raw[ph]["WRITE_SIZE"]
@@ -79,5 +85,5 @@ for ph in raw:
                "read_correction": round(rf, 4), "write_correction": round(wf, 4)}
 res["calibration"] = {"kernel": "avse_cconv_fwd (B=64, D=1024, L=3999): reads x once, writes out once",
                       "known_read_bytes": known, "known_write_bytes": known,
-                      "dword_read_correction": cal_r, "dword_write_correction": cal_w}
+                      "dword_read_correction": cal_r, "dword_write_correction": cal_w, "source": cal_src}
 print(json.dumps(res, indent=1))
