@@ -142,6 +142,7 @@ SIGNATURES = {
     "avse_prelu_gln_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_prelu_gln_fwd": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
     "avse_prelu_gln_bwd": (c_i32, [c_i64, c_i64, c_i64] + [c_vp] * 11),
+    "avse_prelu_gln_bwd_q": (c_i32, [c_i64, c_i64, c_i64] + [c_vp] * 7 + [c_i64] + [c_vp] * 6),
     "avse_dwconv_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_dwconv_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_dwconv_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_i64] + [c_vp] * 7),

@@ -65,8 +65,11 @@ class _PointwiseFn(torch.autograd.Function):
     keeps.  Otherwise batched hipBLASLt GEMMs (torch.bmm)."""
 
     @staticmethod
-    def forward(ctx, w, x):
+    def forward(ctx, w, x, dy_planes=False):
         ctx.split = _pw_split_ok(w, x)
+        ctx.dy_planes = dy_planes
+        if dy_planes and not ctx.split:
+            raise RuntimeError("_PointwiseFn: gradient planes requested without the split-fp16 GEMM path")
         if not ctx.split:
             ctx.save_for_backward(w, x)
             return torch.bmm(w.expand(x.shape[0], *w.shape), x)
@@ -86,8 +89,11 @@ class _PointwiseFn(torch.autograd.Function):
                 dw = torch.bmm(dy, x.transpose(1, 2)).sum(0)
             if ctx.needs_input_grad[1]:
                 dx = torch.bmm(w.t().expand(dy.shape[0], w.shape[1], w.shape[0]), dy)
-            return dw, dx
+            return dw, dx, None
         w, xh, xl, xm, wh, wl, wm = ctx.saved_tensors
+        if ctx.dy_planes and K.planes_of(dy) is None:
+            raise RuntimeError("_PointwiseFn: the output gradient arrived without its split planes (its consumer must "
+                               "be the only one and write them: prelu_gln(planes_bwd=True))")
         dys = _split_act(dy)
         if ctx.needs_input_grad[0]:
             xs = K.Split(xh, xl, xm)
@@ -99,12 +105,13 @@ class _PointwiseFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dx = torch.empty(dy.shape[0], w.shape[1], dy.shape[2], device=dy.device, dtype=torch.float32)
             K.gemm_f32s_split(dys.t(), K.Split(wh, wl, wm).t(), dx)
-        return dw, dx
+        return dw, dx, None
 
 
-def _pw(conv, x):
-    """1x1 Conv1d without bias: (Cout, Cin) @ (B, Cin, K)."""
-    return _PointwiseFn.apply(conv.weight[:, :, 0], x)
+def _pw(conv, x, dy_planes=False):
+    """1x1 Conv1d without bias: (Cout, Cin) @ (B, Cin, K).  dy_planes: the output's consumer hands back its gradient as
+    split planes (prelu_gln(planes_bwd=True)); the backward raises if they are missing."""
+    return _PointwiseFn.apply(conv.weight[:, :, 0], x, dy_planes)
 
 
 _INTERP = {}
@@ -166,7 +173,9 @@ class TemporalBlock(nn.Module):
 
     def forward(self, x):
         c1, pr, nm, ds = self.net
-        y = prelu_gln(_pw(c1, x), pr.weight, nm.gamma, nm.beta)
+        # with the 1x1 conv on the split-fp16 GEMM, the gLN backward writes that GEMM's dy planes (its only consumer)
+        planes = _pw_split_ok(c1.weight[:, :, 0], x)
+        y = prelu_gln(_pw(c1, x, dy_planes=planes), pr.weight, nm.gamma, nm.beta, planes_bwd=planes)
         return ds(y) + x
 
 

@@ -148,6 +148,31 @@ struct QOut {
     int kp;
 };
 
+// the row's quadruple t .. t + 3 (t < K) into the planes, elements past K as 0
+__device__ inline void q_store_quad(const QOut& q, int row, int t, int K, const float (&o4)[4], float sc) {
+    uint32_t h[2], l[2];
+#pragma unroll
+    for (int e2 = 0; e2 < 2; ++e2) {
+        const float s0 = t + 2 * e2 < K ? o4[2 * e2] * sc : 0.f;
+        const float s1 = t + 2 * e2 + 1 < K ? o4[2 * e2 + 1] * sc : 0.f;
+        const _Float16 h0 = (_Float16)s0, h1 = (_Float16)s1;
+        const _Float16 l0 = (_Float16)(s0 - (float)h0), l1 = (_Float16)(s1 - (float)h1);
+        h[e2] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+        l[e2] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+    }
+    const int64_t off = (int64_t)row * q.kp + t;
+    *reinterpret_cast<uint2*>(q.hi + off) = uint2{h[0], h[1]};
+    *reinterpret_cast<uint2*>(q.lo + off) = uint2{l[0], l[1]};
+}
+// the row's padding columns past its last quadruple: 0
+__device__ inline void q_zero_pad(const QOut& q, int row, int K) {
+    for (int t = (K + 3) / 4 * 4 + 4 * (int)threadIdx.x; t < q.kp; t += 4 * THREADS) {
+        const int64_t off = (int64_t)row * q.kp + t;
+        *reinterpret_cast<uint2*>(q.hi + off) = uint2{0u, 0u};
+        *reinterpret_cast<uint2*>(q.lo + off) = uint2{0u, 0u};
+    }
+}
+
 // apply with the finalize folded in: every row block re-derives its sample's statistics from the row partials (the
 // same sums in the same order in every block: bitwise equal), the channel-0 block stores them for the backward.
 // shift_src: the tensor whose (b, 0, 0) element defines the shift (y1 here)
@@ -181,33 +206,13 @@ __global__ __launch_bounds__(THREADS) void apply_fused_kernel(int row0, int C, i
 #pragma unroll
             for (int e = 0; e < V4; ++e) o4[e] = g * prelu(f4at(xv[jj], e), a) + o;
             if constexpr (QO) {
-                if (t < K) {
-                    uint32_t h[2], l[2];
-#pragma unroll
-                    for (int e2 = 0; e2 < 2; ++e2) {
-                        const float s0 = t + 2 * e2 < K ? o4[2 * e2] * sc : 0.f;
-                        const float s1 = t + 2 * e2 + 1 < K ? o4[2 * e2 + 1] * sc : 0.f;
-                        const _Float16 h0 = (_Float16)s0, h1 = (_Float16)s1;
-                        const _Float16 l0 = (_Float16)(s0 - (float)h0), l1 = (_Float16)(s1 - (float)h1);
-                        h[e2] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-                        l[e2] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
-                    }
-                    const int64_t off = (int64_t)row * q.kp + t;
-                    *reinterpret_cast<uint2*>(q.hi + off) = uint2{h[0], h[1]};
-                    *reinterpret_cast<uint2*>(q.lo + off) = uint2{l[0], l[1]};
-                }
+                if (t < K) q_store_quad(q, row, t, K, o4, sc);
             } else {
                 st4_row(ry, yr, t, K, o4);
             }
         }
     }
-    if constexpr (QO) {
-        for (int t = (K + 3) / 4 * 4 + 4 * (int)threadIdx.x; t < q.kp; t += 4 * THREADS) {
-            const int64_t off = (int64_t)row * q.kp + t;
-            *reinterpret_cast<uint2*>(q.hi + off) = uint2{0u, 0u};
-            *reinterpret_cast<uint2*>(q.lo + off) = uint2{0u, 0u};
-        }
-    }
+    if constexpr (QO) q_zero_pad(q, row, K);
 }
 
 // An upper bound of max |y| for the split planes, before any apply block writes: per row, y = g p + o is affine in
@@ -242,9 +247,11 @@ __global__ __launch_bounds__(256) void q_bound_kernel(int C, int K, const float*
 
 // backward pass 1: per row S1 = sum dy, S2 = sum dy * xhat.  4 consecutive elements per thread (dwordx4 loads, rows
 // need only dword alignment; the row's last partial quadruple is masked per element), 2 quadruples in flight
+template <bool MM = false>
 __global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int row0, int C, int K, const float* __restrict__ x,
                                                              const float* __restrict__ alpha, const float2* __restrict__ stats,
-                                                             const float* __restrict__ dy, float2* __restrict__ ws) {
+                                                             const float* __restrict__ dy, float2* __restrict__ ws,
+                                                             float2* __restrict__ mm = nullptr) {
     constexpr int V = 4, UB = 2;                  // 1 / 4 in flight: within +-2 % (tools/gln_ub_ab.sh @ 8f1eec2)
     __shared__ float red[4];
     const int row = row0 + (int)blockIdx.x, b = row / C;
@@ -252,6 +259,7 @@ __global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int row0, int C, in
     const float2 st = stats[b];
     const auto rx = make_rsrc(x + (int64_t)row * K, K), rg = make_rsrc(dy + (int64_t)row * K, K);
     float s1 = 0.f, s2 = 0.f;
+    float gmax = 0.f, xhmax = 0.f;                       // MM: the row's max |dy|, max |xhat| (the dx planes' bound)
     for (int t0 = 0; t0 < K; t0 += UB * V * THREADS) {
         float4 gv[UB], xv[UB];
 #pragma unroll
@@ -269,12 +277,52 @@ __global__ __launch_bounds__(THREADS) void bwd_reduce_kernel(int row0, int C, in
                 const float xh = (prelu(f4at(xv[j], e), a) - st.x) * st.y;
                 s1 += g;
                 s2 += g * xh;
+                if constexpr (MM) {
+                    gmax = fmaxf(gmax, fabsf(g));
+                    xhmax = (t + e < K) ? fmaxf(xhmax, fabsf(xh)) : xhmax;
+                }
             }
         }
     }
     s1 = block_sum(s1, red);
     s2 = block_sum(s2, red);
     if (threadIdx.x == 0) ws[row] = make_float2(s1, s2);
+    if constexpr (MM) {
+        gmax = block_sum_max(gmax, red);
+        xhmax = block_sum_max(xhmax, red);
+        if (threadIdx.x == 0) mm[row] = make_float2(gmax, xhmax);
+    }
+}
+
+// An upper bound of max |dx| of the PReLU -> gLN backward before its apply pass writes the planes: per row
+// |dx| <= max(1, |a|) rstd (|gamma_c| max|dy| + |mean_g| + max|xhat| |mean_gxh|) from the reduction's row maxima (mm).
+// One block per sample re-derives (mean_g, mean_gxh) as the apply pass does.
+__global__ __launch_bounds__(256) void q_bwd_bound_kernel(int C, int K, const float* __restrict__ alpha,
+                                                          const float* __restrict__ gamma,
+                                                          const float2* __restrict__ stats,
+                                                          const float2* __restrict__ ws_rows,
+                                                          const float2* __restrict__ mm, uint32_t* __restrict__ maxbits) {
+    __shared__ double dred[8];
+    __shared__ float fred[4];
+    const int b = blockIdx.x;
+    const float a = alpha[0];
+    const float2 st = stats[b];
+    const double2 sg12 = sample_sums(ws_rows, b, C, dred, gamma);
+    const double nn = (double)C * K;
+    const float smx = fabsf((float)(sg12.x / nn)), smy = fabsf((float)(sg12.y / nn));
+    const float sl = fmaxf(1.f, fabsf(a)) * st.y;
+    float m = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        const float2 e = mm[(int64_t)b * C + c];
+        m = fmaxf(m, sl * (fabsf(gamma[c]) * e.x + smx + e.y * smy));
+    }
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) fred[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t v = __float_as_uint(fmaxf(fmaxf(fred[0], fred[1]), fmaxf(fred[2], fred[3])) * 1.001f);
+        if (v) atomicMax(maxbits, v);
+    }
 }
 
 // per sample: (mean_g, mean_gxh) over (C, K) with g = dy * gamma; per channel dgamma, dbeta (sum over b)
@@ -324,12 +372,13 @@ __global__ void bwd_finalize(int B, int C, int K, const float2* __restrict__ ws,
 // backward pass 2: dx = (x > 0 ? 1 : a) * rstd * (dy*gamma - mean_g - xhat*mean_gxh); dalpha row partial.  The
 // sample's (mean_g, mean_gxh) re-derived per row block from the row partials (as dwconv_gln_bwd does), so a sample
 // group needs no finalize launch between its two passes
+template <bool QO = false>
 __global__ __launch_bounds__(THREADS) void bwd_apply_kernel(int row0, int C, int K, const float* __restrict__ x,
                                                             const float* __restrict__ alpha, const float* __restrict__ gamma,
                                                             const float2* __restrict__ stats,
                                                             const float2* __restrict__ ws_rows,
                                                             const float* __restrict__ dy, float* __restrict__ dx,
-                                                            float* __restrict__ ws_alpha) {
+                                                            float* __restrict__ ws_alpha, QOut q = QOut{}) {
     __shared__ float red[4];
     __shared__ double dred[8];
     const int row = row0 + second_pass_row(), b = row / C, c = row % C;
@@ -341,8 +390,10 @@ __global__ __launch_bounds__(THREADS) void bwd_apply_kernel(int row0, int C, int
     const float gm = gamma[c];
     const float* xr = x + (int64_t)row * K;
     const float* gr = dy + (int64_t)row * K;
-    float* dr = dx + (int64_t)row * K;
-    const auto rx = make_rsrc(xr, K), rg = make_rsrc(gr, K), rd = make_rsrc(dr, K);
+    float* dr = QO ? nullptr : dx + (int64_t)row * K;
+    const auto rx = make_rsrc(xr, K), rg = make_rsrc(gr, K), rd = make_rsrc(QO ? gr : dr, K);
+    float sc = 1.f;
+    if constexpr (QO) sc = __builtin_ldexpf(1.f, split_exp_gln(*q.maxbits));
     float da = 0.f;
     for (int t0 = 0; t0 < K; t0 += UB4 * V4 * THREADS) {
         float4 xv[UB4], gv[UB4];
@@ -364,9 +415,14 @@ __global__ __launch_bounds__(THREADS) void bwd_apply_kernel(int row0, int C, int
                 o4[e] = xvv > 0.f ? dp : a * dp;
                 da += (xvv > 0.f || t + e >= K) ? 0.f : dp * xvv;
             }
-            st4_row(rd, dr, t, K, o4);
+            if constexpr (QO) {
+                if (t < K) q_store_quad(q, row, t, K, o4, sc);
+            } else {
+                st4_row(rd, dr, t, K, o4);
+            }
         }
     }
+    if constexpr (QO) q_zero_pad(q, row, K);
     da = block_sum(da, red);
     if (threadIdx.x == 0) ws_alpha[row] = da;
 }
@@ -738,7 +794,8 @@ using namespace avse::gln;
 
 extern "C" {
 
-int64_t avse_prelu_gln_workspace_bytes(int64_t B, int64_t C) { return 8 * B * C + 4 * B * C + 16 * B; }
+// ws rows (float2) | slope partials (float) | sample means (float2) | the split-output bound's row maxima (float2)
+int64_t avse_prelu_gln_workspace_bytes(int64_t B, int64_t C) { return 8 * B * C + 4 * B * C + 16 * B + 8 * B * C; }
 
 int avse_prelu_gln_fwd(int64_t B, int64_t C, int64_t K, const float* x, const float* alpha, const float* gamma,
                        const float* beta, float eps, float* y, float* stats, float* workspace, avse_stream_t stream) {
@@ -775,10 +832,10 @@ int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
     for (int64_t b0 = 0; b0 < B; b0 += S) {
         const int row0 = (int)(b0 * C);
         const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
-        hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha,
+        hipLaunchKernelGGL(bwd_reduce_kernel<false>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha,
                            (const float2*)stats, dy, ws);
         AVSE_CHECK_LAUNCH();
-        hipLaunchKernelGGL(bwd_apply_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
+        hipLaunchKernelGGL(bwd_apply_kernel<false>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, x, alpha, gamma,
                            (const float2*)stats, (const float2*)ws, dy, dx, ws_a);
         AVSE_CHECK_LAUNCH();
     }
@@ -788,6 +845,42 @@ int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
                        smeans, dgamma, dbeta);
     AVSE_CHECK_LAUNCH();
     hipLaunchKernelGGL(alpha_finalize, dim3(1), dim3(256), 0, st, (int)all_rows, ws_a, dalpha);
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+int avse_prelu_gln_bwd_q(int64_t B, int64_t C, int64_t K, const float* x, const float* alpha, const float* gamma,
+                         const float* stats, const float* dy, void* dx_hi, void* dx_lo, int64_t kp, uint32_t* dx_maxbits,
+                         float* dalpha, float* dgamma, float* dbeta, float* workspace, avse_stream_t stream) {
+    if (!x || !alpha || !gamma || !stats || !dy || !dx_hi || !dx_lo || !dx_maxbits || !dalpha || !dgamma || !dbeta ||
+        !workspace)
+        return AVSE_EINVAL;
+    if (B <= 0 || C <= 0 || K <= 0 || B * C > (1LL << 31) - 1) return AVSE_ESHAPE;
+    if (kp < K || kp % 8 || B * C * kp >= (1LL << 40)) return AVSE_ESHAPE;
+    if (((uintptr_t)dx_hi | (uintptr_t)dx_lo) % 16 || ((uintptr_t)workspace % 8)) return AVSE_EALIGN;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned rows = (unsigned)(B * C);
+    float2* ws = (float2*)workspace;
+    float* ws_a = (float*)(ws + B * C);
+    float2* smeans = (float2*)(ws_a + B * C);
+    float2* mm = smeans + B;
+    if ((uintptr_t)smeans % 8) return AVSE_EALIGN;
+    if (hipMemsetAsync(dx_maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
+    hipLaunchKernelGGL(bwd_reduce_kernel<true>, dim3(rows), dim3(THREADS), 0, st, 0, (int)C, (int)K, x, alpha,
+                       (const float2*)stats, dy, ws, mm);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(q_bwd_bound_kernel, dim3((unsigned)B), dim3(256), 0, st, (int)C, (int)K, alpha, gamma,
+                       (const float2*)stats, (const float2*)ws, (const float2*)mm, dx_maxbits);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bwd_apply_kernel<true>, dim3(rows), dim3(THREADS), 0, st, 0, (int)C, (int)K, x, alpha, gamma,
+                       (const float2*)stats, (const float2*)ws, dy, nullptr, ws_a,
+                       QOut{dx_maxbits, (_Float16*)dx_hi, (_Float16*)dx_lo, (int)kp});
+    AVSE_CHECK_LAUNCH();
+    const unsigned cblocks = (unsigned)((C + 255) / 256);
+    hipLaunchKernelGGL(bwd_finalize, dim3((unsigned)B + cblocks), dim3(256), 0, st, (int)B, (int)C, (int)K, ws, gamma,
+                       smeans, dgamma, dbeta);
+    AVSE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(alpha_finalize, dim3(1), dim3(256), 0, st, (int)rows, ws_a, dalpha);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
@@ -882,7 +975,7 @@ int avse_dwconv_gln_bwd(int64_t B, int64_t C, int64_t K, int64_t P, int64_t dil,
     for (int64_t b0 = 0; b0 < B; b0 += S) {
     const int row0 = (int)(b0 * C);
     const unsigned rows = (unsigned)((b0 + S <= B ? S : B - b0) * C);
-    hipLaunchKernelGGL(bwd_reduce_kernel, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha,
+    hipLaunchKernelGGL(bwd_reduce_kernel<false>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, y1, alpha,
                        (const float2*)stats, dy, ws);
     AVSE_CHECK_LAUNCH();
 #define L_(PP) hipLaunchKernelGGL(dwconv_gln_bwd_kernel<PP>, dim3(rows), dim3(THREADS), 0, st, row0, (int)C, (int)K, \

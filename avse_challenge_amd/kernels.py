@@ -994,16 +994,26 @@ def prelu_gln_fwd(x, alpha, gamma, beta, eps=1e-8):
     return y, stats
 
 
-def prelu_gln_bwd(x, alpha, gamma, stats, dy):
+def prelu_gln_bwd(x, alpha, gamma, stats, dy, planes=False):
+    """(dx, dalpha, dgamma, dbeta) of gLN(PReLU(x)).  planes: dx is written only as the split-fp16 planes of the GEMM
+    that produced x (avse_prelu_gln_bwd_q) and returned as their carrier (PLANES_ATTR)."""
     _need_gpu(x, alpha, gamma, stats, dy)
     x, dy = x.float().contiguous(), dy.float().contiguous()
     Bn, C, Kn = x.shape
-    dx = torch.empty_like(x)
     dalpha = torch.empty((1,), device=x.device, dtype=torch.float32)
     dgamma = torch.empty((C,), device=x.device, dtype=torch.float32)
     dbeta = torch.empty((C,), device=x.device, dtype=torch.float32)
     L = _lib.lib()
     ws = torch.empty((L.avse_prelu_gln_workspace_bytes(Bn, C) + 3) // 4, device=x.device, dtype=torch.float32)
+    if planes:
+        dx, sp, cp = _planes_carrier((Bn, C, Kn), x.device)
+        tap = _tap_begin("avse_prelu_gln_bwd_q", x.device)
+        check(L.avse_prelu_gln_bwd_q(Bn, C, Kn, ptr(x), ptr(alpha.float().contiguous()), ptr(gamma.float().contiguous()),
+                                     ptr(stats), ptr(dy), ptr(sp.hi), ptr(sp.lo), cp, ptr(sp.mb), ptr(dalpha),
+                                     ptr(dgamma), ptr(dbeta), ptr(ws), stream_ptr(x.device)), "avse_prelu_gln_bwd_q")
+        _tap_end(tap)
+        return dx, dalpha, dgamma, dbeta
+    dx = torch.empty_like(x)
     tap = _tap_begin("avse_prelu_gln_bwd", x.device)
     check(L.avse_prelu_gln_bwd(Bn, C, Kn, ptr(x), ptr(alpha.float().contiguous()), ptr(gamma.float().contiguous()),
                                ptr(stats), ptr(dy), ptr(dx), ptr(dalpha), ptr(dgamma), ptr(dbeta), ptr(ws),

@@ -654,23 +654,26 @@ class TrunkConv2d(nn.Conv2d):
 
 class _PReluGLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, alpha, gamma, beta, eps):
+    def forward(ctx, x, alpha, gamma, beta, eps, planes_bwd=False):
         y, stats = K.prelu_gln_fwd(x, alpha, gamma.reshape(-1), beta.reshape(-1), eps)
         ctx.save_for_backward(x, alpha, gamma, stats)
+        ctx.planes_bwd = planes_bwd
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, alpha, gamma, stats = ctx.saved_tensors
-        dx, da, dg, db = K.prelu_gln_bwd(x, alpha, gamma.reshape(-1), stats, dy)
-        return dx, da.view_as(alpha), dg.view_as(gamma), db.view_as(gamma), None
+        dx, da, dg, db = K.prelu_gln_bwd(x, alpha, gamma.reshape(-1), stats, dy, planes=ctx.planes_bwd)
+        return dx, da.view_as(alpha), dg.view_as(gamma), db.view_as(gamma), None, None
 
 
-def prelu_gln(x, alpha, gamma, beta, eps=1e-8):
-    """GlobalLayerNorm(PReLU(x)) for (B, C, K) fp32 GPU tensors (one PReLU slope)."""
+def prelu_gln(x, alpha, gamma, beta, eps=1e-8, planes_bwd=False):
+    """GlobalLayerNorm(PReLU(x)) for (B, C, K) fp32 GPU tensors (one PReLU slope).  planes_bwd: the input gradient is
+    written only as the split-fp16 planes of the 1x1 Conv1d GEMM that produced x (kernels.PLANES_ATTR), which must
+    then be x's only consumer (avse4.TemporalBlock)."""
     if not x.is_cuda:
         raise RuntimeError("prelu_gln runs on the GPU kernels only")
-    return _PReluGLNFn.apply(x, alpha, gamma, beta, eps)
+    return _PReluGLNFn.apply(x, alpha, gamma, beta, eps, planes_bwd)
 
 
 class _DWConvGLNFn(torch.autograd.Function):

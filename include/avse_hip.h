@@ -314,6 +314,13 @@ int avse_prelu_gln_fwd(int64_t B, int64_t C, int64_t K, const float* x, const fl
 int avse_prelu_gln_bwd(int64_t B, int64_t C, int64_t K, const float* x, const float* alpha, const float* gamma,
                        const float* stats, const float* dy, float* dx, float* dalpha, float* dgamma, float* dbeta,
                        float* workspace, avse_stream_t stream);
+/* the same with dx written only as the split-fp16 planes of the 1x1 Conv1d GEMM whose output x is (TemporalBlock's
+ * first conv, model.py:259-266): dx_hi / dx_lo rows of kp elements (kp >= K, kp % 8 == 0, pads written as 0, 16-B
+ * aligned planes), scaled by *dx_maxbits = an upper bound of max |dx| from the reduction pass's row maxima
+ * (|dx| <= max(1, |a|) rstd (|gamma_c| max|dy| + |mean_g| + max|xhat| |mean_gxh|); bits of a float). */
+int avse_prelu_gln_bwd_q(int64_t B, int64_t C, int64_t K, const float* x, const float* alpha, const float* gamma,
+                         const float* stats, const float* dy, void* dx_hi, void* dx_lo, int64_t kp, uint32_t* dx_maxbits,
+                         float* dalpha, float* dgamma, float* dbeta, float* workspace, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- depthwise dilated conv1d --
  * nn.Conv1d(C, C, P, padding=(P-1)/2*dil, dilation=dil, groups=C, bias=False) — avse4

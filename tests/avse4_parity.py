@@ -42,9 +42,9 @@ def capture_masks(model):
             masks[names[id(bn)]] = layers.K.positive(y).detach().cpu()    # (split-output tensors: from their planes)
         return y
 
-    def pg_spy(x, alpha, gamma, beta, eps=1e-8):
+    def pg_spy(x, alpha, gamma, beta, eps=1e-8, **kw):
         masks[pnames[id(alpha)]] = (x > 0).detach().cpu()
-        return orig[1](x, alpha, gamma, beta, eps)
+        return orig[1](x, alpha, gamma, beta, eps, **kw)
 
     def dpg_spy(x, w, alpha, gamma, beta, dilation, eps=1e-8, **kw):
         y = orig[2](x, w, alpha, gamma, beta, dilation, eps, **kw)

@@ -319,3 +319,36 @@ def test_dwconv_gln_planes_output(k, dil):
         for pl in (sp.hi, sp.lo):
             pad = torch.as_strided(pl, (b, c, cp - k), pl.stride(), pl.storage_offset() + k)
             assert bool((pad == 0).all())
+
+
+@pytest.mark.parametrize("k", [3999, 37])
+def test_prelu_gln_bwd_planes_output(k):
+    """avse_prelu_gln_bwd_q: the PReLU -> gLN input gradient written only as the planes of the GEMM that produced x decodes
+    to the fp32 path's dx within 2^-21 of max |dx|; its bound is >= max |dx| (and within 16x of it); the parameter
+    gradients equal the fp32 path's bit for bit; the padding columns are 0."""
+    from avse_challenge_amd import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(k)
+    b, c = 2, 64
+    x = torch.randn(b, c, k, device=DEV, generator=g)
+    alpha = torch.full((1,), 0.25, device=DEV)
+    gamma = 1.0 + 0.5 * torch.randn(c, device=DEV, generator=g)
+    beta = 0.1 * torch.randn(c, device=DEV, generator=g)
+    _, st = K.prelu_gln_fwd(x, alpha, gamma, beta)
+    dy = torch.randn(b, c, k, device=DEV, generator=g)
+    dx, da, dg, db = K.prelu_gln_bwd(x, alpha, gamma, st, dy)
+    dq, daq, dgq, dbq = K.prelu_gln_bwd(x, alpha, gamma, st, dy, planes=True)
+    assert torch.equal(da, daq) and torch.equal(dg, dgq) and torch.equal(db, dbq)
+    sp = K.planes_of(dq)
+    assert sp is not None and sp.hi.shape == dx.shape
+    m = float(dx.abs().max())
+    bound = float(sp.mb.view(torch.float32).item())
+    assert m <= bound <= 16 * m, (m, bound)
+    bits = int(sp.mb.item())
+    e = max(-100, min(100, 14 - (((bits >> 23) & 0xFF) - 127)))
+    dec = (sp.hi.double() + sp.lo.double()) * 2.0 ** -e
+    assert float((dec - dx.double()).abs().max()) <= 2.0 ** -21 * m
+    cp = sp.hi.stride(1)
+    if cp != k:
+        for pl in (sp.hi, sp.lo):
+            pad = torch.as_strided(pl, (b, c, cp - k), pl.stride(), pl.storage_offset() + k)
+            assert bool((pad == 0).all())
