@@ -833,7 +833,7 @@ int avse_gemm_f32s(const avse_gemm_f32s_args* g, avse_stream_t stream) {
 
 static int split16_planes_impl(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
                                void* lo, int64_t h_bs, int64_t h_rs, uint32_t* maxbits, bool known,
-                               avse_stream_t stream) {
+                               avse_stream_t stream, bool zero_pad = false) {
     if (!x || !hi || !lo || !maxbits) return AVSE_EINVAL;
     if (b <= 0 || r <= 0 || c <= 0 || x_rs < c || (b > 1 && x_bs < (r - 1) * x_rs + c)) return AVSE_ESHAPE;
     if (h_rs < c || (b > 1 && h_bs < (r - 1) * h_rs + c)) return AVSE_ESHAPE;
@@ -858,8 +858,9 @@ static int split16_planes_impl(int64_t b, int64_t r, int64_t c, const float* x, 
     if (blocks >= (1LL << 31)) return AVSE_ESHAPE;
     const bool xvec = ((uintptr_t)x % 16 == 0) && (x_rs % 4 == 0) && (b == 1 || x_bs % 4 == 0);
     const bool hvec = ((uintptr_t)hi % 8 == 0) && ((uintptr_t)lo % 8 == 0) && (h_rs % 4 == 0) && (b == 1 || h_bs % 4 == 0);
-    // padded output rows (8-B aligned) differing from x's: the quadruple kernel, which writes the pads as 0
-    const bool pad = hvec && (h_rs != x_rs || (b > 1 && h_bs != x_bs));
+    // padded output rows (8-B aligned) differing from x's, or zero_pad with pad columns: the quadruple kernel, which
+    // writes the pads as 0
+    const bool pad = hvec && (h_rs != x_rs || (b > 1 && h_bs != x_bs) || (zero_pad && h_rs > c));
     if (!known) {
         const int64_t n = b * r * c;
         if (xvec) {
@@ -933,7 +934,7 @@ int avse_split16_planes_known(int64_t b, int64_t r, int64_t c, const float* x, i
 
 int avse_split16_planes_to(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
                            void* lo, int64_t h_bs, int64_t h_rs, uint32_t* maxbits, int32_t known, avse_stream_t stream) {
-    return split16_planes_impl(b, r, c, x, x_bs, x_rs, hi, lo, h_bs, h_rs, maxbits, known != 0, stream);
+    return split16_planes_impl(b, r, c, x, x_bs, x_rs, hi, lo, h_bs, h_rs, maxbits, known != 0, stream, true);
 }
 
 }  // extern "C"

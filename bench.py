@@ -935,6 +935,33 @@ def roofline_hip(dev):
                                          "counts the fp32 algorithmic FLOPs"} if split else {}))
         del h, f, bk
         torch.cuda.empty_cache()
+    # avse4 1x1 Conv1d (avse4._PointwiseFn, baseline/avse4/model.py:255-293) at C4: TemporalBlock's first conv
+    # (256 -> 512 channels, B = 16, K = 3999) on avse_gemm_f32s
+    from avse_challenge_amd import avse4 as A4
+    b, cin, cout, kk = 16, 256, 512, 3999
+    x4 = torch.randn(b, cin, kk, device=dev, generator=g)                  # contiguous, as the model's activations
+    g4 = torch.randn(b, cout, kk, device=dev, generator=g)
+    w4 = rnd(cout, cin, scale=0.05)
+    xs4, ws4, gs4 = K.split_rows8(x4), K.split_planes(w4[None]), K.split_rows8(g4)
+    y4 = torch.empty(b, cout, kk, device=dev)
+    flops = 2.0 * b * kk * cin * cout
+    for pname, fn, note in (
+            ("forward (incl. splitting x and W)", lambda: A4._PointwiseFn.apply(w4, x4), "time includes the operand splits"),
+            ("forward GEMM", lambda: K.gemm_f32s_split(xs4.t(), ws4, y4), "planes given"),
+            ("weight gradient over time chunks", lambda: K.gemm_f32s_time_chunks(xs4, gs4),
+             "planes given; time chunks as batches + the partial-output sum")):
+        with torch.no_grad():
+            ms = _event_ms(fn)
+        ach = flops / (ms * 1e-3) / 1e12
+        pk = BF16_PEAK_TFS / 3
+        proj.append({"gemm": f"avse4 1x1 Conv1d {pname} (C4)", "shape": [b, cin, cout, kk], "dtype": "float32",
+                     "path": f"avse_gemm_f32s (csrc/projgemm.hip: split-fp16 planes, 3 f16 MFMAs per product; {note})",
+                     "bound": "mfma", "flops_per_launch": flops, "avg_ms": round(ms, 4), "achieved": round(ach, 2),
+                     "peak": pk, "unit": "TFLOP/s", "frac": round(ach / pk, 4),
+                     "peak_note": "dense f16 2500 TFLOP/s / 3 (three f16 MFMAs per fp32 product); achieved counts the "
+                                  "fp32 algorithmic FLOPs"})
+    del x4, w4, g4, xs4, ws4, gs4, y4
+    torch.cuda.empty_cache()
     return hbm, proj
 
 

@@ -440,7 +440,8 @@ int avse_split16_planes_known(int64_t b, int64_t r, int64_t c, const float* x, i
                               void* lo, const uint32_t* maxbits, avse_stream_t stream);
 /* the same into planes with their own strides (rows h_rs, batches h_bs apart: e.g. rows padded to a multiple of 8
  * elements, so that an (b, c, K) activation with K % 8 != 0 can be a GEMM operand read along K or along c — the avse4
- * 1x1 Conv1d, baseline/avse4/model.py:255-293); known != 0: *maxbits is already max |x| (no absmax pass).  avse_gemm_f32s
+ * 1x1 Conv1d, baseline/avse4/model.py:255-293), the padding columns c .. h_rs - 1 written as 0 (h_rs % 4 == 0, 8-B
+ * aligned planes); known != 0: *maxbits is already max |x| (no absmax pass).  avse_gemm_f32s
  * with fold == 1 takes an output row stride c_sq that is not a multiple of 4 (those rows are stored per element). */
 int avse_split16_planes_to(int64_t b, int64_t r, int64_t c, const float* x, int64_t x_bs, int64_t x_rs, void* hi,
                            void* lo, int64_t h_bs, int64_t h_rs, uint32_t* maxbits, int32_t known, avse_stream_t stream);

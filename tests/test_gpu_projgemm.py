@@ -352,3 +352,20 @@ def test_prelu_gln_bwd_planes_output(k):
         for pl in (sp.hi, sp.lo):
             pad = torch.as_strided(pl, (b, c, cp - k), pl.stride(), pl.storage_offset() + k)
             assert bool((pad == 0).all())
+
+
+def test_split_rows8_zeroes_pads_of_padded_rows():
+    """split_rows8 of a view whose rows are already padded to the planes' row length (K = 3999 in rows of 4000, pad
+    columns holding NaN): the planes' pad columns are still written as 0 (the time-chunked weight gradient sums them)."""
+    from avse_challenge_amd import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(5)
+    base = torch.full((2, 16, 4000), float("nan"), device=DEV)
+    x = base[..., :3999]
+    x.copy_(torch.randn(2, 16, 3999, device=DEV, generator=g))
+    s = K.split_rows8(x)
+    assert s.hi.stride(1) == 4000
+    for pl in (s.hi, s.lo):
+        pad = torch.as_strided(pl, (2, 16, 1), pl.stride(), pl.storage_offset() + 3999)
+        assert bool((pad == 0).all())
+    ref = K.split_planes(x.contiguous())
+    assert torch.equal(s.hi, ref.hi) and torch.equal(s.lo, ref.lo) and torch.equal(s.mb, ref.mb)
