@@ -165,6 +165,19 @@ class DepthwiseSeparableConv(nn.Module):
         return _pw(pw, y)
 
 
+class _ResidualAddFn(torch.autograd.Function):
+    """y = a + b (TemporalBlock's residual, model.py:268) as one pass that also keeps max |y| (kernels.add_max_flat):
+    the next block's first 1x1 conv splits y without an absmax pass."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        return K.add_max_flat(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
 class TemporalBlock(nn.Module):
     def __init__(self, cin, cout, k, stride, padding, dilation):
         super().__init__()
@@ -176,7 +189,10 @@ class TemporalBlock(nn.Module):
         # with the 1x1 conv on the split-fp16 GEMM, the gLN backward writes that GEMM's dy planes (its only consumer)
         planes = _pw_split_ok(c1.weight[:, :, 0], x)
         y = prelu_gln(_pw(c1, x, dy_planes=planes), pr.weight, nm.gamma, nm.beta, planes_bwd=planes)
-        return ds(y) + x
+        out = ds(y)
+        if planes and K.add_max_flat_ok(out, x):
+            return _ResidualAddFn.apply(out, x)
+        return out + x
 
 
 class VisualConv1D(nn.Module):

@@ -689,20 +689,39 @@ __global__ __launch_bounds__(256) void planes_split_pad_kernel(PlanesArgs a) {
 // y = a + b over the padded (rows, lp) storage of two (b, c, l) operands (one vectorised pass; the pad columns hold
 // don't-care values) and max |y| over the logical columns c < l: the C3 out_proj input with its producer-side max
 // (the BiMamba direction sum, bimamba.py:253), so the projection's split skips its absmax pass
+template <bool MASK>
 __global__ __launch_bounds__(256) void add_max_kernel(int n4, int lp4, int l, const float4* __restrict__ a,
                                                       const float4* __restrict__ b, float4* __restrict__ y,
                                                       uint32_t* __restrict__ maxbits) {
     __shared__ uint32_t red[4];
     float m = 0.f;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
-        const float4 u = a[i], v = b[i];
-        const float4 s = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
-        y[i] = s;
-        const int c = 4 * (i % lp4);
-        m = fmaxf(m, c < l ? fabsf(s.x) : 0.f);
-        m = fmaxf(m, c + 1 < l ? fabsf(s.y) : 0.f);
-        m = fmaxf(m, c + 2 < l ? fabsf(s.z) : 0.f);
-        m = fmaxf(m, c + 3 < l ? fabsf(s.w) : 0.f);
+    const int stride = gridDim.x * 256;
+    for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += 4 * stride) {    // 4 float4 pairs in flight
+        float4 u[4], v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + k * stride;
+            if (i < n4) {
+                u[k] = a[i];
+                v[k] = b[i];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + k * stride;
+            if (i >= n4) break;
+            const float4 s = make_float4(u[k].x + v[k].x, u[k].y + v[k].y, u[k].z + v[k].z, u[k].w + v[k].w);
+            y[i] = s;
+            if constexpr (MASK) {
+                const int c = 4 * (i % lp4);
+                m = fmaxf(m, c < l ? fabsf(s.x) : 0.f);
+                m = fmaxf(m, c + 1 < l ? fabsf(s.y) : 0.f);
+                m = fmaxf(m, c + 2 < l ? fabsf(s.z) : 0.f);
+                m = fmaxf(m, c + 3 < l ? fabsf(s.w) : 0.f);
+            } else {
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fmaxf(fabsf(s.z), fabsf(s.w))));
+            }
+        }
     }
     uint32_t v = __float_as_uint(m);
     for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
@@ -914,10 +933,15 @@ int avse_add_max(int64_t rows, int64_t lp, int64_t l, const float* a, const floa
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
     const int n4 = (int)(rows * lp / 4);
-    const unsigned grid = (unsigned)std::min<int64_t>((n4 + 255) / 256, 8 * cu_count_cached());
-    hipLaunchKernelGGL(add_max_kernel, dim3(grid), dim3(256), 0, st, n4, (int)(lp / 4), (int)l,
-                       reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(b),
-                       reinterpret_cast<float4*>(y), maxbits);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 1023) / 1024, 4 * cu_count_cached()));
+    if (lp == l)
+        hipLaunchKernelGGL(add_max_kernel<false>, dim3(grid), dim3(256), 0, st, n4, (int)(lp / 4), (int)l,
+                           reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(b),
+                           reinterpret_cast<float4*>(y), maxbits);
+    else
+        hipLaunchKernelGGL(add_max_kernel<true>, dim3(grid), dim3(256), 0, st, n4, (int)(lp / 4), (int)l,
+                           reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(b),
+                           reinterpret_cast<float4*>(y), maxbits);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

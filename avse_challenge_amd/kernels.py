@@ -1373,6 +1373,24 @@ def add_max(a_full, b_full, l):
     return v
 
 
+def add_max_flat(a, b):
+    """a + b for two contiguous fp32 tensors of one shape (numel % 4 == 0, 16-B aligned) -> the sum carrying max |sum|
+    as its producer-side max (avse_add_max over one row): a residual sum whose consumer splits it skips its absmax pass."""
+    _need_gpu(a, b)
+    n = a.numel()
+    y = torch.empty_like(a)
+    mb = torch.empty(1, device=a.device, dtype=torch.int32)
+    check(_lib.lib().avse_add_max(1, n, n, ptr(a), ptr(b), ptr(y), ptr(mb), stream_ptr(a.device)), "avse_add_max")
+    _set_absmax(y, mb)
+    return y
+
+
+def add_max_flat_ok(a, b):
+    return (a.is_cuda and a.dtype == b.dtype == torch.float32 and a.shape == b.shape and a.is_contiguous()
+            and b.is_contiguous() and a.numel() % 4 == 0 and a.numel() < (1 << 33) and a.data_ptr() % 16 == 0
+            and b.data_ptr() % 16 == 0)
+
+
 def split_planes(t):
     """t (b, r, c) fp32 view with stride(2) == 1 or stride(1) == 1 -> Split(hi, lo, maxbits): fp16 planes of t's shape and
     strides holding fp16(t 2^e) and the remainder (csrc/projgemm.hip avse_split16_planes), and max |t|'s bits."""

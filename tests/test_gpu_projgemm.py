@@ -369,3 +369,18 @@ def test_split_rows8_zeroes_pads_of_padded_rows():
         assert bool((pad == 0).all())
     ref = K.split_planes(x.contiguous())
     assert torch.equal(s.hi, ref.hi) and torch.equal(s.lo, ref.lo) and torch.equal(s.mb, ref.mb)
+
+
+def test_add_max_flat_residual():
+    """kernels.add_max_flat (the avse4 TemporalBlock residual): equals a + b, carries max |a + b| exactly, and a
+    split of it (known max: no absmax pass) equals the split of a copy."""
+    from avse_challenge_amd import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(3)
+    a = torch.randn(3, 256, 3999, device=DEV, generator=g)
+    b = 2 * torch.randn(3, 256, 3999, device=DEV, generator=g)
+    assert K.add_max_flat_ok(a, b)
+    y = K.add_max_flat(a, b)
+    assert torch.equal(y, a + b)
+    assert int(getattr(y, K.ABSMAX_ATTR).item()) == int((a + b).abs().max().view(torch.int32).item())
+    s1, s2 = K.split_rows8(y), K.split_rows8(y.clone())
+    assert torch.equal(s1.hi, s2.hi) and torch.equal(s1.lo, s2.lo) and torch.equal(s1.mb, s2.mb)
