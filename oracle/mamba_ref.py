@@ -49,6 +49,23 @@ class _ScanFn(torch.autograd.Function):
                 cast(g["dD"], D), cast(g["dz"], z), cast(g["ddelta_bias"], delta_bias), None, None)
 
 
+def _time_major(x):
+    """(b, d, n, l) -> contiguous (l, b, d, n)."""
+    return x.permute(3, 0, 1, 2).contiguous()
+
+
+class _one_thread:
+    """The per-step loops work on (b, d, n) slabs of a few hundred KB: intra-op threads cost more than they give
+    (a C3-sized fp64 scan: 0.42 s on one thread, 2.3 s on eight)."""
+
+    def __enter__(self):
+        self.n = torch.get_num_threads()
+        torch.set_num_threads(1)
+
+    def __exit__(self, *exc):
+        torch.set_num_threads(self.n)
+
+
 def selective_scan(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
                    return_last_state=False, acc_dtype=torch.float32):
     """Sequential recurrence (selective_scan_ref semantics, see _selective_scan_loop); differentiable through the
@@ -77,21 +94,27 @@ def _selective_scan_loop(u, delta, A, B, C, D=None, z=None, delta_bias=None, del
     n = A.shape[1]
     A = A.to(acc_dtype)
 
-    def expand(M):
+    def expand_t(M):      # time-major (l, b, d|1, n)
         M = M.to(acc_dtype)
         if M.dim() == 3:  # (b, n, l): shared across d
-            return M[:, None, :, :]
+            return M.permute(2, 0, 1)[:, :, None, :].contiguous()
         g = M.shape[1]    # (b, g, n, l): group g serves d/g channels
-        return M.repeat_interleave(d // g, dim=1)
+        if g == 1:
+            return M[:, 0].permute(2, 0, 1)[:, :, None, :].contiguous()
+        return _time_major(M.repeat_interleave(d // g, dim=1))
 
-    Bx, Cx = expand(B), expand(C)                      # (b, d|1, n, l)
-    dA = torch.exp(dt[:, :, None, :] * A[None, :, :, None])     # (b, d, n, l)
-    dBu = (dt * u)[:, :, None, :] * Bx                            # (b, d, n, l)
+    # the per-step operands time-major (l, b, d, n), built in that layout: each step reads contiguous slabs (the same
+    # values and elementwise ops as the (b, d, n, l) form of selective_scan_ref)
+    dt_t = dt.permute(2, 0, 1).contiguous()[..., None]                           # (l, b, d, 1)
+    dA = torch.exp(dt_t * A)                                                      # (l, b, d, n)
+    dBu = (dt * u).permute(2, 0, 1).contiguous()[..., None] * expand_t(B)
+    Ct = expand_t(C)
     h = torch.zeros(b, d, n, dtype=acc_dtype, device=u.device)
     ys = []
-    for t in range(l):
-        h = dA[..., t] * h + dBu[..., t]
-        ys.append((h * Cx[..., t]).sum(-1))
+    with _one_thread():
+        for t in range(l):
+            h = dA[t] * h + dBu[t]
+            ys.append((h * Ct[t]).sum(-1))
     y = torch.stack(ys, dim=-1) if l > 0 else torch.zeros(b, d, 0, dtype=acc_dtype, device=u.device)
     out = y if D is None else y + u * D.to(acc_dtype)[:, None]
     if z is not None:
@@ -118,11 +141,15 @@ def selective_scan_grads(u, delta, A, B, C, D, z, delta_bias, delta_softplus, do
     dt = F.softplus(xpre) if delta_softplus else xpre         # (b, d, l)
     dA = torch.exp(dt[:, :, None, :] * A[None, :, :, None])    # (b, d, n, l)
     dBu = (dt * u)[:, :, None, :] * Bv[:, None]               # (b, d, n, l)
-    H = torch.empty_like(dA)
+    # the recurrences run on time-major copies (l, b, d, n): contiguous per-step slabs, same values and ops
+    dAt, dBt = _time_major(dA), _time_major(dBu)
+    Ht = torch.empty_like(dAt)
     h = torch.zeros(b, d, A.shape[1], dtype=acc_dtype, device=u.device)
-    for t in range(l):
-        h = dA[..., t] * h + dBu[..., t]
-        H[..., t] = h
+    with _one_thread():
+        for t in range(l):
+            h = dAt[t] * h + dBt[t]
+            Ht[t] = h
+    H = Ht.permute(1, 2, 3, 0)                                # (b, d, n, l) view
     y = (H * Cv[:, None]).sum(2)                              # (b, d, l)
     out = y + (u * D[:, None] if D is not None else 0.0)
     if z is not None:
@@ -131,12 +158,15 @@ def selective_scan_grads(u, delta, A, B, C, D, z, delta_bias, delta_softplus, do
         dz = dout * out * sz * (1 + z * (1 - sz))
     else:
         g, dz = dout, None
-    lam = torch.empty_like(dA)
+    lamt = torch.empty_like(dAt)
+    gt, Cvt = _time_major(g[:, :, None, :]), _time_major(Cv[:, None])   # (l, b, d, 1), (l, b, 1, n)
     acc = torch.zeros(b, d, A.shape[1], dtype=acc_dtype, device=u.device)
-    for t in range(l - 1, -1, -1):                            # lambda_t = g_t C_t + dA_{t+1} lambda_{t+1}
-        acc = g[:, :, None, t] * Cv[:, None, :, t] + acc
-        lam[..., t] = acc
-        acc = acc * dA[..., t]
+    with _one_thread():
+        for t in range(l - 1, -1, -1):                        # lambda_t = g_t C_t + dA_{t+1} lambda_{t+1}
+            acc = gt[t] * Cvt[t] + acc
+            lamt[t] = acc
+            acc = acc * dAt[t]
+    lam = lamt.permute(1, 2, 3, 0)
     Hprev = torch.cat([torch.zeros_like(H[..., :1]), H[..., :-1]], -1)
     lam_dA_h = lam * dA * Hprev                               # (b, d, n, l)
     dC = (g[:, :, None, :] * H).sum(1)                        # (b, n, l)
