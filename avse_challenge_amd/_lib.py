@@ -118,8 +118,6 @@ SIGNATURES = {
     "avse_conv3d_fwd": (c_i32, [c_i64] * 5 + [c_i32] + [c_vp] * 5),
     "avse_dconv_wgrad_workspace_bytes": (c_i64, [c_i64] * 4),
     "avse_dconv_wgrad": (c_i32, [c_i64] * 4 + [c_vp] * 6),
-    "avse_rconv_wgrad_workspace_bytes": (c_i64, [c_i64] * 6),
-    "avse_rconv_wgrad": (c_i32, [c_i64] * 6 + [c_i32] + [c_vp] * 5),
     "avse_prelu_fwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "avse_prelu_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_prelu_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

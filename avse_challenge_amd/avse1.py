@@ -15,8 +15,6 @@ MI355X specifics:
   * the remaining convolutions / BatchNorm / GEMMs are MIOpen / hipBLASLt MFMA kernels (fp32,
     exact f32 MFMA on gfx950 — no TF32 shortcut exists), channels-first like the reference.
 """
-import os
-
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -35,7 +33,7 @@ def _prelu(c):
 class _BasicBlock(nn.Module):            # utils/resnet.py:26-67 (relu_type='prelu')
     def __init__(self, cin, cout, stride=1, downsample=None):
         super().__init__()
-        self.conv1 = TrunkConv2d(cin, cout, stride)      # weight gradient on csrc/rconv_wgrad.hip (NCHW)
+        self.conv1 = TrunkConv2d(cin, cout, stride)      # csrc/sconv.hip on the channels-last trunk
         self.bn1 = nn.BatchNorm2d(cout)
         self.relu1, self.relu2 = _prelu(cout), _prelu(cout)
         self.conv2 = TrunkConv2d(cout, cout, 1)
@@ -226,27 +224,25 @@ class FusionNet(nn.Module):               # model.py:81-96
 
 
 _STREAMS = {}
+# the lip branch on a second HIP stream (default); set_branch_streams(False) runs both branches on the current stream
+BRANCH_STREAMS = True
+
+
+def set_branch_streams(on):
+    """Run the lip branch on a second HIP stream, concurrent with the audio branch (True, the default), or both
+    branches on the current stream; returns the previous setting."""
+    global BRANCH_STREAMS
+    old, BRANCH_STREAMS = BRANCH_STREAMS, bool(on)
+    return old
 
 
 def _branch_stream(device):
-    """Second HIP stream for the lip branch (default; AVSE_AVSE1_STREAMS=0 runs both branches on the current stream)."""
-    if device.type != "cuda" or os.environ.get("AVSE_AVSE1_STREAMS", "1") != "1":
+    """Second HIP stream for the lip branch, one per device (BRANCH_STREAMS)."""
+    if device.type != "cuda" or not BRANCH_STREAMS:
         return None
     if device not in _STREAMS:
-        # AVSE_AVSE1_SIDE_PRIO: the side stream's priority (0 = the default; lower = dispatched first)
-        _STREAMS[device] = torch.cuda.Stream(device, priority=int(os.environ.get("AVSE_AVSE1_SIDE_PRIO", "0")))
+        _STREAMS[device] = torch.cuda.Stream(device)
     return _STREAMS[device]
-
-
-def _audio_stream(device):
-    """AVSE_AVSE1_AUDIO_PRIO=<p> (A/B knob): run the audio branch on its own stream of priority p, else None."""
-    v = os.environ.get("AVSE_AVSE1_AUDIO_PRIO")
-    if device.type != "cuda" or v is None:
-        return None
-    key = (device, "audio")
-    if key not in _STREAMS:
-        _STREAMS[key] = torch.cuda.Stream(device, priority=int(v))
-    return _STREAMS[key]
 
 
 class _JoinFromSide(torch.autograd.Function):
@@ -302,23 +298,11 @@ class AVNet(nn.Module):
             with torch.cuda.stream(side):
                 vis = self.net_visualfeat(lips)          # (B, 75, 512); lips.float() of model.py:122 in the conv
             lips.record_stream(side)
-        ast = _audio_stream(spec.device) if side is not None else None
-        if ast is not None:
-            main = torch.cuda.current_stream(spec.device)
-            ast.wait_stream(main)
-            with torch.cuda.stream(ast):
-                audio = self.net_audiofeat(spec)
-            spec.record_stream(ast)
-            main.wait_stream(ast)
-            audio.record_stream(main)
-            audio = _JoinFromSide.apply(audio, ast)
-        else:
-            audio = self.net_audiofeat(spec)
+        audio = self.net_audiofeat(spec)
         if side is not None:
             main.wait_stream(side)
             vis.record_stream(main)
-            if os.environ.get("AVSE_AVSE1_JOIN_HOLD", "1") == "1":
-                vis = _JoinFromSide.apply(vis, side)
+            vis = _JoinFromSide.apply(vis, side)
         if self.a_only:
             comb = audio
         else:

@@ -13,7 +13,6 @@ MFMA implicit GEMM; every 1x1 Conv1d (forward, input and weight gradient) on the
 (csrc/projgemm.hip avse_gemm_f32s, fp32-accurate); the encoder / decoder basis are hipBLASLt GEMMs.
 """
 import copy
-import os
 
 import numpy as np
 import torch
@@ -28,12 +27,8 @@ from .layers import (LipConv3d, PointwiseConv2d, TrunkConv2d, _PReLUFn, bn_act, 
 NORM_MEAN, NORM_STD = 0.4161, 0.1688
 
 
-# "0": the 1x1 convolutions on hipBLASLt fp32 batched GEMMs (torch.bmm) instead of avse_gemm_f32s
-_PW_SPLIT = os.environ.get("AVSE_AVSE4_PW_SPLIT", "1") != "0"
-
-
 def _pw_split_ok(w, x):
-    return (_PW_SPLIT and x.is_cuda and x.dtype == w.dtype == torch.float32 and x.dim() == 3
+    return (x.is_cuda and x.dtype == w.dtype == torch.float32 and x.dim() == 3
             and (x.stride(2) == 1 or x.stride(1) == 1) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0
             and w.stride(1) == 1)
 

@@ -4,7 +4,6 @@ Each wrapper validates shapes/dtypes/strides, allocates its outputs and workspac
 (caching allocator, stream-ordered) and enqueues the HIP kernels on torch's current stream.
 """
 import functools
-import os
 
 import torch
 
@@ -54,7 +53,7 @@ def _dtype_code(dt):
 # (b, d, l) outputs of the scan / conv kernels (and the Mamba projections feeding them) get a time stride rounded
 # up to this many bytes: every row starts on a 128-B cache line, so a 64-step row segment touches 2 lines, not 3
 # (L = 3999 fp32 rows were read 1.42x, profiles/r01_traffic.json).  0 = plain contiguous tensors.
-TIME_ALIGN_BYTES = int(os.environ.get("AVSE_TIME_ALIGN_BYTES", "128"))
+TIME_ALIGN_BYTES = 128
 
 
 def bdl_empty(b, d, l, dtype, dev):
@@ -382,8 +381,9 @@ def istft(mag, phase_spec, length):
 # ------------------------------------------------------------------------ lip front-end Conv3d dW
 
 CONV3D_WGRAD_MAX_WO = 64      # output width the MFMA kernel stages per LDS row (conv3d_wgrad.hip MAX_WO)
-# uint8 frames: the f16 MFMA weight gradient with dy split (avse_conv3d_wgrad_u8_split); "0": the exact-fp32 kernel
-C3W_F16 = os.environ.get("AVSE_C3W_F16", "1") == "1"
+# uint8 frames: the f16 MFMA weight gradient with dy split (avse_conv3d_wgrad_u8_split); False (a test's comparison):
+# the exact-fp32 kernel
+C3W_F16 = True
 
 
 def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
@@ -695,37 +695,6 @@ def sconv_wgrad(xs, dys, xshape, cout, stride):
                              stream_ptr(xq.device)), "avse_sconv_wgrad")
     _tap_end(tap)
     return dw
-
-
-# ------------------------------------------------------------------------ ResNet trunk 3x3 Conv2d dW
-
-def rconv_wgrad_supported(x, cout, stride):
-    """True when csrc/rconv_wgrad.hip takes this weight gradient (NCHW fp32 input, channels multiples of 64)."""
-    n, cin, h, w = x.shape
-    return (x.is_cuda and x.dtype == torch.float32 and stride in (1, 2)
-            and _lib.lib().avse_rconv_wgrad_workspace_bytes(n, cin, cout, h, w, stride) > 0)
-
-
-def rconv_wgrad(x, dy, stride):
-    """dW (COUT, CIN, 3, 3) of Conv2d(CIN, COUT, 3, stride, padding=1, bias=False) from the input x (N, CIN, H, W) and
-    the output gradient dy (N, COUT, HO, WO), fp32; channels-last x takes the NHWC kernel (dy made channels-last),
-    anything else is read as contiguous NCHW."""
-    _need_gpu(x, dy)
-    nhwc = x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
-    fmt = torch.channels_last if nhwc else torch.contiguous_format
-    x = x.float().contiguous(memory_format=fmt)
-    dy = dy.float().contiguous(memory_format=fmt)
-    n, cin, h, w = x.shape
-    cout = dy.shape[1]
-    L = _lib.lib()
-    nb = L.avse_rconv_wgrad_workspace_bytes(n, cin, cout, h, w, stride)
-    if nb <= 0:
-        raise RuntimeError(f"rconv_wgrad: unsupported shape x {tuple(x.shape)}, cout {cout}, stride {stride}")
-    out = torch.empty((cout, cin, 3, 3), device=x.device, dtype=torch.float32)
-    ws = torch.empty((nb + 3) // 4, device=x.device, dtype=torch.float32)
-    check(L.avse_rconv_wgrad(n, cin, cout, h, w, stride, int(nhwc), ptr(x), ptr(dy), ptr(out), ptr(ws),
-                             stream_ptr(x.device)), "avse_rconv_wgrad")
-    return out
 
 
 # ------------------------------------------------------------------------ PReLU
@@ -1186,12 +1155,18 @@ class no_grouped_lstm:
         return False
 
 
+# the grouped recurrence (csrc/lstm_group.hip) where it applies; False: lstm.hip everywhere (a test's comparison)
+LSTM_GROUP = True
+# a test hook: pretend the device holds at most this many grouped-LSTM workgroups at once (None: the device's capacity)
+LSTM_GROUP_CAPACITY_LIMIT = None
+
+
 def lstm_group_allowed():
-    return NO_GROUPED_LSTM == 0 and os.environ.get("AVSE_LSTM_GROUP", "1") == "1"
+    return NO_GROUPED_LSTM == 0 and LSTM_GROUP
 
 
 def _lstm_group_ws(L, Bn, H, device, backward):
-    """Workspace of the grouped LSTM kernels, or None when they do not apply: AVSE_LSTM_GROUP=0 or inside
+    """Workspace of the grouped LSTM kernels, or None when they do not apply: LSTM_GROUP False or inside
     no_grouped_lstm(); B * G > 256 or H > 384 (avse_lstm_group_size); or B * G workgroups cannot be co-resident on
     this device (avse_lstm_group_capacity).  Those cases run lstm.hip's one-workgroup-per-sequence kernels."""
     if not lstm_group_allowed():
@@ -1204,8 +1179,8 @@ def _lstm_group_ws(L, Bn, H, device, backward):
         with torch.cuda.device(device):
             _GROUP_CAPACITY[key] = int(L.avse_lstm_group_capacity(H, int(bool(backward))))
     cap = _GROUP_CAPACITY[key]
-    if os.environ.get("AVSE_LSTM_GROUP_CAPACITY"):      # test hook: pretend the device holds fewer workgroups
-        cap = min(cap, int(os.environ["AVSE_LSTM_GROUP_CAPACITY"]))
+    if LSTM_GROUP_CAPACITY_LIMIT is not None:
+        cap = min(cap, int(LSTM_GROUP_CAPACITY_LIMIT))
     if Bn * G > cap:
         return None
     nb = int(L.avse_lstm_group_workspace_bytes(Bn, H))

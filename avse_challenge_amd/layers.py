@@ -11,15 +11,14 @@ HipLSTM      nn.LSTM(..., num_layers=1, batch_first=True[, bidirectional]) whose
              per direction (avse1 FusionNet, avse2 DPRNN)
 DilatedConv2d  nn.Conv2d(64, 64, 5, padding=2d, dilation=d) of the avse1 AudioFeatNet: weight gradient on the
              MFMA implicit-GEMM kernel (channels-last activations)
-TrunkConv2d  nn.Conv2d(cin, cout, 3, stride, padding=1, bias=False) of the lip ResNet trunks: frames of <= 36 output
-             pixels as one im2col GEMM (hipBLASLt), the 64 -> 64 layer's weight gradient on the MFMA kernel (NCHW)
+TrunkConv2d  nn.Conv2d(cin, cout, 3, stride, padding=1, bias=False) of the lip ResNet trunks: channels-last activations
+             on the split-fp16 MFMA kernels (csrc/sconv.hip)
 PointwiseConv2d  the 1x1 shortcut convs as one GEMM
 LipConv3d    nn.Conv3d(Cin, 64, k, stride (1,2,2), pad, bias=False) of the lip front-ends:
              forward on MIOpen, weight gradient on the MFMA implicit-GEMM kernel (the lips are
              data: no input gradient is needed on the reference path; if one is requested it is
              computed with the library transposed conv).
 """
-import os
 
 import torch
 import torch.nn as nn
@@ -75,10 +74,6 @@ class _BNActFn(torch.autograd.Function):
                 dalpha if ctx.needs_input_grad[3] else None, dres, None, None, None, None, None, None, None, None)
 
 
-# split-output BatchNorm passes (bn_act q_fwd / q_bwd); "0": fp32 outputs + the consumer's split pass (A/B)
-_BNACT_Q = os.environ.get("AVSE_BNACT_Q", "1") == "1"
-
-
 def bn_act(x, bn, act=None, res=None, folded_bias=None, q_fwd=False, q_bwd=False):
     """act(bn(x) [+ res]) for an nn.BatchNorm{1,2,3}d `bn` (its parameters, buffers, momentum and eps; running
     statistics and num_batches_tracked updated in train mode as torch does).  act: None, "relu" or a PReLU module.
@@ -101,9 +96,6 @@ def bn_act(x, bn, act=None, res=None, folded_bias=None, q_fwd=False, q_bwd=False
         return y
     if not x.is_cuda:
         raise RuntimeError("bn_act runs on the GPU kernels only")
-    if os.environ.get("AVSE_BNACT", "1") != "1":            # A/B switch: the library BatchNorm + separate act
-        y = bn(x) if res is None else bn(x) + res
-        return y if act is None else (F.relu(y) if act == "relu" else act(y))
     training = bn.training or not bn.track_running_stats
     if bn.training and bn.track_running_stats:
         if bn.momentum is None:
@@ -118,8 +110,7 @@ def bn_act(x, bn, act=None, res=None, folded_bias=None, q_fwd=False, q_bwd=False
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
     return _BNActFn.apply(x.float(), bn.weight, bn.bias, alpha, res, rm, rv, training,
-                          bn.momentum if bn.momentum is not None else 0.0, bn.eps, code, _BNACT_Q and bool(q_fwd),
-                          _BNACT_Q and bool(q_bwd))
+                          bn.momentum if bn.momentum is not None else 0.0, bn.eps, code, bool(q_fwd), bool(q_bwd))
 
 
 class _MaxPoolPlanesFn(torch.autograd.Function):
@@ -155,7 +146,7 @@ def _conv3d_fwd_folded(x, w, padding):
     (x_unf[b*T + t, ci*KT + kt] = x_pad[b, ci, t + kt], plane copies), the weight (Cout, Cin, KT, KH, KW) is then
     (Cout, Cin*KT, KH, KW) as it lies, and the (B*T, Cout, Ho, Wo) result is permuted back to (B, Cout, T, Ho, Wo).
     MIOpen runs this 2-D shape (Winograd f3x2, find-db record) in 7.1 ms against 8.6 ms for its 3-D path at the avse1
-    C2 shape, copies included (tools/conv3d_fold_probe.py @ 8f1eec2; AVSE_CONV3D_FOLD=0 restores F.conv3d)."""
+    C2 shape, copies included (tools/conv3d_fold_probe.py @ 8f1eec2)."""
     B, Cin, T, H, W = x.shape
     Co, _, KT, KH, KW = w.shape
     PT, PH, PW = padding
@@ -173,8 +164,7 @@ class _LipConv3dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, stride, padding):
-        hip = (os.environ.get("AVSE_CONV3D_HIP", "1") == "1" and x.is_cuda
-               and K.conv3d_fwd_supported(x, w, stride, padding))
+        hip = x.is_cuda and K.conv3d_fwd_supported(x, w, stride, padding)
         if not hip and x.dtype != torch.float32:
             x = x.float()
         ctx.save_for_backward(x, w)
@@ -184,7 +174,7 @@ class _LipConv3dFn(torch.autograd.Function):
         # other shapes: the avse1 front-end as a Conv2d over frames (Cin = 3); the Cin = 1 front-ends of avse2 /
         # avse4 fold to a 5-channel Conv2d without a find-db record (a find pass over the avse4 step did not finish
         # in 400 s): they keep conv3d
-        if os.environ.get("AVSE_CONV3D_FOLD", "1") == "1" and tuple(stride) == (1, 2, 2) and x.shape[1] == 3:
+        if tuple(stride) == (1, 2, 2) and x.shape[1] == 3:
             return _conv3d_fwd_folded(x, w, padding)
         return F.conv3d(x, w, None, stride, padding)
 
@@ -221,9 +211,8 @@ def _conv2d_dgrad(x, w, dy, stride, padding, dilation):
                                                [0, 0], 1, [True, False, False])[0]
 
 
-# forward and input gradient of the 64 -> 64 dilated convs on csrc/dconv.hip (fp16x3 split-operand MFMA, fp32-accurate);
-# "0": MIOpen's fp32 convolutions
-_DCONV_SPLIT = os.environ.get("AVSE_DCONV_SPLIT", "1") == "1"
+# forward and input gradient of the 64 -> 64 dilated convs on csrc/dconv.hip (fp16x3 split-operand MFMA, fp32-accurate)
+# where K.dconv_split_ok takes the shape; other shapes: MIOpen's fp32 convolutions + the exact-fp32 weight gradient
 
 
 class _DilatedConvFn(torch.autograd.Function):
@@ -235,7 +224,7 @@ class _DilatedConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, dilation, add_bias):
         ctx.dilation = dilation
-        ctx.split = _DCONV_SPLIT and K.dconv_split_ok(x, dilation)
+        ctx.split = K.dconv_split_ok(x, dilation)
         if K.is_split_q(x) and not ctx.split:
             raise RuntimeError("_DilatedConvFn: a split-output input needs the split path (DilatedConv2d.q_ok)")
         if ctx.split:
@@ -304,8 +293,8 @@ def frames_nhwc(x):
     return x.permute(0, 2, 3, 4, 1).reshape(B * T, H, W, C).permute(0, 3, 1, 2)
 
 
-# AudioFeatNet.conv1 on csrc/conv1.hip (direct HBM-streaming kernels); "0": the im2col GEMM form below
-_CONV1_HIP = os.environ.get("AVSE_CONV1_HIP", "1") == "1"
+# AudioFeatNet.conv1 on csrc/conv1.hip (direct HBM-streaming kernels) for frames of >= 128 bins; narrower ones: the
+# im2col GEMM form below
 
 
 class _Conv1Fn(torch.autograd.Function):
@@ -330,7 +319,7 @@ class _Conv1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, add_bias):
         n, _, h, ww = x.shape
-        ctx.hip = _CONV1_HIP and ww >= 128
+        ctx.hip = ww >= 128
         if ctx.hip:                                 # csrc/conv1.hip: direct kernels, x (not the im2col rows) kept
             ctx.save_for_backward(x, w)
             return K.conv1_fwd(x, w, b if add_bias else None)
@@ -368,6 +357,11 @@ class _Conv1Fn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+# the 64 -> 64 dilated convs on the HIP kernels (DilatedConv2d.hip_ok); False: the library convolution with the bias in
+# it (tests/test_gpu_kernels.py builds its comparison with it)
+HIP_DCONV = True
+
+
 class DilatedConv2d(nn.Conv2d):
     """nn.Conv2d(cin, cout, 5, padding=2*dilation, dilation) — the avse1 AudioFeatNet convs (same parameters and
     state_dict keys).  The 64 -> 64 ones on GPU tensors in channels-last memory (the benchmarked layout) take their
@@ -386,7 +380,7 @@ class DilatedConv2d(nn.Conv2d):
     nhwc_out = False          # set by AudioFeatNet.use_channels_last: conv1 (1 -> 64) writes channels-last output
 
     def conv1_ok(self, x):
-        return (self.nhwc_out and os.environ.get("AVSE_CONV1_GEMM", "1") == "1" and x.is_cuda and self.in_channels == 1
+        return (self.nhwc_out and x.is_cuda and self.in_channels == 1
                 and self.dilation[0] == 1 and self.bias is not None and x.dtype == torch.float32 and x.is_contiguous())
 
     def hip_ok(self, x):
@@ -394,7 +388,7 @@ class DilatedConv2d(nn.Conv2d):
             return True
         # x.numel() < 2^29: the kernel's 32-bit buffer offsets (csrc/dconv_wgrad.hip; B >= ~87 at 3 s clips exceeds
         # it, and those shapes take the library path instead of failing in the backward)
-        return (os.environ.get("AVSE_DCONV_WGRAD", "1") == "1" and x.is_cuda and self.in_channels == 64
+        return (HIP_DCONV and x.is_cuda and self.in_channels == 64
                 and self.out_channels == 64 and self.dilation[0] <= K.DCONV_WGRAD_MAX_DIL
                 and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
                 and x.numel() < (1 << 29))
@@ -402,7 +396,7 @@ class DilatedConv2d(nn.Conv2d):
     def q_ok(self, x, grad=False):
         """True when this conv's forward (or, grad=True, its backward) takes a split-output tensor for an input of x's
         shape and layout (the split-fp16 path of _DilatedConvFn)."""
-        return (not self.conv1_ok(x)) and self.hip_ok(x) and _DCONV_SPLIT and K.dconv_split_ok(x, self.dilation[0])
+        return (not self.conv1_ok(x)) and self.hip_ok(x) and K.dconv_split_ok(x, self.dilation[0])
 
     def forward(self, x, bias_to_bn=False):
         if self.conv1_ok(x):
@@ -413,27 +407,6 @@ class DilatedConv2d(nn.Conv2d):
         if bias_to_bn:
             raise RuntimeError("DilatedConv2d: bias_to_bn needs the HIP path (check hip_ok first)")
         return super().forward(x)
-
-
-class _TrunkConvFn(torch.autograd.Function):
-    """Conv2d(cin, cout, 3, stride, padding=1, bias=False) with the weight gradient on the MFMA implicit-GEMM kernel
-    (csrc/rconv_wgrad.hip); forward and input gradient on MIOpen."""
-
-    @staticmethod
-    def forward(ctx, x, w, stride):
-        ctx.save_for_backward(x, w)
-        ctx.stride = stride
-        return F.conv2d(x, w, None, stride, 1)
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, w = ctx.saved_tensors
-        dx = dw = None
-        if ctx.needs_input_grad[0]:
-            dx = _conv2d_dgrad(x, w, dy, ctx.stride, 1, 1)
-        if ctx.needs_input_grad[1]:
-            dw = K.rconv_wgrad(x, dy, ctx.stride)
-        return dx, dw, None
 
 
 class _GemmConvFn(torch.autograd.Function):
@@ -495,19 +468,12 @@ class _GemmConvFn(torch.autograd.Function):
 
 
 def gemm_conv_ok(x, k, stride):
-    """AVSE_TRUNK_GEMM: "1x1" (default) runs the 1x1 shortcut convs as one GEMM; "all" also the 3x3 convs whose output
-    frames have <= 36 pixels (lip-trunk layers 3-4), which measured slower in the avse1 step (179.6 vs 199 utt/s: the
-    im2col gathers, the col2im adds and hipBLASLt's fp32 tiles for these shapes, profiles/r03_trunk_gemm_op_profile.txt);
-    "0" keeps MIOpen for all.  fp32 GPU inputs; the 3x3 form NCHW only."""
-    mode = os.environ.get("AVSE_TRUNK_GEMM", "1x1")
-    if mode == "0" or not x.is_cuda or x.dtype != torch.float32:
+    """The 1x1 shortcut convs (NCHW or channels-last fp32 GPU activations) run as one GEMM (_GemmConvFn).  The 3x3 form
+    of _GemmConvFn (small frames as one im2col GEMM) measured slower in the avse1 step than the library (179.6 vs 199
+    utt/s, profiles/r03_trunk_gemm_op_profile.txt) and then than csrc/sconv.hip: the product routes no 3x3 conv to it."""
+    if k != 1 or not x.is_cuda or x.dtype != torch.float32:
         return False
-    if k == 1:                                     # NCHW or channels-last
-        return x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last)
-    if not x.is_contiguous():
-        return False
-    ho, wo = (x.shape[2] - 1) // stride + 1, (x.shape[3] - 1) // stride + 1
-    return mode == "all" and ho * wo <= 36
+    return x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last)
 
 
 class _TimeConv1dFn(torch.autograd.Function):
@@ -576,8 +542,7 @@ class PointwiseConv2d(nn.Conv2d):
         return super().forward(x)
 
 
-# 3x3 trunk convs on csrc/sconv.hip (split-fp16 MFMA, fp32-accurate) for channels-last activations; "0": MIOpen
-_SCONV = os.environ.get("AVSE_SCONV", "1") == "1"
+# 3x3 trunk convs on csrc/sconv.hip (split-fp16 MFMA, fp32-accurate) for channels-last activations
 
 
 class _SConvFn(torch.autograd.Function):
@@ -616,14 +581,13 @@ class _SConvFn(torch.autograd.Function):
 class TrunkConv2d(nn.Conv2d):
     """nn.Conv2d(cin, cout, 3, stride, padding=1, bias=False) of the lip-encoder ResNet trunks (same parameters and
     state_dict keys).  Channels-last fp32 GPU activations with channel counts that are multiples of 64 run on
-    csrc/sconv.hip (_SConvFn; AVSE_SCONV=0: MIOpen); NCHW ones can take their weight gradient from csrc/rconv_wgrad.hip
-    (AVSE_RCONV_WGRAD)."""
+    csrc/sconv.hip (_SConvFn); other layouts and shapes (NCHW trunks, avse2's Swish trunk) run the library convolution."""
 
     def __init__(self, cin, cout, stride=1):
         super().__init__(cin, cout, 3, stride=stride, padding=1, bias=False)
 
     def _sconv(self, x):
-        return (_SCONV and x.is_contiguous(memory_format=torch.channels_last) and x.dtype == self.weight.dtype
+        return (x.is_contiguous(memory_format=torch.channels_last) and x.dtype == self.weight.dtype
                 and K.sconv_ok(x, self.out_channels, self.stride[0]))
 
     def q_ok(self, x, grad=False):
@@ -632,24 +596,9 @@ class TrunkConv2d(nn.Conv2d):
         return self._sconv(x) and (not grad or self.stride[0] == 1)
 
     def forward(self, x):
-        s = self.stride[0]
         if self._sconv(x):
-            return _SConvFn.apply(x, self.weight, s)
-        if gemm_conv_ok(x, 3, s):                          # small frames: one GEMM over all pixels (_GemmConvFn)
-            return _GemmConvFn.apply(x, self.weight, s)
-        if ((x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last)) and self._use_hip(x, s)
-                and K.rconv_wgrad_supported(x, self.out_channels, s)):
-            return _TrunkConvFn.apply(x, self.weight, s)
+            return _SConvFn.apply(x, self.weight, self.stride[0])
         return super().forward(x)
-
-    def _use_hip(self, x, s):
-        # AVSE_RCONV_WGRAD: "all", "layer1" (the 64 -> 64 stride-1 convs) or "0" (default).  On the channels-last trunk
-        # the kernel runs 0.50-0.59 of the fp32 peak against MIOpen NHWC's 0.63-0.80 (profiles/r03_rconv_wgrad_nhwc_bench
-        # .jsonl); in the avse1 step: MIOpen 204.1 / 203.3, layer1 202.8, all 198.8 utt/s (profiles/r03_rconv_modes.txt)
-        mode = os.environ.get("AVSE_RCONV_WGRAD", "0")
-        if mode == "all":
-            return True
-        return mode == "layer1" and s == 1 and self.in_channels == 64 and self.out_channels == 64
 
 
 class _PReluGLNFn(torch.autograd.Function):

@@ -16,7 +16,6 @@ are GEMMs: bf16 (autocast) in_proj / out_proj / x_proj and their input gradients
 CPU tensors raise.
 """
 import math
-import os
 
 import torch
 import torch.nn as nn
@@ -32,14 +31,10 @@ _FWD = torch.amp.custom_fwd(device_type="cuda")
 _BWD = torch.amp.custom_bwd(device_type="cuda")
 
 
-# bf16 projections (BASELINE configs[4]) on the HIP MFMA GEMM (csrc/projgemm.hip).  Default ("1"): the sites where it
-# measured faster than hipBLASLt at C5 (profiles/r04g_projgemm_probe_vs_lib.jsonl: in_proj forward 0.26 vs 0.25 of the
-# bf16 peak, in_proj input gradient 0.34 vs 0.32, out_proj input gradient 0.30 vs 0.25); out_proj forward (0.29 vs 0.35)
-# and the weight gradients (0.29-0.32 vs 0.34-0.36) stay on the library.  "all": every bf16 site; "0": none.  fp32
-# GEMMs always run on the library.
-_PROJ_GEMM = os.environ.get("AVSE_PROJ_GEMM", "1")
-_HIP_GEMM = _PROJ_GEMM in ("1", "all")
-_HIP_GEMM_ALL = _PROJ_GEMM == "all"
+# bf16 projections (BASELINE configs[4]) on the HIP MFMA GEMM (csrc/projgemm.hip) at the sites where it measured faster
+# than hipBLASLt at C5 (profiles/r04g_projgemm_probe_vs_lib.jsonl: in_proj forward 0.26 vs 0.25 of the bf16 peak, in_proj
+# input gradient 0.34 vs 0.32, out_proj input gradient 0.30 vs 0.25); out_proj forward (0.29 vs 0.35) and the bf16 weight
+# gradients (0.29-0.32 vs 0.34-0.36) stay on the library.
 
 
 def _autocast_dtype():
@@ -48,20 +43,18 @@ def _autocast_dtype():
 
 def _hip_gemm(P, Q, out, alpha=1.0, fold=1):
     """out[g, q, p] = alpha sum_{b in group g} sum_k P[b, p, k] Q[b, q, k] on the HIP bf16 GEMM; None when it does not
-    take them.  Reductions shorter than 64 (dt_proj's K = dt_rank with AVSE_DTPROJ=0) stay on the library: their
-    single-stage tiles are all epilogue."""
-    if _HIP_GEMM and min(P.shape[1], Q.shape[1]) >= 128 and P.shape[2] >= 64 and K.gemm_bf16_supported(P, Q, out, fold):
+    take them.  Reductions shorter than 64 stay on the library: their single-stage tiles are all epilogue."""
+    if min(P.shape[1], Q.shape[1]) >= 128 and P.shape[2] >= 64 and K.gemm_bf16_supported(P, Q, out, fold):
         return K.gemm_bf16(P, Q, out, alpha, fold)
     return None
 
 
 # fp32 projections (Mamba-TasNet C3) on the split-fp16 MFMA GEMM (avse_gemm_f32s: both operands split into hi / lo fp16
-# planes, three MFMAs per product, fp32 accumulation; fp32-accurate) where the tiles fill ("0": hipBLASLt fp32).
-_F32_SPLIT = os.environ.get("AVSE_F32_SPLIT", "1") == "1"
+# planes, three MFMAs per product, fp32 accumulation; fp32-accurate) where the tiles fill.
 
 
 def _f32_ok(P, Q, out, fold=1):
-    return (_F32_SPLIT and min(P.shape[1], Q.shape[1]) >= 128 and P.shape[2] >= 64
+    return (min(P.shape[1], Q.shape[1]) >= 128 and P.shape[2] >= 64
             and K.gemm_f32s_supported(P, Q, out, fold))
 
 
@@ -161,22 +154,19 @@ def _bsum_split(a_split, bt_split, m, n, alpha=1.0):
 
 def _bsum_mm(a, bt, alpha=1.0):
     """alpha sum_b a[b] @ bt[b] for a (b, m, l), bt (b, l, n): the weight gradient of a batched projection, fp32.
-    Under bf16 autocast with AVSE_PROJ_GEMM=all: the HIP GEMM with fp32 accumulation (avse_gemm_bf16, batches folded
-    into groups).
-    Otherwise as one strided-batched GEMM + sum while the (b, m, n) partials are small (Mamba-TasNet: b = batch);
+    fp32 operands: the split-fp16 GEMM (avse_gemm_f32s, batches folded into groups).  Under bf16 autocast (the library's
+    bf16 weight gradients measured faster than avse_gemm_bf16) and where the split GEMM does not apply: one
+    strided-batched GEMM + sum while the (b, m, n) partials are small (Mamba-TasNet: b = batch);
     as ONE (m, b*l) x (b*l, n) GEMM when they are not (DPMamba's inter pass has b = B*250 sequences of
     34 frames: the partials would take 33 GB, and each GEMM's depth would be 34)."""
     nb, m, l = a.shape
     n = bt.shape[2]
     dt = _autocast_dtype()
-    if (dt == torch.bfloat16 and _HIP_GEMM_ALL) or (dt is None and _F32_SPLIT and a.dtype == bt.dtype == torch.float32):
+    if dt is None and a.dtype == bt.dtype == torch.float32:
         # batches folded into groups so that the launch has about one 256 x 256 tile per CU; groups summed after
         fold = _fold_for(nb, m, n)
         out = torch.empty(nb // fold, m, n, device=a.device, dtype=torch.float32)
-        if dt is None:
-            if _f32_gemm(bt.transpose(1, 2), a, out, alpha, fold=fold) is not None:
-                return out.sum(0)
-        elif _hip_gemm(bt.to(dt).transpose(1, 2), a.to(dt), out, alpha, fold=fold) is not None:
+        if _f32_gemm(bt.transpose(1, 2), a, out, alpha, fold=fold) is not None:
             return out.sum(0)
     if nb * m * n <= (1 << 27):
         r = torch.bmm(a, bt).float().sum(0)
@@ -185,15 +175,14 @@ def _bsum_mm(a, bt, alpha=1.0):
     return r if alpha == 1.0 else alpha * r
 
 
-# dt_proj with the softplus in its epilogue (csrc/dtproj.hip) feeding the scan in delta_softplus mode 2 (default); "0": the
-# GEMM (hipBLASLt / the bf16 HIP GEMM) and the scan's own per-element softplus (mode 1), as the reference calls it.
-_DTPROJ = os.environ.get("AVSE_DTPROJ", "1") == "1"
+# dt_proj with the softplus in its epilogue (csrc/dtproj.hip) feeding the scan in delta_softplus mode 2; a rank above 64
+# (no reference config): the GEMM and the scan's own per-element softplus (mode 1), as the reference calls it.
 
 
 def _delta(dt_proj_w, x_rows, dt_bias):
     """(delta, delta_bias, delta_softplus) for the scan: softplus(W x + b) from the fused kernel (bias None, mode 2), or
-    the raw GEMM output with the bias and mode 1 (rank > 64, or AVSE_DTPROJ=0)."""
-    if _DTPROJ and dt_proj_w.shape[1] <= 64:
+    the raw GEMM output with the bias and mode 1 (rank > 64)."""
+    if dt_proj_w.shape[1] <= 64:
         dt = _autocast_dtype() or torch.result_type(dt_proj_w, x_rows)
         return K.dtproj(dt_proj_w.to(dt), x_rows.to(dt), dt_bias, True), None, 2
     return _wbmm(dt_proj_w, x_rows), dt_bias, True
@@ -331,12 +320,6 @@ class _BiOutProj(torch.autograd.Function):
                 ctx.split = True
                 return out
         ctx.save_for_backward(y, w)
-        if dt is not None and _HIP_GEMM_ALL:
-            wc, yc = w.to(dt), y.to(dt)
-            out = _hip_gemm(wc[None], yc.transpose(1, 2),
-                            torch.empty(y.shape[0], y.shape[2], w.shape[0], device=y.device, dtype=dt), 0.5)
-            if out is not None:
-                return out
         if dt is None and y.dtype == torch.float32:
             out = _f32_gemm(w[None], y.transpose(1, 2),
                             torch.empty(y.shape[0], y.shape[2], w.shape[0], device=y.device, dtype=torch.float32), 0.5)
@@ -394,13 +377,22 @@ class RMSNorm(nn.Module):
 
 
 _STREAMS = {}
+# the v2 backward direction on a second HIP stream (measured: Mamba-TasNet-L B=64 1443 -> 1402 ms/step, C5 B=32 762 ->
+# 727 ms/step); set_direction_streams(False) launches the two directions serially on the current stream
+DIRECTION_STREAMS = True
+
+
+def set_direction_streams(on):
+    """Run BiMamba v2's backward direction on a second HIP stream (True, the default) or serially on the current
+    stream; returns the previous setting."""
+    global DIRECTION_STREAMS
+    old, DIRECTION_STREAMS = DIRECTION_STREAMS, bool(on)
+    return old
 
 
 def _direction_stream(device):
-    """Second HIP stream for the v2 backward direction, one per device (default; AVSE_BIMAMBA_STREAMS=0 launches
-    the two directions serially on the current stream). Measured: Mamba-TasNet-L B=64 1443 -> 1402 ms/step,
-    C5 B=32 762 -> 727 ms/step."""
-    if device.type != "cuda" or os.environ.get("AVSE_BIMAMBA_STREAMS", "1") != "1":
+    """Second HIP stream for the v2 backward direction, one per device (DIRECTION_STREAMS)."""
+    if device.type != "cuda" or not DIRECTION_STREAMS:
         return None
     if device not in _STREAMS:
         _STREAMS[device] = torch.cuda.Stream(device)

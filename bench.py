@@ -64,6 +64,7 @@ def parse():
     p.add_argument("--size", default="L", choices=["XS", "S", "M", "L"], help="Mamba-TasNet / DPMamba size")
     p.add_argument("--lip-hw", type=int, default=96)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-parity", action="store_true", help="skip the output-waveform parity check vs the oracle")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of captured HIP graphs")
     p.add_argument("--secondary", default="mamba,avse4,avmamba",
@@ -93,6 +94,7 @@ def run_secondary(args):
             keep["config"] = {k: rec["config"].get(k) for k in ("workload", "global_batch", "hip_graph", "max_mem_gb")
                               if k in rec["config"]}
             keep["roofline"] = rec.get("roofline")
+            keep["parity"] = rec.get("parity")
             keep["wall_s"] = round(time.perf_counter() - t, 1)
             out.append({"workload": wl, **keep})
         except Exception as e:      # noqa: BLE001 - the headline line must still print
@@ -143,6 +145,66 @@ def barrier(world):
         dist.barrier()
 
 
+# ------------------------------------------------------------------------------ parity (the CPU-baseline leg's checker)
+
+def _wave_parity(est, ref, clean, n_utt, what):
+    """North-star parity of output WAVEFORMS (BASELINE.json: "within 1e-4 RMS waveform error (SI-SDR within 0.01 dB)"):
+    est (GPU path) / ref (fp64 CPU oracle) / clean: (..., T).  RMS(est - ref) against the bar 1e-4 * max(1, RMS(ref)),
+    and |SI-SDR(clean, est) - SI-SDR(clean, ref)| per utterance (channel, speaker)."""
+    from oracle.losses_ref import si_sdr_db
+    est, ref, clean = est.double().cpu(), ref.double().cpu(), clean.double().cpu()
+    rms = float((est - ref).pow(2).mean().sqrt())
+    bar = 1e-4 * max(1.0, float(ref.pow(2).mean().sqrt()))
+    s_est, s_ref = si_sdr_db(clean, est), si_sdr_db(clean, ref)
+    d = float((s_est - s_ref).abs().max())
+    return {"what": what, "utterances": n_utt, "rms": float(f"{rms:.3e}"), "rms_bar": float(f"{bar:.1e}"),
+            "dsisdr_db": float(f"{d:.3e}"), "si_sdr_db": [round(v, 3) for v in s_est.flatten().tolist()],
+            "ok": bool(rms <= bar and d <= 0.01)}
+
+
+def _oracle_from(model, ref):
+    """The fp64 oracle module ``ref`` with the product model's current weights and buffers (identical state_dict
+    keys, tests/test_ckpt_io.py), in the product model's train / eval mode."""
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    return ref.double().train(model.training)
+
+
+def _avse1_oracle_enhance(ref, noisy, lips):
+    """test.py:79-89 on the oracle: librosa-0.8.1 STFT (numpy) -> AVNet (fp64) -> iSTFT with the noisy phase."""
+    import numpy as np
+    from oracle import stft_ref
+    spec = stft_ref.stft(noisy.numpy())
+    mag_t = np.swapaxes(np.abs(spec), -1, -2).astype(np.float32)              # dataset.py:112-118
+    inp = {"noisy_audio_spec": torch.from_numpy(mag_t).double()[:, None]}
+    if lips is not None:
+        inp["lip_images"] = lips
+    with torch.no_grad():
+        pred = ref(inp)[:, 0]
+    phase = np.angle(spec)
+    est = np.swapaxes(pred.numpy(), -1, -2) * (np.cos(phase) + 1j * np.sin(phase))
+    return torch.from_numpy(stft_ref.istft(est, length=noisy.shape[-1]))
+
+
+def _parity_leg(fn):
+    """Run a workload's parity check (eval mode, no grad) and restore the model's mode; a failure is reported."""
+    def wrapped(self, dev):
+        was = self.model.training
+        t = time.perf_counter()
+        try:
+            self.model.eval()
+            with torch.no_grad():
+                rec = fn(self, dev)
+            rec["wall_s"] = round(time.perf_counter() - t, 1)
+            return rec
+        except Exception as e:      # noqa: BLE001 - the bench line must still print
+            return {"error": f"{type(e).__name__}: {e}"}
+        finally:
+            self.model.train(was)
+            torch.cuda.empty_cache()
+    return wrapped
+
+
+
 # ------------------------------------------------------------------------------ workloads
 
 class Avse1Step:
@@ -154,10 +216,9 @@ class Avse1Step:
         from avse_challenge_amd import avse1, data
         self.B, self.lip_hw = B, lip_hw
         self.model = avse1.AVNet().to(dev).train()
-        if int(os.environ.get("AVSE_CHANNELS_LAST", "1")):      # NHWC audio convs (+4.5% step rate)
-            self.model.net_audiofeat.use_channels_last()
-        if int(os.environ.get("AVSE_LIP_CHANNELS_LAST", "1")):  # NHWC lip trunk: no NCHW<->NHWC transposes around MIOpen's
-            self.model.net_visualfeat.use_channels_last()       # NHWC kernels (201.4 vs 195.7 utt/s, round 3)
+        # channels-last audio net and lip trunk: the layouts of the split-fp16 conv kernels (dconv.hip, sconv.hip)
+        self.model.net_audiofeat.use_channels_last()
+        self.model.net_visualfeat.use_channels_last()
         self.lr, self.clip = self.model.lr, None
         self.noisy, self.clean, self.lips = data.avse1_batch(B, dev, 1234 + rank, lip_hw)
         self.avse1 = avse1
@@ -192,18 +253,15 @@ class Avse1Step:
         from avse_challenge_amd import layers
         cl = torch.channels_last
         flops = 2.0 * self.B * 64 * 64 * 25 * 376 * 257
-        split = layers._DCONV_SPLIT
-        names = ("avse_dconv_fwd", "avse_dconv_wgrad16") if split else ("avse_dconv_wgrad",)
-        peak = BF16_PEAK_TFS / 3 if split else FP32_PEAK_TFS
+        names = ("avse_dconv_fwd", "avse_dconv_wgrad16")
+        peak = BF16_PEAK_TFS / 3
         mark = os.environ.get("AVSE_PROFILE_MARK", "0") == "1"        # tools/ktrace_window.py OUT_ROOF.csv
 
         def taps(serial):
             for n in names:
                 K.LAUNCH_TAPS[n] = []
-            old = os.environ.get("AVSE_AVSE1_STREAMS")
+            old = self.avse1.set_branch_streams(not serial)         # serial: the lip branch on the launch stream
             try:
-                if serial:
-                    os.environ["AVSE_AVSE1_STREAMS"] = "0"              # the lip branch on the launch stream
                 if mark and serial:
                     torch.cuda._sleep(1000)
                 for _ in range(3):
@@ -215,10 +273,7 @@ class Avse1Step:
             finally:
                 for n in names:
                     K.LAUNCH_TAPS.pop(n, None)
-                if old is None:
-                    os.environ.pop("AVSE_AVSE1_STREAMS", None)
-                else:
-                    os.environ["AVSE_AVSE1_STREAMS"] = old
+                self.avse1.set_branch_streams(old)
         per2 = taps(False)
         per = taps(True)
         x = torch.randn(self.B, 64, 376, 257, device=dev).contiguous(memory_format=cl)
@@ -302,6 +357,29 @@ class Avse1Step:
                                          f"Adam), batch {B}, lips {self.lip_hw}x{self.lip_hw}")
 
 
+    @_parity_leg
+    def parity(self, dev):
+        """C2 (and C1): the benchmarked model's enhanced waveforms (HIP STFT -> AVNet in eval mode -> HIP iSTFT with
+        the noisy phase, test.py:79-89) on the batch's first 2 utterances vs the fp64 CPU oracle with the same weights
+        and buffers; C1 (BASELINE configs[0]): the audio-only AVNet (model.py:117-118, det-init weights) on the first
+        utterance, the same comparison."""
+        from avse_challenge_amd import avse1
+        from oracle import avse1_ref
+        from oracle.det_init import det_init_
+        _cpu_threads()
+        P = min(2, self.B)
+        noisy, clean, lips = self.noisy[:P], self.clean[:P], self.lips[:P]
+        est = self.model.enhance(noisy, lips)
+        ref = _avse1_oracle_enhance(_oracle_from(self.model, avse1_ref.AVNet()), noisy.cpu(), lips.cpu())
+        out = {"c2": _wave_parity(est, ref, clean, P, "avse1 AV enhance (trained bench weights, eval) vs fp64 oracle")}
+        net = det_init_(avse1.AVNet(a_only=True), 74).to(dev).eval()
+        est1 = net.enhance(self.noisy[:1], None)
+        ref1 = _avse1_oracle_enhance(_oracle_from(net, avse1_ref.AVNet(a_only=True)), self.noisy[:1].cpu(), None)
+        out["c1"] = _wave_parity(est1, ref1, self.clean[:1], 1, "avse1 audio-only enhance (det-init, eval) vs fp64 "
+                                                                "oracle")
+        return out
+
+
 class MambaStep:
     unit_desc = "4s@8kHz WSJ0-2mix utterance"
     graph_ok = True
@@ -313,8 +391,8 @@ class MambaStep:
         # shared xz, and blocks with pending stream uses are not reusable inside a graph capture: at B >= 48 the
         # captured Mamba-TasNet-L step then exceeds 288 GB, so large batches run both directions on one stream
         # (measured at B=64: captured 1 stream 1402 ms/step; eager at ~200 GB allocator churn 6993 ms/step)
-        self.direction_streams = B < 48 and os.environ.get("AVSE_BIMAMBA_STREAMS", "1") == "1"
-        os.environ["AVSE_BIMAMBA_STREAMS"] = "1" if self.direction_streams else "0"
+        self.direction_streams = B < 48
+        mamba_tasnet.set_direction_streams(self.direction_streams)
         self.model = mamba_tasnet.MambaTasNet(**mamba_tasnet.MAMBA_TASNET_SIZES[size]).to(dev).train()
         self.lr, self.clip = 1.5e-4, 5.0
         self.mix, self.tgt = data.wsj0mix_batch(B, dev, 4321 + rank)
@@ -371,6 +449,20 @@ class MambaStep:
                                          f"time scaled x{cut}", runs=3)
 
 
+    @_parity_leg
+    def parity(self, dev):
+        """C3: the benchmarked separator (eval) on the batch's first 4 s mixture vs the fp64 CPU oracle with the same
+        weights; per speaker in the model's own output order (same weights: no PIT needed)."""
+        from oracle import mamba_ref
+        _cpu_threads()
+        mix, tgt = self.mix[:1], self.tgt[:1]
+        est = self.model(mix)                                        # (1, T, n_spk)
+        ref = _oracle_from(self.model, mamba_ref.MambaTasNet(**mamba_ref.MAMBA_TASNET_SIZES[self.size], n_spk=2))
+        est_r = ref(mix.double().cpu())
+        return {"c3": _wave_parity(est.transpose(1, 2), est_r.transpose(1, 2), tgt.transpose(1, 2), 1,
+                                   f"Mamba-TasNet-{self.size} separation (trained bench weights, eval) vs fp64 oracle")}
+
+
 class DPMambaStep(MambaStep):
     """DPMamba: the same BiMamba kernels on 250-frame chunks (intra) and across chunks
     (inter); 4 s @ 8 kHz WSJ0-2mix-shaped mixtures, PIT SI-SNR, bwd, Adam."""
@@ -382,6 +474,8 @@ class DPMambaStep(MambaStep):
         self.lr, self.clip = 1.5e-4, 5.0
         self.mix, self.tgt = data.wsj0mix_batch(B, dev, 4321 + rank)
         self.losses = losses
+
+    parity = None
 
     def config(self, world):
         return {"workload": f"DPMamba-{self.size} train step (SURVEY 8f row 2; dpmamba_{self.size}.yaml)",
@@ -439,8 +533,7 @@ class AVMambaStep:
         from avse_challenge_amd import avmamba, data
         self.B, self.size = B, size
         self.model = avmamba.AVMambaTasNet(**avmamba.AV_MAMBA_SIZES[size]).to(dev).train()
-        if int(os.environ.get("AVSE_LIP_CHANNELS_LAST", "1")):  # NHWC lip ResNet: 3x3 convs on csrc/sconv.hip
-            self.model.visual_frontend.use_channels_last()
+        self.model.visual_frontend.use_channels_last()         # NHWC lip ResNet: 3x3 convs on csrc/sconv.hip
         self.lr, self.clip = 1.5e-4, 5.0
         g = torch.Generator(device=dev).manual_seed(999 + rank)
         noisy, clean, _ = data.avse1_batch(B, dev, 999 + rank, lip_hw=8)
@@ -483,6 +576,30 @@ class AVMambaStep:
                                          f"scaled x{cut}", runs=3)
 
 
+    @_parity_leg
+    def parity(self, dev):
+        """C5 has no reference model: the assembly of reference components (oracle/avmamba_ref.py) is the
+        checker.  The benchmarked model (eval) on the first utterance with its lip track, in fp32 (autocast off: the
+        kernels' parity) vs the fp64 oracle with the same weights; the bf16-autocast output's SI-SDR vs the same oracle
+        beside it (bf16 keeps 8 mantissa bits: the precision choice of the config, not a parity claim)."""
+        from oracle import avmamba_ref
+        from oracle.losses_ref import si_sdr_db
+        _cpu_threads()
+        noisy, clean, vis = self.batch["noisy_audio"][:1], self.batch["clean"][:1], self.batch["vis_feat"][:1]
+        est = self.model(noisy, vis)
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            est16 = self.model(noisy, vis).float()
+        ref = _oracle_from(self.model, avmamba_ref.AVMambaTasNet(**avmamba_ref.AV_MAMBA_SIZES[self.size]))
+        est_r = ref(noisy.double().cpu(), vis.double().cpu())
+        rec = _wave_parity(est, est_r, clean, 1, f"AV Mamba-TasNet-{self.size} (trained bench weights, eval, fp32 "
+                                                 "kernels) vs fp64 oracle assembly")
+        c = clean.double().cpu()
+        d16 = (si_sdr_db(c, est16.double().cpu()) - si_sdr_db(c, est_r)).abs().max()
+        rec["bf16_autocast"] = {"rms": float(f"{float((est16.double().cpu() - est_r).pow(2).mean().sqrt()):.3e}"),
+                                "dsisdr_db": float(f"{float(d16):.3e}")}
+        return {"c5": rec}
+
+
 class Avse2Step:
     """avse2: time-domain AV separator, 3 s @ 16 kHz + 75 gray lip frames 224x224
     (baseline/avse2/config.py), DPRNN separator, SI-SNR loss, batch 16 (train.py:28)."""
@@ -513,6 +630,8 @@ class Avse2Step:
     def cpu_baseline(self):
         return None
 
+    parity = None
+
 
 class Avse4Step:
     unit_desc = "5s@16kHz binaural utterance + 125 lip frames"
@@ -522,8 +641,7 @@ class Avse4Step:
         from avse_challenge_amd import avse4, data
         self.B = B
         self.model = avse4.AVSE4BaselineModule(num_channels=2).to(dev).train()
-        if int(os.environ.get("AVSE_LIP_CHANNELS_LAST", "1")):  # NHWC lip ResNet: 3x3 convs on csrc/sconv.hip
-            self.model.visual_frontend.use_channels_last()
+        self.model.visual_frontend.use_channels_last()         # NHWC lip ResNet: 3x3 convs on csrc/sconv.hip
         self.lr, self.clip = self.model.lr, None
         self.batch = data.avse4_batch(B, dev, 777 + rank)
 
@@ -574,6 +692,21 @@ class Avse4Step:
             _cpu_train_step(m, opt, m.cal_loss(batch))
         return _cpu_record(step, B, 1.0, f"oracle/avse4_ref train step (fwd + bwd + Adam), batch {B} x 2 ch x 5 s "
                                          f"+ 125 lip frames 112x112")
+
+
+    @_parity_leg
+    def parity(self, dev):
+        """C4: the benchmarked model (eval) on the batch's first binaural utterance + lip track vs the fp64 oracle with
+        the same weights and buffers (forward() casts to fp32, model.py:316-321: the oracle's parts are called in
+        fp64)."""
+        from oracle import avse4_ref
+        _cpu_threads()
+        b1 = {k: v[:1] for k, v in self.batch.items()}
+        est = self.model(b1)
+        r = _oracle_from(self.model, avse4_ref.AVSE4BaselineModule(num_channels=2))
+        ref = r.model(b1["noisy_audio"].double().cpu(), r.visual_frontend(b1["vis_feat"].double().cpu()))
+        return {"c4": _wave_parity(est, ref, b1["clean"], 1, "avse4 binaural enhancement (trained bench weights, "
+                                                             "eval) vs fp64 oracle")}
 
 
 from avse_challenge_amd.ddp import Trainer  # noqa: E402  (the data-parallel step; re-exported for tests)
@@ -632,6 +765,8 @@ class PlumbingStep:
 
     def cpu_baseline(self):
         return None
+
+    parity = None
 
 
 # ------------------------------------------------------------------------------ CPU baseline helpers
@@ -735,15 +870,15 @@ def _in_step_hbm(work, name, byts, desc, isolated=None, traffic_phase=None):
 
 
 class _dconv_library:
-    """Context: the dilated convs on MIOpen (layers._DCONV_SPLIT off) — the library figure beside the own kernels."""
+    """Context: the dilated convs on MIOpen (layers.HIP_DCONV off) — the library figure beside the own kernels."""
 
     def __enter__(self):
         from avse_challenge_amd import layers
-        self.prev, layers._DCONV_SPLIT = layers._DCONV_SPLIT, False
+        self.prev, layers.HIP_DCONV = layers.HIP_DCONV, False
 
     def __exit__(self, *exc):
         from avse_challenge_amd import layers
-        layers._DCONV_SPLIT = self.prev
+        layers.HIP_DCONV = self.prev
         return False
 
 
@@ -921,11 +1056,10 @@ def roofline_hip(dev):
             with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=on, cache_enabled=False):
                 ms = _event_ms(fn)
             ach = flops / (ms * 1e-3) / 1e12
-            split = not on and M._F32_SPLIT
+            split = not on
             pk = BF16_PEAK_TFS / 3 if split else peak
             proj.append({"gemm": f"BiMambaV2 {pname} ({tag})", "shape": [b, l, dm, di], "dtype": str(dt)[6:],
-                         "path": ("avse_gemm_bf16 (csrc/projgemm.hip)"
-                                  if on and (M._HIP_GEMM_ALL or (M._HIP_GEMM and pname == "in_proj"))
+                         "path": ("avse_gemm_bf16 (csrc/projgemm.hip)" if on and pname == "in_proj"
                                   else "avse_gemm_f32s (csrc/projgemm.hip: split-fp16 planes, 3 f16 MFMAs per product; "
                                        "time includes splitting the activation)" if split
                                   else "hipBLASLt (torch.bmm)"),
@@ -1079,9 +1213,14 @@ def main():
     hbm_list = proj = None
     if rank == 0 and world == 1 and cuda and not args.no_roofline_hip:
         hbm_list, proj = roofline_hip(dev)
-    cpu = None
+    # the CPU-baseline leg (rank 0, one rank): the oracle restatement on the host cores, timed (cpu_baseline), and the
+    # same oracle as the CHECKER of the benchmarked model's output waveforms on the batch's first utterances (parity,
+    # the "SI-SDR vs ref" half of the BASELINE metric)
+    cpu = par = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = work.cpu_baseline()
+    if rank == 0 and world == 1 and dev.type == "cuda" and not args.no_parity and getattr(work, "parity", None) is not None:
+        par = work.parity(dev)
     secondary = None
     if rank == 0 and world == 1 and cuda and args.workload == "avse1" and args.secondary:
         secondary = run_secondary(args)
@@ -1105,7 +1244,8 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": getattr(work, "dtype", "fp32"),
                "data": "synthetic (speech-like noise with 4 Hz envelope at SNR {0,3,6,9} dB, uint8 lips; "
                        "random-init weights)",
-               "config": cfg, "roofline": roof, "roofline_hip": hbm_list, "projections": proj, "cpu_baseline": cpu}
+               "config": cfg, "roofline": roof, "roofline_hip": hbm_list, "projections": proj, "cpu_baseline": cpu,
+               "parity": par}
         if secondary is not None:
             rec["secondary"] = secondary
         if not cuda:

@@ -216,17 +216,6 @@ int64_t avse_dconv_wgrad_workspace_bytes(int64_t N, int64_t H, int64_t W, int64_
 int avse_dconv_wgrad(int64_t N, int64_t H, int64_t W, int64_t dil, const float* x, const float* dy, float* dw,
                      float* db, float* workspace, avse_stream_t stream);
 
-/* ---------------------------------------------------------------- ResNet trunk 3x3 Conv2d dW -----
- * Weight gradient of nn.Conv2d(CIN, COUT, 3, stride, padding=1, bias=False) — the lip-encoder BasicBlock convs
- * (baseline/avse1/utils/resnet.py:11-13, 26-67; CIN, COUT multiples of 64, stride 1 or 2).  x: (N, CIN, H, W), dy:
- * (N, COUT, HO, WO) fp32, contiguous NCHW (nhwc = 0) or channels-last (nhwc = 1: memory (N, H, W, C)); dw: (COUT, CIN,
- * 3, 3) contiguous, overwritten.  Exact-fp32 MFMA implicit GEMM for the lip encoders' frame sizes (24 .. 3, 28 .. 4,
- * 56 pixels); workspace_bytes returns 0 for an unsupported shape.
- */
-int64_t avse_rconv_wgrad_workspace_bytes(int64_t N, int64_t CIN, int64_t COUT, int64_t H, int64_t W, int64_t stride);
-int avse_rconv_wgrad(int64_t N, int64_t CIN, int64_t COUT, int64_t H, int64_t W, int64_t stride, int32_t nhwc,
-                     const float* x, const float* dy, float* dw, float* workspace, avse_stream_t stream);
-
 /* ---------------------------------------------------------------- PReLU -----------------
  * nn.PReLU(num_parameters in {1, C}) on an (N, C, S) contiguous view — avse1 lip stream
  * (model.py:32, utils/resnet.py:45-46, utils/tcn.py) and avse4 TCN (model.py:260,282).

@@ -169,8 +169,6 @@ def _worker(rank, world, port, q, workload, bucket_mb):
     try:
         sys.path.insert(0, REPO)
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        os.environ["AVSE_AVSE1_STREAMS"] = "1"
-        os.environ["AVSE_BIMAMBA_STREAMS"] = "1"
         import hashlib
 
         import bench  # noqa: F401  (imports the package before the GPU is touched)
@@ -228,8 +226,9 @@ def _worker(rank, world, port, q, workload, bucket_mb):
         # one-process, one-stream reference on the same weights: the sum of both shards' gradients.  The two ranks
         # evaluate it in turn (a barrier between them), so neither process's reference shares the GPU with the
         # other's; the concurrent evaluation (both at once, as round 5 ran it) is kept as a diagnostic.
-        os.environ["AVSE_AVSE1_STREAMS"] = "0"
-        os.environ["AVSE_BIMAMBA_STREAMS"] = "0"
+        from avse_challenge_amd import avse1, mamba_tasnet
+        avse1.set_branch_streams(False)
+        mamba_tasnet.set_direction_streams(False)
 
         def ref_leg():
             taps, tot = {}, None

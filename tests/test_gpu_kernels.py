@@ -418,7 +418,7 @@ def test_conv3d_wgrad_uint8_vs_fp64(T):
     """avse_conv3d_wgrad_u8(_split) reads the uint8 lip frames themselves (no fp32 copy of the clip) at the avse1
     96 x 96 shape: the f16 MFMA path (frames exact in fp16, dy split into hi + lo under its max, given by the producing
     BatchNorm backward or computed here) vs fp64, every element within 1e-5 of its sum of |terms| (the fp32 class);
-    AVSE_C3W_F16=0's exact-fp32 kernel is bitwise the fp32-frames kernel (same products, same order); deterministic."""
+    kernels.C3W_F16 = False's exact-fp32 kernel is bitwise the fp32-frames kernel (same products, same order); deterministic."""
     import importlib
     g = torch.Generator().manual_seed(704 + T)
     xu = torch.randint(0, 256, (2, 3, T, 96, 96), generator=g, dtype=torch.uint8)
@@ -916,7 +916,7 @@ def test_lstm_vs_torch_fp64(B, T, I, H, bidir, group, monkeypatch):
     gradients of the input and every parameter (max error relative to the tensor's max <= 2e-5 for the output,
     5e-5 for gradients: fp32 accumulation over T steps)."""
     from avse_challenge_amd.layers import HipLSTM
-    monkeypatch.setenv("AVSE_LSTM_GROUP", group)
+    monkeypatch.setattr(K(), "LSTM_GROUP", group == "1")
     torch.manual_seed(T + H)
     ref = torch.nn.LSTM(I, H, 1, batch_first=True, bidirectional=bidir).double()
     ours = HipLSTM(I, H, 1, batch_first=True, bidirectional=bidir).to(DEV)
@@ -952,17 +952,17 @@ def test_lstm_group_kernels_at_the_avse1_shape(monkeypatch):
     gx = det_input((B, T, 4 * H), 1620).to(DEV)
     w = (0.06 * det_input((4 * H, H), 1621)).to(DEV)
     dh = det_input((B, T, H), 1622).to(DEV)
-    monkeypatch.setenv("AVSE_LSTM_GROUP", "1")
+    monkeypatch.setattr(K(), "LSTM_GROUP", True)
     h1, c1, g1 = K().lstm_fwd(gx, w)
     d1 = K().lstm_bwd(dh, g1, c1, w)
     for rev in (False, True):
         hr, cr, gr = K().lstm_fwd(gx, w, reverse=rev)
         dr = K().lstm_bwd(dh, gr, cr, w, reverse=rev)
         K().raise_if_kernel_error()
-        monkeypatch.setenv("AVSE_LSTM_GROUP", "0")
+        monkeypatch.setattr(K(), "LSTM_GROUP", False)
         h0, c0, g0 = K().lstm_fwd(gx, w, reverse=rev)
         d0 = K().lstm_bwd(dh, g0, c0, w, reverse=rev)
-        monkeypatch.setenv("AVSE_LSTM_GROUP", "1")
+        monkeypatch.setattr(K(), "LSTM_GROUP", True)
         for a_, b_, n_ in ((hr, h0, "h"), (cr, c0, "c"), (gr, g0, "gates")):
             close(a_, b_, 1e-5 * float(b_.abs().max()), 0, f"{n_} reverse={rev}")
         close(dr, d0, 1e-5 * float(d0.abs().max()), 0, f"dgates reverse={rev}")
@@ -972,22 +972,22 @@ def test_lstm_group_kernels_at_the_avse1_shape(monkeypatch):
 def test_lstm_group_residency_guard(monkeypatch):
     """The grouped kernels run only when a launch's B * G workgroups fit the device at once: the capacity query
     (occupancy x CUs) covers the avse1 grid (32 x 8 = 256, one 136 KB-LDS workgroup per CU); a device that holds fewer
-    (AVSE_LSTM_GROUP_CAPACITY stands in for it) takes lstm.hip's kernels instead, with their exact results."""
+    (kernels.LSTM_GROUP_CAPACITY_LIMIT stands in for it) takes lstm.hip's kernels instead, with their exact results."""
     L = K()._lib.lib()
     B, T, H = 32, 24, 257
     assert L.avse_lstm_group_capacity(H, 0) >= 256 and L.avse_lstm_group_capacity(H, 1) >= 256
     gx = det_input((B, T, 4 * H), 1630).to(DEV)
     w = (0.06 * det_input((4 * H, H), 1631)).to(DEV)
     dh = det_input((B, T, H), 1632).to(DEV)
-    monkeypatch.setenv("AVSE_LSTM_GROUP", "0")
+    monkeypatch.setattr(K(), "LSTM_GROUP", False)
     h0, c0, g0 = K().lstm_fwd(gx, w)
     d0 = K().lstm_bwd(dh, g0, c0, w)
-    monkeypatch.setenv("AVSE_LSTM_GROUP", "1")
-    monkeypatch.setenv("AVSE_LSTM_GROUP_CAPACITY", "255")
+    monkeypatch.setattr(K(), "LSTM_GROUP", True)
+    monkeypatch.setattr(K(), "LSTM_GROUP_CAPACITY_LIMIT", 255)
     h1, c1, g1 = K().lstm_fwd(gx, w)
     d1 = K().lstm_bwd(dh, g1, c1, w)
     assert torch.equal(h1, h0) and torch.equal(c1, c0) and torch.equal(d1, d0)      # the single-workgroup kernels
-    monkeypatch.delenv("AVSE_LSTM_GROUP_CAPACITY")
+    monkeypatch.setattr(K(), "LSTM_GROUP_CAPACITY_LIMIT", None)
     h2, _, _ = K().lstm_fwd(gx, w)
     assert not torch.equal(h2, h0)          # the grouped kernels again (different summation order)
     close(h2, h0, 1e-5 * float(h0.abs().max()), 0, "h")
@@ -1200,9 +1200,8 @@ def test_dilated_conv2d_module_split_path_vs_torch():
 def test_audiofeat_bias_folded_into_batchnorm():
     """AudioFeatNet (channels-last, training mode) with the conv2..conv5 biases folded into their BatchNorms
     (DilatedConv2d bias_to_bn + bn_act folded_bias) vs the same net with the biases added by the library convolution
-    (AVSE_DCONV_WGRAD=0): output and BatchNorm running statistics agree to fp32 rounding."""
+    (layers.HIP_DCONV = False): output and BatchNorm running statistics agree to fp32 rounding."""
     import copy
-    import os
     from avse_challenge_amd import avse1
     torch.manual_seed(5)
     a = avse1.AudioFeatNet().to(DEV).use_channels_last()
@@ -1215,16 +1214,14 @@ def test_audiofeat_bias_folded_into_batchnorm():
     assert a.conv2.hip_ok(torch.empty(1, 64, 4, 4, device=DEV).contiguous(memory_format=torch.channels_last))
     ya = a(spec)
     (ya * gy).sum().backward()
-    old = os.environ.get("AVSE_DCONV_WGRAD")
-    os.environ["AVSE_DCONV_WGRAD"] = "0"
+    from avse_challenge_amd import layers
+    old = layers.HIP_DCONV
+    layers.HIP_DCONV = False
     try:
         yb = b(spec)
         (yb * gy).sum().backward()
     finally:
-        if old is None:
-            del os.environ["AVSE_DCONV_WGRAD"]
-        else:
-            os.environ["AVSE_DCONV_WGRAD"] = old
+        layers.HIP_DCONV = old
     sc = lambda t: max(1e-6, float(t.detach().abs().max()))                                        # noqa: E731
     close(ya, yb, 1e-4 * sc(yb), 0, "y")
     # gradients: the two fp32 runs round differently, so single ReLU masks flip and the strongly cancelling sums
@@ -1309,40 +1306,11 @@ def test_conv1_module_nhwc_vs_torch(N, H, W):
         close(ours.bias.grad, ref.bias.grad, 2e-5 * sc(ref.bias.grad), 0, "db")
 
 
-# ------------------------------------------------------------------ ResNet trunk 3x3 Conv2d weight gradient
-
-@pytest.mark.parametrize("N,cin,cout,H,W,stride", [(6, 64, 64, 24, 24, 1), (5, 64, 128, 24, 24, 2),
-                                                   (7, 128, 128, 12, 12, 1), (9, 128, 256, 12, 12, 2),
-                                                   (11, 256, 256, 6, 6, 1), (13, 256, 512, 6, 6, 2),
-                                                   (17, 512, 512, 3, 3, 1), (3, 64, 64, 28, 28, 1), (5, 64, 128, 28, 28, 2),
-                                                   (3, 256, 512, 7, 7, 2), (19, 512, 512, 4, 4, 1), (2, 64, 64, 56, 56, 1)])
-@pytest.mark.parametrize("cl", [False, True])
-def test_rconv_wgrad_vs_fp64(N, cin, cout, H, W, stride, cl):
-    """K.rconv_wgrad (csrc/rconv_wgrad.hip) vs the fp64 weight gradient of Conv2d(cin, cout, 3, stride, padding=1,
-    bias=False) (baseline/avse1/utils/resnet.py:11-13): the avse1 trunk shapes at 96x96 lips (24..3 pixels, stride 1
-    and 2), the avse4 / C5 ones at 112x112 (28 .. 4: row bands, odd 7x7), the avse2 56x56 layer, frame counts that leave a
-    partial last chunk; every element within 1e-6 of its sum of |terms| (exact-f32 MFMA: one rounding per product),
-    deterministic on rerun.  Shapes outside the lip encoders' table report no workspace (the module keeps the library)."""
-    from avse_challenge_amd import _lib
-    assert _lib.lib().avse_rconv_wgrad_workspace_bytes(2, 64, 128, 7, 9, 2) == 0
-    x = det_input((N, cin, H, W), 1900 + cin + H)
-    HO, WO = (H - 1) // stride + 1, (W - 1) // stride + 1
-    dy = det_input((N, cout, HO, WO), 1901 + cout + W)
-    xd, dyd = x.double(), dy.double()
-    truth = torch.nn.grad.conv2d_weight(xd, (cout, cin, 3, 3), dyd, stride, 1)
-    bound = torch.nn.grad.conv2d_weight(xd.abs(), (cout, cin, 3, 3), dyd.abs(), stride, 1)
-    fmt = torch.channels_last if cl else torch.contiguous_format          # cl: the NHWC kernel (bench trunk layout)
-    xg, dyg = x.to(DEV).contiguous(memory_format=fmt), dy.to(DEV).contiguous(memory_format=fmt)
-    got = K().rconv_wgrad(xg, dyg, stride)
-    worst = float(((got.double().cpu() - truth).abs() / (bound + 1e-30)).max())
-    assert worst <= 1e-6, worst
-    assert torch.equal(got, K().rconv_wgrad(xg, dyg, stride))
-
-
-def test_trunk_conv2d_module_grads_vs_torch(monkeypatch):
-    """layers.TrunkConv2d (stride 2, NCHW): output and input / weight gradients vs nn.Conv2d in fp64."""
+def test_trunk_conv2d_module_grads_vs_torch():
+    """layers.TrunkConv2d (stride 2, NCHW: the library path) and the same conv on channels-last activations (csrc/sconv.hip
+    forward and weight gradient, MIOpen's stride-2 input gradient): output and input / weight gradients vs nn.Conv2d in
+    fp64."""
     from avse_challenge_amd.layers import TrunkConv2d
-    monkeypatch.setenv("AVSE_RCONV_WGRAD", "all")
     torch.manual_seed(4)
     ref = torch.nn.Conv2d(64, 128, 3, stride=2, padding=1, bias=False).double()
     ours = TrunkConv2d(64, 128, 2).to(DEV)
@@ -1352,13 +1320,16 @@ def test_trunk_conv2d_module_grads_vs_torch(monkeypatch):
     xr = x.double().requires_grad_(True)
     yr = ref(xr)
     (yr * gy.double()).sum().backward()
-    xg = x.to(DEV).requires_grad_(True)
-    y = ours(xg)
-    (y * gy.to(DEV)).sum().backward()
     sc = lambda t: max(1e-6, float(t.abs().max()))                                                 # noqa: E731
-    close(y, yr, 2e-5 * sc(yr), 0, "y")
-    close(xg.grad, xr.grad, 2e-5 * sc(xr.grad), 0, "dx")
-    close(ours.weight.grad, ref.weight.grad, 2e-5 * sc(ref.weight.grad), 0, "dw")
+    for fmt in (torch.contiguous_format, torch.channels_last):
+        ours.to(memory_format=fmt)
+        ours.zero_grad()
+        xg = x.to(DEV).contiguous(memory_format=fmt).requires_grad_(True)
+        y = ours(xg)
+        (y * gy.to(DEV)).sum().backward()
+        close(y, yr, 2e-5 * sc(yr), 0, f"y {fmt}")
+        close(xg.grad, xr.grad, 2e-5 * sc(xr.grad), 0, f"dx {fmt}")
+        close(ours.weight.grad, ref.weight.grad, 2e-5 * sc(ref.weight.grad), 0, f"dw {fmt}")
 
 
 def test_conv3d_fwd_avse4_frontend_vs_fp64():

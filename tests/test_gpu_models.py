@@ -455,7 +455,7 @@ def test_bench_trainer_graph_replay_equals_eager():
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_bimamba_direction_streams_equal_serial(monkeypatch, graph):
-    """AVSE_BIMAMBA_STREAMS=1 (backward direction on a second HIP stream, forward and backward; also inside the
+    """mamba_tasnet.DIRECTION_STREAMS (backward direction on a second HIP stream, forward and backward; also inside the
     captured HIP graphs of bench.Trainer) gives the same losses and weights as the serial launch order."""
     import bench
     from avse_challenge_amd import losses as PL
@@ -472,8 +472,8 @@ def test_bimamba_direction_streams_equal_serial(monkeypatch, graph):
             return PL.si_snr_pit(self.tgt, self.model(self.mix)).mean()
 
     runs = []
-    for streams in ("0", "1"):
-        monkeypatch.setenv("AVSE_BIMAMBA_STREAMS", streams)
+    for streams in (False, True):
+        monkeypatch.setattr(M, "DIRECTION_STREAMS", streams)
         st = Step()
         tr = bench.Trainer(st, 1, torch.device(DEV), use_graph=graph)
         losses = [float(tr())]
@@ -527,12 +527,13 @@ def _avse1_fb_values(graph):
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_avse1_branch_streams_equal_serial(monkeypatch, graph):
-    """AVSE_AVSE1_STREAMS=1 (lip branch on a second HIP stream, forward and backward; eager and as a captured HIP
+    """avse1.BRANCH_STREAMS (lip branch on a second HIP stream, forward and backward; eager and as a captured HIP
     graph) gives the loss and every gradient of the single-stream eager step."""
-    monkeypatch.setenv("AVSE_AVSE1_STREAMS", "0")
+    from avse_challenge_amd import avse1
+    monkeypatch.setattr(avse1, "BRANCH_STREAMS", False)
     l0, g0 = _avse1_fb_values(False)
     _, g0b = _avse1_fb_values(False)               # run-to-run noise of the same launch order (library split-K
-    monkeypatch.setenv("AVSE_AVSE1_STREAMS", "1")  # weight-gradient convolutions accumulate atomically)
+    monkeypatch.setattr(avse1, "BRANCH_STREAMS", True)  # weight-gradient convolutions accumulate atomically)
     l1, g1 = _avse1_fb_values(graph)
     assert abs(l1 - l0) <= 1e-6 * abs(l0)
     assert [a is None for a in g0] == [b is None for b in g1]      # tcn_output is unused on the feature path
@@ -557,7 +558,8 @@ def test_avse1_single_stream_trainer_graph_losses_equal_eager(monkeypatch):
     capture replayed with wrong kernel arguments: loss -1.0) reports the eager losses; the package turns that
     capture off (avse_challenge_amd/__init__.py)."""
     import bench
-    monkeypatch.setenv("AVSE_AVSE1_STREAMS", "0")
+    from avse_challenge_amd import avse1
+    monkeypatch.setattr(avse1, "BRANCH_STREAMS", False)
     runs = []
     for graph in (False, True):
         torch.manual_seed(5)
