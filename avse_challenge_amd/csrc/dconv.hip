@@ -272,13 +272,18 @@ __global__ __launch_bounds__(64 * NW, 1) void fwd_kernel(Args a) {
 // (X split in the forward, dY for the input gradient), scaled back by 2^-(e_dy + e_x).  Per-tap GEMM with M = o, N = i
 // and the reduction over pixels: workgroup (chunk range r, kernel row kh) runs over a contiguous range of 64-pixel raster
 // chunks; per chunk the dY rows and the input segment of row kh (positions as in the forward: the chunk's pixels of one
-// or two rows, 2d halo, 4d gap) are staged by LDS-DMA; wave (o block, i block) accumulates the 5 kw tiles (80
-// accumulators per lane).  Both operands are contiguous along the GEMM's M / N (channels), so the fragments are read with
-// ds_read_b64_tr_b16 (4 pixels x 16 channels per 16-lane group, delivered transposed) from 256-B pixel rows whose 16-B
-// chunk c sits at c ^ ((r & 3) << 2).  The kh = 0 workgroups add one more MFMA pair per k-step against a ones fragment:
-// the bias gradient db[o] = sum dY[.][o].  Per-workgroup partial slabs, summed by a second kernel (deterministic).
+// or two rows, 2d halo, 4d gap) are staged by LDS-DMA.  8 waves: wave (half, o block, i block) accumulates the 5 kw tiles
+// (80 accumulators per lane) over k-steps {2 half, 2 half + 1} of every chunk, so two waves share each SIMD (one
+// wave's fragment reads and DMA issue run under the other's MFMAs; round 5's 4-wave form left one wave per SIMD, whose
+// LDS latency and per-chunk address work were exposed: 0.25 of the split peak in the avse1 step).  Both operands are
+// contiguous along the GEMM's M / N (channels), so the fragments are read with ds_read_b64_tr_b16 (4 pixels x 16
+// channels per 16-lane group, delivered transposed) from 256-B pixel rows whose 16-B chunk c sits at c ^ ((r & 3) << 2).
+// The kh = 0 workgroups add one more MFMA pair per k-step against a ones fragment: the bias gradient db[o] = sum dY[.][o].
+// The chunk positions advance incrementally (no integer division in the loop).  Per-(workgroup, half) partial slabs,
+// summed in a fixed order by a second kernel (deterministic).
 constexpr int WG_CHUNK = 64;                     // pixels per chunk (4 k-steps of 16)
 constexpr int PIXB = 256;                        // LDS / Q4 bytes per pixel
+constexpr int WTHREADS = 512, WWAVES = WTHREADS / 64;
 
 typedef short s4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4_t lds_s4_t;
@@ -309,18 +314,42 @@ struct WArgs {
     const void* dyq;
     const uint32_t* xmax;
     const uint32_t* dymax;
-    float* part;                 // [ranges][kh][kw][o][i]
-    float* dbpart;               // [ranges][o] (kh = 0 workgroups) or NULL
+    float* part;                 // [ranges][2][kh][kw][o][i]
+    float* dbpart;               // [ranges][2][o] (kh = 0 workgroups) or NULL
     int N, H, W, cpi, chunks, ranges;
 };
 
+// a chunk's position: image n, first raster pixel p0 in it, its row hA and column wA0
+struct ChunkPos {
+    int n, p0, hA, wA0;
+    __device__ void init(int c, int cpi, int W) {
+        n = c / cpi;
+        p0 = (c - n * cpi) * WG_CHUNK;
+        hA = p0 / W;
+        wA0 = p0 - hA * W;
+    }
+    __device__ void next(int HW, int W) {                // W >= WG_CHUNK
+        p0 += WG_CHUNK;
+        if (p0 >= HW) {
+            ++n;
+            p0 = hA = wA0 = 0;
+        } else {
+            wA0 += WG_CHUNK;
+            if (wA0 >= W) {
+                wA0 -= W;
+                ++hA;
+            }
+        }
+    }
+};
+
 template <int D>
-__global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(WArgs a) {
+__global__ __launch_bounds__(WTHREADS, 1) void wgrad_kernel(WArgs a) {
     constexpr int NP = WG_CHUNK + 8 * D;           // staged input positions per chunk
     constexpr int YIMG = WG_CHUNK * PIXB, XIMG = NP * PIXB, STG = YIMG + XIMG;
     constexpr int NB = (3 * STG <= 160 * 1024) ? 3 : 2;
     constexpr int PY = YIMG / 1024, PT = PY + XIMG / 1024;       // pieces per chunk (4 pixels per 1-KB piece)
-    constexpr int MAXPW = PT / WAVES + 1;
+    constexpr int MAXPW = PT / WWAVES + 1;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[NB * STG];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -331,39 +360,45 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(WArgs a) {
     const i4_t rx = rsrc_of(a.xq, (int64_t)a.N * HW * PIXB);
     const i4_t ry = rsrc_of(a.dyq, (int64_t)a.N * HW * PIXB);
     const uint32_t lds0 = lds_u32(lds);
-    const int npieces = (PT - wave + WAVES - 1) / WAVES;
+    const int npieces = (PT - wave + WWAVES - 1) / WWAVES;
     const int pr = lane >> 4, pc = lane & 15;                    // a piece's lane: row (of 4), physical chunk
+    // per piece of this wave: the lane's pixel (dY) or position (X) within the chunk and its swizzled chunk byte offset
+    int pj[MAXPW];
+    uint32_t psw[MAXPW];
+#pragma unroll
+    for (int m = 0; m < MAXPW; ++m) {
+        const int k = wave + WWAVES * m;
+        pj[m] = k < PY ? 4 * k + pr : 4 * (k - PY) + pr;
+        psw[m] = 16u * tswz(pj[m], pc);
+    }
 
-    auto issue = [&](int c, int buf) {
-        const int n = c / a.cpi, p0 = (c % a.cpi) * WG_CHUNK;
-        const int hA = p0 / a.W, wA0 = p0 - hA * a.W, nA = min(WG_CHUNK, a.W - wA0);
+    auto issue = [&](const ChunkPos& cp, int buf) {
+        const int nA = min(WG_CHUNK, a.W - cp.wA0);
+        const int row1 = cp.hA + D * (kh - 2), row2 = nA < WG_CHUNK ? row1 + 1 : -1000000;
+        const int ybase = cp.n * HW + cp.p0;                     // dY pixel of chunk position 0
+        const int nHrow = cp.n * a.H;
         const uint32_t img = lds0 + buf * STG;
 #pragma unroll
         for (int m = 0; m < MAXPW; ++m) {
             if (m >= npieces) break;
-            const int k = wave + WAVES * m;
-            if (k < PY) {                                        // dY rows: chunk pixel j = 4 k + pr
-                const int j = 4 * k + pr, p = p0 + j;
-                const uint32_t off = p < HW ? ((uint32_t)(n * HW + p) * PIXB + 16u * tswz(j, pc)) : 0x7FFFFFF0u;
+            const int k = wave + WWAVES * m;
+            if (k < PY) {                                        // dY rows: chunk pixel j
+                const int j = pj[m];
+                const uint32_t off = cp.p0 + j < HW ? (uint32_t)(ybase + j) * PIXB + psw[m] : 0x7FFFFFF0u;
                 dma16(ry, img + k * 1024, off);
             } else {
-                const int q = 4 * (k - PY) + pr;                 // input position
-                int col, row;
-                if (q < nA + 4 * D) {
-                    col = wA0 - 2 * D + q;
-                    row = hA + D * (kh - 2);
-                } else {
-                    col = -2 * D + (q - nA - 4 * D);
-                    row = nA < WG_CHUNK ? hA + 1 + D * (kh - 2) : -1000000;
-                }
-                const bool ok = col >= 0 && col < a.W && row >= 0 && row < a.H;
-                const uint32_t pix = ((uint32_t)n * (uint32_t)a.H + (uint32_t)row) * (uint32_t)a.W + (uint32_t)col;
-                dma16(rx, img + YIMG + (k - PY) * 1024, ok ? pix * PIXB + 16u * tswz(q, pc) : 0x7FFFFFF0u);
+                const int q = pj[m];                             // input position
+                const bool s1 = q < nA + 4 * D;
+                const int col = s1 ? cp.wA0 - 2 * D + q : q - nA - 6 * D;
+                const int row = s1 ? row1 : row2;
+                const bool ok = (unsigned)col < (unsigned)a.W && (unsigned)row < (unsigned)a.H;
+                const uint32_t pix = (uint32_t)((nHrow + row) * a.W + col);
+                dma16(rx, img + YIMG + (k - PY) * 1024, ok ? pix * PIXB + psw[m] : 0x7FFFFFF0u);
             }
         }
     };
 
-    const int ob = wave >> 1, ib = wave & 1;                    // this wave's (o, i) 32 x 32 block
+    const int half = wave >> 2, ob = (wave >> 1) & 1, ib = wave & 1;   // k-steps {2 half, 2 half + 1}, (o, i) block
     const bool want_db = a.dbpart != nullptr && kh == 0 && ib == 0;      // wave-uniform
     floatx16 acc[KS], accb;
 #pragma unroll
@@ -377,8 +412,17 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(WArgs a) {
     for (int e = 0; e < 8; ++e) ones[e] = (_Float16)1.0f;
 
     const int g = lane >> 4, li = lane & 15;
-    if (c_lo < c_hi) issue(c_lo, 0);
-    if (NB == 3 && c_lo + 1 < c_hi) issue(c_lo + 1, 1);
+    ChunkPos cc, ci;                                             // compute cursor (chunk c), issue cursor
+    cc.init(c_lo, a.cpi, a.W);
+    ci = cc;
+    if (c_lo < c_hi) {
+        issue(ci, 0);
+        ci.next(HW, a.W);
+    }
+    if (NB == 3 && c_lo + 1 < c_hi) {
+        issue(ci, 1);
+        ci.next(HW, a.W);
+    }
     for (int c = c_lo; c < c_hi; ++c) {
         const int it = c - c_lo;
         const bool ahead = NB == 3 && c + 1 < c_hi;              // the next chunk's pieces may still fly
@@ -386,12 +430,16 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(WArgs a) {
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (c + NB - 1 < c_hi) issue(c + NB - 1, (it + NB - 1) % NB);
+        if (c + NB - 1 < c_hi) {
+            issue(ci, (it + NB - 1) % NB);
+            ci.next(HW, a.W);
+        }
         const uint8_t* yimg = lds + (it % NB) * STG;
         const uint8_t* ximg = yimg + YIMG;
-        const int p0 = (c % a.cpi) * WG_CHUNK, hA = p0 / a.W, nA = min(WG_CHUNK, a.W - (p0 - hA * a.W));
+        const int nA = min(WG_CHUNK, a.W - cc.wA0);
 #pragma unroll
-        for (int s = 0; s < WG_CHUNK / 16; ++s) {
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int s = 2 * half + s2;
             int ry_[2], rx_[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -413,10 +461,11 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(WArgs a) {
                 accb = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ones, accb, 0, 0, 0);
             }
         }
+        cc.next(HW, a.W);
     }
     // partial tiles: acc[kw] register 4 q + e = row o = 32 ob + 8 q + 4 (lane >> 5) + e, column i = 32 ib + (lane & 31)
     const float sc = __builtin_ldexpf(1.f, -(split_exp(*a.xmax) + split_exp(*a.dymax)));
-    float* pp = a.part + ((int64_t)r * KS + kh) * KS * C * C;
+    float* pp = a.part + (((int64_t)r * 2 + half) * KS + kh) * KS * C * C;
 #pragma unroll
     for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
@@ -431,25 +480,27 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(WArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) a.dbpart[(int64_t)r * C + 32 * ob + 8 * q + 4 * (lane >> 5) + e] = accb[4 * q + e] * sd;
+            for (int e = 0; e < 4; ++e)
+                a.dbpart[((int64_t)r * 2 + half) * C + 32 * ob + 8 * q + 4 * (lane >> 5) + e] = accb[4 * q + e] * sd;
     }
 }
 
-// dW[o][i][kh][kw] = sum over ranges of part[range][kh][kw][o][i]; db[o] = sum over ranges of dbpart[range][o]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ dbpart, int ranges,
+// dW[o][i][kh][kw] = sum over slabs of part[slab][kh][kw][o][i]; db[o] = sum over slabs of dbpart[slab][o] (slab =
+// 2 range + half, summed in order: deterministic)
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ dbpart, int slabs,
                                     float* __restrict__ dw, float* __restrict__ db) {
     constexpr int TOTAL = KS * KS * C * C;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= TOTAL) {
         if (db != nullptr && idx < TOTAL + C) {
             float v = 0.f;
-            for (int g = 0; g < ranges; ++g) v += dbpart[(int64_t)g * C + idx - TOTAL];
+            for (int g = 0; g < slabs; ++g) v += dbpart[(int64_t)g * C + idx - TOTAL];
             db[idx - TOTAL] = v;
         }
         return;
     }
     float v = 0.f;
-    for (int g = 0; g < ranges; ++g) v += part[(int64_t)g * TOTAL + idx];
+    for (int g = 0; g < slabs; ++g) v += part[(int64_t)g * TOTAL + idx];
     const int i = idx % C, o = (idx / C) % C, kw = (idx / (C * C)) % KS, kh = idx / (KS * C * C);
     dw[((o * C + i) * KS + kh) * KS + kw] = v;
 }
@@ -587,7 +638,7 @@ int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* max
 
 int64_t avse_dconv_wgrad16_workspace_bytes(int64_t N, int64_t H, int64_t W) {
     const int64_t chunks = N * ((H * W + WG_CHUNK - 1) / WG_CHUNK);
-    return 4 * (int64_t)wgrad_ranges((int)std::min<int64_t>(chunks, 1 << 30)) * (KS * KS * C * C + C);
+    return 4 * 2 * (int64_t)wgrad_ranges((int)std::min<int64_t>(chunks, 1 << 30)) * (KS * KS * C * C + C);
 }
 
 int avse_dconv_wgrad16(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq, const uint32_t* xmax,
@@ -608,8 +659,8 @@ int avse_dconv_wgrad16(int64_t N, int64_t H, int64_t W, int64_t dil, const void*
     a.chunks = (int)(N * a.cpi);
     a.ranges = wgrad_ranges(a.chunks);
     a.part = workspace;
-    a.dbpart = db ? workspace + (int64_t)a.ranges * KS * KS * C * C : nullptr;
-    const dim3 grid((unsigned)(a.ranges * KS)), block(THREADS);
+    a.dbpart = db ? workspace + (int64_t)2 * a.ranges * KS * KS * C * C : nullptr;
+    const dim3 grid((unsigned)(a.ranges * KS)), block(WTHREADS);
     hipStream_t st = (hipStream_t)stream;
     switch (dil) {
         case 2: hipLaunchKernelGGL(wgrad_kernel<2>, grid, block, 0, st, a); break;
@@ -619,8 +670,8 @@ int avse_dconv_wgrad16(int64_t N, int64_t H, int64_t W, int64_t dil, const void*
     }
     AVSE_CHECK_LAUNCH();
     constexpr int TOTAL = KS * KS * C * C;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((TOTAL + C + 255) / 256), dim3(256), 0, st, a.part, a.dbpart, a.ranges,
-                       dw, db);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((TOTAL + C + 255) / 256), dim3(256), 0, st, a.part, a.dbpart,
+                       2 * a.ranges, dw, db);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

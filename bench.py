@@ -72,6 +72,8 @@ def parse():
                         "B=64, C4 avse4 B=16, C5 AV Mamba-TasNet-L bf16 B=32), each as a child bench run after the "
                         "headline's measurement, reported under 'secondary' in the same JSON line ('' = none)")
     p.add_argument("--secondary-steps", type=int, default=4)
+    p.add_argument("--direction-streams", default="auto", choices=["auto", "on", "off"],
+                   help="Mamba workloads: BiMamba v2's backward direction on a second HIP stream (auto: below B=48)")
     return p.parse_args()
 
 
@@ -241,12 +243,14 @@ class Avse1Step:
         weight gradient (avse_dconv_wgrad).  Algorithmic FLOPs per launch = 2*B*64*64*25*376*257 (fp32 math); the split
         kernels run 3 f16 MFMAs per fp32 product, so their peak is the dense f16 peak / 3 (833 TFLOP/s), the fp32-MFMA
         kernel's the fp32 peak (157.3).
-          * ``achieved`` / ``frac`` / ``avg_ms``: IN-STEP — every launch inside 3 eager train steps of the benchmarked
-            model itself, each bracketed by HIP events on its launch stream (kernels.LAUNCH_TAPS), with the lip branch
-            on the launch stream for these 3 steps: then a launch's event time is its kernel time (with the branch on
-            its side stream, as the timed steps run, the events also count the launch's wait for CUs the lip branch
-            holds: ``in_step_two_streams``, 3 more eager steps); ``roofline`` is the entry point with the most kernel
-            time in them; AVSE_PROFILE_MARK=1 brackets the serial-branch steps (the rocprof window that must agree);
+          * ``achieved`` / ``frac`` / ``avg_ms``: IN-STEP, AS THE TIMED STEPS RUN — every launch inside 3 eager train
+            steps of the benchmarked model with the lip branch on its side stream (the timed schedule), each bracketed
+            by HIP events on its launch stream (kernels.LAUNCH_TAPS): a launch's event time is its duration while it
+            shares the CUs with the lip branch (the rocprofv3 timed window, profiles/*_avse1_timed_window_stats.csv,
+            shows the same per-launch average); ``roofline`` is the entry point with the most kernel time in them;
+          * ``in_step_serial``: the same with the lip branch on the launch stream for 3 more steps (a launch's event
+            time is then its kernel time alone on the GPU); AVSE_PROFILE_MARK=1 brackets these steps (the rocprof window
+            that must agree);
           * ``isolated``: conv3's launch (d = 4) alone on the idle GPU, random operands of the step's shape;
           * ``roofline_library``: the MIOpen forward of the same conv, alone."""
         from avse_challenge_amd import kernels as K
@@ -281,7 +285,7 @@ class Avse1Step:
         w = 0.05 * torch.randn(64, 64, 5, 5, device=dev)
         recs = []
         for n in names:
-            v = per[n]
+            v, vs = per2[n], per[n]                   # two streams (the timed schedule), serial
             if not v:
                 continue
             ms_in = sum(v) / len(v)
@@ -296,40 +300,36 @@ class Avse1Step:
                                                        K.ptr(y), K.stream_ptr(dev)), "avse_dconv_fwd")
                 desc = ("avse_dconv_fwd (AudioFeatNet conv2..5 forward and input gradient: Conv2d 64->64 5x5 dil "
                         "2/4/8/16 as a split-fp16 MFMA implicit GEMM, fp32-accurate)")
-            elif n == "avse_dconv_wgrad16":
+            else:
                 xm, dm = torch.empty(2, device=dev, dtype=torch.int32), torch.empty(2, device=dev, dtype=torch.int32)
                 xq, dq = K.split16(x, xm), K.split16(dy, dm)
                 iso = lambda: K.dconv_wgrad16((xq, xm[:1]), (dq, dm[:1]), tuple(x.shape), 4)  # noqa: E731
                 desc = "avse_dconv_wgrad16 (AudioFeatNet conv2..5 weight gradient, split-fp16 MFMA implicit GEMM)"
-            else:
-                iso = lambda: K.dconv_wgrad(x, dy, 4)  # noqa: E731
-                desc = ("avse_dconv_wgrad (AudioFeatNet conv2..5 weight gradient: Conv2d 64->64 5x5 dil 2/4/8/16, "
-                        "fp32 HIP MFMA implicit GEMM)")
             ms = _event_ms(iso, n=10, warm=3)
             ach = flops / (ms * 1e-3) / 1e12
-            v2 = per2.get(n) or [float("nan")]
-            ms2 = sum(v2) / len(v2)
+            vs = vs or [float("nan")]
+            ms_s = sum(vs) / len(vs)
             recs.append({"kernel": desc, "bound": "mfma", "achieved": round(ach_in, 2), "peak": round(peak, 1),
                          "unit": "TFLOP/s", "frac": round(ach_in / peak, 4), "traffic": None, "avg_ms": round(ms_in, 4),
                          "launches": len(v), "step_ms": round(sum(v) / 3, 3),
-                         "measured": f"in-step: {len(v)} launches in 3 eager train steps of the benchmarked model (lip "
-                                     "branch on the launch stream), HIP events on the launch stream",
-                         "in_step_two_streams": {"avg_ms": round(ms2, 4),
-                                                 "frac": round(flops / (ms2 * 1e-3) / 1e12 / peak, 4),
-                                                 "note": "lip branch on its side stream as in the timed steps: the "
-                                                         "events also count each launch's wait for CUs"},
+                         "measured": f"in-step, timed schedule: {len(v)} launches in 3 eager train steps of the "
+                                     "benchmarked model with the lip branch on its side stream, HIP events on the "
+                                     "launch stream",
+                         "in_step_serial": {"avg_ms": round(ms_s, 4),
+                                            "frac": round(flops / (ms_s * 1e-3) / 1e12 / peak, 4),
+                                            "note": "lip branch on the launch stream (3 more eager steps): the launch "
+                                                    "alone on the GPU"},
                          "per_launch_ms": [round(t, 3) for t in v[:4]], "algorithmic_flops_per_launch": flops,
                          "isolated": {"what": "conv3 (d = 4) alone on the idle GPU", "avg_ms": round(ms, 4),
                                       "achieved": round(ach, 2), "frac": round(ach / peak, 4)}})
         if not recs:
             return None
         roof = dict(max(recs, key=lambda r: r["step_ms"]))
-        if split:
-            roof["peak_note"] = ("split-fp16 kernels: 3 f16 MFMAs per fp32 product, peak = dense f16 2500 TFLOP/s / 3; "
-                                 "achieved counts the fp32 algorithmic FLOPs")
-            roof["other_conv_kernels"] = [{k: r[k] for k in ("kernel", "avg_ms", "achieved", "frac", "launches",
-                                                             "step_ms")} for r in recs if r is not roof]
-        _with_traffic(roof, "dconv_wgrad" if (self.B == 32 and not split) else "-")
+        roof["peak_note"] = ("split-fp16 kernels: 3 f16 MFMAs per fp32 product, peak = dense f16 2500 TFLOP/s / 3; "
+                             "achieved counts the fp32 algorithmic FLOPs")
+        roof["other_conv_kernels"] = [{k: r[k] for k in ("kernel", "avg_ms", "achieved", "frac", "launches",
+                                                         "step_ms")} for r in recs if r is not roof]
+        _with_traffic(roof, "-")
         conv = self.model.net_audiofeat.conv3
         with torch.no_grad(), _dconv_library():
             ms_f = _event_ms(lambda: conv(x), n=10, warm=3)
@@ -380,6 +380,17 @@ class Avse1Step:
         return out
 
 
+DIRECTION_STREAMS_ARG = "auto"     # --direction-streams
+
+
+def _apply_direction_streams(work):
+    """--direction-streams on / off overrides the workload's default (auto)."""
+    from avse_challenge_amd import mamba_tasnet
+    if DIRECTION_STREAMS_ARG != "auto":
+        work.direction_streams = DIRECTION_STREAMS_ARG == "on"
+        mamba_tasnet.set_direction_streams(work.direction_streams)
+
+
 class MambaStep:
     unit_desc = "4s@8kHz WSJ0-2mix utterance"
     graph_ok = True
@@ -393,6 +404,7 @@ class MambaStep:
         # (measured at B=64: captured 1 stream 1402 ms/step; eager at ~200 GB allocator churn 6993 ms/step)
         self.direction_streams = B < 48
         mamba_tasnet.set_direction_streams(self.direction_streams)
+        _apply_direction_streams(self)
         self.model = mamba_tasnet.MambaTasNet(**mamba_tasnet.MAMBA_TASNET_SIZES[size]).to(dev).train()
         self.lr, self.clip = 1.5e-4, 5.0
         self.mix, self.tgt = data.wsj0mix_batch(B, dev, 4321 + rank)
@@ -533,7 +545,9 @@ class AVMambaStep:
         from avse_challenge_amd import avmamba, data
         self.B, self.size = B, size
         self.model = avmamba.AVMambaTasNet(**avmamba.AV_MAMBA_SIZES[size]).to(dev).train()
-        self.model.visual_frontend.use_channels_last()         # NHWC lip ResNet: 3x3 convs on csrc/sconv.hip
+        self.model.visual_frontend.use_channels_last()
+        self.direction_streams = True
+        _apply_direction_streams(self)         # NHWC lip ResNet: 3x3 convs on csrc/sconv.hip
         self.lr, self.clip = 1.5e-4, 5.0
         g = torch.Generator(device=dev).manual_seed(999 + rank)
         noisy, clean, _ = data.avse1_batch(B, dev, 999 + rank, lip_hw=8)
@@ -548,7 +562,7 @@ class AVMambaStep:
         return {"workload": f"AV Mamba-TasNet-{self.size} train step (BASELINE configs[4]): avse4 lip encoder (fp32) + "
                             "Mamba-TasNet separator under bf16 autocast (bf16 scan / conv activations, fp32 state)",
                 "global_batch": self.B * world, "per_gpu_batch": self.B, "seq_len": 48000, "frames": 5999,
-                "lip_frames": 75, "lip_hw": 112, "parallelism": f"dp{world}"}
+                "lip_frames": 75, "lip_hw": 112, "parallelism": f"dp{world}", "direction_streams": self.direction_streams}
 
     tap_kernels = ("avse_scan_bwd", "avse_scan_fwd")
     scan_dtype, scan_len = torch.bfloat16, 5999
@@ -1115,6 +1129,8 @@ def main():
         # MIOpen immediate mode: find mode (benchmark=True, as avse1 train.py:11 sets for cuDNN) JIT-compiles
         # every candidate solver on a fresh box (minutes); immediate mode compiles only the chosen one.
         torch.backends.cudnn.benchmark = bool(int(os.environ.get("AVSE_MIOPEN_FIND", "0")))
+    global DIRECTION_STREAMS_ARG
+    DIRECTION_STREAMS_ARG = args.direction_streams
     if args.workload == "avse1":
         B = args.batch or 32
         work = Avse1Step(B, dev, rank, world, args.lip_hw)
