@@ -377,14 +377,16 @@ class RMSNorm(nn.Module):
 
 
 _STREAMS = {}
-# the v2 backward direction on a second HIP stream (measured: Mamba-TasNet-L B=64 1443 -> 1402 ms/step, C5 B=32 762 ->
-# 727 ms/step); set_direction_streams(False) launches the two directions serially on the current stream
-DIRECTION_STREAMS = True
+# set_direction_streams(True): the v2 backward direction on a second HIP stream.  Off by default: the two directions'
+# selective scans each fill the GPU (C5 B=32: 512 scan-backward workgroups = 2 per CU), so concurrent launches only
+# share the CUs (5.85 vs 2.90 ms per launch) and the step was slower with the streams (571.7 vs 552.5 ms per C5 step,
+# gpurun_out/r06e_c5_*.log; round 1, before the scan kernels filled the GPU, the streams gained 762 -> 727 ms)
+DIRECTION_STREAMS = False
 
 
 def set_direction_streams(on):
-    """Run BiMamba v2's backward direction on a second HIP stream (True, the default) or serially on the current
-    stream; returns the previous setting."""
+    """Run BiMamba v2's backward direction on a second HIP stream (True) or serially on the current stream (False,
+    the default); returns the previous setting."""
     global DIRECTION_STREAMS
     old, DIRECTION_STREAMS = DIRECTION_STREAMS, bool(on)
     return old

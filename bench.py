@@ -73,7 +73,8 @@ def parse():
                         "headline's measurement, reported under 'secondary' in the same JSON line ('' = none)")
     p.add_argument("--secondary-steps", type=int, default=4)
     p.add_argument("--direction-streams", default="auto", choices=["auto", "on", "off"],
-                   help="Mamba workloads: BiMamba v2's backward direction on a second HIP stream (auto: below B=48)")
+                   help="Mamba workloads: BiMamba v2's backward direction on a second HIP stream (auto: off, "
+                        "the measured default)")
     return p.parse_args()
 
 
@@ -402,9 +403,14 @@ class MambaStep:
         # shared xz, and blocks with pending stream uses are not reusable inside a graph capture: at B >= 48 the
         # captured Mamba-TasNet-L step then exceeds 288 GB, so large batches run both directions on one stream
         # (measured at B=64: captured 1 stream 1402 ms/step; eager at ~200 GB allocator churn 6993 ms/step)
-        self.direction_streams = B < 48
-        mamba_tasnet.set_direction_streams(self.direction_streams)
+        # the two BiMamba directions serially on one stream (mamba_tasnet.DIRECTION_STREAMS): at B >= 48 the side
+        # stream's pending record_stream uses would also keep blocks out of the graph pool (the captured C3 step then
+        # exceeds 288 GB); --direction-streams on runs the side stream where it fits
+        self.direction_streams = False
+        mamba_tasnet.set_direction_streams(False)
         _apply_direction_streams(self)
+        if self.direction_streams and B >= 48:
+            raise SystemExit("--direction-streams on needs B < 48 (the captured step's memory, see above)")
         self.model = mamba_tasnet.MambaTasNet(**mamba_tasnet.MAMBA_TASNET_SIZES[size]).to(dev).train()
         self.lr, self.clip = 1.5e-4, 5.0
         self.mix, self.tgt = data.wsj0mix_batch(B, dev, 4321 + rank)
@@ -546,7 +552,9 @@ class AVMambaStep:
         self.B, self.size = B, size
         self.model = avmamba.AVMambaTasNet(**avmamba.AV_MAMBA_SIZES[size]).to(dev).train()
         self.model.visual_frontend.use_channels_last()
-        self.direction_streams = True
+        from avse_challenge_amd import mamba_tasnet
+        self.direction_streams = False                         # C5 B=32: 552.5 vs 571.7 ms/step with the side stream
+        mamba_tasnet.set_direction_streams(False)
         _apply_direction_streams(self)         # NHWC lip ResNet: 3x3 convs on csrc/sconv.hip
         self.lr, self.clip = 1.5e-4, 5.0
         g = torch.Generator(device=dev).manual_seed(999 + rank)

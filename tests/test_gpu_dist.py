@@ -182,6 +182,8 @@ def _worker(rank, world, port, q, workload, bucket_mb):
         kernels.no_grouped_lstm().__enter__()
         dist.init_process_group("gloo", rank=rank, world_size=world)
         st = _make(workload, rank, world)
+        from avse_challenge_amd import mamba_tasnet
+        mamba_tasnet.set_direction_streams(True)          # buckets holding gradients of two streams (module docstring)
         tr = bench.Trainer(st, world, torch.device("cuda", 0), use_graph=False, bucket_mb=bucket_mb)
         rec = {}
         orig_opt, orig_launch = tr._opt, tr._launch

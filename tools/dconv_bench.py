@@ -35,6 +35,7 @@ def main():
     p.add_argument("--batch", type=int, default=32)
     p.add_argument("--iters", type=int, default=5)
     p.add_argument("--no-miopen", action="store_true")
+    p.add_argument("--dils", default="2,4,8,16")
     a = p.parse_args()
     B, H, W = a.batch, 376, 257
     cl = torch.channels_last
@@ -42,7 +43,7 @@ def main():
     dy = torch.randn(B, 64, H, W, device="cuda").contiguous(memory_format=cl)
     w = (0.05 * torch.randn(64, 64, 5, 5, device="cuda")).contiguous(memory_format=cl)
     flops = 2.0 * B * 64 * 64 * 25 * H * W
-    for d in (2, 4, 8, 16):
+    for d in [int(v) for v in a.dils.split(",")]:
         rec = {"dilation": d, "batch": B, "gflop": round(flops / 1e9, 1)}
         ms = timeit(lambda: K.dconv_wgrad(x, dy, d), a.iters)
         rec["hip_wgrad"] = {"ms": round(ms, 3), "tflops": round(flops / ms / 1e9, 1), "frac": round(flops / ms / 1e9 / 157.3, 3)}
