@@ -117,13 +117,14 @@ struct Args {
 // NW waves, tile = TP = 64 NW raster pixels spanning up to NSEG rows (W >= 256): row segment k of the tile sits at LDS
 // positions S_k .. S_k + n_k + 4 D (its n_k pixels with the 2 D halo each side), S_k = n_0 + .. + n_{k-1} + 4 D k, so
 // output pixel j of segment k reads position j + 4 D k + D kw for tap kw.
-template <int D, int NW>
-__global__ __launch_bounds__(64 * NW, 1) void fwd_kernel(Args a) {
+// WGS workgroups per CU: 2 (NW = 4) takes 2 LDS buffers, so that two workgroups fit; 1: 3 buffers where they fit.
+template <int D, int NW, int WGS = 1>
+__global__ __launch_bounds__(64 * NW, WGS) void fwd_kernel(Args a) {
     constexpr int TPX = 64 * NW, NSEG = NW == 4 ? 2 : 3;
     constexpr int NP = (TPX + 4 * D * NSEG + 15) / 16 * 16;   // staged positions (whole 1-KB DMA pieces)
     constexpr int XIMG = NP * ROWB;
     constexpr int STG = XIMG + WIMG;
-    constexpr int NB = (3 * STG <= 160 * 1024) ? 3 : 2;
+    constexpr int NB = WGS == 2 ? 2 : ((3 * STG <= 160 * 1024) ? 3 : 2);
     constexpr int PX = XIMG / 1024, PT = PX + WIMG / 1024;      // X pieces, all pieces of a stage
     constexpr int MP = PT / NW + 1;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[NB * STG];
@@ -288,7 +289,12 @@ constexpr int WTHREADS = 512, WWAVES = WTHREADS / 64;
 typedef short s4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4_t lds_s4_t;
 
-__device__ inline int tswz(int r, int c) { return c ^ ((r & 3) << 2); }
+// 16-B chunk c of staged pixel row r sits at physical chunk tswz(r, c).  A transposed fragment read (tfrag) takes, per
+// 32-lane half, 4 consecutive rows x 4 chunks whose logical indices differ in bits 0 and 2; the rows' XOR masks must
+// then differ in bits 1 and 3 for the 16 (row, chunk) pairs to land on 16 distinct 4-bank groups (every row starts on
+// bank 0: 256-B rows).  Round 5's mask ((r & 3) << 2) moved bits 2-3 only: 2-way conflicts on every read
+// (SQ_LDS_BANK_CONFLICT = 0.5 x SQ_LDS_IDX_ACTIVE, gpurun_out/r06f_pmc_dconv); this one is conflict-free.
+__device__ inline int tswz(int r, int c) { return c ^ (((r & 1) << 1) | ((r & 2) << 2)); }
 
 // MFMA operand fragment (32 channels x 16 pixels) of the channel block cb (quarters 2 cb, 2 cb + 1), plane pl (0 hi,
 // 1 lo), k-step rows rows[0..15] given per lane: lane l (group g = l >> 4, i = l & 15) reads pixel rows
@@ -690,23 +696,20 @@ int avse_dconv_fwd(int64_t N, int64_t H, int64_t W, int64_t dil, const void* xq,
     a.N = (int)N;
     a.H = (int)H;
     a.W = (int)W;
-    // tile = 64 NW raster pixels on NW = 8 waves (4 measured slower: half the MFMA work per staged W byte, one wave
-    // per SIMD)
-    constexpr int nw = 8;
+    // d <= 8: tile = 256 raster pixels on 4 waves, two workgroups per CU (2 LDS buffers of <= 40 KB each): the two
+    // workgroups' barriers and DMA phases interleave, 1.61 vs 1.69 ms per launch at C2 against one 8-wave 512-pixel
+    // workgroup per CU (profiles/r06g_dconv_fwd_ab.jsonl; one 4-wave workgroup per CU with 3 buffers measured slower in
+    // round 5).  d = 16: the 4-wave tile's 4d halos need 89 KB per workgroup, so it keeps the 8-wave form.
+    const int nw = dil <= 8 ? 4 : 8;
     a.tiles = (int)((H * W + 64 * nw - 1) / (64 * nw));
     const dim3 grid((unsigned)(N * a.tiles)), block(64 * nw);
     hipStream_t st = (hipStream_t)stream;
-#define AVSE_DCF_L(DD)                                                                  \
-    do {                                                                                \
-        hipLaunchKernelGGL((fwd_kernel<DD, nw>), grid, block, 0, st, a);                \
-    } while (0)
     switch (dil) {
-        case 2: AVSE_DCF_L(2); break;
-        case 4: AVSE_DCF_L(4); break;
-        case 8: AVSE_DCF_L(8); break;
-        default: AVSE_DCF_L(16); break;
+        case 2: hipLaunchKernelGGL((fwd_kernel<2, 4, 2>), grid, block, 0, st, a); break;
+        case 4: hipLaunchKernelGGL((fwd_kernel<4, 4, 2>), grid, block, 0, st, a); break;
+        case 8: hipLaunchKernelGGL((fwd_kernel<8, 4, 2>), grid, block, 0, st, a); break;
+        default: hipLaunchKernelGGL((fwd_kernel<16, 8>), grid, block, 0, st, a); break;
     }
-#undef AVSE_DCF_L
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }
