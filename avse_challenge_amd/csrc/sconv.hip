@@ -276,14 +276,17 @@ struct WArgs {
     int N, Hi, Wi, Ci, Ho, Wo, Co;
     int RS, npw;                 // staged segment length, positions staged per chunk (multiple of 4, <= NPW_MAX)
     int chunks, ranges, nob, nib;
+    int q64, r64;                // WG_CHUNK = q64 Wo + r64
     float inv_ho, inv_wo;
 };
 
 template <int S, int OB>
 __global__ __launch_bounds__(512, 1) void wgrad_kernel(WArgs a) {
-    // OB = 128: 8 waves of (o, i) blocks; OB = 64: the 4 blocks twice, each copy over half of a chunk's 4 k-steps
-    // (KG = 2 k-step groups, two partial slabs per range): 8 waves either way
-    constexpr int KG = OB == 64 ? 2 : 1, BW = OB / 16, WAVES = BW * KG, YRB = OB * 4;   // dY row bytes: the o block
+    // 8 waves; wave = 64 o x 32 i (2 x 1 MFMA blocks) x 3 taps: OB / 32 waves cover the (OB, 64) block, and the
+    // KG = 8 / (OB / 32) copies take disjoint k-steps of every chunk (KG partial slabs per range).  Round 5's wave of
+    // 32 o x 32 i read and addressed its X fragments for one o block only: with ~900 address / DMA-issue instructions
+    // per 36 MFMAs the kernel was instruction-issue bound (MFMA busy 0.24, r06f PMC).
+    constexpr int BW = OB / 32, KG = 8 / BW, WAVES = 8, YRB = OB * 4, KS = (WG_CHUNK / 16) / KG;   // KS k-steps per wave
     constexpr int YIMG = WG_CHUNK * YRB, STG = YIMG + NPW_MAX * XROWB;
     constexpr int PY = YIMG / 1024, YPP = 1024 / YRB;             // dY pieces; pixels per piece
     constexpr int MP = (PY + NPW_MAX / 4 + WAVES - 1) / WAVES;
@@ -309,17 +312,49 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WArgs a) {
     const int ypr = lane / (YRB / 16), ypc = lane % (YRB / 16);  // dY piece lane: pixel of the piece, physical chunk
     const int xpr = lane >> 4, xpc = lane & 15;                    // X piece lane: position of the piece, chunk
 
-    // the lane's staged position of each X piece: (row of the chunk's segment list, column)
-    int qrk[MP], qcol[MP];
+    // per DMA piece of this wave, everything that does not depend on the chunk: dY pieces: the lane's chunk pixel j and
+    // its byte offset within the chunk's dY rows; X pieces: the staged position's row of the chunk's segment list and
+    // the byte offset of its input column within an input row (OOB for padding columns and positions past npw)
+    int pj[MP];
+    uint32_t poff[MP];
 #pragma unroll
     for (int m = 0; m < MP; ++m) {
         const int k = wave + WAVES * m;
-        const int q = 4 * (k - PY) + xpr;
-        qrk[m] = k >= PY ? q / a.RS : 0;
-        qcol[m] = k >= PY ? q - qrk[m] * a.RS : 0;
+        if (k < PY) {
+            const int j = YPP * k + ypr;
+            pj[m] = j;
+            poff[m] = (uint32_t)j * ypixb + (uint32_t)(ob * YRB) + 16u * tswz(j, ypc);
+        } else {
+            const int q = 4 * (k - PY) + xpr;
+            const int rk = q / a.RS, wi = q - rk * a.RS - 1;
+            const bool ok = q < a.npw && wi >= 0 && wi < a.Wi;
+            pj[m] = rk;
+            poff[m] = ok ? (uint32_t)wi * xpixb + (uint32_t)(ib * XROWB) + 16u * tswz(q, xpc) : OOB;
+        }
     }
-    auto issue = [&](int c, int buf) {
-        const int p0 = c * WG_CHUNK, g0 = p0 / a.Wo;
+    const uint32_t xrowb = (uint32_t)a.Wi * xpixb;                // bytes per input row
+    // the chunks' first output row g0 (flat n, ho) and column w0 advance by WG_CHUNK pixels = q64 rows + r64 columns
+    struct Cur {
+        int g0, w0;
+    };
+    auto cur_at = [&](int c) {
+        Cur cu;
+        const int p0 = c * WG_CHUNK;
+        cu.g0 = p0 / a.Wo;
+        cu.w0 = p0 - cu.g0 * a.Wo;
+        return cu;
+    };
+    auto cur_next = [&](Cur& cu) {
+        cu.w0 += a.r64;
+        cu.g0 += a.q64;
+        if (cu.w0 >= a.Wo) {
+            cu.w0 -= a.Wo;
+            ++cu.g0;
+        }
+    };
+    auto issue = [&](int c, const Cur& cu, int buf) {
+        const int p0 = c * WG_CHUNK, g0 = cu.g0;
+        const uint32_t ybase = (uint32_t)p0 * ypixb;
         int n0, ho0;
         divmod_small(g0, a.Ho, a.inv_ho, n0, ho0);
         const uint32_t img = lds0 + buf * STG;
@@ -327,47 +362,50 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WArgs a) {
         for (int m = 0; m < MP; ++m) {
             if (m >= npieces) break;
             const int k = wave + WAVES * m;
-            if (k < PY) {                                        // dY rows: chunk pixel j = YPP k + ypr
-                const int j = YPP * k + ypr, p = p0 + j;
-                const uint32_t off =
-                    p < NHWo ? (uint32_t)p * ypixb + (uint32_t)(ob * YRB) + 16u * tswz(j, ypc) : OOB;
-                dma16(ry, img + k * 1024, off);
-            } else {
-                const int q = 4 * (k - PY) + xpr;
-                int dn, ho;
-                divmod_small(ho0 + qrk[m], a.Ho, a.inv_ho, dn, ho);
-                const int g = g0 + qrk[m], n = n0 + dn;
-                const int hi = S * ho - 1 + kh, wi = qcol[m] - 1;
-                const bool ok = q < a.npw && g < NHo && hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi;
-                const uint32_t pix = (uint32_t)(n * a.Hi + hi) * (uint32_t)a.Wi + (uint32_t)wi;
-                dma16(rx, img + YIMG + (k - PY) * 1024,
-                      ok ? pix * xpixb + (uint32_t)(ib * XROWB) + 16u * tswz(q, xpc) : OOB);
+            if (k < PY) {                                        // dY rows: chunk pixel pj
+                dma16(ry, img + k * 1024, p0 + pj[m] < NHWo ? ybase + poff[m] : OOB);
+            } else {                                             // input position of segment row pj at kernel row kh
+                int dn = 0, ho = ho0 + pj[m];
+                if (ho >= a.Ho) divmod_small(ho, a.Ho, a.inv_ho, dn, ho);
+                const int hi = S * ho - 1 + kh;
+                const bool ok = poff[m] != OOB && g0 + pj[m] < NHo && hi >= 0 && hi < a.Hi;
+                const uint32_t off = (uint32_t)((n0 + dn) * a.Hi + hi) * xrowb + poff[m];
+                dma16(rx, img + YIMG + (k - PY) * 1024, ok ? off : OOB);
             }
         }
     };
 
     const int kg = wave / BW, lw = wave % BW;
-    const int obw = lw >> 1, ibw = lw & 1;                       // this wave's (o, i) 32 x 32 block
-    floatx16 acc[3];
+    const int obw = lw >> 1, ibw = lw & 1;                       // this wave's 64 o (blocks 2 obw, 2 obw + 1) x 32 i
+    floatx16 acc[2][3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[k][e] = 0.f;
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[t][k][e] = 0.f;
 
     const int g = lane >> 4, li = lane & 15;
-    if (c_lo < c_hi) issue(c_lo, 0);
+    Cur ci_ = cur_at(c_lo), cc_ = ci_;                           // issue and compute cursors
+    if (c_lo < c_hi) {
+        issue(c_lo, ci_, 0);
+        cur_next(ci_);
+    }
     for (int c = c_lo; c < c_hi; ++c) {
         const int it = c - c_lo;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (c + 1 < c_hi) issue(c + 1, (it + 1) & 1);
+        if (c + 1 < c_hi) {
+            issue(c + 1, ci_, (it + 1) & 1);
+            cur_next(ci_);
+        }
         const uint8_t* yimg = lds + (it & 1) * STG;
         const uint8_t* ximg = yimg + YIMG;
-        const int p0 = c * WG_CHUNK, g0 = p0 / a.Wo, w0 = p0 - g0 * a.Wo;
+        const int w0 = cc_.w0;
 #pragma unroll
-        for (int s2 = 0; s2 < WG_CHUNK / 16 / KG; ++s2) {
-            const int s = kg * (WG_CHUNK / 16 / KG) + s2;
+        for (int s2 = 0; s2 < KS; ++s2) {
+            const int s = kg * KS + s2;
             int ry_[2], rx_[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -377,7 +415,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WArgs a) {
                 ry_[u] = j;
                 rx_[u] = dr * a.RS + S * wo;
             }
-            const half8 ah = tfrag<YRB>(yimg, ry_, obw, 0, lane), al = tfrag<YRB>(yimg, ry_, obw, 1, lane);
+            half8 ah[2], al[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                ah[t] = tfrag<YRB>(yimg, ry_, 2 * obw + t, 0, lane);
+                al[t] = tfrag<YRB>(yimg, ry_, 2 * obw + t, 1, lane);
+            }
             half8 bh[3], bl[3];
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw) {
@@ -385,28 +428,42 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(WArgs a) {
                 bh[kw] = tfrag<XROWB>(ximg, rk, ibw, 0, lane);
                 bl[kw] = tfrag<XROWB>(ximg, rk, ibw, 1, lane);
             }
+            // product-major over the 6 independent accumulators
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[kw], acc[kw], 0, 0, 0);
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[kw], acc[kw], 0, 0, 0);
+                for (int kw = 0; kw < 3; ++kw)
+                    acc[t][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], bh[kw], acc[t][kw], 0, 0, 0);
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[kw], acc[kw], 0, 0, 0);
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw)
+                    acc[t][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], bl[kw], acc[t][kw], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw)
+                    acc[t][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t], bh[kw], acc[t][kw], 0, 0, 0);
         }
+        cur_next(cc_);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    // partial tiles: acc[kw] register 4 q + e = row o = OB ob + 32 obw + 8 q + 4 (lane >> 5) + e, column
+    // partial tiles: acc[t][kw] register 4 q + e = row o = OB ob + 64 obw + 32 t + 8 q + 4 (lane >> 5) + e, column
     // i = 64 ib + 32 ibw + (lane & 31)
     const float sc = __builtin_ldexpf(1.f, -(split_exp(*a.xmax) + split_exp(*a.dymax)));
     float* pp = a.part + ((int64_t)(r * KG + kg) * 9 + kh * 3) * a.Co * a.Ci;
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int o = OB * ob + 32 * obw + 8 * q + 4 * (lane >> 5) + e, i = 64 * ib + 32 * ibw + (lane & 31);
-                pp[((int64_t)kw * a.Co + o) * a.Ci + i] = acc[kw][4 * q + e] * sc;
-            }
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int o = OB * ob + 64 * obw + 32 * t + 8 * q + 4 * (lane >> 5) + e;
+                    const int i = 64 * ib + 32 * ibw + (lane & 31);
+                    pp[((int64_t)kw * a.Co + o) * a.Ci + i] = acc[t][kw][4 * q + e] * sc;
+                }
 }
 
 // dW[o][i][kh][kw] = sum over ranges of part[range][kh][kw][o][i]: workgroup = 64 consecutive elements x 4 range
@@ -566,13 +623,18 @@ static int wg_setup(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, i
     a.ranges = wg_ranges(a.chunks, 3 * a.nob * a.nib);
     a.inv_ho = 1.f / (float)a.Ho;
     a.inv_wo = 1.f / (float)a.Wo;
+    a.q64 = WG_CHUNK / a.Wo;
+    a.r64 = WG_CHUNK % a.Wo;
     return AVSE_OK;
 }
+
+// k-step groups of the weight-gradient kernel (partial slabs per range): 8 / (OB / 32)
+static int wg_kg(int64_t co) { return co % 128 ? 4 : 2; }
 
 int64_t avse_sconv_wgrad_workspace_bytes(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride) {
     WArgs a;
     if (wg_setup(N, Hi, Wi, ci, co, stride, a) != AVSE_OK) return -1;
-    return (int64_t)a.ranges * (co % 128 ? 2 : 1) * 9 * co * ci * 4;      // KG partial slabs per range
+    return (int64_t)a.ranges * wg_kg(co) * 9 * co * ci * 4;               // KG partial slabs per range
 }
 
 int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride, const void* xq,
@@ -600,7 +662,7 @@ int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, 
     AVSE_CHECK_LAUNCH();
     const int64_t total = 9 * co * ci;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, a.part,
-                       a.ranges * (ob128 ? 1 : 2), (int)co, (int)ci, dw);
+                       a.ranges * wg_kg(co), (int)co, (int)ci, dw);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

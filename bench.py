@@ -83,8 +83,10 @@ def run_secondary(args):
     started after this process's measurement is complete; returns one record per config."""
     out = []
     for wl in [w for w in args.secondary.split(",") if w]:
+        # 2 warm-up steps: the in-step roofline taps the last one, past the first step's one-time work (MIOpen's
+        # first-call solver selection ran its naive fallback kernels there: 0.5 s per C4 / C5 step, r06i profiles)
         cmd = [sys.executable, os.path.abspath(__file__), "--workload", wl, "--steps", str(args.secondary_steps),
-               "--warmup", "1", "--secondary", "", "--no-cpu-baseline", "--no-roofline-hip"]
+               "--warmup", "2", "--secondary", "", "--no-cpu-baseline", "--no-roofline-hip"]
         t = time.perf_counter()
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
