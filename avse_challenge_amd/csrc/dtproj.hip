@@ -198,7 +198,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 
     const T* w = reinterpret_cast<const T*>(a.w);
     T* ob = reinterpret_cast<T*>(a.out) + (int64_t)b * a.o_bs;
-    const int tl = t0 + tc + 4 * (lane >> 5);                 // + 32 j + 8 g + e: this lane's steps
     const int kl = 8 * (lane >> 5);
     // channel tiles of 32 (one MFMA column block): 32 accumulators, the x fragments and the next tile's W in flight
     // fit ~100 VGPRs, i.e. 4+ waves per SIMD to cover the loads' and stores' latency
@@ -242,49 +241,77 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
             for (int s = 0; s < NKS; ++s) wload<T>(w, a.w_ds, a.D, a.R, d + CH, 16 * s + kl, a.wvec, wn[s]);
         }
-        const float bv = (a.bias && d < a.D) ? a.bias[d] : 0.f;
         floatx16 acc[2];                                      // [step block j]
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+        if constexpr (F32) {
+            // C^T = W x: the W fragment as the A operand (its rows are the channels), the x fragment as B (its columns
+            // are the steps), so a lane ends with ONE step of 16 channels and a store instruction writes whole 128-B
+            // rows: per register a wave instruction writes 32 consecutive steps of two channel rows.  Round 5's order
+            // (a lane = one channel, 4 steps; 32 rows x 32 B per instruction) ran the C3 call in 0.439 ms, this one in
+            // 0.327 (profiles/r06k_dtproj_ab.jsonl).  bf16 keeps that order: 2-B stores per lane would write 64-B
+            // half rows (0.243 vs 0.177 ms at C5).
 #pragma unroll
-        for (int s = 0; s < NKS; ++s)
+            for (int s = 0; s < NKS; ++s)
 #pragma unroll
-            for (int pr = 0; pr < (F32 ? 3 : 1); ++pr)
+                for (int pr = 0; pr < 3; ++pr)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    if constexpr (F32) {
-                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr == 2 ? xl[j][s] : xh[j][s],
-                                                                        pr == 1 ? wl[s] : wh[s], acc[j], 0, 0, 0);
-                    } else {
-                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, xh[j][s]),
-                                                                         __builtin_bit_cast(bf16x8, wh[s]), acc[j], 0, 0, 0);
-                    }
-                }
-        // epilogue: acc[j] register 4 g + e = step tl + 32 j + 8 g + e of channel d: four consecutive steps per lane
-        // -> one 16-B (fp32) / 8-B (bf16) store; a wave instruction writes 32 B into each of 32 channel rows
-        if (d >= a.D) continue;
-        T* orow = ob + (int64_t)d * a.o_ds;
+                    for (int j = 0; j < 2; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr == 1 ? wl[s] : wh[s],
+                                                                        pr == 2 ? xl[j][s] : xh[j][s], acc[j], 0, 0, 0);
+            // acc[j] register 4 g + e = channel d0 + 8 g + 4 (lane >> 5) + e at step ts + 32 j
+            const int ts = t0 + tc + (lane & 31);
+            float bv[4][4];
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int t = tl + 32 * j + 8 * g;
-                if (t >= a.L) continue;
-                float v[4];
+            for (int g = 0; g < 4; ++g)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    v[e] = acc[j][4 * g + e] * unscale + bv;
-                    if (a.softplus) v[e] = softplus2(v[e]);
+                    const int dd = d0 + 8 * g + 4 * (lane >> 5) + e;
+                    bv[g][e] = (a.bias && dd < a.D) ? a.bias[dd] : 0.f;
                 }
-                T* o = orow + t;
-                if constexpr (F32) {
-                    if (t + 3 < a.L && ((uintptr_t)o & 15) == 0) {
-                        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-                        continue;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int t = ts + 32 * j;
+                if (t >= a.L) continue;
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int dd = d0 + 8 * g + 4 * (lane >> 5) + e;
+                        if (dd >= a.D) continue;
+                        float v = acc[j][4 * g + e] * unscale + bv[g][e];
+                        if (a.softplus) v = softplus2(v);
+                        ob[(int64_t)dd * a.o_ds + t] = v;
                     }
-                } else {
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < NKS; ++s)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, xh[j][s]),
+                                                                     __builtin_bit_cast(bf16x8, wh[s]), acc[j], 0, 0, 0);
+            // acc[j] register 4 g + e = step tl + 32 j + 8 g + e of channel d: four consecutive steps per lane -> one
+            // 8-B store
+            if (d >= a.D) continue;
+            const float bvd = a.bias ? a.bias[d] : 0.f;
+            const int tl = t0 + tc + 4 * (lane >> 5);
+            T* orow = ob + (int64_t)d * a.o_ds;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int t = tl + 32 * j + 8 * g;
+                    if (t >= a.L) continue;
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[e] = acc[j][4 * g + e] * unscale + bvd;
+                        if (a.softplus) v[e] = softplus2(v[e]);
+                    }
+                    T* o = orow + t;
                     if (t + 3 < a.L && ((uintptr_t)o & 7) == 0) {
                         bf16_t h[4];
 #pragma unroll
@@ -293,11 +320,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                                                                   (uint32_t)h[2].x | ((uint32_t)h[3].x << 16));
                         continue;
                     }
-                }
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (t + e < a.L) io<T>::st(o + e, v[e]);
-            }
+                    for (int e = 0; e < 4; ++e)
+                        if (t + e < a.L) io<T>::st(o + e, v[e]);
+                }
+        }
     }
 }
 

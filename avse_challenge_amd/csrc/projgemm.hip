@@ -689,36 +689,65 @@ __global__ __launch_bounds__(256) void planes_split_pad_kernel(PlanesArgs a) {
 // y = a + b over the padded (rows, lp) storage of two (b, c, l) operands (one vectorised pass; the pad columns hold
 // don't-care values) and max |y| over the logical columns c < l: the C3 out_proj input with its producer-side max
 // (the BiMamba direction sum, bimamba.py:253), so the projection's split skips its absmax pass
+// MASK (padded rows): row-major walk, rows grid-strided over the workgroups and each row's float4 columns over the
+// threads (4 in flight per thread), so the logical-column test needs no division (round 5's flat index took a modulo
+// per float4: 0.98 ms per C3 call, 3.2 TB/s, r06j profile)
 template <bool MASK>
 __global__ __launch_bounds__(256) void add_max_kernel(int n4, int lp4, int l, const float4* __restrict__ a,
                                                       const float4* __restrict__ b, float4* __restrict__ y,
                                                       uint32_t* __restrict__ maxbits) {
     __shared__ uint32_t red[4];
     float m = 0.f;
-    const int stride = gridDim.x * 256;
-    for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += 4 * stride) {    // 4 float4 pairs in flight
-        float4 u[4], v[4];
+    if constexpr (MASK) {
+        const int rows = n4 / lp4, lfull = l / 4;                 // float4 columns wholly inside the logical row
+        for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+            const int64_t base = (int64_t)row * lp4;
+            for (int c0 = threadIdx.x; c0 < lp4; c0 += 4 * 256) {
+                float4 u[4], v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = i0 + k * stride;
-            if (i < n4) {
-                u[k] = a[i];
-                v[k] = b[i];
+                for (int k = 0; k < 4; ++k) {
+                    const int c = c0 + k * 256;
+                    if (c < lp4) {
+                        u[k] = a[base + c];
+                        v[k] = b[base + c];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int c = c0 + k * 256;
+                    if (c >= lp4) break;
+                    const float4 s = make_float4(u[k].x + v[k].x, u[k].y + v[k].y, u[k].z + v[k].z, u[k].w + v[k].w);
+                    y[base + c] = s;
+                    if (c < lfull) {
+                        m = fmaxf(m, fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fmaxf(fabsf(s.z), fabsf(s.w))));
+                    } else {
+                        const int e = 4 * c;
+                        m = fmaxf(m, e < l ? fabsf(s.x) : 0.f);
+                        m = fmaxf(m, e + 1 < l ? fabsf(s.y) : 0.f);
+                        m = fmaxf(m, e + 2 < l ? fabsf(s.z) : 0.f);
+                        m = fmaxf(m, e + 3 < l ? fabsf(s.w) : 0.f);
+                    }
+                }
             }
         }
+    } else {
+        const int stride = gridDim.x * 256;
+        for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += 4 * stride) {    // 4 float4 pairs in flight
+            float4 u[4], v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = i0 + k * stride;
-            if (i >= n4) break;
-            const float4 s = make_float4(u[k].x + v[k].x, u[k].y + v[k].y, u[k].z + v[k].z, u[k].w + v[k].w);
-            y[i] = s;
-            if constexpr (MASK) {
-                const int c = 4 * (i % lp4);
-                m = fmaxf(m, c < l ? fabsf(s.x) : 0.f);
-                m = fmaxf(m, c + 1 < l ? fabsf(s.y) : 0.f);
-                m = fmaxf(m, c + 2 < l ? fabsf(s.z) : 0.f);
-                m = fmaxf(m, c + 3 < l ? fabsf(s.w) : 0.f);
-            } else {
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + k * stride;
+                if (i < n4) {
+                    u[k] = a[i];
+                    v[k] = b[i];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + k * stride;
+                if (i >= n4) break;
+                const float4 s = make_float4(u[k].x + v[k].x, u[k].y + v[k].y, u[k].z + v[k].z, u[k].w + v[k].w);
+                y[i] = s;
                 m = fmaxf(m, fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fmaxf(fabsf(s.z), fabsf(s.w))));
             }
         }
@@ -917,7 +946,30 @@ static int split16_planes_impl(int64_t b, int64_t r, int64_t c, const float* x, 
         if (pblocks >= (1LL << 31)) return AVSE_ESHAPE;
         hipLaunchKernelGGL(planes_split_pad_kernel, dim3((unsigned)pblocks), dim3(256), 0, st, p2);
     } else if (xvec && hvec) {
-        hipLaunchKernelGGL(planes_split_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+        const int64_t n = b * r * c;
+        const bool flat = x_rs == c && h_rs == c && (b == 1 || (x_bs == r * c && h_bs == r * c));
+        if (flat && c < 1024 && n >= 4096) {
+            // contiguous rows shorter than the workgroup's 1024-float4 pass (the (b, l, d_model = 512) projection
+            // operands): the flat array as 4096-element rows, every thread busy (512-element rows left half of the
+            // threads idle, one row at a time), the tail as one more row
+            PlanesArgs f = a;
+            f.rows = f.r = n / 4096;
+            f.c = f.rs = f.hrs = 4096;
+            f.bs = f.hbs = 0;
+            f.rpb = 1;
+            hipLaunchKernelGGL(planes_split_kernel<true>, dim3((unsigned)f.rows), dim3(256), 0, st, f);
+            if (n % 4096) {
+                AVSE_CHECK_LAUNCH();
+                f.x = x + f.rows * 4096;
+                f.hi = a.hi + f.rows * 4096;
+                f.lo = a.lo + f.rows * 4096;
+                f.rows = f.r = 1;
+                f.c = f.rs = f.hrs = n % 4096;
+                hipLaunchKernelGGL(planes_split_kernel<true>, dim3(1), dim3(256), 0, st, f);
+            }
+        } else {
+            hipLaunchKernelGGL(planes_split_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+        }
     } else {
         hipLaunchKernelGGL(planes_split_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
     }
@@ -933,7 +985,9 @@ int avse_add_max(int64_t rows, int64_t lp, int64_t l, const float* a, const floa
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(maxbits, 0, 4, st) != hipSuccess) return AVSE_ELAUNCH;
     const int n4 = (int)(rows * lp / 4);
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 1023) / 1024, 4 * cu_count_cached()));
+    const unsigned grid = lp == l
+        ? (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 1023) / 1024, 4 * cu_count_cached()))
+        : (unsigned)std::max<int64_t>(1, std::min<int64_t>(rows, 8 * cu_count_cached()));
     if (lp == l)
         hipLaunchKernelGGL(add_max_kernel<false>, dim3(grid), dim3(256), 0, st, n4, (int)(lp / 4), (int)l,
                            reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(b),

@@ -117,10 +117,13 @@ __global__ __launch_bounds__(512, 1) void fwd_kernel(FArgs a) {
     const int npieces = (PT - wave + WAVES - 1) / WAVES;
     const uint32_t pixb = (uint32_t)a.Ci * 4u;
 
-    // this wave's DMA pieces: X pieces (position r = 16 k + lane / 4) carry (n Hi, s ho - 1, input column or -1) and
-    // the lane's source chunk; W pieces the lane's byte offset inside a stage's weight rows
-    int pnh[MP], ph[MP], pcol[MP];
-    uint32_t pchunk[MP];
+    // this wave's DMA pieces, everything that does not depend on the stage precomputed: X pieces (position r = 16 k +
+    // lane / 4) the byte offset of their input pixel at kernel row 0 plus the lane's source chunk (or OOB for padding
+    // columns / rows past the tile) and the valid kernel rows [khlo, khhi); W pieces the lane's byte offset inside a
+    // stage's weight rows.  Per stage a piece then costs an add and a compare (round 5 recomputed the pixel with two
+    // 32-bit multiplies per piece and stage)
+    uint32_t pbase[MP];
+    int khlo[MP], khhi[MP];
 #pragma unroll
     for (int m = 0; m < MP; ++m) {
         const int k = wave + WAVES * m;
@@ -129,34 +132,31 @@ __global__ __launch_bounds__(512, 1) void fwd_kernel(FArgs a) {
             const int rk = r / a.RS, col = r - rk * a.RS, g = g0 + rk;
             const int n = g / a.Ho, ho = g - n * a.Ho, wi = col - 1;
             const bool ok = g < NHo && wi >= 0 && wi < a.Wi;
-            pnh[m] = n * a.Hi;
-            ph[m] = S * ho - 1;
-            pcol[m] = ok ? wi : -1;
-            pchunk[m] = 16u * c;
+            const int h0 = S * ho - 1;                                  // input row at kernel row 0
+            khlo[m] = ok ? max(0, -h0) : 3;
+            khhi[m] = ok ? min(3, a.Hi - h0) : 0;
+            pbase[m] = ok ? ((uint32_t)(n * a.Hi + h0) * (uint32_t)a.Wi + (uint32_t)wi) * pixb + 16u * c : 0u;
         } else {
             const int r = 16 * (k - PX) + (lane >> 2), c = (lane & 3) ^ swz(r);    // W row r = kw TN + ol
             const int kw = r / TN, ol = r - kw * TN;
-            pnh[m] = 0;
-            ph[m] = 0;
-            pcol[m] = kw * a.Co + o0 + ol;                                           // row within the stage's block
-            pchunk[m] = 16u * c;
+            khlo[m] = khhi[m] = 0;
+            pbase[m] = (uint32_t)(kw * a.Co + o0 + ol) * 64u + 16u * c;             // row within the stage's block
         }
     }
+    const uint32_t rowb = (uint32_t)a.Wi * pixb, wstage = 3u * (uint32_t)a.Co * 64u;
     auto issue = [&](int s) {
         const int kh = s / NQ, q = s - kh * NQ;
         const uint32_t img = lds0 + (s & 1) * STG;
+        const uint32_t xadd = (uint32_t)kh * rowb + (uint32_t)(q * 64), wadd = (uint32_t)s * wstage;
 #pragma unroll
         for (int m = 0; m < MP; ++m) {
             if (m >= npieces) break;
             const int k = wave + WAVES * m;
             if (k < PX) {
-                const int hi = ph[m] + kh;
-                const bool ok = pcol[m] >= 0 && hi >= 0 && hi < a.Hi;
-                const uint32_t pix = (uint32_t)(pnh[m] + hi) * (uint32_t)a.Wi + (uint32_t)pcol[m];
-                dma16(rx, img + k * 1024, ok ? pix * pixb + (uint32_t)(q * 64) + pchunk[m] : OOB);
+                const bool ok = kh >= khlo[m] && kh < khhi[m];
+                dma16(rx, img + k * 1024, ok ? pbase[m] + xadd : OOB);
             } else {
-                const uint32_t row = (uint32_t)(kh * NQ + q) * 3u * (uint32_t)a.Co + (uint32_t)pcol[m];
-                dma16(rw, img + XIMG + (k - PX) * 1024, row * 64u + pchunk[m]);
+                dma16(rw, img + XIMG + (k - PX) * 1024, pbase[m] + wadd);
             }
         }
     };
