@@ -32,6 +32,7 @@ class ScanFwdArgs(ctypes.Structure):
         ("out", c_vp), ("out_bs", c_i64), ("out_ds", c_i64),
         ("x", c_vp),
         ("out_z", c_vp), ("out_z_bs", c_i64), ("out_z_ds", c_i64),
+        ("out_z_accumulate", c_i32),
     ]
 
 
@@ -59,6 +60,7 @@ class ScanBwdArgs(ctypes.Structure):
         ("dz", c_vp), ("dz_bs", c_i64), ("dz_ds", c_i64),
         ("out_z", c_vp), ("out_z_bs", c_i64), ("out_z_ds", c_i64),
         ("workspace", c_vp),
+        ("dz_accumulate", c_i32),
     ]
 
 
@@ -101,9 +103,9 @@ SIGNATURES = {
     "avse_cconv_fwd_bf16": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                                     c_i32, c_i32, c_vp]),
     "avse_cconv_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
-                               c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+                               c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp]),
     "avse_cconv_bwd_bf16": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
-                                    c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+                                    c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp]),
     "avse_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_rmsnorm_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -114,6 +116,7 @@ SIGNATURES = {
     "avse_conv3d_wgrad": (c_i32, [c_i64] * 11 + [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "avse_conv3d_wgrad_u8": (c_i32, [c_i64] * 11 + [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "avse_conv3d_wgrad_u8_split": (c_i32, [c_i64] * 11 + [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
+    "avse_conv3d_wgrad_split": (c_i32, [c_i64] * 11 + [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "avse_conv3d_fwd_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "avse_conv3d_fwd": (c_i32, [c_i64] * 5 + [c_i32] + [c_vp] * 5),
     "avse_dconv_wgrad_workspace_bytes": (c_i64, [c_i64] * 4),
@@ -190,6 +193,9 @@ class HipLibraryError(RuntimeError):
     pass
 
 
+ABI_VERSION = 2          # include/avse_hip.h avse_abi_version (2, round 6: the scan out_z / dz and cconv dx accumulate)
+
+
 def lib():
     """The loaded library; raises HipLibraryError (never falls back) when it is unavailable."""
     global _lib
@@ -206,6 +212,9 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.avse_abi_version() != ABI_VERSION:        # the argument structs above are this version's layout
+            raise HipLibraryError(f"{LIB_PATH} has C-ABI version {L.avse_abi_version()}, the bindings expect "
+                                  f"{ABI_VERSION}: rebuild it (make -C avse_challenge_amd/csrc)")
         _lib = L
     return _lib
 

@@ -3,7 +3,7 @@
 
 extern "C" {
 
-int avse_abi_version(void) { return 1; }
+int avse_abi_version(void) { return 2; }   // 2 (round 6): out_z / dz / dx accumulate
 
 const char* avse_strerror(int code) {
     switch (code) {

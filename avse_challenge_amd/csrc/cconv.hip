@@ -62,7 +62,8 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __r
                                                       int64_t x_ds, const float* __restrict__ w,
                                                       const float* __restrict__ bias, const T* __restrict__ dout,
                                                       int64_t g_bs, int64_t g_ds, T* __restrict__ dx,
-                                                      int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws, int rev) {
+                                                      int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws, int rev,
+                                                      int dx_acc) {
     __shared__ float sx[TILE + 2 * MAXW];
     __shared__ float sg[TILE + MAXW];
     __shared__ float sred[THREADS / 64][MAXW + 1];
@@ -111,7 +112,8 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __r
                 float acc = 0.f;
 #pragma unroll
                 for (int k = 0; k < W; ++k) acc += wk[k] * sg[i + (W - 1) - k];
-                io<T>::st(&dxr[rev ? L - 1 - t : t], acc);
+                T* q = &dxr[rev ? L - 1 - t : t];
+                io<T>::st(q, dx_acc ? acc + io<T>::ld(q) : acc);
                 const float g = sg[i];
                 db += g;
 #pragma unroll
@@ -240,7 +242,8 @@ __global__ __launch_bounds__(THREADS) void bwd_vec_kernel(int D, int L, const T*
                                                           int64_t x_ds, const float* __restrict__ w,
                                                           const float* __restrict__ bias, const T* __restrict__ dout,
                                                           int64_t g_bs, int64_t g_ds, T* __restrict__ dx,
-                                                          int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws) {
+                                                          int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws,
+                                                          int dx_acc) {
     __shared__ float sred[THREADS / 64][MAXW + 1];
     const int row = blockIdx.x;
     const int b = row / D, d = row % D;
@@ -294,6 +297,12 @@ __global__ __launch_bounds__(THREADS) void bwd_vec_kernel(int D, int L, const T*
 #pragma unroll
                 for (int k = 0; k < W; ++k) dw[k] = fmaf(g[4 + j], xs[4 + j + (W - 1) - k], dw[k]);
             }
+        }
+        if (dx_acc) {                             // the other BiMamba direction's dx, summed in place (round 6)
+            float p[4];
+            ld4z<T>(dxr, t, L, p);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] += p[j];
         }
         st4<T>(dxr, t, L, o);
     }
@@ -357,7 +366,7 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
                                                             const float* __restrict__ bias,
                                                             const T* __restrict__ dout, int64_t g_bs, int64_t g_ds,
                                                             T* __restrict__ dx, int64_t dx_bs, int64_t dx_ds,
-                                                            float* __restrict__ ws, int rev) {
+                                                            float* __restrict__ ws, int rev, int dx_acc) {
     __shared__ float sx[4][SPAD];
     __shared__ float sg[4][SPAD];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -404,7 +413,8 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
         float acc = 0.f;
 #pragma unroll
         for (int k = 0; k < W; ++k) acc += wk[k] * pg[t + (W - 1) - k];
-        io<T>::st(&dxr[rev ? L - 1 - t : t], acc);
+        T* q = &dxr[rev ? L - 1 - t : t];
+        io<T>::st(q, dx_acc ? acc + io<T>::ld(q) : acc);
         const float g = pg[t];
         db += g;
 #pragma unroll
@@ -486,23 +496,25 @@ void launch_fwd(int64_t batch, int64_t dim, int64_t seqlen, const T* x, int64_t 
 template <typename T, int W, bool S, bool HB>
 void launch_bwd(int64_t batch, int64_t dim, int64_t seqlen, const T* x, int64_t x_bs, int64_t x_ds, const float* w,
                 const float* bias, const T* dout, int64_t g_bs, int64_t g_ds, T* dx, int64_t dx_bs, int64_t dx_ds,
-                float* ws, int rev, hipStream_t st) {
+                float* ws, int rev, int dx_acc, hipStream_t st) {
     const int rows = (int)(batch * dim);
     if (seqlen <= SHORT_L)
         hipLaunchKernelGGL((bwd_short_kernel<T, W, S, HB>), dim3((unsigned)((rows + 3) / 4)), dim3(THREADS), 0, st,
                            rows, (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws,
-                           rev);
+                           rev, dx_acc);
     else if (vec_rows<T>(x, x_bs, x_ds, seqlen, true) && vec_rows<T>(dout, g_bs, g_ds, seqlen, true) &&
              vec_rows<T>(dx, dx_bs, dx_ds, seqlen, false)) {
         if (rev)
             hipLaunchKernelGGL((bwd_vec_kernel<T, W, S, HB, true>), dim3((unsigned)rows), dim3(THREADS), 0, st,
-                               (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws);
+                               (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws,
+                               dx_acc);
         else
             hipLaunchKernelGGL((bwd_vec_kernel<T, W, S, HB, false>), dim3((unsigned)rows), dim3(THREADS), 0, st,
-                               (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws);
+                               (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws,
+                               dx_acc);
     } else
         hipLaunchKernelGGL((bwd_kernel<T, W, S, HB>), dim3((unsigned)rows), dim3(THREADS), 0, st, (int)dim,
-                           (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws, rev);
+                           (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws, rev, dx_acc);
 }
 
 // width / silu / bias -> template instance
@@ -552,14 +564,15 @@ template <typename T>
 int cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const T* x, int64_t x_bs, int64_t x_ds,
               const float* weight, const float* bias, const T* dout, int64_t dout_bs, int64_t dout_ds, T* dx,
               int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias, int32_t silu, int32_t reverse,
-              float* workspace, avse_stream_t stream) {
+              float* workspace, int32_t dx_accumulate, avse_stream_t stream) {
     if (!x || !weight || !dout || !dx || !dweight || !workspace) return AVSE_EINVAL;
     if (bias && !dbias) return AVSE_EINVAL;
     if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
     if (batch * dim > (1LL << 31) - 1) return AVSE_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
     const int rc = dispatch<Bwd, T>(width, silu != 0, bias != nullptr, batch, dim, seqlen, x, x_bs, x_ds, weight, bias,
-                                    dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse, st);
+                                    dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse,
+                                    (int)(dx_accumulate != 0), st);
     if (rc != AVSE_OK) return rc;
     AVSE_CHECK_LAUNCH();
     hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)dim), dim3(THREADS), 0, st, workspace, (int)batch, (int)dim,
@@ -587,9 +600,9 @@ int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, co
 int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const float* x, int64_t x_bs,
                    int64_t x_ds, const float* weight, const float* bias, const float* dout, int64_t dout_bs,
                    int64_t dout_ds, float* dx, int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias,
-                   int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream) {
+                   int32_t silu, int32_t reverse, float* workspace, int32_t dx_accumulate, avse_stream_t stream) {
     return cconv_bwd<float>(batch, dim, seqlen, width, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs,
-                            dx_ds, dweight, dbias, silu, reverse, workspace, stream);
+                            dx_ds, dweight, dbias, silu, reverse, workspace, dx_accumulate, stream);
 }
 
 int avse_cconv_fwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const uint16_t* x, int64_t x_bs,
@@ -602,10 +615,11 @@ int avse_cconv_fwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t widt
 int avse_cconv_bwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const uint16_t* x, int64_t x_bs,
                         int64_t x_ds, const float* weight, const float* bias, const uint16_t* dout, int64_t dout_bs,
                         int64_t dout_ds, uint16_t* dx, int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias,
-                        int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream) {
+                        int32_t silu, int32_t reverse, float* workspace, int32_t dx_accumulate,
+                        avse_stream_t stream) {
     return cconv_bwd<bf16_t>(batch, dim, seqlen, width, (const bf16_t*)x, x_bs, x_ds, weight, bias,
                              (const bf16_t*)dout, dout_bs, dout_ds, (bf16_t*)dx, dx_bs, dx_ds, dweight, dbias, silu,
-                             reverse, workspace, stream);
+                             reverse, workspace, dx_accumulate, stream);
 }
 
 }  // extern "C"

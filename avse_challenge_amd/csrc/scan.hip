@@ -298,6 +298,9 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
         }
         RowRegs<Tin> rz;       // this chunk's z for the gate, issued before the barrier wait (issuing it with the
         if (HAS_Z) rz.load(z, a.z_bs, a.z_ds, b, d0, D, t0, tn, L, rev);   // prefetch measured the same, round 3)
+        RowRegs<Tin> racc;     // out_z_accumulate: the other direction's gated output, added at the flush
+        if (HAS_Z && a.out_z_accumulate)
+            racc.load((const Tin*)a.out_z, a.out_z_bs, a.out_z_ds, b, d0, D, t0, tn, L, rev);
         __syncthreads();
         // flush chunk k outputs (lane = time column, rows wave + 4i): buffer stores, row step in soffset
         {
@@ -320,6 +323,10 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                 const int vz = wave * (int)a.out_z_ds + tpos(t0 + lane, L, rev);
 #pragma unroll
                 for (int i = 0; i < RPT; ++i) outv[i] *= siluf_(rz.at(i));   // 16 independent gates (ILP)
+                if (a.out_z_accumulate) {
+#pragma unroll
+                    for (int i = 0; i < RPT; ++i) outv[i] += racc.at(i);
+                }
                 if (lane < tn) {
 #pragma unroll
                     for (int i = 0; i < RPT; ++i) bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds, outv[i]);
@@ -655,6 +662,9 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                 }
             }
         }
+        RowRegs<Tin> rdz;      // dz_accumulate: the other direction's dz, loaded across the barrier (its latency was
+        if (HAS_Z && a.dz_accumulate)   // exposed per chunk when loaded at the store: +0.35 ms per C5 launch)
+            rdz.load((const Tin*)a.dz, a.dz_bs, a.dz_ds, b, d0, D, t0, tn, L, rev);
         __syncthreads();
         // write du, ddelta, dz (+ out_z) tiles (lane = time column): buffer stores, row step in soffset
         {
@@ -681,6 +691,10 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                 float dzv[RPT];
 #pragma unroll
                 for (int i = 0; i < RPT; ++i) dzv[i] = s_zg[(wave + 4 * i) * Z_STRIDE + 2 * lane];
+                if (a.dz_accumulate) {             // the other BiMamba direction's dz, summed in place (round 6)
+#pragma unroll
+                    for (int i = 0; i < RPT; ++i) dzv[i] += rdz.at(i);
+                }
                 if (lane < tn) {
 #pragma unroll
                     for (int i = 0; i < RPT; ++i) bufst<Tin>::st(r_dz, v_dz, 4 * i * (int)a.dz_ds, dzv[i]);

@@ -14,7 +14,9 @@ NSTATE = 16
 
 # Launch timing taps (bench.py's in-step roofline): while ``LAUNCH_TAPS`` maps a C entry point's name to a list, each
 # eager launch of that entry point appends a (start, end) pair of HIP timing events recorded on its launch stream.
+# Entry points whose work differs per launch (the split GEMM's shapes) append it to ``LAUNCH_WORK[name]`` beside the pair.
 LAUNCH_TAPS = {}
+LAUNCH_WORK = {}
 
 
 def _tap_begin(name, device):
@@ -23,16 +25,18 @@ def _tap_begin(name, device):
         return None
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(torch.cuda.current_stream(device))
-    return taps, e0, e1, device
+    return taps, e0, e1, device, name
 
 
-def _tap_end(tap):
+def _tap_end(tap, work=None):
     """Called after the launch returned AVSE_OK: only then is the pair appended (a failed launch leaves no
-    half-recorded pair behind for bench.roofline's elapsed_time)."""
+    half-recorded pair behind for bench.roofline's elapsed_time).  work: the launch's algorithmic FLOPs or bytes."""
     if tap is not None:
-        taps, e0, e1, device = tap
+        taps, e0, e1, device, name = tap
         e1.record(torch.cuda.current_stream(device))
         taps.append((e0, e1))
+        if work is not None:
+            LAUNCH_WORK.setdefault(name, []).append(float(work))
 
 
 def _need_gpu(*ts):
@@ -127,11 +131,13 @@ def dtproj(w, x, bias=None, softplus=True):
 
 
 def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False, reverse=False,
-                       return_out=True):
+                       return_out=True, out_z_acc=None):
     """Returns (out, x, out_z|None) — the selective_scan_cuda.fwd contract.
     reverse=True scans time backwards (== flip(scan(flip(inputs))) with no flip copies).
     return_out=False (only with z): skip writing the pre-gate ``out`` (returned as None); the
-    backward recomputes it, so training saves one (b, d, l) write and its activation memory."""
+    backward recomputes it, so training saves one (b, d, l) write and its activation memory.
+    out_z_acc (with z): a (b, d, l) tensor of u's dtype, time-contiguous, that the gated output is ADDED to in place
+    (the BiMamba v2 direction sum, round 6); returned as out_z."""
     _need_gpu(u, delta, A, B, C, D, z, delta_bias)
     u = _last_contig(u)
     dt = u.dtype
@@ -151,6 +157,12 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
     out = _bdl_empty(b, d, l, dt, u.device) if return_out else None
     x = torch.empty((b, d, nck, 2 * NSTATE), device=u.device, dtype=torch.float32)
     out_z = _bdl_empty(b, d, l, dt, u.device) if z is not None else None
+    if out_z_acc is not None:
+        if z is None or tuple(out_z_acc.shape) != (b, d, l) or out_z_acc.dtype != dt or out_z_acc.stride(2) != 1 \
+                or out_z_acc.device != u.device:
+            raise RuntimeError("selective_scan_fwd: out_z_acc must be a time-contiguous (b, d, l) tensor of u's dtype "
+                               "(and z given)")
+        out_z = out_z_acc
     a = ScanFwdArgs()
     a.batch, a.dim, a.seqlen, a.dstate = b, d, l, NSTATE
     a.in_dtype, a.delta_softplus, a.reverse = _dtype_code(dt), _sp_mode(delta_softplus, delta_bias), int(bool(reverse))
@@ -163,6 +175,7 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
     if z is not None:
         a.z, a.z_bs, a.z_ds = z.data_ptr(), z.stride(0), z.stride(1)
         a.out_z, a.out_z_bs, a.out_z_ds = out_z.data_ptr(), out_z.stride(0), out_z.stride(1)
+        a.out_z_accumulate = int(out_z_acc is not None)
     a.delta_bias = delta_bias.data_ptr() if delta_bias is not None else None
     if out is not None:
         a.out, a.out_bs, a.out_ds = out.data_ptr(), out.stride(0), out.stride(1)
@@ -174,11 +187,15 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
 
 
 def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, dz=None,
-                       delta_softplus=False, recompute_out_z=False, reverse=False, dB_out=None, dC_out=None):
+                       delta_softplus=False, recompute_out_z=False, reverse=False, dB_out=None, dC_out=None,
+                       dz_accumulate=False):
     """Returns [du, ddelta, dA, dB, dC, dD, ddelta_bias, dz, out_z] — selective_scan_cuda.bwd contract.
     dB, dC are fp32 shaped (b, 1, n, l); a passed-in ``dz`` view is written in place, and so are
     ``dB_out`` / ``dC_out`` (fp32 (b, n, l) or (b, 1, n, l) views with unit last stride, e.g. rows of
-    the x_proj output gradient), which are then returned as dB / dC."""
+    the x_proj output gradient), which are then returned as dB / dC.  dz_accumulate (round 6, with a passed
+    ``dz``): dz += the gradient instead of dz = (the serial BiMamba directions' shared xz gradient)."""
+    if dz_accumulate and dz is None:
+        raise RuntimeError("selective_scan_bwd: dz_accumulate needs the dz to add into")
     _need_gpu(u, delta, A, B, C, D, z, delta_bias, dout, x)
     u = _last_contig(u)
     dt = u.dtype
@@ -234,6 +251,7 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
         a.dz, a.dz_bs, a.dz_ds = dz.data_ptr(), dz.stride(0), dz.stride(1)
     if out_z is not None:
         a.out_z, a.out_z_bs, a.out_z_ds = out_z.data_ptr(), out_z.stride(0), out_z.stride(1)
+    a.dz_accumulate = int(bool(dz_accumulate) and dz is not None)
     a.delta_bias = delta_bias.data_ptr() if delta_bias is not None else None
     a.dout, a.dout_bs, a.dout_ds = dout.data_ptr(), dout.stride(0), dout.stride(1)
     a.x = x.data_ptr()
@@ -272,9 +290,10 @@ def causal_conv1d_fwd(x, weight, bias=None, silu=False, reverse=False):
     return out
 
 
-def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False):
+def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False, dx_accumulate=False):
     """[dx, dweight, dbias]: dx in x's dtype (fp32 or bf16; a passed ``dx`` view of that dtype with unit last
-    stride is written in place), dweight / dbias fp32."""
+    stride is written in place), dweight / dbias fp32.  dx_accumulate (round 6, with such a ``dx``): dx += the input
+    gradient (the serial BiMamba directions' shared xz gradient)."""
     _need_gpu(x, weight, bias, dout)
     dt = x.dtype
     _dtype_code(dt)
@@ -286,6 +305,8 @@ def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False)
     b, d, l = x.shape
     w = weight.shape[1]
     dx_ret = dx
+    if dx_accumulate and (dx is None or dx.dtype != dt or dx.stride(-1) != 1):
+        raise RuntimeError("causal_conv1d_bwd: dx_accumulate needs a dx of x's dtype with unit last stride")
     if dx is None or dx.dtype != dt or dx.stride(-1) != 1:
         dx = _bdl_empty(b, d, l, dt, x.device)
     dweight = torch.empty((d, w), device=x.device, dtype=torch.float32)
@@ -295,7 +316,7 @@ def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False)
     fn = _lib.lib().avse_cconv_bwd if dt == torch.float32 else _lib.lib().avse_cconv_bwd_bf16
     check(fn(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(dout), dout.stride(0),
              dout.stride(1), ptr(dx), dx.stride(0), dx.stride(1), ptr(dweight), ptr(dbias), int(bool(silu)),
-             int(bool(reverse)), ptr(ws), stream_ptr(x.device)), "avse_cconv_bwd")
+             int(bool(reverse)), ptr(ws), int(bool(dx_accumulate)), stream_ptr(x.device)), "avse_cconv_bwd")
     if dx_ret is not None and dx_ret is not dx:
         dx_ret.copy_(dx)
         dx = dx_ret
@@ -381,21 +402,29 @@ def istft(mag, phase_spec, length):
 # ------------------------------------------------------------------------ lip front-end Conv3d dW
 
 CONV3D_WGRAD_MAX_WO = 64      # output width the MFMA kernel stages per LDS row (conv3d_wgrad.hip MAX_WO)
-# uint8 frames: the f16 MFMA weight gradient with dy split (avse_conv3d_wgrad_u8_split); False (a test's comparison):
-# the exact-fp32 kernel
+# the f16 MFMA weight gradient with dy split (uint8 frames: avse_conv3d_wgrad_u8_split; fp32 frames split too:
+# avse_conv3d_wgrad_split); False (a test's comparison): the exact-fp32 kernel
 C3W_F16 = True
 
 
-def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
+def _absmax_bits(t):
+    """max |t| as float bits in a 1-element int32 device tensor (the split kernels' scale input)."""
+    return t.abs().amax().float().reshape(1).view(torch.int32)
+
+
+def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False, xmax=None):
     """dW of Conv3d(Cin, 64, kernel_size, stride (1,2,2), padding, bias=False) -> (64, Cin, KT, KH, KW).
-    x: fp32, or the uint8 lip frames as stored (read as their float values, no fp32 copy)."""
+    x: fp32, or the uint8 lip frames as stored (read as their float values, no fp32 copy).  xmax (fp32 x, optional):
+    max |x| bits as conv3d_fwd(..., return_xmax=True) returned them; computed here when not given."""
     _need_gpu(x, dy)
     u8 = x.dtype == torch.uint8
     x = x.contiguous() if u8 else x.float().contiguous()
-    dymax = _known_absmax(dy) if u8 and C3W_F16 else None     # the BatchNorm -> act backward's max |dy|
+    dymax = _known_absmax(dy) if C3W_F16 else None            # the BatchNorm -> act backward's max |dy|
     dy = dy.float().contiguous()
-    if u8 and C3W_F16 and dymax is None:
-        dymax = dy.abs().amax().reshape(1).view(torch.int32)
+    if C3W_F16 and dymax is None:
+        dymax = _absmax_bits(dy)
+    if C3W_F16 and not u8 and xmax is None:
+        xmax = _absmax_bits(x)
     Bn, Cin, Tn, H, W = x.shape
     KT, KH, KW = kernel_size
     PT, PH, PW = padding
@@ -408,10 +437,15 @@ def conv3d_wgrad(x, dy, kernel_size, padding, out=None, accumulate=False):
     L = _lib.lib()
     ws = torch.empty((L.avse_conv3d_wgrad_workspace_bytes(Bn, dy.shape[2], dy.shape[3], N) + 3) // 4,
                      device=x.device, dtype=torch.float32)
-    if dymax is not None:              # uint8 frames on the f16 MFMA, dy split under its max
+    if C3W_F16 and u8:                 # uint8 frames on the f16 MFMA, dy split under its max
         check(L.avse_conv3d_wgrad_u8_split(Bn, Cin, Tn, H, W, KT, KH, KW, PT, PH, PW, ptr(x), ptr(dy), ptr(dymax),
                                            ptr(out), int(bool(accumulate)), ptr(ws), stream_ptr(x.device)),
               "avse_conv3d_wgrad_u8_split")
+        return out
+    if C3W_F16:                        # fp32 frames: x and dy split under their maxima
+        check(L.avse_conv3d_wgrad_split(Bn, Cin, Tn, H, W, KT, KH, KW, PT, PH, PW, ptr(x), ptr(xmax), ptr(dy),
+                                        ptr(dymax), ptr(out), int(bool(accumulate)), ptr(ws), stream_ptr(x.device)),
+              "avse_conv3d_wgrad_split")
         return out
     fn = L.avse_conv3d_wgrad_u8 if u8 else L.avse_conv3d_wgrad
     check(fn(Bn, Cin, Tn, H, W, KT, KH, KW, PT, PH, PW, ptr(x), ptr(dy), ptr(out),
@@ -428,9 +462,11 @@ def conv3d_fwd_supported(x, w, stride, padding):
             and _lib.lib().avse_conv3d_fwd_workspace_bytes(x.shape[1], x.shape[3], x.shape[4]) > 0)
 
 
-def conv3d_fwd(x, w):
+def conv3d_fwd(x, w, return_xmax=False):
     """Conv3d(Cin, 64, (5, 7, 7), stride (1, 2, 2), padding (2, 3, 3), bias=False) forward of the lip front-end:
-    x (B, Cin, T, H, W) uint8 frames or fp32, w (64, Cin, 5, 7, 7) fp32 -> (B, 64, T, Ho, Wo) fp32."""
+    x (B, Cin, T, H, W) uint8 frames or fp32, w (64, Cin, 5, 7, 7) fp32 -> (B, 64, T, Ho, Wo) fp32.
+    return_xmax (fp32 x): also return max |x| bits (1-element int32, from the forward's absmax pass) for
+    conv3d_wgrad."""
     _need_gpu(x, w)
     if x.dtype not in (torch.uint8, torch.float32):
         raise RuntimeError(f"conv3d_fwd: x must be uint8 or float32, got {x.dtype}")
@@ -447,7 +483,11 @@ def conv3d_fwd(x, w):
     y = torch.empty((Bn, 64, Tn, (H - 1) // 2 + 1, (W - 1) // 2 + 1), device=x.device, dtype=torch.float32)
     check(L.avse_conv3d_fwd(Bn, Cin, Tn, H, W, 2 if x.dtype == torch.uint8 else 0, ptr(x), ptr(w), ptr(y), ptr(ws),
                             stream_ptr(x.device)), "avse_conv3d_fwd")
-    return y
+    if not return_xmax:
+        return y
+    # workspace: the split weights (2 * Cin * 5 * 8192 bytes), then max |W|, max |x| (conv3d_fwd.hip ws_bytes)
+    xmax = ws.view(torch.int32)[(2 * Cin * 5 * 8192) // 4 + 1:(2 * Cin * 5 * 8192) // 4 + 2]
+    return y, (xmax if x.dtype == torch.float32 else None)
 
 
 # ------------------------------------------------------------------------ dilated Conv2d dW (AudioFeatNet)
@@ -1474,7 +1514,7 @@ def gemm_f32s_split(sp, sq, out, alpha=1.0, fold=1):
     a.nsub = 1
     tap = _tap_begin("avse_gemm_f32s", out.device)
     check(_lib.lib().avse_gemm_f32s(a, stream_ptr(out.device)), "avse_gemm_f32s")
-    _tap_end(tap)
+    _tap_end(tap, 2.0 * a.batch * a.mp * a.mq * a.k)
     return out
 
 
@@ -1528,5 +1568,5 @@ def gemm_f32s_time_chunks(sp, sq, alpha=1.0):
     a.nsub, a.p_bs2, a.q_bs2 = nsub, kc, kc
     tap = _tap_begin("avse_gemm_f32s", out.device)
     check(_lib.lib().avse_gemm_f32s(a, stream_ptr(out.device)), "avse_gemm_f32s")
-    _tap_end(tap)
+    _tap_end(tap, 2.0 * nb * mp * mq * kn)
     return out.sum(0)

@@ -167,10 +167,14 @@ class _LipConv3dFn(torch.autograd.Function):
         hip = x.is_cuda and K.conv3d_fwd_supported(x, w, stride, padding)
         if not hip and x.dtype != torch.float32:
             x = x.float()
-        ctx.save_for_backward(x, w)
         ctx.stride, ctx.padding = stride, padding
-        if hip:                           # MFMA implicit GEMM (csrc/conv3d_fwd.hip)
-            return K.conv3d_fwd(x, w)
+        ctx.xmax = None
+        if hip:                           # split-fp16 MFMA implicit GEMM (csrc/conv3d_fwd.hip)
+            y, xmax = K.conv3d_fwd(x, w, return_xmax=True)
+            ctx.save_for_backward(x, w, xmax if xmax is not None else x.new_zeros(0, dtype=torch.int32))
+            ctx.xmax = xmax is not None   # fp32 frames: the forward's max |x| scales the weight gradient's x split
+            return y
+        ctx.save_for_backward(x, w, x.new_zeros(0, dtype=torch.int32))
         # other shapes: the avse1 front-end as a Conv2d over frames (Cin = 3); the Cin = 1 front-ends of avse2 /
         # avse4 fold to a 5-channel Conv2d without a find-db record (a find pass over the avse4 step did not finish
         # in 400 s): they keep conv3d
@@ -180,14 +184,14 @@ class _LipConv3dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x, w, xmax = ctx.saved_tensors
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.nn.grad.conv3d_input(x.shape, w, dy, ctx.stride, ctx.padding)
         dw = None
         if ctx.needs_input_grad[1]:
             if dy.shape[-1] <= K.CONV3D_WGRAD_MAX_WO:
-                dw = K.conv3d_wgrad(x, dy, tuple(w.shape[2:]), ctx.padding)
+                dw = K.conv3d_wgrad(x, dy, tuple(w.shape[2:]), ctx.padding, xmax=xmax if ctx.xmax else None)
             else:   # wider frames (avse2's 224x224 lips -> 112 output columns): the library's GPU kernel
                 dw = torch.nn.grad.conv3d_weight(x.float(), w.shape, dy, ctx.stride, ctx.padding)
         return dx, dw, None, None

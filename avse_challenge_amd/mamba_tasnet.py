@@ -188,6 +188,49 @@ def _delta(dt_proj_w, x_rows, dt_bias):
     return _wbmm(dt_proj_w, x_rows), dt_bias, True
 
 
+def _dir_fwd(xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias, reverse, acc=None):
+    """One BiMamba direction's forward (MambaInnerNoOutProj): -> (out_z, tensors to save).  acc: a tensor the gated
+    output is added to in place (the scan's flush) and returned as out_z."""
+    R = dt_proj_w.shape[1]
+    x, z = xz.chunk(2, dim=1)
+    conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=reverse)     # (b, d, l)
+    x_dblT = _wbmm(x_proj_w, conv_out)                                       # (b, R + 2n, l)
+    delta, bias, mode = _delta(dt_proj_w, x_dblT[:, :R], dt_bias)             # (b, d, l)
+    Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]                 # (b, n, l) views
+    # the pre-gate `out` is neither written nor saved (the reference saves it, :212): the scan
+    # backward recomputes y + D u per step anyway, so it only cost HBM traffic and memory
+    _, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, bias, mode, reverse=reverse,
+                                         return_out=False, out_z_acc=acc)
+    return out_z, (xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck)
+
+
+def _dir_bwd(saved, dout, reverse, dxz=None, accumulate=False):
+    """One direction's backward -> (dxz, dconv_w, dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias).  dxz /
+    accumulate: write the xz gradient into the given buffer, or add it there (the other direction's, round 6)."""
+    xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck = saved
+    R = dt_proj_w.shape[1]
+    x, z = xz.chunk(2, dim=1)
+    conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=reverse)
+    delta, bias, mode = _delta(dt_proj_w, x_dblT[:, :R], dt_bias)             # the forward's values bit for bit
+    Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]
+    if dxz is None:
+        dxz = K.bdl_empty(xz.shape[0], xz.shape[1], xz.shape[2], xz.dtype, xz.device)
+    dx, dz = dxz.chunk(2, dim=1)
+    dx_dblT = K.bdl_empty(*x_dblT.shape, torch.float32, x_dblT.device)         # scan writes fp32 dB/dC
+    # ddelta / ddt_bias: gradients w.r.t. the pre-softplus dt_proj output and the bias in either mode
+    dconv, ddelta, dA, _, _, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
+        conv_out, delta, A, Bm, Cm, D, z, bias, dout, xck, None, dz, mode, False, reverse=reverse,
+        dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:], dz_accumulate=accumulate)
+    dx_dblT[:, :R] = _wbmm(dt_proj_w.t(), ddelta)
+    ddt_proj_w = _bsum_mm(ddelta, x_dblT[:, :R].transpose(1, 2))               # (d, R)
+    dx_proj_w = _bsum_mm(dx_dblT, conv_out.transpose(1, 2))                    # (R + 2n, d)
+    wxt = x_proj_w.t().to(dconv.dtype)
+    dconv.baddbmm_(wxt.expand(dconv.shape[0], *wxt.shape), dx_dblT.to(dconv.dtype))
+    _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True, reverse=reverse,
+                                              dx_accumulate=accumulate)
+    return dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias
+
+
 class MambaInnerNoOutProj(torch.autograd.Function):
     """Conv1d(k4)+SiLU -> x_proj -> dt_proj -> selective scan (z-gated); checkpoint_lvl 1.
 
@@ -203,44 +246,40 @@ class MambaInnerNoOutProj(torch.autograd.Function):
     @staticmethod
     @_FWD
     def forward(ctx, xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias, reverse=False):
-        R = dt_proj_w.shape[1]
-        x, z = xz.chunk(2, dim=1)
-        conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=reverse)     # (b, d, l)
-        x_dblT = _wbmm(x_proj_w, conv_out)                                       # (b, R + 2n, l)
-        delta, bias, mode = _delta(dt_proj_w, x_dblT[:, :R], dt_bias)             # (b, d, l)
-        Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]                 # (b, n, l) views
-        # the pre-gate `out` is neither written nor saved (the reference saves it, :212): the scan
-        # backward recomputes y + D u per step anyway, so it only cost HBM traffic and memory
-        _, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, bias, mode, reverse=reverse,
-                                             return_out=False)
-        ctx.save_for_backward(xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck)
+        out_z, saved = _dir_fwd(xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias, reverse)
+        ctx.save_for_backward(*saved)
         ctx.reverse = reverse
         return out_z
 
     @staticmethod
     @_BWD
     def backward(ctx, dout):
-        xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck = ctx.saved_tensors
-        rev = ctx.reverse
-        R = dt_proj_w.shape[1]
-        x, z = xz.chunk(2, dim=1)
-        conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=rev)
-        delta, bias, mode = _delta(dt_proj_w, x_dblT[:, :R], dt_bias)             # the forward's values bit for bit
-        Bm, Cm = x_dblT[:, R:R + NSTATE], x_dblT[:, R + NSTATE:]
-        dxz = K.bdl_empty(xz.shape[0], xz.shape[1], xz.shape[2], xz.dtype, xz.device)
-        dx, dz = dxz.chunk(2, dim=1)
-        dx_dblT = K.bdl_empty(*x_dblT.shape, torch.float32, x_dblT.device)         # scan writes fp32 dB/dC
-        # ddelta / ddt_bias: gradients w.r.t. the pre-softplus dt_proj output and the bias in either mode
-        dconv, ddelta, dA, _, _, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
-            conv_out, delta, A, Bm, Cm, D, z, bias, dout, xck, None, dz, mode, False, reverse=rev,
-            dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:])
-        dx_dblT[:, :R] = _wbmm(dt_proj_w.t(), ddelta)
-        ddt_proj_w = _bsum_mm(ddelta, x_dblT[:, :R].transpose(1, 2))               # (d, R)
-        dx_proj_w = _bsum_mm(dx_dblT, conv_out.transpose(1, 2))                    # (R + 2n, d)
-        wxt = x_proj_w.t().to(dconv.dtype)
-        dconv.baddbmm_(wxt.expand(dconv.shape[0], *wxt.shape), dx_dblT.to(dconv.dtype))
-        _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True, reverse=rev)
-        return (dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias, None)
+        return (*_dir_bwd(ctx.saved_tensors, dout, ctx.reverse), None)
+
+
+class BiMambaSerial(torch.autograd.Function):
+    """Both v2 directions as ONE autograd node, run one after the other on one stream (round 6, the bf16 C5 path):
+    -> y = out_f + out_b (natural time order; the 0.5 of bimamba.py:253 is the out_proj's alpha).  The backward
+    direction's scan adds its gated output to the forward one's in its flush, and in the backward the two
+    directions sum their xz gradients in one buffer (the scan's dz and the conv's dx accumulate): no (b, d_inner, l)
+    add in the forward and no (b, 2 d_inner, l) add in the backward (~0.2 + 0.4 ms per C5 layer as torch bf16 adds)."""
+
+    @staticmethod
+    @_FWD
+    def forward(ctx, xz, cw, cb, xw, dw, A, D, db, cw_b, cb_b, xw_b, dw_b, A_b, D_b, db_b):
+        f, sf = _dir_fwd(xz, cw, cb, xw, dw, A, D, db, False)
+        y, sb = _dir_fwd(xz, cw_b, cb_b, xw_b, dw_b, A_b, D_b, db_b, True, acc=f)
+        ctx.save_for_backward(*sf, *sb)
+        return y
+
+    @staticmethod
+    @_BWD
+    def backward(ctx, dy):
+        saved = ctx.saved_tensors
+        n = len(saved) // 2
+        gb = _dir_bwd(saved[n:], dy, True)                        # writes the xz gradient
+        gf = _dir_bwd(saved[:n], dy, False, gb[0], True)         # adds its own to it
+        return (gf[0], *gf[1:], *gb[1:])
 
 
 class _InProj(torch.autograd.Function):
@@ -303,6 +342,7 @@ class _BiOutProj(torch.autograd.Function):
     def forward(ctx, f, bk, w):
         dt = _autocast_dtype()
         y = None
+        ctx.two = bk is not None                   # bk None: f already holds the direction sum
         if dt is None and f.dtype == bk.dtype == w.dtype == torch.float32 and f.stride() == bk.stride():
             fa, fb = _padded_full(f), _padded_full(bk)
             if fa is not None and fb is not None and fa.is_contiguous() and fb.is_contiguous():
@@ -342,11 +382,11 @@ class _BiOutProj(torch.autograd.Function):
             else:
                 torch.bmm((0.5 * w.t()).expand(dout.shape[0], *w.t().shape), dout.transpose(1, 2), out=dy)
             dw = _bsum_split(dsp.t(), ys.t(), w.shape[0], w.shape[1], 0.5)         # 0.5 sum_b dout^T y^T
-            return dy, dy, dw
+            return dy, (dy if ctx.two else None), dw
         y, w = ctx.saved_tensors
         dy = _wbmm(w.t(), dout.transpose(1, 2), 0.5)                             # (b, d_inner, l)
         dw = _bsum_mm(dout.transpose(1, 2), y.transpose(1, 2), 0.5)               # (d_model, d_inner)
-        return dy, dy, dw
+        return dy, (dy if ctx.two else None), dw
 
 
 class AddRMSNorm(torch.autograd.Function):
@@ -434,10 +474,19 @@ class BiMambaV2(nn.Module):
 
     def forward(self, h):                                        # (b, l, d_model)
         xz = _InProj.apply(h, self.in_proj.weight)                               # (b, 2di, l), no copy
-        xz, xz_b = _Fork.apply(xz)                # one input per direction; their gradients meet in _padded_add
         A = -torch.exp(self.A_log.float())
         A_b = -torch.exp(self.A_b_log.float())
         side = _direction_stream(xz.device)
+        if side is None and _autocast_dtype() is not None:
+            # serial bf16 directions (C5): one node that sums both the outputs and the xz gradients in place (the
+            # fp32 C3 path keeps K.add_max in _BiOutProj and _Fork, which also yields the sums' maxima for the
+            # projections' splits)
+            y = BiMambaSerial.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight, self.dt_proj.weight,
+                                    A, self.D.float(), self.dt_proj.bias.float(), self.conv1d_b.weight,
+                                    self.conv1d_b.bias, self.x_proj_b.weight, self.dt_proj_b.weight, A_b,
+                                    self.D_b.float(), self.dt_proj_b.bias.float())
+            return _BiOutProj.apply(y, None, self.out_proj.weight)
+        xz, xz_b = _Fork.apply(xz)                # one input per direction; their gradients meet in _padded_add
         if side is not None:
             # the two directions are independent: the backward one runs on a second HIP stream, so its conv /
             # projection / scan kernels fill the CUs the forward one leaves idle (the scan grid at B=32 is

@@ -678,13 +678,18 @@ class Avse4Step:
                 "global_batch": self.B * world, "per_gpu_batch": self.B, "seq_len": 80000, "channels": 2,
                 "frames": 3999, "lip_frames": 125, "lip_hw": 112, "parallelism": f"dp{world}"}
 
-    # the TCN's hand-written kernels (32 TemporalBlocks: fused dwconv -> PReLU -> gLN and PReLU -> gLN, each way)
-    tap_kernels = ("avse_dwconv_gln_bwd", "avse_dwconv_gln_fwd", "avse_prelu_gln_bwd", "avse_prelu_gln_fwd")
+    # the TCN's hand-written kernels (32 TemporalBlocks: fused dwconv -> PReLU -> gLN and PReLU -> gLN, each way) and
+    # the split-fp16 GEMM of its 1x1 convs (forward, input and weight gradients: the step's most kernel time)
+    tap_kernels = ("avse_dwconv_gln_bwd", "avse_dwconv_gln_fwd", "avse_prelu_gln_bwd", "avse_prelu_gln_fwd",
+                   "avse_gemm_f32s")
 
     def roofline(self, dev):
         """In-step figures of the TCN's hand-written kernels (main._in_step_hbm) on (B, 512, 3999): algorithmic bytes
         per element dwconv_gln fwd 12 (x read, y1 + y written), bwd 16 (x, y1, dy read, dx written), prelu_gln fwd 8,
-        bwd 12.  ``roofline`` is the one with the most kernel time in the step; all four are listed."""
+        bwd 12; and of every avse_gemm_f32s launch of the step (the 1x1 convs 256 <-> 512 and the bottleneck / mask
+        convs, forward + both gradients): the launches' fp32 algorithmic FLOPs (2 M N K each) over their summed
+        HIP-event time against the split peak.  ``roofline`` is the one with the most kernel time in the step (the
+        GEMM); the TCN kernels are listed beside it."""
         ne = self.B * 512 * 3999
         recs = []
         for name, bpe, desc in (("avse_dwconv_gln_bwd", 16, "fused dwconv <- PReLU <- gLN backward"),
@@ -696,9 +701,15 @@ class Avse4Step:
                 recs.append(r)
         if not recs:
             return None
-        roof = dict(max(recs, key=lambda r: r["step_ms"]))
-        roof["tcn_kernels"] = [{k: r[k] for k in ("kernel", "avg_ms", "achieved", "frac", "launches", "step_ms")}
-                               for r in recs]
+        tcn = [{k: r[k] for k in ("kernel", "avg_ms", "achieved", "frac", "launches", "step_ms")} for r in recs]
+        gemm = _in_step_flops(self, "avse_gemm_f32s", round(BF16_PEAK_TFS / 3, 1),
+                              "avse_gemm_f32s (TCN 1x1 convs and the bottleneck / mask convs on the split-fp16 GEMM: "
+                              "forward, input and weight gradients)")
+        top = max(recs + ([gemm] if gemm else []), key=lambda r: r["step_ms"])
+        roof = dict(top)
+        roof["tcn_kernels"] = tcn
+        if gemm is not None and top is not gemm:
+            roof["gemm"] = gemm
         return roof
 
     def cpu_baseline(self):
@@ -891,6 +902,26 @@ def _in_step_hbm(work, name, byts, desc, isolated=None, traffic_phase=None):
     if isolated is not None:
         rec["isolated"] = isolated
     return rec
+
+
+def _in_step_flops(work, name, peak_tflops, desc):
+    """roofline record of an entry point whose launches differ in size (kernels.LAUNCH_WORK: the fp32 algorithmic
+    FLOPs of each launch): the step's FLOPs over the launches' summed HIP-event time."""
+    per = getattr(work, "step_taps", {}).get(name) or []
+    flops = getattr(work, "step_work", {}).get(name) or []
+    if not per or len(flops) != len(per):
+        return None
+    tot_ms = sum(per)
+    ach = sum(flops) / (tot_ms * 1e-3) / 1e12
+    return {"kernel": desc, "bound": "mfma", "achieved": round(ach, 2), "peak": peak_tflops, "unit": "TFLOP/s",
+            "frac": round(ach / peak_tflops, 4), "traffic": None, "avg_ms": round(tot_ms / len(per), 4),
+            "launches": len(per), "step_ms": round(tot_ms, 3),
+            "per_launch_ms": [round(v, 3) for v in per[:4]],
+            "measured": f"in-step: all {len(per)} launches of {name} in the last eager warm-up train step of the "
+                        "benchmarked model, HIP events on each launch's stream; achieved = the step's fp32 algorithmic "
+                        "FLOPs (2 M N K per launch) / the launches' summed time",
+            "algorithmic_flops_per_step": sum(flops),
+            "peak_note": "split-fp16: 3 f16 MFMAs per fp32 product, peak = dense f16 2500 TFLOP/s / 3"}
 
 
 class _dconv_library:
@@ -1181,6 +1212,7 @@ def main():
             from avse_challenge_amd import kernels as K
             for n in taps:
                 K.LAUNCH_TAPS[n] = []
+                K.LAUNCH_WORK.pop(n, None)
             if roof_mark:
                 torch.cuda._sleep(1000)
         try:
@@ -1190,10 +1222,12 @@ def main():
             sync(dev)
             if tapping:
                 work.step_taps = {n: [a.elapsed_time(b) for a, b in K.LAUNCH_TAPS[n]] for n in taps}
+                work.step_work = {n: list(K.LAUNCH_WORK.get(n, [])) for n in taps}
         finally:
             if tapping:
                 for n in taps:
                     K.LAUNCH_TAPS.pop(n, None)
+                    K.LAUNCH_WORK.pop(n, None)
         if rank == 0:
             print(f"[bench] warmup {i + 1}/{args.warmup}: {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
     graph = False

@@ -64,6 +64,8 @@ typedef struct {
     void* out;          int64_t out_bs, out_ds;      /* y + D*u (before gating); may be NULL when z is given (bwd recomputes it) */
     float* x;                                        /* (b, d, n_chunks, 2n) contiguous */
     void* out_z;        int64_t out_z_bs, out_z_ds;  /* out * silu(z); ignored when z == NULL */
+    int32_t out_z_accumulate;  /* 1: out_z += out * silu(z) (round 6: the BiMamba v2 direction sum of bimamba.py:253,
+                                  0.5 f + 0.5 b up to the out_proj's 0.5, added by the second direction's flush) */
 } avse_scan_fwd_args;
 
 typedef struct {
@@ -92,6 +94,7 @@ typedef struct {
     void* dz;           int64_t dz_bs, dz_ds;        /* written when z != NULL */
     void* out_z;        int64_t out_z_bs, out_z_ds;  /* written when recompute_out_z */
     float* workspace;                                /* avse_scan_bwd_workspace_bytes() */
+    int32_t dz_accumulate;     /* 1: dz += (round 6: the serial BiMamba v2 directions sum their xz gradients in place) */
 } avse_scan_bwd_args;
 
 int64_t avse_scan_n_chunks(int64_t seqlen);
@@ -131,7 +134,8 @@ int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
                    const float* dout, int64_t dout_bs, int64_t dout_ds,
                    float* dx, int64_t dx_bs, int64_t dx_ds,
                    float* dweight /* (d, w) */, float* dbias /* (d) or NULL */,
-                   int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream);
+                   int32_t silu, int32_t reverse, float* workspace,
+                   int32_t dx_accumulate /* 1: dx += (the BiMamba v2 direction sum, round 6) */, avse_stream_t stream);
 /* bf16 activations (x, out, dout, dx as raw bf16 bit patterns; weights, bias and their gradients fp32;
  * fp32 arithmetic): the dtype causal_conv1d_cuda sees under bf16 autocast (selective_scan_interface.py:182). */
 int avse_cconv_fwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
@@ -145,7 +149,7 @@ int avse_cconv_bwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t widt
                         const uint16_t* dout, int64_t dout_bs, int64_t dout_ds,
                         uint16_t* dx, int64_t dx_bs, int64_t dx_ds,
                         float* dweight, float* dbias,
-                        int32_t silu, int32_t reverse, float* workspace, avse_stream_t stream);
+                        int32_t silu, int32_t reverse, float* workspace, int32_t dx_accumulate, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- add + RMSNorm -------
  * Replaces the Block pre-norm of Mamba-TasNet/modules/mamba/bimamba.py:447-451
@@ -176,11 +180,13 @@ int avse_stft_fwd(int64_t batch, int64_t T, const float* wave, float* mag, float
 int avse_istft(int64_t batch, int64_t frames, int64_t length, const float* mag, const float* phase_spec,
                float* frames_buf, float* wave_out, avse_stream_t stream);
 
-/* Forward of the avse1 lip front-end nn.Conv3d(3, 64, (5, 7, 7), stride (1, 2, 2), padding (2, 3, 3), bias=False)
- * (baseline/avse1/model.py:29-34, frontend3D[0]) as an MFMA implicit GEMM that reads the lips in their stored dtype.
+/* Forward of the lip front-end nn.Conv3d(CIN, 64, (5, 7, 7), stride (1, 2, 2), padding (2, 3, 3), bias=False)
+ * (baseline/avse1/model.py:29-34, frontend3D[0]; baseline/avse4/utils.py:97-118) as a split-fp16 MFMA implicit GEMM
+ * that reads the lips in their stored dtype (fp32-accurate: the weights split into hi + lo fp16, fp32 frames too).
  * x: (B, CIN, T, H, W) contiguous, x_dtype AVSE_U8 (the raw uint8 frames) or AVSE_F32; w: (64, CIN, 5, 7, 7) fp32;
- * y: (B, 64, T, HO, WO) fp32 with HO = (H - 1) / 2 + 1.  Compiled shapes: CIN 3, 96 x 96 (workspace_bytes returns 0
- * for any other; the call then returns AVSE_ESHAPE).  workspace: the weights re-laid per plane pair. */
+ * y: (B, 64, T, HO, WO) fp32 with HO = (H - 1) / 2 + 1.  Compiled shapes: CIN 3, 96 x 96 and CIN 1, 112 x 112
+ * (workspace_bytes returns 0 for any other; the call then returns AVSE_ESHAPE).  workspace: the split weights
+ * (2 * CIN * 5 * 8192 bytes), then max |W| and max |x| as float bits (uint32 words 0 and 1), then scratch. */
 int64_t avse_conv3d_fwd_workspace_bytes(int64_t CIN, int64_t H, int64_t W);
 int avse_conv3d_fwd(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int32_t x_dtype, const void* x,
                     const float* w, float* y, float* workspace, avse_stream_t stream);
@@ -189,7 +195,7 @@ int avse_conv3d_fwd(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int
  * Weight gradient of nn.Conv3d(CIN, 64, (KT,KH,KW), stride (1,2,2), pad (PT,PH,PW), bias=False)
  * — baseline/avse1/model.py:29-34 (CIN 3, (5,7,7), pad (2,3,3)); baseline/avse4/utils.py:100-106
  * (CIN 1).  x: (B, CIN, T, H, W), dy: (B, 64, TO, HO, WO) contiguous fp32; dw: (64, CIN, KT, KH, KW).
- * accumulate != 0 adds into dw.  Exact-fp32 MFMA implicit GEMM; WO <= 64.
+ * accumulate != 0 adds into dw.  avse_conv3d_wgrad / _u8: the exact-fp32 MFMA implicit GEMM; WO <= 64.
  */
 int64_t avse_conv3d_wgrad_workspace_bytes(int64_t B, int64_t TO, int64_t HO, int64_t N);
 int avse_conv3d_wgrad(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,
@@ -202,6 +208,12 @@ int avse_conv3d_wgrad_u8_split(int64_t B, int64_t CIN, int64_t T, int64_t H, int
                                int64_t KW, int64_t PT, int64_t PH, int64_t PW, const uint8_t* x, const float* dy,
                                const uint32_t* dymax, float* dw, int32_t accumulate, float* workspace,
                                avse_stream_t stream);
+/* fp32 frames on the f16 MFMA (round 6): x split under max |x| (*xmax, e.g. the bits avse_conv3d_fwd leaves in its
+ * workspace) and dy under max |dy|, 3 MFMAs per product (hi hi, lo hi, hi lo): fp32-accurate. */
+int avse_conv3d_wgrad_split(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH,
+                            int64_t KW, int64_t PT, int64_t PH, int64_t PW, const float* x, const uint32_t* xmax,
+                            const float* dy, const uint32_t* dymax, float* dw, int32_t accumulate, float* workspace,
+                            avse_stream_t stream);
 int avse_conv3d_wgrad_u8(int64_t B, int64_t CIN, int64_t T, int64_t H, int64_t W, int64_t KT, int64_t KH, int64_t KW,
                          int64_t PT, int64_t PH, int64_t PW, const uint8_t* x, const float* dy, float* dw,
                          int32_t accumulate, float* workspace, avse_stream_t stream);

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_side_validation_without_gpu():
     from avse_challenge_amd import _lib
     L = _lib.lib()
-    assert L.avse_abi_version() == 1
+    assert L.avse_abi_version() == 2                 # round 6: avse_scan_fwd_args.out_z_accumulate
     assert L.avse_scan_n_chunks(3999) == 125 and L.avse_scan_n_chunks(64) == 2 and L.avse_scan_n_chunks(65) == 3
     assert L.avse_stft_frames(48000) == 376           # baseline/avse1/config.py:19
     a = _lib.ScanFwdArgs()
@@ -61,7 +61,9 @@ def test_host_side_validation_without_gpu():
     assert L.avse_dconv_wgrad_workspace_bytes(32, 376, 257, 16) % (4 * (25 * 64 * 64 + 64)) == 0
     # lip Conv3d forward: compiled shape table, null pointers, unsupported shape / dtype
     # the fp32 path's prepped weights, or the f16 path's split weights (15 planes x 4 k-steps x 64 x 16 x hi/lo) + max
-    assert L.avse_conv3d_fwd_workspace_bytes(3, 96, 96) == max(4 * 8 * 49 * 2 * 64, 2 * 15 * 4 * 64 * 16 * 2 + 16)
+    # split weights (hi + lo: 2 x planes x 4 k16-steps x 64 x 16 fp16) | max |W|, max |x| (16 B) | 512 partial maxima
+    assert L.avse_conv3d_fwd_workspace_bytes(3, 96, 96) == 2 * 15 * 4 * 64 * 16 * 2 + 16 + 4 * 512
+    assert L.avse_conv3d_fwd_workspace_bytes(1, 112, 112) == 2 * 5 * 4 * 64 * 16 * 2 + 16 + 4 * 512
     assert L.avse_conv3d_fwd_workspace_bytes(1, 88, 88) == 0
     assert L.avse_conv3d_fwd(2, 3, 75, 96, 96, 2, None, dummy, dummy, dummy, None) == -1
     assert L.avse_conv3d_fwd(2, 1, 75, 88, 88, 2, dummy, dummy, dummy, dummy, None) == -2

@@ -411,6 +411,21 @@ def test_conv3d_wgrad_vs_fp64(cin, T, H, W):
     close(got, ref, 2e-6 * scale * (1 + x.numel() / 1e5) ** 0.5, 0, "dW")
     got2 = K().conv3d_wgrad(x.to(DEV), dy.to(DEV), (5, 7, 7), (2, 3, 3), out=got.clone(), accumulate=True)
     close(got2, 2 * ref, 4e-6 * scale * (1 + x.numel() / 1e5) ** 0.5, 0, "dW accumulate")
+    # the split kernel (x and dy split into hi + lo fp16 under their maxima, round 6) against each element's sum of
+    # |terms|, as the uint8 test bounds it; and the exact-fp32 kernel (C3W_F16 = False) to the same bar as before
+    bound = torch.nn.grad.conv3d_weight(x.double().abs(), w.shape, dy.double().abs(), (1, 2, 2), (2, 3, 3))
+    worst = float(((got.double().cpu() - ref).abs() / (bound + 1e-30)).max())
+    print(f"conv3d wgrad fp32 split {cin}x{H}x{W}: {worst:.2e} of sum|terms|")
+    assert worst <= 1e-5, worst
+    xm = x.abs().amax().reshape(1).view(torch.int32).to(DEV)
+    assert torch.equal(got, K().conv3d_wgrad(x.to(DEV), dy.to(DEV), (5, 7, 7), (2, 3, 3), xmax=xm))
+    old = K().C3W_F16
+    try:
+        K().C3W_F16 = False
+        ex = K().conv3d_wgrad(x.to(DEV), dy.to(DEV), (5, 7, 7), (2, 3, 3))
+    finally:
+        K().C3W_F16 = old
+    close(ex, ref, 2e-6 * scale * (1 + x.numel() / 1e5) ** 0.5, 0, "dW exact fp32")
 
 
 @pytest.mark.parametrize("T", [5, 1])
@@ -444,27 +459,36 @@ def test_conv3d_wgrad_uint8_vs_fp64(T):
     assert torch.equal(b, c)
 
 
-@pytest.mark.parametrize("dtype,T", [(torch.uint8, 7), (torch.float32, 6), (torch.uint8, 1)])
-def test_conv3d_fwd_vs_fp64(dtype, T):
-    """K.conv3d_fwd (csrc/conv3d_fwd.hip) vs the fp64 Conv3d(3, 64, (5,7,7), (1,2,2), (2,3,3)) of the avse1 lip
-    front-end (baseline/avse1/model.py:29-34) at its 96 x 96 frames: every output within 1e-6 of its sum of |terms|
-    (fp32 frames: exact-f32 MFMA; uint8 frames, read as stored, on the f16 MFMA -- exact in fp16 -- against the
-    weights split into hi + lo fp16 (22 bits), fp32 accumulation); clips of 1 .. 7 frames cover the zero time padding
-    on both sides."""
-    g = torch.Generator().manual_seed(707 + T)
+@pytest.mark.parametrize("dtype,T,cin,hw", [(torch.uint8, 7, 3, 96), (torch.float32, 6, 3, 96), (torch.uint8, 1, 3, 96),
+                                             (torch.float32, 5, 1, 112), (torch.float32, 1, 1, 112)])
+def test_conv3d_fwd_vs_fp64(dtype, T, cin, hw):
+    """K.conv3d_fwd (csrc/conv3d_fwd.hip) vs the fp64 Conv3d(cin, 64, (5,7,7), (1,2,2), (2,3,3)) of the avse1 lip
+    front-end (baseline/avse1/model.py:29-34, 3 x 96 x 96) and the avse4 one (baseline/avse4/utils.py:97-118, 1 x 112
+    x 112 normalised frames): every output within 1e-6 of its sum of |terms| (the f16 MFMA against the weights split
+    into hi + lo fp16, 22 bits; uint8 frames read as stored, exact in fp16; fp32 frames split as well under their
+    max, round 6), fp32 accumulation; clips of 1 .. 7 frames cover the zero time padding on both sides."""
+    g = torch.Generator().manual_seed(707 + T + cin)
     if dtype == torch.uint8:
-        x = torch.randint(0, 256, (2, 3, T, 96, 96), generator=g, dtype=torch.uint8)
-    else:
-        x = det_input((2, 3, T, 96, 96), 708, "uniform", 255.0)
-    w = det_input((64, 3, 5, 7, 7), 709) / 50
+        x = torch.randint(0, 256, (2, cin, T, hw, hw), generator=g, dtype=torch.uint8)
+    elif cin == 3:
+        x = det_input((2, cin, T, hw, hw), 708, "uniform", 255.0)
+    else:      # avse4: (x / 255 - 0.421) / 0.165 grey values, with a few frames of much smaller contrast
+        x = (det_input((2, cin, T, hw, hw), 708, "uniform", 1.0) - 0.421) / 0.165
+        x[:, :, :1] *= 1e-3
+    w = det_input((64, cin, 5, 7, 7), 709) / 50
     truth = torch.nn.functional.conv3d(x.double(), w.double(), None, (1, 2, 2), (2, 3, 3))
     bound = torch.nn.functional.conv3d(x.double().abs(), w.double().abs(), None, (1, 2, 2), (2, 3, 3))
     assert K().conv3d_fwd_supported(x, w, (1, 2, 2), (2, 3, 3))
     got = K().conv3d_fwd(x.to(DEV), w.to(DEV))
     assert got.shape == truth.shape and got.dtype == torch.float32
     worst = float(((got.double().cpu() - truth).abs() / (bound + 1e-30)).max())
+    print(f"conv3d fwd {dtype} {cin}x{hw}: {worst:.2e} of sum|terms|")
     assert worst <= 1e-6, worst
     assert torch.equal(got, K().conv3d_fwd(x.to(DEV), w.to(DEV)))          # deterministic
+    if dtype == torch.float32:
+        y2, xmax = K().conv3d_fwd(x.to(DEV), w.to(DEV), return_xmax=True)
+        assert torch.equal(y2, got)
+        assert int(xmax.cpu()[0]) == int(x.abs().amax().reshape(1).view(torch.int32)[0])
 
 
 def test_conv3d_fwd_unsupported_shapes():
@@ -478,7 +502,8 @@ def test_conv3d_fwd_unsupported_shapes():
 
 def test_lip_conv3d_module_uint8_frames():
     """LipConv3d on the uint8 frames (the HIP forward and weight gradient on the f16 MFMA, frames read as stored) and
-    on their float values (the exact-fp32 kernels) both hold the fp32 class against fp64: output within 1e-6 and
+    on their float values (the same kernels with the frames split into hi + lo fp16 as well, round 6) both hold the
+    fp32 class against fp64: output within 1e-6 and
     weight gradient within 1e-5 of each element's sum of |terms| (round 5: the two paths no longer share products, so
     they agree to that bar, not bitwise)."""
     from avse_challenge_amd.layers import LipConv3d
@@ -821,6 +846,87 @@ def test_scan_fwd_without_out_matches():
     out2, x2, oz2 = K().selective_scan_fwd(**ins, delta_softplus=True, return_out=False)
     assert out2 is None
     assert torch.equal(oz, oz2) and torch.equal(x, x2)
+
+
+@pytest.mark.parametrize("dtype,reverse", [(torch.float32, False), (torch.bfloat16, True), (torch.bfloat16, False)])
+def test_scan_fwd_out_z_accumulate(dtype, reverse):
+    """out_z_acc (round 6, the serial BiMamba v2 direction sum): the flush adds the gated output to the given tensor in
+    place -- fp32: bitwise acc + out_z (one fp32 add of the same values); bf16: within one bf16 rounding of
+    (acc + out_z in fp32), one rounding fewer than the separate add of the two bf16 tensors.  Chunk tail (l = 200)."""
+    b, d, l = 2, 80, 200
+    ins = {"u": det_input((b, d, l), 31), "delta": 0.2 * det_input((b, d, l), 32), "A": -torch.exp(0.5 * det_input((d, 16), 33)),
+           "B": det_input((b, 1, 16, l), 34), "C": det_input((b, 1, 16, l), 35), "D": det_input((d,), 36),
+           "z": det_input((b, d, l), 37), "delta_bias": 0.3 * det_input((d,), 38)}
+    ins = {k: (v.to(dtype) if k in ("u", "delta", "B", "C", "z") else v).to(DEV) for k, v in ins.items()}
+    _, x0, oz = K().selective_scan_fwd(**ins, delta_softplus=True, reverse=reverse, return_out=False)
+    acc = det_input((b, d, l), 39).to(dtype).to(DEV)
+    acc0 = acc.clone()
+    _, x1, oz1 = K().selective_scan_fwd(**ins, delta_softplus=True, reverse=reverse, return_out=False, out_z_acc=acc)
+    assert oz1.data_ptr() == acc.data_ptr() and torch.equal(x0, x1)
+    want = acc0.float() + oz.float()
+    if dtype == torch.float32:
+        assert torch.equal(acc, want)
+    else:
+        # oz is the bf16-rounded gated output; the flush adds the fp32 value: |diff| <= one bf16 ulp of the result + oz's
+        err = (acc.float() - want).abs()
+        tol = 2.0 ** -7 * (want.abs() + oz.float().abs()) + 1e-30
+        assert bool((err <= tol).all()), float((err / tol).max())
+    with pytest.raises(RuntimeError):
+        K().selective_scan_fwd(**ins, delta_softplus=True, return_out=False, out_z_acc=acc[:, :, :100])
+
+
+@pytest.mark.parametrize("dtype,l,padded,reverse", [(torch.float32, 300, True, False), (torch.bfloat16, 300, True, True),
+                                                    (torch.float32, 200, True, True), (torch.bfloat16, 301, False, False)])
+def test_cconv_bwd_dx_accumulate(dtype, l, padded, reverse):
+    """dx_accumulate (round 6, the serial BiMamba directions' shared xz gradient): dx += the input gradient, on the
+    vectorised rows (padded time stride), the short-row kernel (l <= 256) and the generic one (odd stride):
+    fp32 bitwise buf + dx, bf16 within one rounding of (buf + dx) in fp32; dweight / dbias unchanged."""
+    b, d, w = 2, 48, 4
+    x = det_input((b, d, l), 41).to(dtype).to(DEV)
+    g = det_input((b, d, l), 42).to(dtype).to(DEV)
+    wt, cb = (0.3 * det_input((d, w), 43)).to(DEV), det_input((d,), 44).to(DEV)
+    dx0, dw0, db0 = K().causal_conv1d_bwd(x, wt, cb, g, silu=True, reverse=reverse)
+    lp = (l + 31) // 32 * 32 if padded else l
+    store = det_input((b, d, lp), 45).to(dtype).to(DEV)
+    buf = store[:, :, :l]
+    buf0 = buf.clone()
+    dx1, dw1, db1 = K().causal_conv1d_bwd(x, wt, cb, g, dx=buf, silu=True, reverse=reverse, dx_accumulate=True)
+    assert dx1.data_ptr() == buf.data_ptr()
+    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+    want = buf0.float() + dx0.float()
+    if dtype == torch.float32:
+        assert torch.equal(buf, want)
+    else:
+        err = (buf.float() - want).abs()
+        assert bool((err <= 2.0 ** -7 * (want.abs() + dx0.float().abs()) + 1e-30).all())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_scan_bwd_dz_accumulate(dtype):
+    """dz_accumulate (round 6): the scan backward adds dz into the given view; every other output unchanged."""
+    b, d, l = 2, 80, 200
+    ins = {"u": det_input((b, d, l), 51), "delta": 0.2 * det_input((b, d, l), 52), "A": -torch.exp(0.5 * det_input((d, 16), 53)),
+           "B": det_input((b, 1, 16, l), 54), "C": det_input((b, 1, 16, l), 55), "D": det_input((d,), 56),
+           "z": det_input((b, d, l), 57), "delta_bias": 0.3 * det_input((d,), 58)}
+    ins = {k: (v.to(dtype) if k in ("u", "delta", "B", "C", "z") else v).to(DEV) for k, v in ins.items()}
+    _, x, _ = K().selective_scan_fwd(**ins, delta_softplus=True, return_out=False)
+    dout = det_input((b, d, l), 59).to(dtype).to(DEV)
+    args = [ins[k] for k in ("u", "delta", "A", "B", "C", "D", "z", "delta_bias")] + [dout, x]
+    r0 = K().selective_scan_bwd(*args, None, None, True)
+    buf = det_input((b, d, l), 60).to(dtype).to(DEV)
+    buf0 = buf.clone()
+    r1 = K().selective_scan_bwd(*args, None, buf, True, dz_accumulate=True)
+    for i in (0, 1, 2, 3, 4, 5, 6):
+        assert torch.equal(r0[i], r1[i]), i
+    assert r1[7].data_ptr() == buf.data_ptr()
+    want = buf0.float() + r0[7].float()
+    if dtype == torch.float32:
+        assert torch.equal(buf, want)
+    else:
+        err = (buf.float() - want).abs()
+        assert bool((err <= 2.0 ** -7 * (want.abs() + r0[7].float().abs()) + 1e-30).all())
+    with pytest.raises(RuntimeError):
+        K().selective_scan_bwd(*args, None, None, True, dz_accumulate=True)
 
 
 # ------------------------------------------------------------------ C5 production shape (bf16, d_inner 1024, L 5999)

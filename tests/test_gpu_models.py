@@ -353,11 +353,14 @@ def test_avse4_full_train_step_vs_oracle():
         # gradient then moves by one term, 1e-2 .. 3e-2 of the gradient's max in every fp32 run alike
         # (profiles/r02c_avse4_grad_diag.txt, tools/avse4_bn_diag.py @ 8f1eec2: layer4.outbna.bias 2.7e-2 in ours, torch
         # GPU and torch CPU), so whether ours and torch's flips coincide varies from box to box; the
-        # cosine bar stays 1e-4
+        # cosine bar stays 1e-4.  Round 6: with the fp32 lip frames on the split-fp16 Conv3d (its own rounding, fp32
+        # class) a different set of trunk ReLUs flips: layer4.conv2a.weight measured 6.2e-2 (cosine 0.999993), so
+        # the trunk's floor is 1e-1; test_avse4_full_train_step_vs_masked_oracle checks the same gradients with the
+        # flips removed at max(3x torch's, 10x the masked CPU fp32 run's, 1e-3)
         if p.numel() == 1:
             floor = 1e-1
         elif k.startswith("visual_frontend.resnet."):
-            floor = 3e-2
+            floor = 1e-1
         else:
             floor = 1e-2
         assert e_gpu <= max(3 * e_torch, floor) and cos > 1 - 1e-4, (k, e_gpu, e_torch, float(cos))
