@@ -33,6 +33,7 @@ class ScanFwdArgs(ctypes.Structure):
         ("x", c_vp),
         ("out_z", c_vp), ("out_z_bs", c_i64), ("out_z_ds", c_i64),
         ("out_z_accumulate", c_i32),
+        ("out_z_max", c_vp),
     ]
 
 
@@ -61,6 +62,7 @@ class ScanBwdArgs(ctypes.Structure):
         ("out_z", c_vp), ("out_z_bs", c_i64), ("out_z_ds", c_i64),
         ("workspace", c_vp),
         ("dz_accumulate", c_i32),
+        ("dz_max", c_vp),
     ]
 
 
@@ -103,9 +105,9 @@ SIGNATURES = {
     "avse_cconv_fwd_bf16": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                                     c_i32, c_i32, c_vp]),
     "avse_cconv_bwd": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
-                               c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp]),
+                               c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "avse_cconv_bwd_bf16": (c_i32, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
-                                    c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp]),
+                                    c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "avse_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_rmsnorm_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

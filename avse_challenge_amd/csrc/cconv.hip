@@ -57,13 +57,20 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const T* __r
     }
 }
 
+// max |.| over the wave's lanes into *p as float bits (one vector atomic per wave): dx_max (round 6)
+__device__ inline void wave_absmax_to(float m, uint32_t* p) {
+    uint32_t bits = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(p, bits);
+}
+
 template <typename T, int W, bool SILU, bool HAS_BIAS>
 __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __restrict__ x, int64_t x_bs,
                                                       int64_t x_ds, const float* __restrict__ w,
                                                       const float* __restrict__ bias, const T* __restrict__ dout,
                                                       int64_t g_bs, int64_t g_ds, T* __restrict__ dx,
                                                       int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws, int rev,
-                                                      int dx_acc) {
+                                                      int dx_acc, uint32_t* __restrict__ dx_max) {
     __shared__ float sx[TILE + 2 * MAXW];
     __shared__ float sg[TILE + MAXW];
     __shared__ float sred[THREADS / 64][MAXW + 1];
@@ -76,7 +83,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __r
 #pragma unroll
     for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
     const float bv = HAS_BIAS ? bias[d] : 0.f;
-    float dw[W], db = 0.f;
+    float dw[W], db = 0.f, dmax = 0.f;
 #pragma unroll
     for (int k = 0; k < W; ++k) dw[k] = 0.f;
 
@@ -113,7 +120,9 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __r
 #pragma unroll
                 for (int k = 0; k < W; ++k) acc += wk[k] * sg[i + (W - 1) - k];
                 T* q = &dxr[rev ? L - 1 - t : t];
-                io<T>::st(q, dx_acc ? acc + io<T>::ld(q) : acc);
+                const float v = dx_acc ? acc + io<T>::ld(q) : acc;
+                io<T>::st(q, v);
+                dmax = fmaxf(dmax, fabsf(v));
                 const float g = sg[i];
                 db += g;
 #pragma unroll
@@ -121,6 +130,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __r
             }
         }
     }
+    if (dx_max) wave_absmax_to(dmax, dx_max);
     // block reduce dw, db
 #pragma unroll
     for (int k = 0; k <= W; ++k) {
@@ -243,7 +253,7 @@ __global__ __launch_bounds__(THREADS) void bwd_vec_kernel(int D, int L, const T*
                                                           const float* __restrict__ bias, const T* __restrict__ dout,
                                                           int64_t g_bs, int64_t g_ds, T* __restrict__ dx,
                                                           int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws,
-                                                          int dx_acc) {
+                                                          int dx_acc, uint32_t* __restrict__ dx_max) {
     __shared__ float sred[THREADS / 64][MAXW + 1];
     const int row = blockIdx.x;
     const int b = row / D, d = row % D;
@@ -254,7 +264,7 @@ __global__ __launch_bounds__(THREADS) void bwd_vec_kernel(int D, int L, const T*
 #pragma unroll
     for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
     const float bv = HAS_BIAS ? bias[d] : 0.f;
-    float dw[W], db = 0.f;
+    float dw[W], db = 0.f, dmax = 0.f;
 #pragma unroll
     for (int k = 0; k < W; ++k) dw[k] = 0.f;
     for (int t = threadIdx.x * 4; t < L; t += THREADS * 4) {
@@ -305,7 +315,13 @@ __global__ __launch_bounds__(THREADS) void bwd_vec_kernel(int D, int L, const T*
             for (int j = 0; j < 4; ++j) o[j] += p[j];
         }
         st4<T>(dxr, t, L, o);
+        if (dx_max) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (t + j < L) dmax = fmaxf(dmax, fabsf(o[j]));
+        }
     }
+    if (dx_max) wave_absmax_to(dmax, dx_max);
 #pragma unroll
     for (int k = 0; k <= W; ++k) {
         float v = (k < W) ? dw[k] : db;
@@ -366,7 +382,8 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
                                                             const float* __restrict__ bias,
                                                             const T* __restrict__ dout, int64_t g_bs, int64_t g_ds,
                                                             T* __restrict__ dx, int64_t dx_bs, int64_t dx_ds,
-                                                            float* __restrict__ ws, int rev, int dx_acc) {
+                                                            float* __restrict__ ws, int rev, int dx_acc,
+                                                            uint32_t* __restrict__ dx_max) {
     __shared__ float sx[4][SPAD];
     __shared__ float sg[4][SPAD];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -406,7 +423,7 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float dw[W], db = 0.f;
+    float dw[W], db = 0.f, dmax = 0.f;
 #pragma unroll
     for (int k = 0; k < W; ++k) dw[k] = 0.f;
     for (int t = lane; t < L; t += 64) {
@@ -414,7 +431,9 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
 #pragma unroll
         for (int k = 0; k < W; ++k) acc += wk[k] * pg[t + (W - 1) - k];
         T* q = &dxr[rev ? L - 1 - t : t];
-        io<T>::st(q, dx_acc ? acc + io<T>::ld(q) : acc);
+        const float v = dx_acc ? acc + io<T>::ld(q) : acc;
+        io<T>::st(q, v);
+        dmax = fmaxf(dmax, fabsf(v));
         const float g = pg[t];
         db += g;
 #pragma unroll
@@ -427,6 +446,7 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
         for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
         if (lane == 0) ws[(int64_t)row * (MAXW + 1) + k] = v;
     }
+    if (dx_max) wave_absmax_to(dmax, dx_max);
 }
 
 // dweight / dbias: per-row partials summed over the batch, one workgroup per channel (deterministic:
@@ -496,25 +516,26 @@ void launch_fwd(int64_t batch, int64_t dim, int64_t seqlen, const T* x, int64_t 
 template <typename T, int W, bool S, bool HB>
 void launch_bwd(int64_t batch, int64_t dim, int64_t seqlen, const T* x, int64_t x_bs, int64_t x_ds, const float* w,
                 const float* bias, const T* dout, int64_t g_bs, int64_t g_ds, T* dx, int64_t dx_bs, int64_t dx_ds,
-                float* ws, int rev, int dx_acc, hipStream_t st) {
+                float* ws, int rev, int dx_acc, uint32_t* dx_max, hipStream_t st) {
     const int rows = (int)(batch * dim);
     if (seqlen <= SHORT_L)
         hipLaunchKernelGGL((bwd_short_kernel<T, W, S, HB>), dim3((unsigned)((rows + 3) / 4)), dim3(THREADS), 0, st,
                            rows, (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws,
-                           rev, dx_acc);
+                           rev, dx_acc, dx_max);
     else if (vec_rows<T>(x, x_bs, x_ds, seqlen, true) && vec_rows<T>(dout, g_bs, g_ds, seqlen, true) &&
              vec_rows<T>(dx, dx_bs, dx_ds, seqlen, false)) {
         if (rev)
             hipLaunchKernelGGL((bwd_vec_kernel<T, W, S, HB, true>), dim3((unsigned)rows), dim3(THREADS), 0, st,
                                (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws,
-                               dx_acc);
+                               dx_acc, dx_max);
         else
             hipLaunchKernelGGL((bwd_vec_kernel<T, W, S, HB, false>), dim3((unsigned)rows), dim3(THREADS), 0, st,
                                (int)dim, (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws,
-                               dx_acc);
+                               dx_acc, dx_max);
     } else
         hipLaunchKernelGGL((bwd_kernel<T, W, S, HB>), dim3((unsigned)rows), dim3(THREADS), 0, st, (int)dim,
-                           (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws, rev, dx_acc);
+                           (int)seqlen, x, x_bs, x_ds, w, bias, dout, g_bs, g_ds, dx, dx_bs, dx_ds, ws, rev, dx_acc,
+                           dx_max);
 }
 
 // width / silu / bias -> template instance
@@ -564,7 +585,7 @@ template <typename T>
 int cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const T* x, int64_t x_bs, int64_t x_ds,
               const float* weight, const float* bias, const T* dout, int64_t dout_bs, int64_t dout_ds, T* dx,
               int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias, int32_t silu, int32_t reverse,
-              float* workspace, int32_t dx_accumulate, avse_stream_t stream) {
+              float* workspace, int32_t dx_accumulate, uint32_t* dx_max, avse_stream_t stream) {
     if (!x || !weight || !dout || !dx || !dweight || !workspace) return AVSE_EINVAL;
     if (bias && !dbias) return AVSE_EINVAL;
     if (batch <= 0 || dim <= 0 || seqlen <= 0 || width < 1 || width > MAXW) return AVSE_ESHAPE;
@@ -572,7 +593,7 @@ int cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const T
     hipStream_t st = (hipStream_t)stream;
     const int rc = dispatch<Bwd, T>(width, silu != 0, bias != nullptr, batch, dim, seqlen, x, x_bs, x_ds, weight, bias,
                                     dout, dout_bs, dout_ds, dx, dx_bs, dx_ds, workspace, (int)reverse,
-                                    (int)(dx_accumulate != 0), st);
+                                    (int)(dx_accumulate != 0), dx_max, st);
     if (rc != AVSE_OK) return rc;
     AVSE_CHECK_LAUNCH();
     hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)dim), dim3(THREADS), 0, st, workspace, (int)batch, (int)dim,
@@ -600,9 +621,10 @@ int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, co
 int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const float* x, int64_t x_bs,
                    int64_t x_ds, const float* weight, const float* bias, const float* dout, int64_t dout_bs,
                    int64_t dout_ds, float* dx, int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias,
-                   int32_t silu, int32_t reverse, float* workspace, int32_t dx_accumulate, avse_stream_t stream) {
+                   int32_t silu, int32_t reverse, float* workspace, int32_t dx_accumulate, uint32_t* dx_max,
+                   avse_stream_t stream) {
     return cconv_bwd<float>(batch, dim, seqlen, width, x, x_bs, x_ds, weight, bias, dout, dout_bs, dout_ds, dx, dx_bs,
-                            dx_ds, dweight, dbias, silu, reverse, workspace, dx_accumulate, stream);
+                            dx_ds, dweight, dbias, silu, reverse, workspace, dx_accumulate, dx_max, stream);
 }
 
 int avse_cconv_fwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const uint16_t* x, int64_t x_bs,
@@ -615,11 +637,11 @@ int avse_cconv_fwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t widt
 int avse_cconv_bwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const uint16_t* x, int64_t x_bs,
                         int64_t x_ds, const float* weight, const float* bias, const uint16_t* dout, int64_t dout_bs,
                         int64_t dout_ds, uint16_t* dx, int64_t dx_bs, int64_t dx_ds, float* dweight, float* dbias,
-                        int32_t silu, int32_t reverse, float* workspace, int32_t dx_accumulate,
+                        int32_t silu, int32_t reverse, float* workspace, int32_t dx_accumulate, uint32_t* dx_max,
                         avse_stream_t stream) {
     return cconv_bwd<bf16_t>(batch, dim, seqlen, width, (const bf16_t*)x, x_bs, x_ds, weight, bias,
                              (const bf16_t*)dout, dout_bs, dout_ds, (bf16_t*)dx, dx_bs, dx_ds, dweight, dbias, silu,
-                             reverse, workspace, dx_accumulate, stream);
+                             reverse, workspace, dx_accumulate, dx_max, stream);
 }
 
 }  // extern "C"

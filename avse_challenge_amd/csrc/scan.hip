@@ -184,6 +184,14 @@ __device__ inline void load_bias_rows(float* bias_r, const float* bias, int d0, 
     for (int i = 0; i < RPT; ++i) bias_r[i] = (HAS_BIAS && d0 + wave + 4 * i < D) ? bias[d0 + wave + 4 * i] : 0.f;
 }
 
+// max |.| over the wave's lanes into *p as float bits (one vector atomic per wave; non-negative floats order as their
+// bits): the producer-side max of an accumulated output, for the split-fp16 GEMM that consumes it (round 6)
+__device__ inline void wave_absmax_to(float m, uint32_t* p) {
+    uint32_t bits = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(p, bits);
+}
+
 // ------------------------------------------------------------------------------- forward
 template <typename Tin, bool HAS_Z, bool HAS_D, bool HAS_BIAS, bool SOFTPLUS>
 __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int nblk_d) {
@@ -231,6 +239,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
     rbc.load((const Tin*)a.B, a.B_bs, a.B_ns, (const Tin*)a.C, a.C_bs, a.C_ns, b, 0, min(TC, L), L, rev);
     __syncthreads();                                   // s_par
     float du_keep[RPT];                                // D u of the thread's staged elements, added at the flush
+    float zmax = 0.f;                                  // out_z_max: running max |out_z| of the thread's elements
 
     for (int k = 0; k < nck; ++k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
@@ -330,11 +339,17 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
                 if (lane < tn) {
 #pragma unroll
                     for (int i = 0; i < RPT; ++i) bufst<Tin>::st(rz_, vz, 4 * i * (int)a.out_z_ds, outv[i]);
+                    if (a.out_z_max) {
+#pragma unroll
+                        for (int i = 0; i < RPT; ++i)
+                            if (wave + 4 * i < nrow) zmax = fmaxf(zmax, fabsf(outv[i]));
+                    }
                 }
             }
         }
         __syncthreads();
     }
+    if (HAS_Z && a.out_z_max) wave_absmax_to(zmax, a.out_z_max);
 }
 
 // ------------------------------------------------------------------------------- backward
@@ -452,6 +467,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
     };
     ck_load((nck - 1) * TC + (TC / TS - 1) * TS);
 
+    float dzmax = 0.f;                                 // dz_max: running max |dz| of the thread's elements
     for (int k = nck - 1; k >= 0; --k) {
         const int t0 = k * TC, tn = min(TC, L - t0);
         {
@@ -698,11 +714,17 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
                 if (lane < tn) {
 #pragma unroll
                     for (int i = 0; i < RPT; ++i) bufst<Tin>::st(r_dz, v_dz, 4 * i * (int)a.dz_ds, dzv[i]);
+                    if (a.dz_max) {
+#pragma unroll
+                        for (int i = 0; i < RPT; ++i)
+                            if (wave + 4 * i < nrow) dzmax = fmaxf(dzmax, fabsf(dzv[i]));
+                    }
                 }
             }
         }
         __syncthreads();
     }
+    if (HAS_Z && a.dz_max) wave_absmax_to(dzmax, a.dz_max);
     // per-(b, d) partials of dA, dD, ddelta_bias
     float* ws_d = ws_bc + (int64_t)a.batch * nblk_d * slab;       // (b, D, 18)
     if (dvalid) {

@@ -131,13 +131,14 @@ def dtproj(w, x, bias=None, softplus=True):
 
 
 def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False, reverse=False,
-                       return_out=True, out_z_acc=None):
+                       return_out=True, out_z_acc=None, out_z_max=None):
     """Returns (out, x, out_z|None) — the selective_scan_cuda.fwd contract.
     reverse=True scans time backwards (== flip(scan(flip(inputs))) with no flip copies).
     return_out=False (only with z): skip writing the pre-gate ``out`` (returned as None); the
     backward recomputes it, so training saves one (b, d, l) write and its activation memory.
     out_z_acc (with z): a (b, d, l) tensor of u's dtype, time-contiguous, that the gated output is ADDED to in place
-    (the BiMamba v2 direction sum, round 6); returned as out_z."""
+    (the BiMamba v2 direction sum, round 6); returned as out_z.  out_z_max (with z): a zeroed 1-element int32 tensor
+    that receives max |out_z| as float bits (the producer-side max of the split GEMM that consumes it)."""
     _need_gpu(u, delta, A, B, C, D, z, delta_bias)
     u = _last_contig(u)
     dt = u.dtype
@@ -176,6 +177,7 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
         a.z, a.z_bs, a.z_ds = z.data_ptr(), z.stride(0), z.stride(1)
         a.out_z, a.out_z_bs, a.out_z_ds = out_z.data_ptr(), out_z.stride(0), out_z.stride(1)
         a.out_z_accumulate = int(out_z_acc is not None)
+        a.out_z_max = ptr(out_z_max)
     a.delta_bias = delta_bias.data_ptr() if delta_bias is not None else None
     if out is not None:
         a.out, a.out_bs, a.out_ds = out.data_ptr(), out.stride(0), out.stride(1)
@@ -188,12 +190,13 @@ def selective_scan_fwd(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta
 
 def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, dz=None,
                        delta_softplus=False, recompute_out_z=False, reverse=False, dB_out=None, dC_out=None,
-                       dz_accumulate=False):
+                       dz_accumulate=False, dz_max=None):
     """Returns [du, ddelta, dA, dB, dC, dD, ddelta_bias, dz, out_z] — selective_scan_cuda.bwd contract.
     dB, dC are fp32 shaped (b, 1, n, l); a passed-in ``dz`` view is written in place, and so are
     ``dB_out`` / ``dC_out`` (fp32 (b, n, l) or (b, 1, n, l) views with unit last stride, e.g. rows of
     the x_proj output gradient), which are then returned as dB / dC.  dz_accumulate (round 6, with a passed
-    ``dz``): dz += the gradient instead of dz = (the serial BiMamba directions' shared xz gradient)."""
+    ``dz``): dz += the gradient instead of dz = (the serial BiMamba directions' shared xz gradient); dz_max: a zeroed
+    1-element int32 tensor that receives max |dz| as float bits."""
     if dz_accumulate and dz is None:
         raise RuntimeError("selective_scan_bwd: dz_accumulate needs the dz to add into")
     _need_gpu(u, delta, A, B, C, D, z, delta_bias, dout, x)
@@ -252,6 +255,7 @@ def selective_scan_bwd(u, delta, A, B, C, D, z, delta_bias, dout, x, out=None, d
     if out_z is not None:
         a.out_z, a.out_z_bs, a.out_z_ds = out_z.data_ptr(), out_z.stride(0), out_z.stride(1)
     a.dz_accumulate = int(bool(dz_accumulate) and dz is not None)
+    a.dz_max = ptr(dz_max) if dz is not None else None
     a.delta_bias = delta_bias.data_ptr() if delta_bias is not None else None
     a.dout, a.dout_bs, a.dout_ds = dout.data_ptr(), dout.stride(0), dout.stride(1)
     a.x = x.data_ptr()
@@ -290,10 +294,11 @@ def causal_conv1d_fwd(x, weight, bias=None, silu=False, reverse=False):
     return out
 
 
-def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False, dx_accumulate=False):
+def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False, dx_accumulate=False, dx_max=None):
     """[dx, dweight, dbias]: dx in x's dtype (fp32 or bf16; a passed ``dx`` view of that dtype with unit last
     stride is written in place), dweight / dbias fp32.  dx_accumulate (round 6, with such a ``dx``): dx += the input
-    gradient (the serial BiMamba directions' shared xz gradient)."""
+    gradient (the serial BiMamba directions' shared xz gradient); dx_max: a zeroed 1-element int32 tensor that receives
+    max |dx| as float bits."""
     _need_gpu(x, weight, bias, dout)
     dt = x.dtype
     _dtype_code(dt)
@@ -316,7 +321,8 @@ def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False,
     fn = _lib.lib().avse_cconv_bwd if dt == torch.float32 else _lib.lib().avse_cconv_bwd_bf16
     check(fn(b, d, l, w, ptr(x), x.stride(0), x.stride(1), ptr(weight), ptr(bias), ptr(dout), dout.stride(0),
              dout.stride(1), ptr(dx), dx.stride(0), dx.stride(1), ptr(dweight), ptr(dbias), int(bool(silu)),
-             int(bool(reverse)), ptr(ws), int(bool(dx_accumulate)), stream_ptr(x.device)), "avse_cconv_bwd")
+             int(bool(reverse)), ptr(ws), int(bool(dx_accumulate)), ptr(dx_max), stream_ptr(x.device)),
+          "avse_cconv_bwd")
     if dx_ret is not None and dx_ret is not dx:
         dx_ret.copy_(dx)
         dx = dx_ret

@@ -188,9 +188,9 @@ def _delta(dt_proj_w, x_rows, dt_bias):
     return _wbmm(dt_proj_w, x_rows), dt_bias, True
 
 
-def _dir_fwd(xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias, reverse, acc=None):
+def _dir_fwd(xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias, reverse, acc=None, out_max=None):
     """One BiMamba direction's forward (MambaInnerNoOutProj): -> (out_z, tensors to save).  acc: a tensor the gated
-    output is added to in place (the scan's flush) and returned as out_z."""
+    output is added to in place (the scan's flush) and returned as out_z; out_max: a zeroed word for max |out_z|."""
     R = dt_proj_w.shape[1]
     x, z = xz.chunk(2, dim=1)
     conv_out = K.causal_conv1d_fwd(x, conv_w, conv_b, silu=True, reverse=reverse)     # (b, d, l)
@@ -200,13 +200,14 @@ def _dir_fwd(xz, conv_w, conv_b, x_proj_w, dt_proj_w, A, D, dt_bias, reverse, ac
     # the pre-gate `out` is neither written nor saved (the reference saves it, :212): the scan
     # backward recomputes y + D u per step anyway, so it only cost HBM traffic and memory
     _, xck, out_z = K.selective_scan_fwd(conv_out, delta, A, Bm, Cm, D, z, bias, mode, reverse=reverse,
-                                         return_out=False, out_z_acc=acc)
+                                         return_out=False, out_z_acc=acc, out_z_max=out_max)
     return out_z, (xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck)
 
 
-def _dir_bwd(saved, dout, reverse, dxz=None, accumulate=False):
+def _dir_bwd(saved, dout, reverse, dxz=None, accumulate=False, dmax=None):
     """One direction's backward -> (dxz, dconv_w, dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias).  dxz /
-    accumulate: write the xz gradient into the given buffer, or add it there (the other direction's, round 6)."""
+    accumulate: write the xz gradient into the given buffer, or add it there (the other direction's, round 6); dmax: a
+    zeroed word for max |dxz| (both halves: the scan's dz and the conv's dx)."""
     xz, conv_w, conv_b, x_dblT, x_proj_w, dt_proj_w, A, D, dt_bias, xck = saved
     R = dt_proj_w.shape[1]
     x, z = xz.chunk(2, dim=1)
@@ -220,14 +221,14 @@ def _dir_bwd(saved, dout, reverse, dxz=None, accumulate=False):
     # ddelta / ddt_bias: gradients w.r.t. the pre-softplus dt_proj output and the bias in either mode
     dconv, ddelta, dA, _, _, dD, ddt_bias, dz, _ = K.selective_scan_bwd(
         conv_out, delta, A, Bm, Cm, D, z, bias, dout, xck, None, dz, mode, False, reverse=reverse,
-        dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:], dz_accumulate=accumulate)
+        dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:], dz_accumulate=accumulate, dz_max=dmax)
     dx_dblT[:, :R] = _wbmm(dt_proj_w.t(), ddelta)
     ddt_proj_w = _bsum_mm(ddelta, x_dblT[:, :R].transpose(1, 2))               # (d, R)
     dx_proj_w = _bsum_mm(dx_dblT, conv_out.transpose(1, 2))                    # (R + 2n, d)
     wxt = x_proj_w.t().to(dconv.dtype)
     dconv.baddbmm_(wxt.expand(dconv.shape[0], *wxt.shape), dx_dblT.to(dconv.dtype))
     _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True, reverse=reverse,
-                                              dx_accumulate=accumulate)
+                                              dx_accumulate=accumulate, dx_max=dmax)
     return dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias
 
 
@@ -258,18 +259,23 @@ class MambaInnerNoOutProj(torch.autograd.Function):
 
 
 class BiMambaSerial(torch.autograd.Function):
-    """Both v2 directions as ONE autograd node, run one after the other on one stream (round 6, the bf16 C5 path):
+    """Both v2 directions as ONE autograd node, run one after the other on one stream (round 6):
     -> y = out_f + out_b (natural time order; the 0.5 of bimamba.py:253 is the out_proj's alpha).  The backward
     direction's scan adds its gated output to the forward one's in its flush, and in the backward the two
     directions sum their xz gradients in one buffer (the scan's dz and the conv's dx accumulate): no (b, d_inner, l)
-    add in the forward and no (b, 2 d_inner, l) add in the backward (~0.2 + 0.4 ms per C5 layer as torch bf16 adds)."""
+    add in the forward and no (b, 2 d_inner, l) add in the backward (C5 bf16: torch adds, 18.5 ms per step; C3 fp32:
+    avse_add_max, 0.62 ms per call).  fp32: the accumulating kernels also report max |y| and max |dxz| (atomic max per
+    wave), attached as the producer-side max that the projections' operand splits would otherwise compute."""
 
     @staticmethod
     @_FWD
     def forward(ctx, xz, cw, cb, xw, dw, A, D, db, cw_b, cb_b, xw_b, dw_b, A_b, D_b, db_b):
+        mx = torch.zeros(1, device=xz.device, dtype=torch.int32) if xz.dtype == torch.float32 else None
         f, sf = _dir_fwd(xz, cw, cb, xw, dw, A, D, db, False)
-        y, sb = _dir_fwd(xz, cw_b, cb_b, xw_b, dw_b, A_b, D_b, db_b, True, acc=f)
+        y, sb = _dir_fwd(xz, cw_b, cb_b, xw_b, dw_b, A_b, D_b, db_b, True, acc=f, out_max=mx)
         ctx.save_for_backward(*sf, *sb)
+        if mx is not None:
+            K._set_absmax(y, mx)
         return y
 
     @staticmethod
@@ -277,8 +283,12 @@ class BiMambaSerial(torch.autograd.Function):
     def backward(ctx, dy):
         saved = ctx.saved_tensors
         n = len(saved) // 2
+        xz = saved[0]
+        mx = torch.zeros(1, device=xz.device, dtype=torch.int32) if xz.dtype == torch.float32 else None
         gb = _dir_bwd(saved[n:], dy, True)                        # writes the xz gradient
-        gf = _dir_bwd(saved[:n], dy, False, gb[0], True)         # adds its own to it
+        gf = _dir_bwd(saved[:n], dy, False, gb[0], True, mx)     # adds its own to it
+        if mx is not None:
+            K._set_absmax(gf[0], mx)
         return (gf[0], *gf[1:], *gb[1:])
 
 
@@ -343,7 +353,8 @@ class _BiOutProj(torch.autograd.Function):
         dt = _autocast_dtype()
         y = None
         ctx.two = bk is not None                   # bk None: f already holds the direction sum
-        if dt is None and f.dtype == bk.dtype == w.dtype == torch.float32 and f.stride() == bk.stride():
+        if (bk is not None and dt is None and f.dtype == bk.dtype == w.dtype == torch.float32
+                and f.stride() == bk.stride()):
             fa, fb = _padded_full(f), _padded_full(bk)
             if fa is not None and fb is not None and fa.is_contiguous() and fb.is_contiguous():
                 y = K.add_max(fa, fb, f.size(2))        # the sum with its max: the split below skips the absmax pass
@@ -477,10 +488,9 @@ class BiMambaV2(nn.Module):
         A = -torch.exp(self.A_log.float())
         A_b = -torch.exp(self.A_b_log.float())
         side = _direction_stream(xz.device)
-        if side is None and _autocast_dtype() is not None:
-            # serial bf16 directions (C5): one node that sums both the outputs and the xz gradients in place (the
-            # fp32 C3 path keeps K.add_max in _BiOutProj and _Fork, which also yields the sums' maxima for the
-            # projections' splits)
+        if side is None:
+            # serial directions (C3, C5): one node that sums both the outputs and the xz gradients in place (fp32:
+            # with the sums' maxima for the projections' splits)
             y = BiMambaSerial.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight, self.dt_proj.weight,
                                     A, self.D.float(), self.dt_proj.bias.float(), self.conv1d_b.weight,
                                     self.conv1d_b.bias, self.x_proj_b.weight, self.dt_proj_b.weight, A_b,

@@ -66,6 +66,8 @@ typedef struct {
     void* out_z;        int64_t out_z_bs, out_z_ds;  /* out * silu(z); ignored when z == NULL */
     int32_t out_z_accumulate;  /* 1: out_z += out * silu(z) (round 6: the BiMamba v2 direction sum of bimamba.py:253,
                                   0.5 f + 0.5 b up to the out_proj's 0.5, added by the second direction's flush) */
+    uint32_t* out_z_max;       /* NULL, or a word (zeroed by the caller) that receives max |out_z| as float bits by
+                                  atomic max: the producer-side max for the split GEMM that consumes out_z */
 } avse_scan_fwd_args;
 
 typedef struct {
@@ -95,6 +97,7 @@ typedef struct {
     void* out_z;        int64_t out_z_bs, out_z_ds;  /* written when recompute_out_z */
     float* workspace;                                /* avse_scan_bwd_workspace_bytes() */
     int32_t dz_accumulate;     /* 1: dz += (round 6: the serial BiMamba v2 directions sum their xz gradients in place) */
+    uint32_t* dz_max;          /* NULL, or a zeroed word that receives max |dz| as float bits by atomic max */
 } avse_scan_bwd_args;
 
 int64_t avse_scan_n_chunks(int64_t seqlen);
@@ -135,7 +138,9 @@ int avse_cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
                    float* dx, int64_t dx_bs, int64_t dx_ds,
                    float* dweight /* (d, w) */, float* dbias /* (d) or NULL */,
                    int32_t silu, int32_t reverse, float* workspace,
-                   int32_t dx_accumulate /* 1: dx += (the BiMamba v2 direction sum, round 6) */, avse_stream_t stream);
+                   int32_t dx_accumulate /* 1: dx += (the BiMamba v2 direction sum, round 6) */,
+                   uint32_t* dx_max /* NULL, or a zeroed word: max |dx| as float bits by atomic max */,
+                   avse_stream_t stream);
 /* bf16 activations (x, out, dout, dx as raw bf16 bit patterns; weights, bias and their gradients fp32;
  * fp32 arithmetic): the dtype causal_conv1d_cuda sees under bf16 autocast (selective_scan_interface.py:182). */
 int avse_cconv_fwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t width,
@@ -149,7 +154,8 @@ int avse_cconv_bwd_bf16(int64_t batch, int64_t dim, int64_t seqlen, int64_t widt
                         const uint16_t* dout, int64_t dout_bs, int64_t dout_ds,
                         uint16_t* dx, int64_t dx_bs, int64_t dx_ds,
                         float* dweight, float* dbias,
-                        int32_t silu, int32_t reverse, float* workspace, int32_t dx_accumulate, avse_stream_t stream);
+                        int32_t silu, int32_t reverse, float* workspace, int32_t dx_accumulate, uint32_t* dx_max,
+                        avse_stream_t stream);
 
 /* ---------------------------------------------------------------- add + RMSNorm -------
  * Replaces the Block pre-norm of Mamba-TasNet/modules/mamba/bimamba.py:447-451

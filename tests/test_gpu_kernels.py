@@ -861,8 +861,12 @@ def test_scan_fwd_out_z_accumulate(dtype, reverse):
     _, x0, oz = K().selective_scan_fwd(**ins, delta_softplus=True, reverse=reverse, return_out=False)
     acc = det_input((b, d, l), 39).to(dtype).to(DEV)
     acc0 = acc.clone()
-    _, x1, oz1 = K().selective_scan_fwd(**ins, delta_softplus=True, reverse=reverse, return_out=False, out_z_acc=acc)
+    mx = torch.zeros(1, device=DEV, dtype=torch.int32)
+    _, x1, oz1 = K().selective_scan_fwd(**ins, delta_softplus=True, reverse=reverse, return_out=False, out_z_acc=acc,
+                                        out_z_max=mx)
     assert oz1.data_ptr() == acc.data_ptr() and torch.equal(x0, x1)
+    if dtype == torch.float32:              # the producer-side max: max |acc| over the logical elements, as float bits
+        assert int(mx.cpu()[0]) == int(acc.abs().amax().reshape(1).view(torch.int32).cpu()[0])
     want = acc0.float() + oz.float()
     if dtype == torch.float32:
         assert torch.equal(acc, want)
@@ -890,8 +894,12 @@ def test_cconv_bwd_dx_accumulate(dtype, l, padded, reverse):
     store = det_input((b, d, lp), 45).to(dtype).to(DEV)
     buf = store[:, :, :l]
     buf0 = buf.clone()
-    dx1, dw1, db1 = K().causal_conv1d_bwd(x, wt, cb, g, dx=buf, silu=True, reverse=reverse, dx_accumulate=True)
+    mx = torch.zeros(1, device=DEV, dtype=torch.int32)
+    dx1, dw1, db1 = K().causal_conv1d_bwd(x, wt, cb, g, dx=buf, silu=True, reverse=reverse, dx_accumulate=True,
+                                          dx_max=mx)
     assert dx1.data_ptr() == buf.data_ptr()
+    if dtype == torch.float32:              # max |dx| over the logical elements as float bits (fp32: the stored values)
+        assert int(mx.cpu()[0]) == int(buf.abs().amax().reshape(1).view(torch.int32).cpu()[0])
     assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
     want = buf0.float() + dx0.float()
     if dtype == torch.float32:
@@ -915,9 +923,12 @@ def test_scan_bwd_dz_accumulate(dtype):
     r0 = K().selective_scan_bwd(*args, None, None, True)
     buf = det_input((b, d, l), 60).to(dtype).to(DEV)
     buf0 = buf.clone()
-    r1 = K().selective_scan_bwd(*args, None, buf, True, dz_accumulate=True)
+    mx = torch.zeros(1, device=DEV, dtype=torch.int32)
+    r1 = K().selective_scan_bwd(*args, None, buf, True, dz_accumulate=True, dz_max=mx)
     for i in (0, 1, 2, 3, 4, 5, 6):
         assert torch.equal(r0[i], r1[i]), i
+    if dtype == torch.float32:
+        assert int(mx.cpu()[0]) == int(buf.abs().amax().reshape(1).view(torch.int32).cpu()[0])
     assert r1[7].data_ptr() == buf.data_ptr()
     want = buf0.float() + r0[7].float()
     if dtype == torch.float32:
