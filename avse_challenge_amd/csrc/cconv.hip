@@ -57,11 +57,12 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(int D, int L, const T* __r
     }
 }
 
-// max |.| over the wave's lanes into *p as float bits (one vector atomic per wave): dx_max (round 6)
-__device__ inline void wave_absmax_to(float m, uint32_t* p) {
-    uint32_t bits = __float_as_uint(m);
-    for (int o = 32; o >= 1; o >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, o, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(p, bits);
+// dx_max (round 6): every row's max |dx| goes to the workspace after the rows' dw / db partials (wsmax[row]), and
+// rowmax_kernel folds them into *dx_max with one atomic: one same-word atomic per wave of a (b * d)-row grid cost
+// ~1.3 ms per C3 launch
+__device__ inline float wave_max(float m) {
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    return m;
 }
 
 template <typename T, int W, bool SILU, bool HAS_BIAS>
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __r
                                                       int dx_acc, uint32_t* __restrict__ dx_max) {
     __shared__ float sx[TILE + 2 * MAXW];
     __shared__ float sg[TILE + MAXW];
-    __shared__ float sred[THREADS / 64][MAXW + 1];
+    __shared__ float sred[THREADS / 64][MAXW + 2];
     const int row = blockIdx.x;
     const int b = row / D, d = row % D;
     const T* xr = x + b * x_bs + (int64_t)d * x_ds;
@@ -130,8 +131,7 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __r
             }
         }
     }
-    if (dx_max) wave_absmax_to(dmax, dx_max);
-    // block reduce dw, db
+    // block reduce dw, db (and the row's max |dx|)
 #pragma unroll
     for (int k = 0; k <= W; ++k) {
         float v = (k < W) ? dw[k] : db;
@@ -139,11 +139,20 @@ __global__ __launch_bounds__(THREADS) void bwd_kernel(int D, int L, const T* __r
         for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
         if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6][k] = v;
     }
+    if (dx_max) {
+        const float m = wave_max(dmax);
+        if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6][MAXW + 1] = m;
+    }
     __syncthreads();
     if (threadIdx.x <= W) {
         float v = 0.f;
         for (int i = 0; i < THREADS / 64; ++i) v += sred[i][threadIdx.x];
         ws[(int64_t)row * (MAXW + 1) + threadIdx.x] = v;
+    }
+    if (dx_max && threadIdx.x == MAXW + 1) {
+        float m = 0.f;
+        for (int i = 0; i < THREADS / 64; ++i) m = fmaxf(m, sred[i][MAXW + 1]);
+        ws[(int64_t)gridDim.x * (MAXW + 1) + row] = m;          // wsmax[row]
     }
 }
 
@@ -254,7 +263,7 @@ __global__ __launch_bounds__(THREADS) void bwd_vec_kernel(int D, int L, const T*
                                                           int64_t g_bs, int64_t g_ds, T* __restrict__ dx,
                                                           int64_t dx_bs, int64_t dx_ds, float* __restrict__ ws,
                                                           int dx_acc, uint32_t* __restrict__ dx_max) {
-    __shared__ float sred[THREADS / 64][MAXW + 1];
+    __shared__ float sred[THREADS / 64][MAXW + 2];
     const int row = blockIdx.x;
     const int b = row / D, d = row % D;
     const T* xr = x + b * x_bs + (int64_t)d * x_ds;
@@ -321,7 +330,6 @@ __global__ __launch_bounds__(THREADS) void bwd_vec_kernel(int D, int L, const T*
                 if (t + j < L) dmax = fmaxf(dmax, fabsf(o[j]));
         }
     }
-    if (dx_max) wave_absmax_to(dmax, dx_max);
 #pragma unroll
     for (int k = 0; k <= W; ++k) {
         float v = (k < W) ? dw[k] : db;
@@ -329,11 +337,20 @@ __global__ __launch_bounds__(THREADS) void bwd_vec_kernel(int D, int L, const T*
         for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
         if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6][k] = v;
     }
+    if (dx_max) {
+        const float m = wave_max(dmax);
+        if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6][MAXW + 1] = m;
+    }
     __syncthreads();
     if (threadIdx.x <= W) {
         float v = 0.f;
         for (int i = 0; i < THREADS / 64; ++i) v += sred[i][threadIdx.x];
         ws[(int64_t)row * (MAXW + 1) + threadIdx.x] = v;
+    }
+    if (dx_max && threadIdx.x == MAXW + 1) {
+        float m = 0.f;
+        for (int i = 0; i < THREADS / 64; ++i) m = fmaxf(m, sred[i][MAXW + 1]);
+        ws[(int64_t)gridDim.x * (MAXW + 1) + row] = m;          // wsmax[row]
     }
 }
 
@@ -446,11 +463,28 @@ __global__ __launch_bounds__(THREADS) void bwd_short_kernel(int rows, int D, int
         for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
         if (lane == 0) ws[(int64_t)row * (MAXW + 1) + k] = v;
     }
-    if (dx_max) wave_absmax_to(dmax, dx_max);
+    if (dx_max) {
+        const float m = wave_max(dmax);
+        if (lane == 0) ws[(int64_t)rows * (MAXW + 1) + row] = m;   // wsmax[row]
+    }
 }
 
 // dweight / dbias: per-row partials summed over the batch, one workgroup per channel (deterministic:
 // fixed per-thread strides, then a fixed tree)
+// max over the rows' wsmax entries -> *out (atomic max: the scan's dz max may share the word)
+__global__ __launch_bounds__(1024) void rowmax_kernel(const float* __restrict__ wsmax, int rows, uint32_t* out) {
+    __shared__ float red[16];
+    float m = 0.f;
+    for (int i = threadIdx.x; i < rows; i += 1024) m = fmaxf(m, wsmax[i]);
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 16; ++i) m = fmaxf(m, red[i]);
+        atomicMax(out, __float_as_uint(m));
+    }
+}
+
 __global__ __launch_bounds__(THREADS) void reduce_kernel(const float* ws, int batch, int D, int W, float* dw, float* db) {
     __shared__ float red[THREADS / 64][MAXW + 1];
     const int d = blockIdx.x;
@@ -596,6 +630,12 @@ int cconv_bwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const T
                                     (int)(dx_accumulate != 0), dx_max, st);
     if (rc != AVSE_OK) return rc;
     AVSE_CHECK_LAUNCH();
+    if (dx_max) {
+        const int rows = (int)(batch * dim);
+        hipLaunchKernelGGL(rowmax_kernel, dim3(1), dim3(1024), 0, st, workspace + (int64_t)rows * (MAXW + 1), rows,
+                           dx_max);
+        AVSE_CHECK_LAUNCH();
+    }
     hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)dim), dim3(THREADS), 0, st, workspace, (int)batch, (int)dim,
                        (int)width, dweight, dbias);
     AVSE_CHECK_LAUNCH();
@@ -608,7 +648,7 @@ extern "C" {
 
 int64_t avse_cconv_bwd_workspace_bytes(int64_t batch, int64_t dim, int64_t width) {
     (void)width;
-    return 4 * batch * dim * (MAXW + 1);
+    return 4 * batch * dim * (MAXW + 2);         // per row: dw / db partials, then (after all rows) max |dx|
 }
 
 int avse_cconv_fwd(int64_t batch, int64_t dim, int64_t seqlen, int64_t width, const float* x, int64_t x_bs,

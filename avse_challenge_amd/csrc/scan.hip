@@ -184,12 +184,19 @@ __device__ inline void load_bias_rows(float* bias_r, const float* bias, int d0, 
     for (int i = 0; i < RPT; ++i) bias_r[i] = (HAS_BIAS && d0 + wave + 4 * i < D) ? bias[d0 + wave + 4 * i] : 0.f;
 }
 
-// max |.| over the wave's lanes into *p as float bits (one vector atomic per wave; non-negative floats order as their
-// bits): the producer-side max of an accumulated output, for the split-fp16 GEMM that consumes it (round 6)
-__device__ inline void wave_absmax_to(float m, uint32_t* p) {
+// max |.| over the workgroup's 4 waves into *p as float bits (one vector atomic per workgroup -- same-word atomics
+// serialise far from the CUs; non-negative floats order as their bits): the producer-side max of an accumulated
+// output, for the split-fp16 GEMM that consumes it (round 6).  Every thread of the workgroup calls it.
+__device__ inline void block_absmax_to(float m, uint32_t* p) {
+    __shared__ uint32_t s_mx[THREADS / 64];
     uint32_t bits = __float_as_uint(m);
     for (int o = 32; o >= 1; o >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, o, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(p, bits);
+    if ((threadIdx.x & 63) == 0) s_mx[threadIdx.x >> 6] = bits;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < THREADS / 64; ++w) bits = max(bits, s_mx[w]);
+        atomicMax(p, bits);
+    }
 }
 
 // ------------------------------------------------------------------------------- forward
@@ -349,7 +356,7 @@ __global__ __launch_bounds__(THREADS) void fwd_kernel(avse_scan_fwd_args a, int 
         }
         __syncthreads();
     }
-    if (HAS_Z && a.out_z_max) wave_absmax_to(zmax, a.out_z_max);
+    if (HAS_Z && a.out_z_max) block_absmax_to(zmax, a.out_z_max);     // a.out_z_max: uniform over the grid
 }
 
 // ------------------------------------------------------------------------------- backward
@@ -724,7 +731,7 @@ __global__ __launch_bounds__(THREADS, 2) void bwd_kernel(avse_scan_bwd_args a, i
         }
         __syncthreads();
     }
-    if (HAS_Z && a.dz_max) wave_absmax_to(dzmax, a.dz_max);
+    if (HAS_Z && a.dz_max) block_absmax_to(dzmax, a.dz_max);
     // per-(b, d) partials of dA, dD, ddelta_bias
     float* ws_d = ws_bc + (int64_t)a.batch * nblk_d * slab;       // (b, D, 18)
     if (dvalid) {

@@ -50,13 +50,19 @@ class Trainer:
         self.use_graph = bool(use_graph) and dev.type == "cuda"
         self.params = [p for p in step.model.parameters() if p.requires_grad]
         n = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(n, device=dev)
+        # world > 1: every .grad is a view of one flat buffer (the bucketed all-reduce's operand), zeroed per step,
+        # into which autograd accumulates (one add per parameter).  world == 1 (round 6): no flat buffer -- each
+        # .grad is reset to None before the backward, so autograd hands the computed gradient over without an add
+        # (~120 add launches per avse1 step, ~1.5 ms); under graph capture the gradients then live in the graph's pool
+        # at fixed addresses, which the captured optimizer step reads
+        self.flat = torch.zeros(n, device=dev) if world > 1 else None
         ranges, off = [], 0
         for p in self.params:
-            # same strides as the parameter (channels_last conv weights too): autograd accumulates in place
-            # without a layout copy (dense, non-overlapping parameters only)
-            seg = self.flat[off:off + p.numel()]
-            p.grad = seg.as_strided(p.size(), p.stride()) if _dense(p) else seg.view_as(p)
+            if self.flat is not None:
+                # same strides as the parameter (channels_last conv weights too): autograd accumulates in place
+                # without a layout copy (dense, non-overlapping parameters only)
+                seg = self.flat[off:off + p.numel()]
+                p.grad = seg.as_strided(p.size(), p.stride()) if _dense(p) else seg.view_as(p)
             ranges.append((off, off + p.numel()))
             off += p.numel()
         self.buf_f = self.buf_i = None
@@ -223,7 +229,11 @@ class Trainer:
 
     # ------------------------------------------------------------------ step
     def _fwd_bwd(self, out=None):
-        self.flat.zero_()
+        if self.flat is not None:
+            self.flat.zero_()
+        else:
+            for p in self.params:
+                p.grad = None
         if self.world > 1:
             self._arm()
         loss = self.step.loss()
