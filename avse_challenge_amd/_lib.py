@@ -186,6 +186,8 @@ SIGNATURES = {
     "avse_sconv_fwd": (c_i32, [c_i64] * 6 + [c_vp] * 6),
     "avse_sconv_wgrad_workspace_bytes": (c_i64, [c_i64] * 6),
     "avse_sconv_wgrad": (c_i32, [c_i64] * 6 + [c_vp] * 7),
+    "avse_sconv_dgrad2_supported": (c_i32, [c_i64] * 5),
+    "avse_sconv_dgrad2": (c_i32, [c_i64] * 5 + [c_vp] * 6),
 }
 
 _lib = None

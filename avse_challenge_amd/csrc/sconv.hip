@@ -234,6 +234,190 @@ __global__ __launch_bounds__(512, 1) void fwd_kernel(FArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------ stride-2 input gradient
+// dX[n][y][x][ci] = sum dY[n][ho][wo][co] W[co][ci][kh][kw] over y = 2 ho + kh - 1, x = 2 wo + kw - 1, split by the
+// parity (py, px) of (y, x) into 4 phases, each a stride-1 correlation over dY with only the taps of that parity (no
+// zero-inserted dY, no MFMA on zeros): phase pixel (n, a, b) = dX pixel (n, 2a + py, 2b + px), output channel o = ci,
+// reduction over i = co.  Row taps th: py = 0 -> kh = 1 at dY row a; py = 1 -> kh = 0 at row a + 1, kh = 2 at row a.
+// Column taps tw the same for px.  The forward tile's scheme: stage (th, 16-channel chunk q) stages, per output row
+// (n, a) of the tile, the dY row segment of RS = Wb + 1 columns b = 0 .. Wb (zeros past Wo), pixel (row k, column b)
+// reads position k RS + b + cofs[tw] for its NTW column taps.  One launch covers the 4 phases (heaviest first).
+// Weights: avse_sconv_wprep(transposed = 2): per phase ph = 2 py + px, [th][q][tw][o = ci][64 B] (9 taps in all).
+struct DArgs {
+    const void* dyq;           // Q-split output gradient (N Ho Wo pixels x Co 4 B)
+    const void* wq;            // avse_sconv_wprep(transposed = 2) image
+    const uint32_t* dymax;
+    const uint32_t* wmax;
+    float* dx;                 // NHWC fp32 (N Hi Wi x Ci)
+    int N, Hi, Wi, O, I, Ho, Wo;
+    int tiles_n;               // O / TN
+    int tile0[5];              // launch slot -> first workgroup (prefix sums over the tile counts)
+    int py[4], px[4], Ha[4], Wb[4], RS[4], npos[4];
+    uint32_t woff[4];          // byte offset of the slot's phase image in wq
+};
+
+__host__ __device__ inline uint32_t dg2_tap_off(int ph) {      // taps before phase ph in the image: 0, 1, 3, 5
+    return ph == 0 ? 0u : ph == 1 ? 1u : ph == 2 ? 3u : 5u;
+}
+
+template <int NTH, int NTW, int TN>
+__device__ __forceinline__ void dgrad2_body(const DArgs& a, int slot, int tile, uint8_t* lds) {
+    constexpr int WAVES = 8, WN = TN / 64, WM = WAVES / WN, TM = 64 * WM;
+    constexpr int WIMG = NTW * TN * ROWB, WIMG_MAX = 2 * TN * ROWB;
+    constexpr int STG = XIMG + WIMG_MAX;
+    constexpr int PW = WIMG / 1024;
+    constexpr int MP = (NPOS_MAX / 16 + PW + WAVES - 1) / WAVES;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int py = a.py[slot], px = a.px[slot], Ha = a.Ha[slot], Wb = a.Wb[slot], RS = a.RS[slot];
+    const int tn = tile % a.tiles_n, tm = tile / a.tiles_n;
+    const int p0 = tm * TM, o0 = tn * TN;
+    const int NP = a.N * Ha * Wb, NHa = a.N * Ha;
+    const int g0 = p0 / Wb;
+    const int NQ = a.I / 16, NSTG = NTH * NQ;
+    const i4_t rx = rsrc_of(a.dyq, (int64_t)a.N * a.Ho * a.Wo * a.I * 4);
+    const i4_t rw = rsrc_of(a.wq, (int64_t)9 * a.I * a.O * 4);
+    const uint32_t lds0 = lds_u32(lds);
+    const int PX = a.npos[slot] / 16, PT = PX + PW;
+    const int npieces = (PT - wave + WAVES - 1) / WAVES;
+    const uint32_t pixb = (uint32_t)a.I * 4u;
+    const uint32_t rowb = (uint32_t)a.Wo * pixb;
+    // row tap th reads dY row a + rofs(th): rofs = 1 for (py = 1, th = 0), else 0
+    uint32_t pbase[MP];
+    int thok[MP];                                                  // bit th: the row exists for tap th
+#pragma unroll
+    for (int m = 0; m < MP; ++m) {
+        const int k = wave + WAVES * m;
+        if (k < PX) {
+            const int r = 16 * k + (lane >> 2), c = (lane & 3) ^ swz(r);
+            const int rk = r / RS, col = r - rk * RS, g = g0 + rk;
+            const int n = g / Ha, ar = g - n * Ha;
+            const bool ok = g < NHa && col < a.Wo;
+            int bits = 0;
+            if (ok) bits = (NTH == 2) ? ((ar + 1 < a.Ho ? 1 : 0) | 2) : 1;
+            thok[m] = bits;
+            pbase[m] = ok ? ((uint32_t)(n * a.Ho + ar) * (uint32_t)a.Wo + (uint32_t)col) * pixb + 16u * c : 0u;
+        } else {
+            const int r = 16 * (k - PX) + (lane >> 2), c = (lane & 3) ^ swz(r);    // W row r = tw TN + ol
+            const int tw = r / TN, ol = r - tw * TN;
+            thok[m] = 0;
+            pbase[m] = a.woff[slot] + (uint32_t)(tw * a.O + o0 + ol) * 64u + 16u * c;
+        }
+    }
+    const uint32_t wstage = (uint32_t)NTW * (uint32_t)a.O * 64u;
+    auto issue = [&](int s) {
+        const int th = s / NQ, q = s - th * NQ;
+        const uint32_t img = lds0 + (s & 1) * STG;
+        const uint32_t xadd = (NTH == 2 && th == 0 ? rowb : 0u) + (uint32_t)(q * 64), wadd = (uint32_t)s * wstage;
+#pragma unroll
+        for (int m = 0; m < MP; ++m) {
+            if (m >= npieces) break;
+            const int k = wave + WAVES * m;
+            if (k < PX) {
+                const bool ok = (thok[m] >> th) & 1;
+                dma16(rx, img + k * 1024, ok ? pbase[m] + xadd : OOB);
+            } else {
+                dma16(rw, img + XIMG + (k - PX) * 1024, pbase[m] + wadd);
+            }
+        }
+    };
+
+    const int wm = wave / WN, wn = wave % WN;
+    int posA[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int p = min(p0 + 64 * wm + 32 * i + (lane & 31), NP - 1);
+        const int gr = p / Wb, b = p - gr * Wb;
+        posA[i] = (gr - g0) * RS + b;
+    }
+    const int hc = lane >> 5;
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    issue(0);
+    for (int s = 0; s < NSTG; ++s) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + 1 < NSTG) issue(s + 1);
+        const uint8_t* ximg = lds + (s & 1) * STG;
+        const uint8_t* wimg = ximg + XIMG;
+#pragma unroll
+        for (int tw = 0; tw < NTW; ++tw) {
+            const int cofs = (NTW == 2 && tw == 0) ? 1 : 0;         // px = 1: kw = 0 reads column b + 1
+            half8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int r = posA[i] + cofs;
+                ah[i] = frag(ximg, r, hc);
+                al[i] = frag(ximg, r, 2 + hc);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = tw * TN + 64 * wn + 32 * j + (lane & 31);
+                bh[j] = frag(wimg, r, hc);
+                bl[j] = frag(wimg, r, 2 + hc);
+            }
+#pragma unroll
+            for (int pr = 0; pr < 3; ++pr)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr == 2 ? al[i] : ah[i], pr == 1 ? bl[j] : bh[j],
+                                                                           acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    // epilogue: phase pixel p -> dX pixel (n, 2 ar + py, 2 b + px); 4 consecutive phase pixels per (i, g)
+    const float scale = __builtin_ldexpf(1.f, -(split_exp(*a.dymax) + split_exp(*a.wmax)));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int pf = p0 + 64 * wm + 32 * i + 8 * g + 4 * (lane >> 5);
+            int gr = pf / Wb, b = pf - gr * Wb;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int p = pf + e;
+                if (p < NP) {
+                    const int n = gr / Ha, ar = gr - n * Ha;
+                    const int64_t pix = ((int64_t)n * a.Hi + 2 * ar + py) * a.Wi + 2 * b + px;
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int o = o0 + 64 * wn + 32 * j + (lane & 31);
+                        a.dx[pix * a.O + o] = acc[i][j][4 * g + e] * scale;
+                    }
+                }
+                if (++b == Wb) {
+                    b = 0;
+                    ++gr;
+                }
+            }
+        }
+}
+
+template <int TN>
+__global__ __launch_bounds__(512, 1) void dgrad2_kernel(DArgs a) {
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * (XIMG + 2 * TN * ROWB)];
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    int slot = 0;
+    while (slot < 3 && bid >= a.tile0[slot + 1]) ++slot;
+    const int tile = bid - a.tile0[slot];
+    const int nth = a.py[slot] ? 2 : 1, ntw = a.px[slot] ? 2 : 1;
+    if (nth == 2 && ntw == 2) dgrad2_body<2, 2, TN>(a, slot, tile, lds);
+    else if (nth == 2) dgrad2_body<2, 1, TN>(a, slot, tile, lds);
+    else if (ntw == 2) dgrad2_body<1, 2, TN>(a, slot, tile, lds);
+    else dgrad2_body<1, 1, TN>(a, slot, tile, lds);
+}
+
 // ------------------------------------------------------------------------------------------------ weight gradient
 // Per kernel row kh: dW[o][i][kh][kw] for the 3 kw taps, a GEMM with M = o, N = i and the reduction over output pixels.
 // Workgroup (pixel-chunk range, o block of OB = 64 or 128, i block of 64, kh): OB / 32 x 2 waves of 32 x 32 (o, i)
@@ -521,6 +705,34 @@ __global__ void wsplit_kernel(const float* w, int Co, int Ci, int transposed, co
     }
 }
 
+// W (Co, Ci, 3, 3) fp32 -> the stride-2 input gradient's phase images: phase ph = 2 py + px at tap offset
+// dg2_tap_off(ph), [th][q][tw][o = ci][hi 16 | lo 16] over i = co (q = co / 16); kh = py ? (th ? 2 : 0) : 1, kw likewise
+__global__ void wsplit_dgrad2_kernel(const float* w, int Co, int Ci, const uint32_t* maxbits, uint16_t* wq) {
+    const int O = Ci, NQ = Co / 16;
+    const int64_t tap = (int64_t)O * Co;                        // (o, i) elements per tap
+    const int64_t total = 9 * tap;
+    const float sc = __builtin_ldexpf(1.f, split_exp(*maxbits));
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e % 16);
+        const int64_t rrow = e / 16;                            // row of 16 channels over the whole image
+        const int64_t t9 = rrow / (tap / 16);                   // global tap index 0 .. 8
+        const int ph = t9 < 1 ? 0 : t9 < 3 ? 1 : t9 < 5 ? 2 : 3;
+        const int py = ph >> 1, px = ph & 1, ntw = px ? 2 : 1;
+        const int64_t lr = rrow - (int64_t)dg2_tap_off(ph) * (tap / 16);     // row within the phase image
+        const int o = (int)(lr % O);
+        const int64_t u = lr / O;                               // (th NQ + q) NTW + tw
+        const int tw = (int)(u % ntw);
+        const int64_t sq = u / ntw;
+        const int q = (int)(sq % NQ), th = (int)(sq / NQ);
+        const int kh = py ? (th ? 2 : 0) : 1, kw = px ? (tw ? 2 : 0) : 1;
+        const int i = q * 16 + c;
+        const float sv = w[(((int64_t)i * Ci + o) * 3 + kh) * 3 + kw] * sc;
+        const _Float16 h = (_Float16)sv, l = (_Float16)(sv - (float)h);
+        wq[rrow * 32 + c] = __builtin_bit_cast(uint16_t, h);
+        wq[rrow * 32 + 16 + c] = __builtin_bit_cast(uint16_t, l);
+    }
+}
+
 inline int out_dim(int x, int s) { return (x - 1) / s + 1; }     // k 3, padding 1
 
 // forward geometry: the tile's rows span at most (TM - 1 + Wo - 1) / Wo + 1 output rows
@@ -554,8 +766,75 @@ int avse_sconv_wprep(int64_t co, int64_t ci, const float* w, int32_t transposed,
     const int n = (int)(9 * co * ci);
     hipLaunchKernelGGL(wmax_kernel, dim3((unsigned)std::min(256, (n + 255) / 256)), dim3(256), 0, st, w, n, wmax);
     AVSE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(wsplit_kernel, dim3((unsigned)std::min(2048, (n + 255) / 256)), dim3(256), 0, st, w, (int)co,
-                       (int)ci, transposed, wmax, reinterpret_cast<uint16_t*>(wq));
+    if (transposed == 2)
+        hipLaunchKernelGGL(wsplit_dgrad2_kernel, dim3((unsigned)std::min(2048, (n + 255) / 256)), dim3(256), 0, st, w,
+                           (int)co, (int)ci, wmax, reinterpret_cast<uint16_t*>(wq));
+    else
+        hipLaunchKernelGGL(wsplit_kernel, dim3((unsigned)std::min(2048, (n + 255) / 256)), dim3(256), 0, st, w, (int)co,
+                           (int)ci, transposed, wmax, reinterpret_cast<uint16_t*>(wq));
+    AVSE_CHECK_LAUNCH();
+    return AVSE_OK;
+}
+
+// stride-2 input gradient geometry; AVSE_ESHAPE when the kernel does not take the shape
+static int dg2_setup(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, DArgs& a, int& TN) {
+    if (N <= 0 || Hi <= 0 || Wi <= 0 || ci <= 0 || co <= 0 || ci % 64 || co % 64 || ci > 4096 || co > 4096)
+        return AVSE_ESHAPE;
+    if (N * Hi * Wi * ci * 4 >= (1LL << 31) - 4096 || N * Hi * Wi * co * 4 >= (1LL << 31) - 4096) return AVSE_ESHAPE;
+    a.N = (int)N;
+    a.Hi = (int)Hi;
+    a.Wi = (int)Wi;
+    a.O = (int)ci;
+    a.I = (int)co;
+    a.Ho = out_dim((int)Hi, 2);
+    a.Wo = out_dim((int)Wi, 2);
+    TN = ci % 128 ? 64 : 128;
+    const int TM = TN == 64 ? 512 : 256;
+    a.tiles_n = (int)(ci / TN);
+    static const int order[4] = {3, 2, 1, 0};                   // heaviest phase first
+    int64_t t0 = 0;
+    for (int s = 0; s < 4; ++s) {
+        const int ph = order[s], py = ph >> 1, px = ph & 1;
+        a.py[s] = py;
+        a.px[s] = px;
+        a.Ha[s] = ((int)Hi - py + 1) / 2;
+        a.Wb[s] = ((int)Wi - px + 1) / 2;
+        a.RS[s] = a.Wb[s] + 1;
+        a.woff[s] = dg2_tap_off(ph) * (uint32_t)(ci * co * 4);
+        a.tile0[s] = (int)t0;
+        const int64_t np = N * a.Ha[s] * a.Wb[s];
+        a.npos[s] = np > 0 ? fwd_npos(TM, a.Wb[s], a.RS[s]) : 0;
+        if (a.npos[s] > NPOS_MAX) return AVSE_ESHAPE;
+        t0 += (np + TM - 1) / TM * a.tiles_n;
+        if (t0 >= (1LL << 31)) return AVSE_ESHAPE;
+    }
+    a.tile0[4] = (int)t0;
+    return AVSE_OK;
+}
+
+int avse_sconv_dgrad2_supported(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co) {
+    DArgs a;
+    int TN;
+    return dg2_setup(N, Hi, Wi, ci, co, a, TN) == AVSE_OK ? 1 : 0;
+}
+
+int avse_sconv_dgrad2(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, const void* dyq,
+                      const uint32_t* dymax, const void* wq, const uint32_t* wmax, float* dx, avse_stream_t stream) {
+    if (!dyq || !dymax || !wq || !wmax || !dx) return AVSE_EINVAL;
+    DArgs a;
+    int TN;
+    const int rc = dg2_setup(N, Hi, Wi, ci, co, a, TN);
+    if (rc != AVSE_OK) return rc;
+    a.dyq = dyq;
+    a.wq = wq;
+    a.dymax = dymax;
+    a.wmax = wmax;
+    a.dx = dx;
+    if (a.tile0[4] == 0) return AVSE_OK;
+    const dim3 grid((unsigned)a.tile0[4]), block(512);
+    hipStream_t st = (hipStream_t)stream;
+    if (TN == 64) hipLaunchKernelGGL((dgrad2_kernel<64>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((dgrad2_kernel<128>), grid, block, 0, st, a);
     AVSE_CHECK_LAUNCH();
     return AVSE_OK;
 }

@@ -724,6 +724,34 @@ def sconv_fwd(xs, xshape, w, stride, transposed=False):
     return y
 
 
+def sconv_dgrad2_ok(xshape, cout):
+    """True when csrc/sconv.hip's stride-2 input gradient takes Conv2d(ci, cout, 3, 2, padding=1) on an input of shape
+    xshape = (N, ci, H, W)."""
+    n, ci, h, w = xshape
+    return bool(_lib.lib().avse_sconv_dgrad2_supported(n, h, w, ci, cout))
+
+
+def sconv_dgrad2(dys, xshape, w):
+    """Input gradient (N, ci, H, W) (channels-last memory) of conv2d(x, w, stride=2, padding=1) from the split output
+    gradient dys = (dyq, dymax) (csrc/sconv.hip: the 4 parity phases of dX as stride-1 split-fp16 MFMA GEMMs over dY,
+    only the taps of each phase)."""
+    dyq, dym = dys
+    _need_gpu(dyq, w)
+    n, ci, h, wd = xshape
+    co = w.shape[0]
+    L = _lib.lib()
+    wm = torch.empty(1, device=w.device, dtype=torch.int32)
+    wq = torch.empty(int(L.avse_sconv_wprep_bytes(co, ci)), device=w.device, dtype=torch.uint8)
+    check(L.avse_sconv_wprep(co, ci, ptr(w.float().contiguous()), 2, ptr(wq), ptr(wm), stream_ptr(w.device)),
+          "avse_sconv_wprep")
+    dx = torch.empty((n, ci, h, wd), device=dyq.device, dtype=torch.float32, memory_format=torch.channels_last)
+    tap = _tap_begin("avse_sconv_dgrad2", dyq.device)
+    check(L.avse_sconv_dgrad2(n, h, wd, ci, co, ptr(dyq), ptr(dym), ptr(wq), ptr(wm), ptr(dx), stream_ptr(dyq.device)),
+          "avse_sconv_dgrad2")
+    _tap_end(tap)
+    return dx
+
+
 def sconv_wgrad(xs, dys, xshape, cout, stride):
     """dW (cout, ci, 3, 3) of Conv2d(ci, cout, 3, stride, padding=1, bias=False) from the splits of the input
     (xs = (xq, xmax), shape xshape = (N, ci, H, W)) and of the output gradient (dys), csrc/sconv.hip."""

@@ -550,10 +550,10 @@ class PointwiseConv2d(nn.Conv2d):
 
 
 class _SConvFn(torch.autograd.Function):
-    """Conv2d(ci, co, 3, stride, padding=1, bias=False) on csrc/sconv.hip: forward, weight gradient and the stride-1
-    input gradient as split-fp16 MFMA implicit GEMMs (the stride-2 input gradient, 3 of the 16 trunk convs, stays on
-    MIOpen).  The input's split is made once and kept for the weight gradient in place of the input (same bytes);
-    the output gradient is split once for both of its GEMMs."""
+    """Conv2d(ci, co, 3, stride, padding=1, bias=False) on csrc/sconv.hip: forward, weight gradient and the input
+    gradient (stride 1: the flipped-weight forward; stride 2: the 4 parity phases, avse_sconv_dgrad2) as split-fp16
+    MFMA implicit GEMMs, no library convolution.  The input's split is made once and kept for the weight gradient in
+    place of the input (same bytes); the output gradient is split once for both of its GEMMs."""
 
     @staticmethod
     def forward(ctx, x, w, stride):
@@ -567,16 +567,12 @@ class _SConvFn(torch.autograd.Function):
         xq, xm, w = ctx.saved_tensors
         s, shape = ctx.stride, ctx.shape
         dyq, dym = K.split_q(dy)                   # (the incoming gradient keeps its producer's max, if any)
-        if K.is_split_q(dy) and s != 1 and ctx.needs_input_grad[0]:
-            raise RuntimeError("_SConvFn: the stride-2 input gradient needs an fp32 output gradient (TrunkConv2d.q_ok)")
-        dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             if s == 1:
                 dx = K.sconv_fwd((dyq, dym), tuple(dy.shape), w, 1, transposed=True)
             else:
-                x_like = torch.empty(shape, device=dy.device, dtype=torch.float32, memory_format=torch.channels_last)
-                dx = _conv2d_dgrad(x_like, w, dy, s, 1, 1)
+                dx = K.sconv_dgrad2((dyq, dym), shape, w)
         if ctx.needs_input_grad[1]:
             dw = K.sconv_wgrad((xq, xm), (dyq, dym), shape, w.shape[0], s)
         return dx, dw, None
@@ -592,12 +588,13 @@ class TrunkConv2d(nn.Conv2d):
 
     def _sconv(self, x):
         return (x.is_contiguous(memory_format=torch.channels_last) and x.dtype == self.weight.dtype
-                and K.sconv_ok(x, self.out_channels, self.stride[0]))
+                and K.sconv_ok(x, self.out_channels, self.stride[0])
+                and (self.stride[0] == 1 or K.sconv_dgrad2_ok(tuple(x.shape), self.out_channels)))
 
     def q_ok(self, x, grad=False):
         """True when this conv's forward (grad=True: its backward, given its input x) takes a split-output tensor:
-        the sconv path, and for the backward stride 1 (the stride-2 input gradient is MIOpen's, on fp32)."""
-        return self._sconv(x) and (not grad or self.stride[0] == 1)
+        the sconv path (both input-gradient forms read the output gradient's split)."""
+        return self._sconv(x)
 
     def forward(self, x):
         if self._sconv(x):

@@ -479,10 +479,14 @@ int avse_dconv_wprep(const float* w, int32_t transposed, void* wq, uint32_t* max
  * (pixels, C) tensor split as (pixels C / 64, 64)); max |x| bits from avse_split16, max |w| bits from avse_sconv_wprep.
  *   avse_sconv_wprep: W (co, ci, 3, 3) fp32 -> wq (avse_sconv_wprep_bytes(co, ci)); transposed = 1 prepares the
  *     stride-1 input gradient's W'[ci][co][kh][kw] = W[co][ci][2 - kh][2 - kw] (then call avse_sconv_fwd with ci, co
- *     swapped);
+ *     swapped); transposed = 2 the stride-2 input gradient's phase images (avse_sconv_dgrad2);
  *   avse_sconv_fwd: y (N, Ho, Wo, co) fp32, Ho = (Hi - 1) / stride + 1;
  *   avse_sconv_wgrad: dW (co, ci, 3, 3) from the split input (N, Hi, Wi, ci) and output gradient (N, Ho, Wo, co);
- *     workspace of avse_sconv_wgrad_workspace_bytes (< 0: shape not supported). */
+ *     workspace of avse_sconv_wgrad_workspace_bytes (< 0: shape not supported);
+ *   avse_sconv_dgrad2: the stride-2 input gradient dX (N, Hi, Wi, ci) fp32 NHWC (every pixel written) from the split
+ *     output gradient (N, Ho, Wo, co) and wq = avse_sconv_wprep(co, ci, W, transposed = 2) (the 4 parity phases'
+ *     taps, same byte count); replaces the stride-2 blocks' input gradient of resnet.py:26-67 (conv1 of layer2..4)
+ *     that torch's conv2d backward computes; avse_sconv_dgrad2_supported(...) = 1 when the kernel takes the shape. */
 /* AudioFeatNet.conv1 = nn.Conv2d(1, 64, 5, padding=2) (baseline/avse1/model.py:199-215) on x (N, 1, H, W) fp32
  * (csrc/conv1.hip): y (N, H, W, 64) NHWC fp32 = conv(x, w (64, 1, 5, 5)) + b (b may be null); dx (N, 1, H, W) from
  * dy (N, H, W, 64); dW (64, 1, 5, 5) and db (64, may be null) from x and dy (workspace:
@@ -500,6 +504,9 @@ int avse_sconv_wprep(int64_t co, int64_t ci, const float* w, int32_t transposed,
 int avse_sconv_fwd(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride, const void* xq,
                    const uint32_t* xmax, const void* wq, const uint32_t* wmax, float* y, avse_stream_t stream);
 int64_t avse_sconv_wgrad_workspace_bytes(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride);
+int avse_sconv_dgrad2_supported(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co);
+int avse_sconv_dgrad2(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, const void* dyq,
+                      const uint32_t* dymax, const void* wq, const uint32_t* wmax, float* dx, avse_stream_t stream);
 int avse_sconv_wgrad(int64_t N, int64_t Hi, int64_t Wi, int64_t ci, int64_t co, int64_t stride, const void* xq,
                      const uint32_t* xmax, const void* dyq, const uint32_t* dymax, float* dw, float* workspace,
                      avse_stream_t stream);

@@ -73,6 +73,34 @@ def test_sconv_dgrad_vs_fp64(N, ci, H, W, co, s):
     assert worst <= 1e-5, worst
 
 
+# stride-2 trunk layers plus odd / tiny frames: phases with fewer rows or columns (Hi = 1: no odd-row phase at all)
+DGRAD2_SHAPES = [sh for sh in SHAPES if sh[5] == 2] + [(1, 64, 5, 7, 128, 2), (2, 128, 11, 11, 128, 2),
+                                                        (3, 64, 1, 9, 64, 2), (2, 192, 2, 9, 64, 2)]
+
+
+@pytest.mark.parametrize("N,ci,H,W,co,s", DGRAD2_SHAPES)
+def test_sconv_dgrad2_vs_fp64(N, ci, H, W, co, s):
+    """K.sconv_dgrad2: the stride-2 input gradient (4 parity phases, only their taps) vs fp64
+    conv2d_input(stride 2, padding 1), every pixel written, bit-identical on rerun."""
+    _, w = _inputs(N, ci, H, W, co, 2250 + ci + co + H)
+    ho, wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dy = det_input((N, co, ho, wo), 2253 + co) * torch.exp(2.0 * det_input((N, co, ho, wo), 2254))
+    truth = torch.nn.grad.conv2d_input((N, ci, H, W), w.double(), dy.double(), 2, 1)
+    bound = torch.nn.grad.conv2d_input((N, ci, H, W), w.double().abs(), dy.double().abs(), 2, 1)
+    assert K().sconv_dgrad2_ok((N, ci, H, W), co)
+    dyg = dy.to(DEV).contiguous(memory_format=CL)
+    dm = torch.empty(1, device=DEV, dtype=torch.int32)
+    dq = K().split_nhwc(dyg, dm)
+    torch.full((4 * N * ci * H * W,), float("nan"), device=DEV)    # the allocator's next block holds NaNs
+    got = K().sconv_dgrad2((dq, dm), (N, ci, H, W), w.to(DEV))
+    assert got.shape == truth.shape and got.is_contiguous(memory_format=CL)
+    assert bool(torch.isfinite(got).all())
+    worst = _rel(got, truth, bound)
+    print(f"sconv dgrad2 {N, ci, H, W, co}: {worst:.2e} of sum|terms|")
+    assert worst <= 1e-5, worst
+    assert torch.equal(K().sconv_dgrad2((dq, dm), (N, ci, H, W), w.to(DEV)), got)
+
+
 @pytest.mark.parametrize("N,ci,H,W,co,s", SHAPES)
 def test_sconv_wgrad_vs_fp64(N, ci, H, W, co, s):
     """K.sconv_wgrad: the weight gradient from the split input and output gradient vs fp64 (64-pixel chunks spanning
@@ -93,10 +121,10 @@ def test_sconv_wgrad_vs_fp64(N, ci, H, W, co, s):
     assert torch.equal(K().sconv_wgrad((xq, xm), (dq, dm), tuple(x.shape), co, s), dw)
 
 
-@pytest.mark.parametrize("ci,co,s,H", [(64, 64, 1, 24), (128, 256, 2, 12), (512, 512, 1, 3)])
+@pytest.mark.parametrize("ci,co,s,H", [(64, 64, 1, 24), (128, 256, 2, 12), (512, 512, 1, 3), (64, 128, 2, 7)])
 def test_trunk_conv2d_module_vs_fp64(ci, co, s, H):
     """layers.TrunkConv2d on channels-last activations (the _SConvFn path: forward, input gradient -- the stride-2 one on
-    MIOpen -- and weight gradient) vs nn.Conv2d in fp64 on the same weight."""
+    avse_sconv_dgrad2 -- and weight gradient) vs nn.Conv2d in fp64 on the same weight."""
     from avse_challenge_amd.layers import TrunkConv2d
     torch.manual_seed(7)
     ref = torch.nn.Conv2d(ci, co, 3, stride=s, padding=1, bias=False).double()

@@ -1,5 +1,5 @@
 """Micro-benchmark of csrc/sconv.hip (split-fp16 MFMA 3x3 trunk convs) vs MIOpen fp32 at the avse1 C2 lip-trunk shapes
-(2400 frames, channels-last): forward, input gradient (stride 1), weight gradient; split passes timed apart.
+(2400 frames, channels-last): forward, input gradient (stride 1 and the stride-2 phases), weight gradient; split passes timed apart.
 One JSON line per layer shape; frac_fp32 = fp32 algorithmic TFLOP/s / 157.3, frac_f16x3 = / (2500 / 3)."""
 import argparse
 import json
@@ -63,6 +63,8 @@ def main():
         r["split_x_ms"] = round(ev_ms(lambda: K.split_nhwc(x, xm)), 3)
         if s == 1:
             rec("split_dgrad", ev_ms(lambda: K.sconv_fwd((dq, dm), tuple(dy.shape), w, 1, transposed=True)))
+        else:
+            rec("split_dgrad", ev_ms(lambda: K.sconv_dgrad2((dq, dm), tuple(x.shape), w)))
         rec("split_wgrad", ev_ms(lambda: K.sconv_wgrad((xq, xm), (dq, dm), tuple(x.shape), co, s)))
         if not args.no_miopen:
             rec("miopen_fwd", ev_ms(lambda: F.conv2d(x, w, None, s, 1)))
