@@ -181,6 +181,10 @@ SIGNATURES = {
     "avse_conv1_dgrad": (c_i32, [c_i64] * 3 + [c_vp] * 4),
     "avse_conv1_wgrad_workspace_bytes": (c_i64, [c_i64] * 3),
     "avse_conv1_wgrad": (c_i32, [c_i64] * 3 + [c_vp] * 6),
+    "avse_convf_fwd": (c_i32, [c_i64] + [c_vp] * 5),
+    "avse_convf_dgrad": (c_i32, [c_i64] + [c_vp] * 4),
+    "avse_convf_wgrad_workspace_bytes": (c_i64, [c_i64]),
+    "avse_convf_wgrad": (c_i32, [c_i64] + [c_vp] * 6),
     "avse_sconv_wprep_bytes": (c_i64, [c_i64, c_i64]),
     "avse_sconv_wprep": (c_i32, [c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "avse_sconv_fwd": (c_i32, [c_i64] * 6 + [c_vp] * 6),

@@ -20,8 +20,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .layers import (DilatedConv2d, HipLSTM, LipConv3d, PointwiseConv2d, PReLU, TrunkConv2d, bn_act, frames_nhwc,
-                     maxpool3d, time_conv1d, time_major_4d)
+from .layers import (DilatedConv2d, HipLSTM, LipConv3d, PointwiseConv2d, PReLU, TrunkConv2d, bn_act, conv1x1_to4,
+                     frames_nhwc, maxpool3d, time_conv1d, time_major_4d)
 
 STFT_BINS, NUM_STFT_FRAMES, NUM_FRAMES, SAMPLES = 257, 376, 75, 48000
 
@@ -208,7 +208,7 @@ class AudioFeatNet(nn.Module):            # model.py:181-267 (5 dilated 5x5 conv
                            q_bwd=conv.q_ok(x, grad=True))
             else:
                 x = bn_act(conv(x), bn, "relu")
-        x = bn_act(self.convf(x), self.bn_last, "relu")
+        x = bn_act(conv1x1_to4(x, self.convf), self.bn_last, "relu")     # csrc/convf.hip (HBM-streaming 1x1)
         return x.permute(0, 2, 1, 3).reshape(-1, T, Fb * self.last_filter)
 
 

@@ -646,6 +646,43 @@ def conv1_bwd(x, w, dy, need_dx=True, need_dw=True):
     return dx, dw, db
 
 
+# ------------------------------------------------------------------------ AudioFeatNet.convf (64 -> 4, 1x1)
+
+def convf_fwd(x, w, b=None):
+    """conv2d(x, w (4, 64, 1, 1), b) for x (N, 64, H, W) fp32 in channels-last memory (csrc/convf.hip) -> (N, 4, H, W)
+    in channels-last memory."""
+    _need_gpu(x, w, b)
+    n, c, h, wd = x.shape
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.empty((n, 4, h, wd), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+    check(_lib.lib().avse_convf_fwd(n * h * wd, ptr(x), ptr(w.float().contiguous()),
+                                    ptr(None if b is None else b.float().contiguous()), ptr(y), stream_ptr(x.device)),
+          "avse_convf_fwd")
+    return y
+
+
+def convf_bwd(x, w, dy, need_dx=True, need_dw=True):
+    """(dx (N, 64, H, W) channels-last or None, dW (4, 64, 1, 1) or None, db (4) or None) of convf_fwd from its input x
+    and the output gradient dy (N, 4, H, W) (read as channels-last memory)."""
+    _need_gpu(x, w, dy)
+    n, c, h, wd = x.shape
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    L = _lib.lib()
+    dx = dw = db = None
+    if need_dx:
+        dx = torch.empty((n, c, h, wd), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+        check(L.avse_convf_dgrad(n * h * wd, ptr(dy), ptr(w.float().contiguous()), ptr(dx), stream_ptr(x.device)),
+              "avse_convf_dgrad")
+    if need_dw:
+        x = x.contiguous(memory_format=torch.channels_last)
+        dw = torch.empty((4, c, 1, 1), device=x.device, dtype=torch.float32)
+        db = torch.empty(4, device=x.device, dtype=torch.float32)
+        ws = torch.empty((L.avse_convf_wgrad_workspace_bytes(n * h * wd) + 3) // 4, device=x.device, dtype=torch.float32)
+        check(L.avse_convf_wgrad(n * h * wd, ptr(x), ptr(dy), ptr(dw), ptr(db), ptr(ws), stream_ptr(x.device)),
+              "avse_convf_wgrad")
+    return dx, dw, db
+
+
 # ------------------------------------------------------------------------ ResNet trunk 3x3 Conv2d (split fp16 MFMA)
 
 def sconv_ok(x, cout, stride):
@@ -1573,6 +1610,50 @@ def _chunk_plan(kp, nb, tiles_out, cus=256):
             if best is None or cost < best[0]:
                 best = (cost, kc, fold)
     return best[1], best[2]
+
+
+@functools.lru_cache(maxsize=None)
+def _rows_plan(rows, units, tiles_out, cus=256):
+    """(nb, fold) for a reduction over ``rows`` rows made of ``units`` equal units (utterances, frames): nb | units
+    chunks of rows / nb rows each run as batches, folded by ``fold`` into partial outputs (_chunk_plan's cost model)."""
+    best = None
+    for nb in range(1, units + 1):
+        if units % nb:
+            continue
+        kc = rows // nb
+        for fold in range(1, nb + 1):
+            if nb % fold:
+                continue
+            g = nb // fold
+            rounds = -(-(g * tiles_out) // cus)
+            cost = rounds * (fold * (-(-kc // 32)) * 3.5 + 10.0) + (g * tiles_out * 65536 * 8 / 4e6 if g > 1 else 0.0)
+            if best is None or cost < best[0]:
+                best = (cost, nb, fold)
+    return best[1], best[2]
+
+
+def _row_chunks(sp, nb):
+    """Split of a (1, rows, c) row-major operand -> the (nb, c, rows / nb) views of its planes (p = column, stride 1;
+    k = row within the chunk)."""
+    _, r, c = sp.hi.shape
+    sr = sp.hi.stride(1)
+    kc = r // nb
+    v = lambda t: t.as_strided((nb, c, kc), (kc * sr, 1, sr), t.storage_offset())          # noqa: E731
+    return Split(v(sp.hi), v(sp.lo), sp.mb)
+
+
+def gemm_f32s_rows_tn(sa, sb, units):
+    """sum_r b[r, q] a[r, p] -> (cb, ca) fp32 (a weight gradient b^T a) from the Splits of two (1, rows, c) row-major
+    operands (row strides multiples of 8, unit column stride) on the split-fp16 MFMA GEMM: the rows are cut into
+    chunks of whole ``units`` (rows % units == 0) that run as batches, folded into partial outputs, then summed —
+    the output has few 256 x 256 tiles (512 x 1536, 128 x 64), so the reduction is what the workgroups share."""
+    rows, ca, cb = sa.hi.shape[1], sa.hi.shape[2], sb.hi.shape[2]
+    if sb.hi.shape[1] != rows or rows % units:
+        raise RuntimeError(f"gemm_f32s_rows_tn: {tuple(sa.hi.shape)} / {tuple(sb.hi.shape)} in {units} units")
+    nb, fold = _rows_plan(rows, units, -(-ca // 256) * -(-cb // 256))
+    out = torch.empty(nb // fold, cb, ca, device=sa.hi.device, dtype=torch.float32)
+    gemm_f32s_split(_row_chunks(sa, nb), _row_chunks(sb, nb), out, fold=fold)
+    return out[0] if out.shape[0] == 1 else out.sum(0)
 
 
 def gemm_f32s_time_chunks(sp, sq, alpha=1.0):

@@ -456,7 +456,12 @@ class _GemmConvFn(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[1]:
             a, _, _ = _GemmConvFn._rows(x, k, s)
-            dw = (dy2.t() @ a).view_as(w)
+            if _f32s_rows_ok(a, dy2):
+                # split-fp16 MFMA GEMM with the N * P pixel reduction cut per frame group (hipBLASLt: 10-20 TF/s on
+                # these 128 x 64 .. 512 x 256 outputs)
+                dw = K.gemm_f32s_rows_tn(K.split_planes(a[None]), K.split_planes(dy2[None]), n).view_as(w)
+            else:
+                dw = (dy2.t() @ a).view_as(w)
         if ctx.needs_input_grad[0]:
             da = (dy2 @ w.reshape(cout, -1)).view(n, ho, wo, cin, k, k)           # im2col-row gradients
             if k == 1:
@@ -510,13 +515,57 @@ class _TimeConv1dFn(torch.autograd.Function):
         To = T + pad
         Co = wm.shape[0]
         dy2 = dy.reshape(B * To, Co)
-        dw = (dy2.t() @ cols).view(Co, k, C).permute(0, 2, 1)
+        if _f32s_rows_ok(cols, dy2):
+            # both GEMMs on the split-fp16 MFMA GEMM (csrc/projgemm.hip): the weight gradient's reduction over B To rows
+            # cut per utterance (hipBLASLt ran these 512 x 1536 outputs at 3-26 TF/s, tools/avse1_op_profile.py)
+            sd = K.split_planes(dy2[None])                                          # shared by both GEMMs
+            dw = K.gemm_f32s_rows_tn(K.split_planes(cols[None]), sd, B).view(Co, k, C).permute(0, 2, 1)
+            dcols = K.gemm_f32s_split(K.split_planes(wm[None]).t(), sd,
+                                      torch.empty((1, B * To, k * C), device=dy.device, dtype=torch.float32))
+            dcols = dcols.view(B, To, k, C)
+        else:
+            dw = (dy2.t() @ cols).view(Co, k, C).permute(0, 2, 1)
+            dcols = (dy2 @ wm).view(B, To, k, C)
         db = dy2.sum(0) if has_b else None
-        dcols = (dy2 @ wm).view(B, To, k, C)
         dxp = torch.zeros((B, T + 2 * pad, C), device=dy.device, dtype=dy.dtype)
         for j in range(k):
             dxp[:, j * dil:j * dil + To] += dcols[:, :, j]
         return dxp[:, pad:pad + T], dw, db, None
+
+
+class _ConvFFn(torch.autograd.Function):
+    """AudioFeatNet.convf = Conv2d(64, 4, 1) on channels-last activations (csrc/convf.hip: HBM-streaming forward, input
+    gradient and weight / bias gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return K.convf_fwd(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        need_w = ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2])
+        dx, dw, db = K.convf_bwd(x, w, dy, need_dx=ctx.needs_input_grad[0], need_dw=need_w)
+        return dx, dw if ctx.needs_input_grad[1] else None, db if ctx.has_b and ctx.needs_input_grad[2] else None
+
+
+def conv1x1_to4(x, conv):
+    """nn.Conv2d(64, 4, 1) ``conv`` (AudioFeatNet.convf, baseline/avse1/model.py:211-213) on x: csrc/convf.hip for
+    channels-last fp32 GPU activations, the module itself otherwise."""
+    if (x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32 and x.dim() == 4
+            and x.shape[1] == 64 and tuple(conv.weight.shape) == (4, 64, 1, 1) and conv.stride == (1, 1)
+            and conv.padding == (0, 0) and conv.groups == 1 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.data_ptr() % 16 == 0):
+        return _ConvFFn.apply(x, conv.weight, conv.bias)
+    return conv(x)
+
+
+def _f32s_rows_ok(a, b):
+    """Two (rows, c) fp32 GPU operands the split GEMM reads row-major (unit column stride, 16-B rows)."""
+    return (a.is_cuda and a.dtype == b.dtype == torch.float32 and a.dim() == b.dim() == 2 and a.shape[0] == b.shape[0]
+            and a.stride(1) == 1 and b.stride(1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0)
 
 
 def time_conv1d(x, conv):

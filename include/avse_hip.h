@@ -497,6 +497,15 @@ int avse_conv1_dgrad(int64_t N, int64_t H, int64_t W, const float* dy, const flo
 int64_t avse_conv1_wgrad_workspace_bytes(int64_t N, int64_t H, int64_t W);
 int avse_conv1_wgrad(int64_t N, int64_t H, int64_t W, const float* x, const float* dy, float* dw, float* db,
                      float* workspace, avse_stream_t stream);
+/* AudioFeatNet.convf = nn.Conv2d(64, 4, 1) (baseline/avse1/model.py:211-213, called at :246-249) on npix NHWC pixels
+ * (csrc/convf.hip): y (npix, 4) = x (npix, 64) W^T (4, 64) + b (b may be null); dx (npix, 64) = dy (npix, 4) W; dW (4, 64)
+ * and db (4, may be null) = sums over the pixels (workspace: avse_convf_wgrad_workspace_bytes).  x, dy, dx, W 16-B
+ * aligned. */
+int avse_convf_fwd(int64_t npix, const float* x, const float* w, const float* b, float* y, avse_stream_t stream);
+int avse_convf_dgrad(int64_t npix, const float* dy, const float* w, float* dx, avse_stream_t stream);
+int64_t avse_convf_wgrad_workspace_bytes(int64_t npix);
+int avse_convf_wgrad(int64_t npix, const float* x, const float* dy, float* dw, float* db, float* workspace,
+                     avse_stream_t stream);
 
 int64_t avse_sconv_wprep_bytes(int64_t co, int64_t ci);
 int avse_sconv_wprep(int64_t co, int64_t ci, const float* w, int32_t transposed, void* wq, uint32_t* wmax,

@@ -1423,10 +1423,45 @@ def test_conv1_module_nhwc_vs_torch(N, H, W):
         close(ours.bias.grad, ref.bias.grad, 2e-5 * sc(ref.bias.grad), 0, "db")
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 376, 257), (3, 7, 13)])
+def test_convf_vs_fp64(N, H, W):
+    """AudioFeatNet.convf = Conv2d(64, 4, 1) on channels-last activations (layers.conv1x1_to4 -> csrc/convf.hip): output,
+    input, weight and bias gradients vs nn.Conv2d in fp64 (fp32 class: 1e-5 of each quantity's sum of |terms|), at the
+    avse1 C2 frame shape and a ragged pixel count; deterministic on rerun."""
+    from avse_challenge_amd.layers import conv1x1_to4
+    torch.manual_seed(6)
+    ref = torch.nn.Conv2d(64, 4, 1).double()
+    ours = torch.nn.Conv2d(64, 4, 1).to(DEV)
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = det_input((N, 64, H, W), 1880) * torch.exp(det_input((N, 64, H, W), 1881))
+    gy = det_input((N, 4, H, W), 1882)
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr)
+    (yr * gy.double()).sum().backward()
+    aw, ab = ref.weight.detach().abs(), ref.bias.detach().abs()
+    bound_y = F.conv2d(x.double().abs(), aw, ab)
+    bound_dx = torch.nn.grad.conv2d_input(x.shape, aw, gy.double().abs())
+    bound_dw = torch.nn.grad.conv2d_weight(x.double().abs(), aw.shape, gy.double().abs())
+    runs = []
+    for _ in range(2):
+        ours.zero_grad()
+        xg = x.to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        y = conv1x1_to4(xg, ours)
+        assert y.grad_fn is not None and "ConvF" in type(y.grad_fn).__name__, type(y.grad_fn).__name__
+        assert y.is_contiguous(memory_format=torch.channels_last)
+        (y * gy.to(DEV)).sum().backward()
+        runs.append((y.detach().clone(), xg.grad.clone(), ours.weight.grad.clone(), ours.bias.grad.clone()))
+    y, dx, dw, db = runs[0]
+    for got, want, bound, what in ((y, yr, bound_y, "y"), (dx, xr.grad, bound_dx, "dx"),
+                                   (dw, ref.weight.grad, bound_dw, "dw"), (db, ref.bias.grad, gy.double().abs().sum((0, 2, 3)), "db")):
+        err = float(((got.double().cpu() - want.detach()).abs() / (bound + 1e-30)).max())
+        assert err <= 1e-5, (what, err)
+    assert all(torch.equal(a, b) for a, b in zip(runs[0], runs[1]))
+
+
 def test_trunk_conv2d_module_grads_vs_torch():
     """layers.TrunkConv2d (stride 2, NCHW: the library path) and the same conv on channels-last activations (csrc/sconv.hip
-    forward and weight gradient, MIOpen's stride-2 input gradient): output and input / weight gradients vs nn.Conv2d in
-    fp64."""
+    forward, weight gradient and stride-2 input gradient): output and input / weight gradients vs nn.Conv2d in fp64."""
     from avse_challenge_amd.layers import TrunkConv2d
     torch.manual_seed(4)
     ref = torch.nn.Conv2d(64, 128, 3, stride=2, padding=1, bias=False).double()

@@ -384,3 +384,68 @@ def test_add_max_flat_residual():
     assert int(getattr(y, K.ABSMAX_ATTR).item()) == int((a + b).abs().max().view(torch.int32).item())
     s1, s2 = K.split_rows8(y), K.split_rows8(y.clone())
     assert torch.equal(s1.hi, s2.hi) and torch.equal(s1.lo, s2.lo) and torch.equal(s1.mb, s2.mb)
+
+
+# ------------------------------------------------------------------ row-chunked weight gradients (TCN / shortcuts)
+
+@pytest.mark.parametrize("rows,units,ca,cb", [(2464, 32, 1536, 512), (2912, 32, 1536, 512), (30 * 144, 30, 64, 128),
+                                              (77 * 5, 5, 40, 24)])
+def test_gemm_f32s_rows_tn_vs_fp64(rows, units, ca, cb):
+    """kernels.gemm_f32s_rows_tn: b^T a over ``rows`` rows cut into whole units (utterances / frames) that run as
+    folded batches, at the avse1 TCN weight-gradient shapes (B To = 32 x 77 / 91 rows, 1536 / 512 columns) and a
+    lip-shortcut shape (frames x 144 pixels), within 1e-5 of sum |a b| of fp64."""
+    g = torch.Generator(device=DEV).manual_seed(rows + ca)
+    a = torch.randn(rows, ca, device=DEV, generator=g) * torch.exp(2.0 * torch.randn(rows, ca, device=DEV, generator=g))
+    b = torch.randn(rows, cb, device=DEV, generator=g)
+    got = K().gemm_f32s_rows_tn(K().split_planes(a[None]), K().split_planes(b[None]), units)
+    ref = b.double().t() @ a.double()
+    mag = b.double().abs().t() @ a.double().abs()
+    assert got.shape == (cb, ca)
+    err = float(((got.double() - ref).abs() / (mag + 1e-300)).max())
+    print(f"rows_tn {rows, units, ca, cb}: {err:.2e} of sum|ab|")
+    assert err <= 1e-5, err
+
+
+def test_time_conv1d_split_gemm_backward_vs_fp64():
+    """layers._TimeConv1dFn on the GPU (the avse1 TCN conv: hipBLASLt forward, split-GEMM weight and input gradients)
+    vs nn.Conv1d in fp64 on the same weights: output, input, weight and bias gradients."""
+    from avse_challenge_amd.layers import time_conv1d
+    torch.manual_seed(5)
+    B, T, C, k, dil = 4, 75, 512, 3, 4
+    conv = torch.nn.Conv1d(C, C, k, padding=(k - 1) * dil, dilation=dil).double()
+    x = torch.randn(B, T, C, dtype=torch.float64)
+    gy = torch.randn(B, T + (k - 1) * dil, C, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    (conv(xr.transpose(1, 2)).transpose(1, 2) * gy).sum().backward()
+    cg = torch.nn.Conv1d(C, C, k, padding=(k - 1) * dil, dilation=dil).to(DEV)
+    cg.load_state_dict({n: v.float() for n, v in conv.state_dict().items()})
+    xg = x.float().to(DEV).requires_grad_(True)
+    y = time_conv1d(xg, cg)
+    (y * gy.float().to(DEV)).sum().backward()
+    for got, want, what in ((y, conv(x.transpose(1, 2)).transpose(1, 2), "y"), (xg.grad, xr.grad, "dx"),
+                            (cg.weight.grad, conv.weight.grad, "dw"), (cg.bias.grad, conv.bias.grad, "db")):
+        err = float((got.detach().double().cpu() - want.detach()).abs().max())
+        sc = float(want.detach().abs().max())
+        assert err <= 2e-5 * sc, (what, err, sc)
+
+
+@pytest.mark.parametrize("cin,cout,s,H", [(64, 128, 2, 24), (256, 512, 2, 6), (64, 64, 1, 12)])
+def test_pointwise_conv2d_split_wgrad_vs_fp64(cin, cout, s, H):
+    """layers.PointwiseConv2d (the lip ResNet 1x1 shortcut: one GEMM forward, split-GEMM weight gradient over frame
+    groups) on channels-last activations vs nn.Conv2d in fp64."""
+    from avse_challenge_amd.layers import PointwiseConv2d
+    torch.manual_seed(11)
+    ref = torch.nn.Conv2d(cin, cout, 1, stride=s, bias=False).double()
+    ours = PointwiseConv2d(cin, cout, s).to(DEV).to(memory_format=torch.channels_last)
+    ours.load_state_dict({n: v.float() for n, v in ref.state_dict().items()})
+    x = torch.randn(40, cin, H, H, dtype=torch.float64)
+    ho = (H - 1) // s + 1
+    gy = torch.randn(40, cout, ho, ho, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    (ref(xr) * gy).sum().backward()
+    xg = x.float().to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    (ours(xg) * gy.float().to(DEV)).sum().backward()
+    for got, want, what in ((xg.grad, xr.grad, "dx"), (ours.weight.grad, ref.weight.grad, "dw")):
+        err = float((got.double().cpu() - want).abs().max())
+        sc = float(want.abs().max())
+        assert err <= 2e-5 * sc, (what, err, sc)
