@@ -27,6 +27,9 @@ def golden():
 
 
 def pytest_collection_modifyitems(config, items):
+    # Multi-process tests (several ranks sharing one card) run after the single-process suite, so under -x a
+    # failure there cannot hide the kernel / model parity results (stable: file order kept otherwise).
+    items.sort(key=lambda it: os.path.basename(str(it.fspath)) in ("test_gpu_dist.py", "test_dist_cpu.py"))
     # GPU tests need the card; skip them cleanly (not fail) when torch sees no GPU and
     # the user did not explicitly select them.
     try:

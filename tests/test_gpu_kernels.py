@@ -9,6 +9,7 @@ import os
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from conftest import load_golden
 from oracle import mamba_ref, stft_ref
