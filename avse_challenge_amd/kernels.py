@@ -1685,3 +1685,4 @@ def gemm_f32s_time_chunks(sp, sq, alpha=1.0):
     check(_lib.lib().avse_gemm_f32s(a, stream_ptr(out.device)), "avse_gemm_f32s")
     _tap_end(tap, 2.0 * nb * mp * mq * kn)
     return out.sum(0)
+

@@ -1,4 +1,4 @@
-"""torch.profiler view of one eager avse1 C2 train step (bench.Avse1Step, B=32): device time per aten op and input
+"""torch.profiler view of one eager avse1 C2 train step (bench.Avse1Step, B=32; --workload: C3 / C4 / C5): device time per aten op and input
 shapes, to attribute the copy / transpose / add kernels of the step to their callers.
 python tools/avse1_op_profile.py [--batch 32] [--top 40] [--kernels PATTERN]
 --kernels PAT[/PAT...]: instead of the op table, list every launch of a kernel whose name contains PATTERN with the
@@ -28,11 +28,20 @@ def main():
     p.add_argument("--batch", type=int, default=32)
     p.add_argument("--top", type=int, default=40)
     p.add_argument("--kernels", default=None)
+    p.add_argument("--workload", default="avse1", choices=["avse1", "mamba", "avse4", "avmamba"],
+                   help="the bench step to profile (batch: --batch, default the BASELINE config's)")
     a = p.parse_args()
     # the profiler's post-processing (with stacks) can run for minutes without output: keep a heartbeat on stdout
     threading.Thread(target=lambda: [print(f"alive {i * 30}s", flush=True) or time.sleep(30) for i in range(10 ** 6)],
                      daemon=True).start()
-    st = bench.Avse1Step(a.batch, torch.device("cuda"), 0, 1, 96)
+    dev = torch.device("cuda")
+    if a.workload == "avse1":
+        st = bench.Avse1Step(a.batch, dev, 0, 1, 96)
+    elif a.workload == "avse4":
+        st = bench.Avse4Step(a.batch if a.batch != 32 else 16, dev, 0, 1)
+    else:
+        cls = bench.MambaStep if a.workload == "mamba" else bench.AVMambaStep
+        st = cls(a.batch if a.batch != 32 or a.workload == "avmamba" else 64, dev, 0, 1, "L")
     params = [q for q in st.model.parameters()]
 
     def step():
