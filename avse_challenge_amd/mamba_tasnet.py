@@ -308,6 +308,11 @@ class _InProj(torch.autograd.Function):
                 ctx.save_for_backward(hs.hi, hs.lo, hs.mb, w)
                 ctx.split = True
                 return out
+        dt = _autocast_dtype()
+        if dt is not None and h.dtype != dt:
+            # under autocast: cast once and keep the copy for the weight gradient (its bmm would cast h again: one
+            # (b, l, d_model) copy per layer and step, profiles/r06z_c5_library_ops.txt)
+            h = h.to(dt)
         ctx.save_for_backward(h, w)
         ctx.split = False
         return _wbmm(w, h.transpose(1, 2))
@@ -395,6 +400,9 @@ class _BiOutProj(torch.autograd.Function):
             dw = _bsum_split(dsp.t(), ys.t(), w.shape[0], w.shape[1], 0.5)         # 0.5 sum_b dout^T y^T
             return dy, (dy if ctx.two else None), dw
         y, w = ctx.saved_tensors
+        dt = _autocast_dtype()
+        if dt is not None and dout.dtype != dt:
+            dout = dout.to(dt)                          # one cast for both GEMMs below (each would cast its own copy)
         dy = _wbmm(w.t(), dout.transpose(1, 2), 0.5)                             # (b, d_inner, l)
         dw = _bsum_mm(dout.transpose(1, 2), y.transpose(1, 2), 0.5)               # (d_model, d_inner)
         return dy, (dy if ctx.two else None), dw
