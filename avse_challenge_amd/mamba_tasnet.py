@@ -224,9 +224,10 @@ def _dir_bwd(saved, dout, reverse, dxz=None, accumulate=False, dmax=None):
         dB_out=dx_dblT[:, R:R + NSTATE], dC_out=dx_dblT[:, R + NSTATE:], dz_accumulate=accumulate, dz_max=dmax)
     dx_dblT[:, :R] = _wbmm(dt_proj_w.t(), ddelta)
     ddt_proj_w = _bsum_mm(ddelta, x_dblT[:, :R].transpose(1, 2))               # (d, R)
-    dx_proj_w = _bsum_mm(dx_dblT, conv_out.transpose(1, 2))                    # (R + 2n, d)
+    dxd = dx_dblT.to(dconv.dtype)          # bf16 under autocast: one cast for both GEMMs (the bmm would cast its own)
+    dx_proj_w = _bsum_mm(dxd if _autocast_dtype() is not None else dx_dblT, conv_out.transpose(1, 2))  # (R + 2n, d)
     wxt = x_proj_w.t().to(dconv.dtype)
-    dconv.baddbmm_(wxt.expand(dconv.shape[0], *wxt.shape), dx_dblT.to(dconv.dtype))
+    dconv.baddbmm_(wxt.expand(dconv.shape[0], *wxt.shape), dxd)
     _, dconv_w, dconv_b = K.causal_conv1d_bwd(x, conv_w, conv_b, dconv, dx=dx, silu=True, reverse=reverse,
                                               dx_accumulate=accumulate, dx_max=dmax)
     return dxz, dconv_w.view_as(conv_w), dconv_b, dx_proj_w, ddt_proj_w, dA, dD, ddt_bias
