@@ -111,6 +111,8 @@ SIGNATURES = {
     "avse_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "avse_rmsnorm_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "avse_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "avse_add_rmsnorm_fwd2": (c_i32, [c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "avse_rmsnorm_bwd2": (c_i32, [c_i64, c_i64, c_vp, c_i32] + [c_vp] * 9),
     "avse_stft_frames": (c_i64, [c_i64]),
     "avse_stft_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "avse_istft": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),

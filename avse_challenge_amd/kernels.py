@@ -331,29 +331,44 @@ def causal_conv1d_bwd(x, weight, bias, dout, dx=None, silu=False, reverse=False,
 
 # ------------------------------------------------------------------------ add + RMSNorm
 
-def add_rmsnorm_fwd(h, res, weight, eps=1e-5):
-    """(norm(h + res) * w, h + res, rstd) over the last dim; res may be None."""
+def _rows_in(t, n):
+    """(rows, n) view of t for the RMSNorm kernels: fp32 or bf16 rows as they are (contiguous), anything else as fp32."""
+    if t.dtype not in (torch.float32, torch.bfloat16):
+        t = t.float()
+    return t.contiguous().view(-1, n)
+
+
+def add_rmsnorm_fwd(h, res, weight, eps=1e-5, out_dtype=None):
+    """(norm(h + res) * w, h + res, rstd) over the last dim; res may be None.  h fp32 or bf16 (read as it is); the output
+    in out_dtype (fp32 default, or bf16: rounded once); h + res and the statistics in fp32."""
     _need_gpu(h, res, weight)
     n = h.shape[-1]
-    h2 = h.float().contiguous().view(-1, n)
+    h2 = _rows_in(h, n)
     r2 = None if res is None else res.float().contiguous().view(-1, n)
     w = weight.float().contiguous()
     rows = h2.shape[0]
-    y = torch.empty_like(h2)
-    res_out = torch.empty_like(h2)
+    out_dtype = out_dtype or torch.float32
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise RuntimeError(f"add_rmsnorm_fwd: output dtype {out_dtype} (fp32 or bf16)")
+    y = torch.empty((rows, n), device=h.device, dtype=out_dtype)
+    res_out = torch.empty((rows, n), device=h.device, dtype=torch.float32)
     rstd = torch.empty((rows,), device=h.device, dtype=torch.float32)
     ymax = torch.empty(1, device=h.device, dtype=torch.int32)
-    check(_lib.lib().avse_add_rmsnorm_fwd(rows, n, ptr(h2), ptr(r2), ptr(w), float(eps), ptr(y), ptr(res_out),
-                                          ptr(rstd), ptr(ymax), stream_ptr(h.device)), "avse_add_rmsnorm_fwd")
+    dt = lambda t: AVSE_BF16 if t.dtype == torch.bfloat16 else AVSE_F32          # noqa: E731
+    check(_lib.lib().avse_add_rmsnorm_fwd2(rows, n, ptr(h2), dt(h2), ptr(r2), ptr(w), float(eps), ptr(y), dt(y),
+                                           ptr(res_out), ptr(rstd), ptr(ymax), stream_ptr(h.device)),
+          "avse_add_rmsnorm_fwd2")
     y = y.view(h.shape)
-    _set_absmax(y, ymax)                      # the producer-side max: the projection's split_planes skips its pass
+    if out_dtype == torch.float32:
+        _set_absmax(y, ymax)                  # the producer-side max: the projection's split_planes skips its pass
     return y, res_out.view(h.shape), rstd
 
 
 def rmsnorm_bwd(dy, dres_out, res_out, weight, rstd):
+    """(dx fp32, dweight) of add_rmsnorm_fwd; dy fp32 or bf16 (read as it is)."""
     _need_gpu(dy, dres_out, res_out, weight, rstd)
     n = res_out.shape[-1]
-    dy2 = dy.float().contiguous().view(-1, n)
+    dy2 = _rows_in(dy, n)
     dr2 = None if dres_out is None else dres_out.float().contiguous().view(-1, n)
     x2 = res_out.float().contiguous().view(-1, n)
     rows = x2.shape[0]
@@ -362,9 +377,9 @@ def rmsnorm_bwd(dy, dres_out, res_out, weight, rstd):
     ws = torch.empty((_lib.lib().avse_rmsnorm_bwd_workspace_bytes(rows, n) + 3) // 4, device=dy.device,
                      dtype=torch.float32)
     dxmax = torch.empty(1, device=dy.device, dtype=torch.int32)
-    check(_lib.lib().avse_rmsnorm_bwd(rows, n, ptr(dy2), ptr(dr2), ptr(x2), ptr(weight.float().contiguous()),
-                                      ptr(rstd), ptr(dx), ptr(dw), ptr(ws), ptr(dxmax), stream_ptr(dy.device)),
-          "avse_rmsnorm_bwd")
+    check(_lib.lib().avse_rmsnorm_bwd2(rows, n, ptr(dy2), AVSE_BF16 if dy2.dtype == torch.bfloat16 else AVSE_F32,
+                                       ptr(dr2), ptr(x2), ptr(weight.float().contiguous()), ptr(rstd), ptr(dx),
+                                       ptr(dw), ptr(ws), ptr(dxmax), stream_ptr(dy.device)), "avse_rmsnorm_bwd2")
     dx = dx.view(res_out.shape)
     _set_absmax(dx, dxmax)
     return dx, dw

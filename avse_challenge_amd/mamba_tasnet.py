@@ -413,8 +413,12 @@ class AddRMSNorm(torch.autograd.Function):
     """(RMSNorm(h + res) * w, h + res) — bimamba.py:447-451 with mamba-ssm RMSNorm (eps 1e-5)."""
 
     @staticmethod
-    def forward(ctx, h, res, weight, eps):
-        y, res_out, rstd = K.add_rmsnorm_fwd(h, res, weight, eps)
+    def forward(ctx, h, res, weight, eps, mixer_input=False):
+        # mixer_input (Block): under bf16 autocast the norm output is written in bf16 — the mixer's in_proj casts it
+        # there anyway, and mamba-ssm's fused add_norm returns its input's dtype (bf16 under autocast) — and h (the
+        # previous mixer's bf16 output) is read as it is; h + res and the statistics stay fp32 (residual_in_fp32)
+        dt = _autocast_dtype() if mixer_input else None
+        y, res_out, rstd = K.add_rmsnorm_fwd(h, res, weight, eps, out_dtype=dt if dt == torch.bfloat16 else None)
         ctx.has_res = res is not None
         ctx.save_for_backward(res_out, weight, rstd)
         return y, res_out
@@ -423,7 +427,7 @@ class AddRMSNorm(torch.autograd.Function):
     def backward(ctx, dy, dres):
         res_out, weight, rstd = ctx.saved_tensors
         dx, dw = K.rmsnorm_bwd(dy, dres, res_out, weight, rstd)
-        return dx, (dx if ctx.has_res else None), dw, None
+        return dx, (dx if ctx.has_res else None), dw, None, None
 
 
 class RMSNorm(nn.Module):
@@ -538,7 +542,7 @@ class Block(nn.Module):
         self.norm = RMSNorm(d_model, eps)
 
     def forward(self, h, residual=None):
-        y, residual = AddRMSNorm.apply(h, residual, self.norm.weight, self.norm.eps)
+        y, residual = AddRMSNorm.apply(h, residual, self.norm.weight, self.norm.eps, True)
         return self.mixer(y), residual
 
 

@@ -171,6 +171,15 @@ int64_t avse_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t n);
 int avse_rmsnorm_bwd(int64_t rows, int64_t n, const float* dy, const float* dres_out /* or NULL */,
                      const float* res_out, const float* weight, const float* rstd,
                      float* dx, float* dweight, float* workspace, uint32_t* dx_max, avse_stream_t stream);
+/* The same with the row dtypes named (round 6): h / y (forward) and dy (backward) AVSE_F32 or AVSE_BF16 (bf16 rows 8-B
+ * aligned; y rounded to nearest even; the statistics, res_in / res_out and dx stay fp32): the autocast Block of C5, whose
+ * mixer output enters and whose norm output leaves in bf16, as mamba-ssm's fused add_norm returns its input's dtype. */
+int avse_add_rmsnorm_fwd2(int64_t rows, int64_t n, const void* h, int32_t h_dtype, const float* res_in /* or NULL */,
+                          const float* weight, float eps, void* y, int32_t y_dtype, float* res_out, float* rstd,
+                          uint32_t* y_max, avse_stream_t stream);
+int avse_rmsnorm_bwd2(int64_t rows, int64_t n, const void* dy, int32_t dy_dtype, const float* dres_out /* or NULL */,
+                      const float* res_out, const float* weight, const float* rstd, float* dx, float* dweight,
+                      float* workspace, uint32_t* dx_max, avse_stream_t stream);
 
 /* ---------------------------------------------------------------- STFT / iSTFT --------
  * Replaces the CPU librosa 0.8.1 calls of baseline/avse1/dataset.py:112-118 (stft, n_fft

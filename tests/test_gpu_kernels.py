@@ -365,6 +365,26 @@ def test_add_rmsnorm_vs_oracle(n, with_res):
         assert torch.equal(sk.hi, sf.hi) and torch.equal(sk.lo, sf.lo) and torch.equal(sk.mb, sf.mb)
 
 
+@pytest.mark.parametrize("n", [512, 256])
+def test_add_rmsnorm_bf16_rows_equal_fp32_path(n):
+    """bf16 rows (the C5 Block under autocast, avse_add_rmsnorm_fwd2 / avse_rmsnorm_bwd2): h read as bf16 and y written
+    in bf16 give bit for bit the fp32 path's results on h.float() with y rounded once; a bf16 dy gives the fp32 path's
+    dx / dweight on dy.float()."""
+    rows = 333
+    h = det_input((rows, n), 410).to(DEV).to(torch.bfloat16)
+    r = det_input((rows, n), 411).to(DEV)
+    w = (1.0 + 0.1 * det_input((n,), 412)).to(DEV)
+    y32, r32, s32 = K().add_rmsnorm_fwd(h.float(), r, w, 1e-5)
+    y16, r16, s16 = K().add_rmsnorm_fwd(h, r, w, 1e-5, out_dtype=torch.bfloat16)
+    assert y16.dtype == torch.bfloat16 and r16.dtype == torch.float32
+    assert torch.equal(y16, y32.to(torch.bfloat16)) and torch.equal(r16, r32) and torch.equal(s16, s32)
+    gy = det_input((rows, n), 413).to(DEV).to(torch.bfloat16)
+    gr = det_input((rows, n), 414).to(DEV)
+    d32, w32 = K().rmsnorm_bwd(gy.float(), gr, r32, w, s32)
+    d16, w16 = K().rmsnorm_bwd(gy, gr, r32, w, s32)
+    assert torch.equal(d16, d32) and torch.equal(w16, w32)
+
+
 # ------------------------------------------------------------------ STFT / iSTFT (librosa 0.8.1 semantics)
 
 @pytest.mark.parametrize("T", [48000, 16000, 1000])
