@@ -44,7 +44,7 @@ os.environ.setdefault("PYTORCH_MIOPEN_SUGGEST_NHWC_BATCHNORM", "1")
 METRIC = "utterances/sec (3s@16kHz + 75 lip frames)"
 # HBM bytes per launch of each roofline kernel, from rocprofv3 PMC passes (tools/pmc_traffic.sh:
 # FETCH_SIZE and WRITE_SIZE in separate passes, corrected as MI355X_MICROARCH.md prescribes)
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r04_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r06_traffic.json")   # tools/runs/r06ad.sh (final round-6 tree)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFS = 157.3          # FP32 matrix (= vector) peak, spec
 
